@@ -1,0 +1,81 @@
+"""ctypes binding of the CPU restatement (oracle/sccg_oracle.c) -- the parity CHECKER.
+
+Test infrastructure only: never imported by the product package."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(REPO, "oracle", "libsccg_oracle.so")
+_lib = None
+
+
+class OracleError(RuntimeError):
+    def __init__(self, rc: int, partial: bytes | None = None):
+        super().__init__(f"oracle rc={rc}")
+        self.rc = rc
+        self.partial = partial
+
+
+class OrcRec(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("p", ctypes.c_int32), ("l", ctypes.c_int32),
+                ("t", ctypes.c_int64)]
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
+        lib = ctypes.CDLL(LIB_PATH)
+        pp, psz = ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)
+        lib.orc_compress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, pp, psz]
+        lib.orc_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, pp, psz]
+        lib.orc_match.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                  ctypes.POINTER(ctypes.POINTER(OrcRec)), ctypes.POINTER(ctypes.c_int64)]
+        lib.orc_free.argtypes = [ctypes.c_void_p]
+        lib.orc_last_mode_global.restype = ctypes.c_int
+        lib.orc_last_switch_segment.restype = ctypes.c_int64
+        _lib = lib
+    return _lib
+
+
+def _call(fn, a: bytes, b: bytes) -> bytes:
+    lib = _load()
+    out, n = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = fn(a, len(a), b, len(b), ctypes.byref(out), ctypes.byref(n))
+    data = ctypes.string_at(out, n.value) if out.value else None
+    if out.value:
+        lib.orc_free(out)
+    if rc:
+        raise OracleError(rc, data)
+    return data
+
+
+def compress(ref_fa: bytes, tgt_fa: bytes) -> bytes:
+    """compressed_genome.txt bytes (compression.cpp:320-580, without 7z)."""
+    return _call(_load().orc_compress, ref_fa, tgt_fa)
+
+
+def last_mode() -> tuple[bool, int]:
+    lib = _load()
+    return bool(lib.orc_last_mode_global()), int(lib.orc_last_switch_segment())
+
+
+def decompress(record: bytes, ref_fa: bytes) -> bytes:
+    """reconstructed_genome.fa bytes (decompression.cpp, after 7z)."""
+    return _call(_load().orc_decompress, record, ref_fa)
+
+
+def match(sr: bytes, st: bytes, k: int, m: int, glob: bool, offset: int = 0):
+    """compression.cpp:36 match_sequences -> [(kind, p, l, t)]"""
+    lib = _load()
+    recs, n = ctypes.POINTER(OrcRec)(), ctypes.c_int64()
+    rc = lib.orc_match(sr, len(sr), st, len(st), k, m, int(glob), offset, ctypes.byref(recs), ctypes.byref(n))
+    if rc:
+        raise OracleError(rc)
+    out = [(recs[i].kind, recs[i].p, recs[i].l, recs[i].t) for i in range(n.value)]
+    lib.orc_free(recs)
+    return out

@@ -1,0 +1,92 @@
+"""Pin the CPU restatement (oracle/) against the reference's own outputs.
+
+* every committed fixture (tests/golden/cases, produced by the compiled reference) must be
+  reproduced byte-for-byte, including the exit-code behaviour;
+* the larger generator seeds must hash to the reference's sha256 (synth_manifest.json);
+* when oracle/_ref exists (the build container), a wider differential fuzz runs live.
+"""
+import hashlib
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+import fuzzgen
+import goldens
+import oraclelib
+import synthlib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_BIN = os.path.join(REPO, "oracle", "_ref")
+HAVE_REF = os.path.exists(os.path.join(REF_BIN, "compression"))
+
+
+def _check_case(c):
+    try:
+        rec = oraclelib.compress(c["ref_fa"], c["tgt_fa"])
+        rc = 0
+    except oraclelib.OracleError as e:
+        rec, rc = e.partial, 1
+    assert rc == c["compress_rc"], c["name"]
+    assert rec == c["record"], c["name"]
+    if c["decompress_rc"] is None:
+        return
+    try:
+        fa = oraclelib.decompress(rec, c["ref_fa"])
+        drc = 0
+    except oraclelib.OracleError:
+        fa, drc = None, 1
+    assert drc == c["decompress_rc"], c["name"]
+    if drc == 0:
+        assert fa == c["fasta"], c["name"]
+
+
+def test_golden_fixtures(golden_cases):
+    assert len(golden_cases) >= 40
+    for c in golden_cases:
+        _check_case(c)
+
+
+def test_quirk_b1_sentinel(golden_cases):
+    c = next(c for c in golden_cases if c["name"] == "b1_pn0_sentinel")
+    # the tie between candidate 0 and candidate 100 goes to 100 (compression.cpp:125)
+    assert b"(100,30)" in c["record"]
+
+
+def test_quirk_b2_stuck(golden_cases):
+    c = next(c for c in golden_cases if c["name"] == "b2_stuck_walk")
+    tail = c["record"].rsplit(b")", 1)[1]
+    assert len(tail) > 5000 and set(tail) <= set(b"ACGT")
+
+
+@pytest.mark.parametrize("entry", goldens.synth_manifest(), ids=lambda e: f"{e['profile']}-{e['seed']}")
+def test_synth_manifest(entry):
+    if entry["ref_len"] > 3_000_000:
+        pytest.skip("large seed: covered on the GPU box")
+    rfa, tfa = synthlib.synth_pair(entry["profile"], entry["ref_len"], entry["tgt_len"], entry["seed"])
+    assert hashlib.sha256(rfa).hexdigest() == entry["ref_fa_sha256"]
+    assert hashlib.sha256(tfa).hexdigest() == entry["tgt_fa_sha256"]
+    rec = oraclelib.compress(rfa, tfa)
+    assert hashlib.sha256(rec).hexdigest() == entry["record_sha256"]
+    fa = oraclelib.decompress(rec, rfa)
+    assert hashlib.sha256(fa).hexdigest() == entry["fasta_sha256"]
+
+
+def _run_ref(rfa, tfa):
+    env = dict(os.environ, PATH=os.path.join(REPO, "oracle", "stub7z") + os.pathsep + os.environ["PATH"])
+    with tempfile.TemporaryDirectory() as d:
+        rp, tp = os.path.join(d, "r.fa"), os.path.join(d, "t.fa")
+        open(rp, "wb").write(rfa)
+        open(tp, "wb").write(tfa)
+        subprocess.run([os.path.join(REF_BIN, "compression"), rp, tp, os.path.join(d, "o")], env=env,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True)
+        return open(os.path.join(d, "o", "compressed_genome.txt"), "rb").read()
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built (reference sources absent)")
+@pytest.mark.parametrize("kind,seed", [("local", s) for s in range(100, 160)] +
+                         [("global", s) for s in range(100, 124)])
+def test_differential_vs_reference(kind, seed):
+    rfa, tfa = (fuzzgen.local_case if kind == "local" else fuzzgen.global_case)(seed)
+    assert oraclelib.compress(rfa, tfa) == _run_ref(rfa, tfa)
