@@ -1,0 +1,114 @@
+/*
+ * sccg.h -- C ABI of the MI355X-native SCCG hot path (libsccg.so).
+ *
+ * The reference (Jan-Celin/SCCG-genome-compression) has no library or FFI: its drop-in boundary
+ * is the two command lines plus the record-file format.  This header is the
+ * seam a host program binds to; the repository's `compression` / `decompression` executables are
+ * thin CLIs over it with the reference's argv, output paths, 7z calls and exit codes.
+ *
+ * Entry point                         replaces (reference file:line)
+ * ----------------------------------  -------------------------------------------------------------
+ * sccg_compress / _device             compress_genome up to the 7z call  compression.cpp:320-580
+ *                                     (read_genomes_from_files :181-220, lowercase/N run lines
+ *                                     :341-368/:495-555, local loop :372-481, global pass
+ *                                     :484-574, delta_encode :222-304)
+ * sccg_match                          match_sequences                    compression.cpp:36-179
+ * sccg_reconstruct / _device          decompress_genome after 7z +       decompression.cpp:43-114,
+ *                                     reconstruct_genome + file body     :117-279, :316-323
+ *
+ * Conventions: status ints (0 = OK); the library never calls exit(); host buffers it returns are
+ * malloc'ed and released with sccg_buf_free.  One context per GPU; a context is not re-entrant;
+ * contexts on different GPUs may be driven from different host threads.  Every compute path runs
+ * on the GPU -- there is no CPU fallback; without a usable device sccg_ctx_create fails.
+ */
+#ifndef SCCG_H
+#define SCCG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCCG_OK             0
+#define SCCG_E_INVALID      1  /* bad argument */
+#define SCCG_E_HIP          2  /* HIP runtime error (message in sccg_last_error) */
+#define SCCG_E_NOMEM        3  /* device or host allocation failed */
+#define SCCG_E_DELTA_STOI   4  /* delta_encode's stoi would throw (compression.cpp:279): the
+                                  reference then leaves the un-delta'd text and exits 1; the text
+                                  returned is that un-delta'd text */
+#define SCCG_E_FORMAT       5  /* record file misses a line (decompression.cpp:68-97) */
+#define SCCG_E_RANGE        6  /* token beyond the reference (decompression.cpp:223-229) */
+#define SCCG_E_PARSE        7  /* malformed run line / token (decompression.cpp:309-311) */
+#define SCCG_E_UNSUPPORTED  8  /* shape outside what sccg_match accepts (see below) */
+#define SCCG_E_INTERNAL     9  /* internal consistency check failed */
+
+typedef struct sccg_ctx sccg_ctx;
+
+typedef struct {
+    char* data;
+    size_t len;
+} sccg_buf;
+
+/* match_sequences' vector<Position> as SoA (compression.cpp:20-24): kind 1 = match (pos
+ * includes the offset, :153), kind 0 = literal run St[t, t+len). */
+typedef struct {
+    uint8_t* kind;
+    int32_t* pos;
+    int32_t* len;
+    int64_t* t;
+    int64_t n;
+} sccg_records;
+
+typedef struct {
+    int mode_global;          /* 1 when the local loop switched (compression.cpp:462-473) */
+    int64_t switch_segment;   /* segment index of the switch, -1 if it stayed local */
+    int64_t target_bases;     /* |T| after whitespace strip (compression.cpp:218) */
+    int64_t reference_bases;  /* |R| */
+    int64_t n_matches;        /* (p,l) tokens on the record line */
+    int64_t literal_bases;    /* literal bytes on the record line */
+    int64_t walk_rounds;      /* global walk: speculative + fix-up rounds */
+    int64_t walk_chunks;      /* global walk: chunks */
+    int64_t record_bytes;     /* length of the whole compressed_genome.txt */
+} sccg_stats;
+
+int sccg_ctx_create(int device, sccg_ctx** out);
+void sccg_ctx_destroy(sccg_ctx* ctx);
+const char* sccg_last_error(const sccg_ctx* ctx);
+int sccg_last_stats(const sccg_ctx* ctx, sccg_stats* out);
+
+/* Whole-file compression up to (excluding) 7z: returns the exact bytes of
+ * <out>/compressed_genome.txt for the given reference/target FASTA file contents. */
+int sccg_compress(sccg_ctx* ctx, const char* ref_fa, size_t ref_len, const char* tgt_fa,
+                  size_t tgt_len, sccg_buf* out_text);
+
+/* Same, HBM-resident: inputs are device pointers, the text is written to d_out (capacity
+ * out_cap bytes; sccg_compress_bound gives a safe capacity) and *out_len is set.  `stream` is a
+ * hipStream_t (NULL = the context's own stream).  Synchronises before returning. */
+int sccg_compress_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len, const void* d_tgt_fa,
+                         size_t tgt_len, void* d_out, size_t out_cap, size_t* out_len, void* stream);
+size_t sccg_compress_bound(size_t ref_len, size_t tgt_len);
+
+/* match_sequences(Sr, St, k, m, global, offset) on already-uppercased byte strings.  Accepted
+ * shapes: global == 0 with |Sr| <= 1000 and |St| <= 1000 (the local-segment kernel), or
+ * global == 1 with 0 <= m <= 1000 (the windowed global walk).  Others: SCCG_E_UNSUPPORTED. */
+int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, size_t nt, int k,
+               int m, int global, int64_t offset, sccg_records* out);
+void sccg_records_free(sccg_records* r);
+
+/* Decompression after 7z: record text (contents of the extracted compressed_genome.txt) +
+ * reference FASTA -> exact bytes of <out>/reconstructed_genome.fa. */
+int sccg_reconstruct(sccg_ctx* ctx, const char* ref_fa, size_t ref_len, const char* rec_text,
+                     size_t rec_len, sccg_buf* out_fa);
+/* HBM-resident form.  With d_out == NULL only *out_len (the exact output size) is computed;
+ * with out_cap too small it returns SCCG_E_NOMEM and sets *out_len to the size needed. */
+int sccg_reconstruct_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len, const void* d_rec,
+                            size_t rec_len, void* d_out, size_t out_cap, size_t* out_len, void* stream);
+
+void sccg_buf_free(sccg_buf* b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,68 @@
+// compression -- drop-in for the reference CLI `compression <reference_file> <target_file>
+// <output_folder>` (compression.cpp:584-610): writes <output_folder>/compressed_genome.txt with
+// the record stream computed on the GPU (libsccg) and then runs the same 7z command
+// (compression.cpp:306-318).  Exit codes follow the reference: 1 on usage / open / 7z errors.
+#include "cli_common.h"
+
+int main(int argc, char* argv[]) {
+    if (argc != 4) {
+        std::cerr << "Usage: " << argv[0] << " <reference_file> <target_file> <output_folder>\n";
+        return 1;
+    }
+    const std::string ref_path = argv[1], tgt_path = argv[2], out_dir = argv[3];
+    try {
+        if (!std::filesystem::exists(out_dir)) std::filesystem::create_directory(out_dir);
+    } catch (const std::exception& ex) {
+        std::cerr << "Error: " << ex.what() << "\n";
+        return 1;
+    }
+    std::cout << "Successfully created output folder: " << out_dir << "\n";
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    std::string ref, tgt;
+    if (!slurp(ref_path, ref)) {
+        std::cerr << "Error opening reference file: " << ref_path << "\n";
+        return 1;
+    }
+    if (!slurp(tgt_path, tgt)) {
+        std::cerr << "Error opening target file: " << tgt_path << "\n";
+        return 1;
+    }
+    sccg_ctx* ctx = nullptr;
+    int rc = sccg_ctx_create(cli_device(), &ctx);
+    if (rc) {
+        std::cerr << "Error: no usable GPU (sccg_ctx_create rc=" << rc << ")\n";
+        return 1;
+    }
+    sccg_buf text{};
+    rc = sccg_compress(ctx, ref.data(), ref.size(), tgt.data(), tgt.size(), &text);
+    if (rc && rc != SCCG_E_DELTA_STOI) {
+        std::cerr << "Error: " << sccg_last_error(ctx) << " (rc=" << rc << ")\n";
+        sccg_ctx_destroy(ctx);
+        return 1;
+    }
+    std::filesystem::create_directories(out_dir);
+    const std::string txt = out_dir + "/compressed_genome.txt";
+    if (!spit(txt, text.data, text.len)) {
+        std::cerr << "Greska pri otvaranju datoteke: " << txt << "\n";
+        return 1;
+    }
+    sccg_buf_free(&text);
+    sccg_stats st{};
+    sccg_last_stats(ctx, &st);
+    sccg_ctx_destroy(ctx);
+    if (rc == SCCG_E_DELTA_STOI) {   // the reference throws from stoi inside delta_encode
+        std::cerr << "Error: stoi\n";
+        return 1;
+    }
+    std::cout << "mode=" << (st.mode_global ? "global" : "local") << " switch=" << st.switch_segment
+              << " matches=" << st.n_matches << " bytes=" << st.record_bytes << "\n";
+    const std::string cmd = "7z a -mx=9 \"" + txt + ".7z\" \"" + txt + "\"";
+    const int r = std::system(cmd.c_str());
+    if (r != 0) {
+        std::cerr << "Greska prilikom komprimiranja datoteke 7-zipom: " << r << " !\n";
+        return 1;
+    }
+    const std::chrono::duration<double> dt = std::chrono::high_resolution_clock::now() - t0;
+    std::cout << "Time taken to compress: " << dt.count() << " s\n";
+    return 0;
+}

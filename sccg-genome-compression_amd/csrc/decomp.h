@@ -1,0 +1,26 @@
+// decomp.h -- launchers of decomp.hip (reconstruction), driven by sccg_api.cpp.
+#pragma once
+#include "internal.h"
+
+struct DcRuns {
+    int32_t* start;   // run starts (ascending, disjoint)
+    int32_t* len;     // run lengths
+    int64_t* cum;     // exclusive prefix of len
+    int64_t n;        // runs
+    int64_t total;    // sum of len
+};
+
+// positions of the first four '\n' of the record text (n when absent) -> d_nl[0..3]
+int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl, hipStream_t s);
+// parse a lowercase / N run line (decompression.cpp:126-207) into r (arrays pre-allocated with
+// capacity n/2+1); d_err bit0 set on text outside the grammar
+int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
+                  int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s);
+// record line: per-byte output contribution / token deltas, output offsets, absolute p, range
+// check (d_err bit1 = token beyond the reference); *d_total = decoded length
+int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,
+                      int64_t* d_dsum, int64_t nref, int64_t* d_partial, int32_t* d_err, int64_t* d_total, hipStream_t s);
+int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
+                   const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s);
+// N insertion + lowercase + 50-column wrap of nres result bytes into d_out (no final '\n')
+int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, uint8_t* d_out, hipStream_t s);

@@ -1,0 +1,327 @@
+// decomp.hip -- reconstruction of the target FASTA from the record text (decompression.cpp).
+//
+//   line split                  decompression.cpp:66-101
+//   run-line parse              decompression.cpp:126-207 ("(d,len)" / "d," items, running start)
+//   token decode                decompression.cpp:210-236 ("(dp,l)" -> ref[p, p+l), literals)
+//   N insertion, lowercase      decompression.cpp:241-262
+//   50-column output            decompression.cpp:266-274, :322
+//
+// All of it is data-parallel: item starts are found with a scan of "last parenthesis" positions,
+// numbers are parsed one item per thread, running starts / absolute p are prefix sums, output
+// offsets are prefix sums, and the final FASTA is written position-by-position with N and
+// lowercase membership found by binary search over the (sorted, disjoint) run lists.
+// Inputs the reference's own compressor can produce are handled exactly; text outside that
+// grammar is reported as SCCG_E_PARSE instead of reproducing the reference's undefined paths.
+#include "internal.h"
+#include "decomp.h"
+
+namespace {
+
+__device__ __forceinline__ bool is_num(uint8_t c) { return (c >= '0' && c <= '9') || c == '-' || c == '+'; }
+
+// stoi on [s, e): optional sign then digits, all of [s,e) consumed; returns false otherwise
+__device__ __forceinline__ bool parse_int(const uint8_t* s, int64_t n, int64_t a, int64_t e, int64_t* v) {
+    if (a >= e) return false;
+    bool neg = false;
+    if (s[a] == '-' || s[a] == '+') { neg = s[a] == '-'; a++; }
+    if (a >= e || e - a > 10) return false;
+    int64_t x = 0;
+    for (int64_t i = a; i < e; i++) {
+        const uint8_t c = s[i];
+        if (c < '0' || c > '9') return false;
+        x = x * 10 + (c - '0');
+    }
+    x = neg ? -x : x;
+    if (x > INT32_MAX || x < INT32_MIN) return false;
+    *v = x;
+    (void)n;
+    return true;
+}
+
+__global__ void k_find_from(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ from_slot,
+                            int64_t* __restrict__ res, uint8_t c) {
+    const int64_t from = from_slot ? *from_slot + 1 : 0;
+    const int64_t CH = 1 << 16;
+    const int64_t base = from + (int64_t)blockIdx.x * CH;
+    if (from > n) return;
+    if (base >= (int64_t)__hip_atomic_load((unsigned long long*)res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    for (int64_t i = base + threadIdx.x; i < base + CH && i < n; i += blockDim.x)
+        if (s[i] == c) atomicMin((unsigned long long*)res, (unsigned long long)i);
+}
+
+// positions of '(' / ')' -> value i, else -1 (for a max-scan: last parenthesis at or before i)
+__global__ void k_paren_pos(const uint8_t* __restrict__ s, int64_t n, int64_t* __restrict__ v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        v[i] = (s[i] == '(' || s[i] == ')') ? i : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// run lines: item start flags (exclusive max-scan `lp` = last paren strictly before i)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool run_item_start(const uint8_t* s, int64_t i, int64_t lp_excl) {
+    const uint8_t c = s[i];
+    if (c == '(') return true;
+    if (!is_num(c)) return false;
+    const bool inside = lp_excl >= 0 && s[lp_excl] == '(';
+    return !inside && (i == 0 || !is_num(s[i - 1]));
+}
+
+__global__ void k_run_items_flag(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ lp,
+                                 int64_t* __restrict__ flag, int32_t* __restrict__ err) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const bool st = run_item_start(s, i, lp[i]);
+        flag[i] = st;
+        // bytes outside any item must be ',' (a ')' closes a tuple)
+        const uint8_t c = s[i];
+        const bool inside = (lp[i] >= 0 && s[lp[i]] == '(') || c == '(' || c == ')';
+        if (!inside && !is_num(c) && c != ',') atomicOr(err, 1);
+    }
+}
+
+__global__ void k_run_items_parse(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ lp,
+                                  const int64_t* __restrict__ rank, int64_t* __restrict__ dlt,
+                                  int32_t* __restrict__ len, int32_t* __restrict__ err) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!run_item_start(s, i, lp[i])) continue;
+        const int64_t r = rank[i];
+        int64_t d = 0, l = 1;
+        bool ok;
+        if (s[i] == '(') {
+            int64_t comma = -1, close = -1;
+            for (int64_t q = i + 1; q < n && q < i + 32; q++) {
+                if (s[q] == ',' && comma < 0) comma = q;
+                if (s[q] == ')') { close = q; break; }
+                if (s[q] == '(') break;
+            }
+            ok = comma > 0 && close > comma && parse_int(s, n, i + 1, comma, &d) && parse_int(s, n, comma + 1, close, &l);
+            // a ',' right after ')' is consumed by the reference parser (decompression.cpp:143-144)
+        } else {
+            int64_t e = i;
+            while (e < n && is_num(s[e])) e++;
+            ok = (e == n || s[e] == ',') && parse_int(s, n, i, e, &d);
+        }
+        if (!ok || l < 0) { atomicOr(err, 1); continue; }
+        dlt[r] = d;
+        len[r] = (int32_t)l;
+    }
+}
+
+// starts = inclusive prefix of deltas (exclusive scan + own delta); runs must be ascending & disjoint
+__global__ void k_run_finish(const int64_t* __restrict__ dex, const int64_t* __restrict__ dlt, const int32_t* __restrict__ len,
+                             int64_t nr, int32_t* __restrict__ start, int32_t* __restrict__ err) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t st = dex[r] + dlt[r];
+        const int64_t pst = r ? dex[r - 1] + dlt[r - 1] : INT64_MIN;
+        const int64_t pend = r ? pst + len[r - 1] : 0;
+        if (st < 0 || st > INT32_MAX || (r && st < pend)) atomicOr(err, 1);
+        start[r] = (int32_t)st;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// record line
+// ---------------------------------------------------------------------------------------------
+// per byte: output contribution (literal 1, token l, else 0) and token delta (tokens only)
+__global__ void k_tok_parse(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ lp,
+                            int64_t* __restrict__ contrib, int64_t* __restrict__ dlt, int32_t* __restrict__ err) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t c = s[i];
+        const bool inside = lp[i] >= 0 && s[lp[i]] == '(';
+        int64_t cb = 0, d = 0;
+        if (c == '(') {
+            int64_t comma = -1, close = -1;
+            for (int64_t q = i + 1; q < n && q < i + 32; q++) {
+                if (s[q] == ',' && comma < 0) comma = q;
+                if (s[q] == ')') { close = q; break; }
+                if (s[q] == '(') break;
+            }
+            int64_t l = 0;
+            if (!(comma > 0 && close > comma && parse_int(s, n, i + 1, comma, &d) && parse_int(s, n, comma + 1, close, &l)) || l < 0)
+                atomicOr(err, 1);
+            cb = l;
+        } else if (c == ')') {
+            if (!inside) atomicOr(err, 1);   // a stray ')' outside a token
+            cb = 0;
+        } else if (!inside) {
+            cb = 1;
+        }
+        contrib[i] = cb;
+        dlt[i] = d;
+    }
+}
+
+// absolute p = running sum of deltas over tokens (decompression.cpp:220-222); range check :223
+__global__ void k_tok_check(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ dsum,
+                            const int64_t* __restrict__ dlt, const int64_t* __restrict__ contrib, int64_t nref,
+                            int32_t* __restrict__ err) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (s[i] != '(') continue;
+        const int64_t p = dsum[i] + dlt[i];
+        if (p < 0 || p + contrib[i] > nref) atomicOr(err, 2);
+    }
+}
+
+__global__ void k_len_to_i64(const int32_t* __restrict__ len, int64_t n, int64_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = len[i];
+}
+
+constexpr int WPB = 4;
+__global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill(const uint8_t* __restrict__ s, int64_t n,
+                                                         const int64_t* __restrict__ lp, const int64_t* __restrict__ off,
+                                                         const int64_t* __restrict__ dsum, const int64_t* __restrict__ dlt,
+                                                         const int64_t* __restrict__ contrib, const uint8_t* __restrict__ R,
+                                                         uint8_t* __restrict__ dec) {
+    // one wave per 64-byte stretch of the record line; tokens are copied by the whole wave
+    const int64_t base = ((int64_t)blockIdx.x * WPB + wave_in_block()) * 64;
+    if (base >= n) return;
+    const int lane = lane_id();
+    const int64_t i = base + lane;
+    bool tok = false;
+    if (i < n) {
+        const uint8_t c = s[i];
+        const bool inside = lp[i] >= 0 && s[lp[i]] == '(';
+        if (c == '(') tok = true;
+        else if (c != ')' && !inside) dec[off[i]] = c;
+    }
+    unsigned long long tm = __ballot(tok);
+    while (tm) {
+        const int j = __ffsll((long long)tm) - 1;
+        tm &= tm - 1;
+        const int64_t ij = base + j;
+        const int64_t p = dsum[ij] + dlt[ij], l = contrib[ij], o = off[ij];
+        for (int64_t q = lane; q < l; q += 64) dec[o + q] = R[p + q];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// output: header '\n' then result wrapped at 50 columns + final '\n'
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t first_run_ending_after(const int32_t* st, const int32_t* ln, int64_t nr, int64_t j) {
+    int64_t a = 0, b = nr;   // first r with st[r] + ln[r] > j
+    while (a < b) {
+        const int64_t m = (a + b) >> 1;
+        if ((int64_t)st[m] + ln[m] > j) b = m; else a = m + 1;
+    }
+    return a;
+}
+
+constexpr int OUT_PER_T = 64;
+__global__ void k_format(const uint8_t* __restrict__ dec, int64_t nres, const int32_t* __restrict__ ns,
+                         const int32_t* __restrict__ nl, const int64_t* __restrict__ ncum, int64_t nn,
+                         const int32_t* __restrict__ ls, const int32_t* __restrict__ ll, int64_t nlr,
+                         uint8_t* __restrict__ out) {
+    const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * OUT_PER_T;
+    if (j0 >= nres) return;
+    int64_t rn = first_run_ending_after(ns, nl, nn, j0);
+    int64_t rl = first_run_ending_after(ls, ll, nlr, j0);
+    for (int64_t j = j0; j < j0 + OUT_PER_T && j < nres; j++) {
+        while (rn < nn && (int64_t)ns[rn] + nl[rn] <= j) rn++;
+        while (rl < nlr && (int64_t)ls[rl] + ll[rl] <= j) rl++;
+        uint8_t c;
+        if (rn < nn && ns[rn] <= j) c = 'N';
+        else {
+            const int64_t nbefore = rn < nn ? ncum[rn] : (nn ? ncum[nn - 1] + nl[nn - 1] : 0);
+            c = dec[j - nbefore];
+        }
+        if (rl < nlr && ls[rl] <= j) c = c_tolower(c);
+        const int64_t o = j + j / 50;
+        out[o] = c;
+        if (j % 50 == 49 && j != nres - 1) out[o + 1] = '\n';
+    }
+}
+
+}  // namespace
+
+// =============================================================================================
+int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl /*4*/, hipStream_t s) {
+    int rc = dev_set_i64(d_nl, 4, {n, n, n, n}, s);
+    if (rc) return rc;
+    const unsigned g = grid_for(n > 0 ? n : 1, 1 << 16);
+    for (int i = 0; i < 4; i++)
+        hipLaunchKernelGGL(k_find_from, dim3(g), dim3(256), 0, s, d_rec, n, i ? (const int64_t*)(d_nl + i - 1) : nullptr,
+                           d_nl + i, (uint8_t)'\n');
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int dc_last_paren(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_partial, hipStream_t s) {
+    if (n <= 0) return 0;
+    const unsigned g = grid_for(n, 256) > 8192 ? 8192 : grid_for(n, 256);
+    hipLaunchKernelGGL(k_paren_pos, dim3(g), dim3(256), 0, s, d_s, n, d_lp);
+    SCCG_HIP(hipGetLastError());
+    // exclusive max-scan: last parenthesis strictly before i; the inclusive form is not needed
+    return dev_excl_max(d_lp, d_lp, n, nullptr, d_partial, s);
+}
+
+int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
+                  int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s) {
+    if (n <= 0) { r->n = 0; return 0; }
+    int rc = dc_last_paren(d_s, n, d_lp, d_partial, s);
+    if (rc) return rc;
+    const unsigned g = grid_for(n, 256) > 8192 ? 8192 : grid_for(n, 256);
+    hipLaunchKernelGGL(k_run_items_flag, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_lp, d_flag, d_err);
+    rc = dev_excl_sum(d_flag, d_flag, n, d_count, d_partial, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_run_items_parse, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_lp,
+                       (const int64_t*)d_flag, d_dlt, r->len, d_err);
+    SCCG_HIP(hipGetLastError());
+    int64_t nr = 0;
+    SCCG_HIP(hipMemcpyAsync(&nr, d_count, sizeof nr, hipMemcpyDeviceToHost, s));
+    SCCG_HIP(hipStreamSynchronize(s));
+    r->n = nr;
+    if (nr == 0) return 0;
+    // exclusive sum of deltas into d_flag (free now), then starts
+    rc = dev_excl_sum(d_dlt, d_flag, nr, nullptr, d_partial, s);
+    if (rc) return rc;
+    const unsigned g2 = grid_for(nr, 256) > 8192 ? 8192 : grid_for(nr, 256);
+    hipLaunchKernelGGL(k_run_finish, dim3(g2), dim3(256), 0, s, (const int64_t*)d_flag, (const int64_t*)d_dlt,
+                       (const int32_t*)r->len, nr, r->start, d_err);
+    // cumulative lengths (for N: count of N positions before a run)
+    hipLaunchKernelGGL(k_len_to_i64, dim3(g2), dim3(256), 0, s, (const int32_t*)r->len, nr, r->cum);
+    SCCG_HIP(hipGetLastError());
+    rc = dev_excl_sum(r->cum, r->cum, nr, d_count, d_partial, s);
+    if (rc) return rc;
+    SCCG_HIP(hipMemcpyAsync(&r->total, d_count, sizeof r->total, hipMemcpyDeviceToHost, s));
+    SCCG_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,
+                      int64_t* d_dsum, int64_t nref, int64_t* d_partial, int32_t* d_err, int64_t* d_total, hipStream_t s) {
+    if (n <= 0) {
+        SCCG_HIP(hipMemsetAsync(d_total, 0, sizeof(int64_t), s));
+        return 0;
+    }
+    int rc = dc_last_paren(d_s, n, d_lp, d_partial, s);
+    if (rc) return rc;
+    const unsigned g = grid_for(n, 256) > 8192 ? 8192 : grid_for(n, 256);
+    hipLaunchKernelGGL(k_tok_parse, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_lp, d_contrib, d_dlt, d_err);
+    SCCG_HIP(hipGetLastError());
+    rc = dev_excl_sum(d_contrib, d_off, n, d_total, d_partial, s);
+    if (rc) return rc;
+    rc = dev_excl_sum(d_dlt, d_dsum, n, nullptr, d_partial, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tok_check, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_dsum, (const int64_t*)d_dlt,
+                       (const int64_t*)d_contrib, nref, d_err);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
+                   const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_tok_fill, dim3(grid_for(n, 64 * WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n, d_lp, d_off, d_dsum, d_dlt,
+                       d_contrib, d_R, d_dec);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, uint8_t* d_out, hipStream_t s) {
+    if (nres <= 0) return 0;
+    hipLaunchKernelGGL(k_format, dim3(grid_for(nres, 256 * OUT_PER_T)), dim3(256), 0, s, d_dec, nres,
+                       (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
+                       (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, d_out);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}

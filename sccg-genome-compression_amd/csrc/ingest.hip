@@ -1,0 +1,429 @@
+// ingest.hip -- FASTA strip, byte filters, run extraction and run-line text.
+//
+// Everything here is HBM-bound byte work: one 8 KiB tile per 256-thread block (32 bytes per
+// thread), reduce-then-scan for the output offsets, no atomics on the data path.
+//
+//   read_genomes_from_files  compression.cpp:181-220 (decompression.cpp:47-58 for the reference)
+//   lowercase / N run lines  compression.cpp:341-368, :495-522, :527-555
+//   N erase + toupper        compression.cpp:369-370, :523-524, :556-557; decompression.cpp:105-110
+#include "internal.h"
+
+namespace {
+
+constexpr int PER_T = INGEST_TILE / SCCG_BLOCK;  // 32 bytes per thread
+
+__device__ __forceinline__ void load_bytes(const uint8_t* __restrict__ buf, int64_t n, int64_t off,
+                                           uint8_t (&b)[PER_T]) {
+    if (off + PER_T <= n && (((uintptr_t)(buf + off)) & 15) == 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(buf + off);
+        uint4 v0 = p[0], v1 = p[1];
+        uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int i = 0; i < PER_T; i++) b[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    } else {
+#pragma unroll
+        for (int i = 0; i < PER_T; i++) b[i] = (off + i < n) ? buf[off + i] : (uint8_t)' ';
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// header search
+// ---------------------------------------------------------------------------------------------
+constexpr int64_t HDR_CHUNK = 1 << 16;
+
+__global__ void k_find_header(const uint8_t* __restrict__ buf, int64_t n, int64_t* __restrict__ sc) {
+    const int64_t base = (int64_t)blockIdx.x * HDR_CHUNK;
+    if (base >= (int64_t)__hip_atomic_load((unsigned long long*)&sc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    for (int64_t i = base + threadIdx.x; i < base + HDR_CHUNK && i < n; i += blockDim.x) {
+        if (buf[i] == '>' && (i == 0 || buf[i - 1] == '\n'))
+            atomicMin((unsigned long long*)&sc[0], (unsigned long long)i);
+    }
+}
+
+__global__ void k_find_eol(const uint8_t* __restrict__ buf, int64_t n, int64_t* __restrict__ sc) {
+    const int64_t h = sc[0];
+    if (h >= n) { if (blockIdx.x == 0 && threadIdx.x == 0) sc[1] = n; return; }
+    const int64_t base = h + (int64_t)blockIdx.x * HDR_CHUNK;
+    if (base >= (int64_t)__hip_atomic_load((unsigned long long*)&sc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    for (int64_t i = base + threadIdx.x; i < base + HDR_CHUNK && i < n; i += blockDim.x)
+        if (buf[i] == '\n') atomicMin((unsigned long long*)&sc[1], (unsigned long long)i);
+}
+
+// ---------------------------------------------------------------------------------------------
+// FASTA strip.  A line's fate is decided by its first byte (REF: '>' lines dropped; TGT: only the
+// header line [h, he) dropped); every isspace byte is dropped.  In REF mode bytes before the first
+// line start of a tile inherit the status of an earlier tile: the per-tile summary keeps those
+// bytes apart (a) from the ones whose status is known (b).
+// ---------------------------------------------------------------------------------------------
+struct ThreadSum {
+    int32_t a, b;   // kept-if-carry-keeps count, kept count
+    int32_t last;   // status of the last line start in range: -1 none, 0 drop, 1 keep
+};
+
+__device__ __forceinline__ ThreadSum thread_summary(IngestMode mode, const uint8_t (&b)[PER_T], uint8_t prev,
+                                                    int64_t off, int64_t n, int64_t h, int64_t he) {
+    ThreadSum r{0, 0, -1};
+    int cur = -1;
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) {
+        const int64_t pos = off + i;
+        const uint8_t c = b[i];
+        const uint8_t pc = i ? b[i - 1] : prev;
+        if (mode == INGEST_REF) {
+            if (pos < n && (pos == 0 || pc == '\n')) cur = (c == '>') ? 0 : 1;
+            const bool sp = pos >= n || c_isspace(c);
+            if (!sp) {
+                if (cur < 0) r.a++;
+                else r.b += cur;
+            }
+        } else {
+            const bool keep = pos < n && !c_isspace(c) && !(pos >= h && pos < he);
+            r.b += keep;
+        }
+    }
+    r.last = cur;
+    return r;
+}
+
+// last-non-null status of the threads before this one in the block (exclusive), -1 if none
+__device__ __forceinline__ int32_t block_prior_status(int32_t last, int32_t* tmp) {
+    const int lane = lane_id(), w = wave_in_block();
+    int32_t v = last;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int32_t o = __shfl_up(v, d, 64);
+        if (lane >= d && v < 0) v = o;
+    }
+    int32_t ex = __shfl_up(v, 1, 64);
+    if (lane == 0) ex = -1;
+    if (lane == 63) tmp[w] = v;
+    __syncthreads();
+    int32_t carry = -1;
+    for (int i = 0; i < w; i++) if (tmp[i] >= 0) carry = tmp[i];
+    __syncthreads();
+    return ex >= 0 ? ex : carry;
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(IngestMode mode, const uint8_t* __restrict__ buf,
+                                                              int64_t n, const int64_t* __restrict__ hdr,
+                                                              int64_t* __restrict__ ta, int64_t* __restrict__ tb,
+                                                              int32_t* __restrict__ tlast) {
+    __shared__ int32_t tmp[8];
+    __shared__ int64_t tmp64[8];
+    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
+    uint8_t b[PER_T];
+    load_bytes(buf, n, off, b);
+    const uint8_t prev = (off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n';
+    const int64_t h = mode == INGEST_TGT ? hdr[0] : 0, he = mode == INGEST_TGT ? hdr[1] : 0;
+    ThreadSum r = thread_summary(mode, b, prev, off, n, h, he);
+    const int32_t prior = block_prior_status(r.last, tmp);
+    // a-bytes of a thread with a prior line start in the block are resolved now
+    int64_t A = prior < 0 ? r.a : 0;
+    int64_t B = r.b + (prior == 1 ? r.a : 0);
+    int64_t At, Bt;
+    block_excl_add<int64_t>(A, tmp64, &At);
+    block_excl_add<int64_t>(B, tmp64, &Bt);
+    // block last status = prior status of a virtual thread after the last one
+    int32_t mylast = r.last >= 0 ? r.last : prior;
+    if (threadIdx.x == blockDim.x - 1) {
+        ta[blockIdx.x] = At;
+        tb[blockIdx.x] = Bt;
+        tlast[blockIdx.x] = mylast;
+    }
+}
+
+// one 1024-thread block: compose the tile summaries in order -> per-tile output offset and
+// carry-in status; total kept bytes -> *d_len
+__global__ __launch_bounds__(1024) void k_strip_scan(int64_t ntiles, const int64_t* __restrict__ ta,
+                                                     const int64_t* __restrict__ tb,
+                                                     const int32_t* __restrict__ tlast,
+                                                     int64_t* __restrict__ toff, int32_t* __restrict__ tcarry,
+                                                     int64_t* __restrict__ d_len) {
+    __shared__ int64_t sA[1024], sB[1024];
+    __shared__ int32_t sL[1024];
+    const int64_t per = (ntiles + 1023) / 1024;
+    const int64_t t0 = (int64_t)threadIdx.x * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
+    int64_t A = 0, B = 0;
+    int32_t last = -1;
+    for (int64_t t = t0; t < t1; t++) {
+        const int32_t yl = tlast[t];
+        const int64_t ya = ta[t], yb = tb[t];
+        B += yb + (last == 1 ? ya : 0);
+        if (last < 0) A += ya;
+        if (yl >= 0) last = yl;
+    }
+    sA[threadIdx.x] = A; sB[threadIdx.x] = B; sL[threadIdx.x] = last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t off = 0;
+        int32_t carry = 1;
+        for (int i = 0; i < 1024; i++) {
+            const int64_t a = sA[i], b = sB[i];
+            const int32_t l = sL[i];
+            sA[i] = off;        // offset at start of thread i's range
+            sL[i] = carry;      // carry-in status
+            off += b + (carry == 1 ? a : 0);
+            if (l >= 0) carry = l;
+        }
+        *d_len = off;
+    }
+    __syncthreads();
+    int64_t off = sA[threadIdx.x];
+    int32_t carry = sL[threadIdx.x];
+    for (int64_t t = t0; t < t1; t++) {
+        toff[t] = off;
+        tcarry[t] = carry;
+        off += tb[t] + (carry == 1 ? ta[t] : 0);
+        if (tlast[t] >= 0) carry = tlast[t];
+    }
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(IngestMode mode, const uint8_t* __restrict__ buf,
+                                                            int64_t n, const int64_t* __restrict__ hdr,
+                                                            const int64_t* __restrict__ toff,
+                                                            const int32_t* __restrict__ tcarry,
+                                                            uint8_t* __restrict__ out, int32_t* __restrict__ flags) {
+    __shared__ int32_t tmp[8];
+    __shared__ int64_t tmp64[8];
+    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
+    uint8_t b[PER_T];
+    load_bytes(buf, n, off, b);
+    const uint8_t prev = (off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n';
+    const int64_t h = mode == INGEST_TGT ? hdr[0] : 0, he = mode == INGEST_TGT ? hdr[1] : 0;
+    ThreadSum r = thread_summary(mode, b, prev, off, n, h, he);
+    int32_t prior = block_prior_status(r.last, tmp);
+    if (prior < 0) prior = tcarry[blockIdx.x];
+    const int64_t mine = r.b + (prior == 1 ? r.a : 0);
+    int64_t pos = toff[blockIdx.x] + block_excl_add<int64_t>(mine, tmp64, nullptr);
+    int cur = prior;
+    bool paren = false;
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) {
+        const int64_t p = off + i;
+        const uint8_t c = b[i];
+        const uint8_t pc = i ? b[i - 1] : prev;
+        bool keep;
+        if (mode == INGEST_REF) {
+            if (p < n && (p == 0 || pc == '\n')) cur = (c == '>') ? 0 : 1;
+            keep = p < n && !c_isspace(c) && cur == 1;
+        } else {
+            keep = p < n && !c_isspace(c) && !(p >= h && p < he);
+        }
+        if (keep) {
+            out[pos++] = c;
+            paren |= (c == '(');
+        }
+    }
+    if (flags && paren) atomicOr(flags, 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// byte filter (count per tile -> scan -> write)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool filter_keep(FilterMode m, uint8_t c) {
+    if (m == FILTER_DROP_N_UPPER) return c != 'N' && c != 'n';
+    if (m == FILTER_DROP_UPPERN_ONLY) return c != 'N';
+    return true;
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_filter_count(FilterMode m, const uint8_t* __restrict__ in,
+                                                             int64_t n, int64_t* __restrict__ cnt) {
+    __shared__ int64_t tmp64[8];
+    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
+    uint8_t b[PER_T];
+    load_bytes(in, n, off, b);
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) c += (off + i < n) && filter_keep(m, b[i]);
+    int64_t tot;
+    block_excl_add<int64_t>(c, tmp64, &tot);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_filter_write(FilterMode m, const uint8_t* __restrict__ in,
+                                                             int64_t n, const int64_t* __restrict__ toff,
+                                                             uint8_t* __restrict__ out) {
+    __shared__ int64_t tmp64[8];
+    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
+    uint8_t b[PER_T];
+    load_bytes(in, n, off, b);
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) c += (off + i < n) && filter_keep(m, b[i]);
+    int64_t pos = toff[blockIdx.x] + block_excl_add<int64_t>(c, tmp64, nullptr);
+#pragma unroll
+    for (int i = 0; i < PER_T; i++)
+        if (off + i < n && filter_keep(m, b[i])) out[pos++] = c_toupper(b[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// runs of a predicate
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool run_pred(RunPred p, uint8_t c) {
+    return p == RUN_LOWER ? c_islower(c) : (c == 'N' || c == 'n');
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_runs_count(RunPred pr, const uint8_t* __restrict__ in, int64_t n,
+                                                           int64_t* __restrict__ cnt) {
+    __shared__ int64_t tmp64[8];
+    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
+    uint8_t b[PER_T];
+    load_bytes(in, n, off, b);
+    bool prev = off > 0 && off - 1 < n && run_pred(pr, in[off - 1]);
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) {
+        const bool cur = off + i < n && run_pred(pr, b[i]);
+        c += cur && !prev;
+        prev = cur;
+    }
+    int64_t tot;
+    block_excl_add<int64_t>(c, tmp64, &tot);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_runs_write(RunPred pr, const uint8_t* __restrict__ in, int64_t n,
+                                                           const int64_t* __restrict__ toff,
+                                                           int32_t* __restrict__ rs, int32_t* __restrict__ re) {
+    __shared__ int64_t tmp64[8];
+    const int64_t tile0 = (int64_t)blockIdx.x * INGEST_TILE;
+    const int64_t off = tile0 + (int64_t)threadIdx.x * PER_T;
+    uint8_t b[PER_T];
+    load_bytes(in, n, off, b);
+    bool prev = off > 0 && off - 1 < n && run_pred(pr, in[off - 1]);
+    const bool nxt_in = off + PER_T < n && run_pred(pr, in[off + PER_T]);
+    int64_t cs = 0, ce = 0;
+    bool cur[PER_T];
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) cur[i] = off + i < n && run_pred(pr, b[i]);
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) {
+        const bool pv = i ? cur[i - 1] : prev;
+        const bool nx = i + 1 < PER_T ? cur[i + 1] : nxt_in;
+        cs += cur[i] && !pv;
+        ce += cur[i] && !nx;
+    }
+    // runs open across the tile start end inside this tile (or later) but started before it
+    const bool open_in = tile0 > 0 && tile0 < n && run_pred(pr, in[tile0 - 1]) && run_pred(pr, in[tile0]);
+    int64_t ps = toff[blockIdx.x] + block_excl_add<int64_t>(cs, tmp64, nullptr);
+    int64_t pe = toff[blockIdx.x] - (open_in ? 1 : 0) + block_excl_add<int64_t>(ce, tmp64, nullptr);
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) {
+        const bool pv = i ? cur[i - 1] : prev;
+        const bool nx = i + 1 < PER_T ? cur[i + 1] : nxt_in;
+        if (cur[i] && !pv) rs[ps++] = (int32_t)(off + i);
+        if (cur[i] && !nx) re[pe++] = (int32_t)(off + i);
+    }
+}
+
+// text of one run: "d," | "(d,len)" | final singleton "d" (compression.cpp:351-366)
+__device__ __forceinline__ int64_t run_text_len(int32_t d, int32_t len, bool at_end) {
+    return len == 1 ? (int64_t)ndigits_i32(d) + (at_end ? 0 : 1) : (int64_t)(3 + ndigits_i32(d) + ndigits_i32(len));
+}
+
+__global__ void k_run_textlen(const int32_t* __restrict__ rs, const int32_t* __restrict__ re, int64_t nr,
+                              int64_t n, int64_t* __restrict__ len) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t d = rs[r] - (r ? rs[r - 1] : 0);
+        len[r] = run_text_len(d, re[r] - rs[r] + 1, (int64_t)re[r] == n - 1);
+    }
+}
+
+__global__ void k_run_textwrite(const int32_t* __restrict__ rs, const int32_t* __restrict__ re, int64_t nr,
+                                int64_t n, const int64_t* __restrict__ off, uint8_t* __restrict__ out) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t d = rs[r] - (r ? rs[r - 1] : 0);
+        const int32_t len = re[r] - rs[r] + 1;
+        uint8_t* o = out + off[r];
+        if (len == 1) {
+            o += write_i32(o, d);
+            if ((int64_t)re[r] != n - 1) *o = ',';
+        } else {
+            *o++ = '(';
+            o += write_i32(o, d);
+            *o++ = ',';
+            o += write_i32(o, len);
+            *o = ')';
+        }
+    }
+}
+
+}  // namespace
+
+// =============================================================================================
+int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t s) {
+    int rc = dev_set_i64(d_sc, 2, {n, n}, s);
+    if (rc) return rc;
+    if (n > 0) {
+        const unsigned g = grid_for(n, (int)HDR_CHUNK);
+        hipLaunchKernelGGL(k_find_header, dim3(g), dim3(256), 0, s, buf, n, d_sc);
+        hipLaunchKernelGGL(k_find_eol, dim3(g), dim3(256), 0, s, buf, n, d_sc);
+    }
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,
+                       int64_t* d_len, int32_t* d_flags, const IngestScratch& sc, int64_t* /*d_partial*/,
+                       hipStream_t s) {
+    if (n <= 0) {
+        SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));
+        return 0;
+    }
+    const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
+    hipLaunchKernelGGL(k_strip_summary, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, buf, n, d_header,
+                       sc.tile_a, sc.tile_b, sc.tile_last);
+    hipLaunchKernelGGL(k_strip_scan, dim3(1), dim3(1024), 0, s, ntiles, sc.tile_a, sc.tile_b, sc.tile_last,
+                       sc.tile_off, sc.tile_carry, d_len);
+    hipLaunchKernelGGL(k_strip_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, buf, n, d_header,
+                       sc.tile_off, sc.tile_carry, out, d_flags);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_filter(FilterMode mode, const uint8_t* in, int64_t n, uint8_t* out, int64_t* d_len,
+                  int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s) {
+    if (n <= 0) {
+        SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));
+        return 0;
+    }
+    const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
+    hipLaunchKernelGGL(k_filter_count, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, in, n, d_tile_cnt);
+    int rc = dev_excl_sum(d_tile_cnt, d_tile_cnt, ntiles, d_len, d_partial, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_filter_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, in, n,
+                       (const int64_t*)d_tile_cnt, out);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_runs(RunPred pred, const uint8_t* in, int64_t n, int32_t* rs, int32_t* re, int64_t* d_nruns,
+                int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s) {
+    if (n <= 0) {
+        SCCG_HIP(hipMemsetAsync(d_nruns, 0, sizeof(int64_t), s));
+        return 0;
+    }
+    const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
+    hipLaunchKernelGGL(k_runs_count, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, pred, in, n, d_tile_cnt);
+    int rc = dev_excl_sum(d_tile_cnt, d_tile_cnt, ntiles, d_nruns, d_partial, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_runs_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, pred, in, n,
+                       (const int64_t*)d_tile_cnt, rs, re);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_run_text(const int32_t* rs, const int32_t* re, int64_t nruns, int64_t n, uint8_t* out, int64_t* d_len,
+                    int64_t* d_tmp, int64_t* d_partial, hipStream_t s) {
+    if (nruns <= 0) {
+        SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));
+        return 0;
+    }
+    const unsigned g = grid_for(nruns, 256) > 4096 ? 4096 : grid_for(nruns, 256);
+    hipLaunchKernelGGL(k_run_textlen, dim3(g), dim3(256), 0, s, rs, re, nruns, n, d_tmp);
+    int rc = dev_excl_sum(d_tmp, d_tmp, nruns, d_len, d_partial, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_run_textwrite, dim3(g), dim3(256), 0, s, rs, re, nruns, n, (const int64_t*)d_tmp, out);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}

@@ -1,0 +1,91 @@
+// internal.h -- launchers shared between the .hip translation units and the host orchestrator.
+#pragma once
+
+#include "common.h"
+#include "../../include/sccg.h"
+
+// ---- scan.hip ---------------------------------------------------------------------------------
+#include <initializer_list>
+int dev_set_i64(int64_t* p, int n, std::initializer_list<int64_t> vals, hipStream_t s);
+int dev_set_i32(int32_t* p, int n, std::initializer_list<int32_t> vals, hipStream_t s);
+int64_t scan_partials_needed(int64_t n);
+int dev_excl_sum(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
+                 hipStream_t s);
+int dev_excl_max(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
+                 hipStream_t s);
+
+// ---- ingest.hip -------------------------------------------------------------------------------
+constexpr int INGEST_TILE = 8192;  // bytes per 256-thread tile (32 per thread)
+enum IngestMode { INGEST_REF = 0, INGEST_TGT = 1 };
+enum FilterMode { FILTER_DROP_N_UPPER = 0, FILTER_DROP_UPPERN_ONLY = 1, FILTER_UPPER = 2 };
+enum RunPred { RUN_LOWER = 0, RUN_N = 1 };
+
+struct IngestScratch {
+    int64_t* tile_a;      // per tile
+    int64_t* tile_b;
+    int32_t* tile_last;
+    int64_t* tile_off;
+    int32_t* tile_carry;
+    int64_t* scalars;     // [0] header start, [1] header end, [2] out len, [3] flags
+};
+
+// Target header: first line starting with '>' (compression.cpp:210); writes [h, he) into
+// scalars[0..1] (h = n when absent).
+int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_scalars, hipStream_t s);
+// read_genomes_from_files (compression.cpp:193-218): compacts the kept, non-space bytes of `buf`
+// into `out` (original case); *d_len = kept count; in TGT mode lines [h, he) are the header.
+// d_flags (optional) gets bit0 when a kept byte is '('.
+int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header,
+                       uint8_t* out, int64_t* d_len, int32_t* d_flags, const IngestScratch& sc,
+                       int64_t* d_partial, hipStream_t s);
+// byte filter + case map (N erase of compression.cpp:556-557 / decompression.cpp:108-110)
+int launch_filter(FilterMode mode, const uint8_t* in, int64_t n, uint8_t* out, int64_t* d_len,
+                  int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s);
+// maximal runs of a predicate -> start/end (inclusive) arrays; *d_nruns = count
+int launch_runs(RunPred pred, const uint8_t* s_in, int64_t n, int32_t* run_s, int32_t* run_e,
+                int64_t* d_nruns, int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s);
+// run line text (compression.cpp:341-368): writes it to out, *d_len = bytes
+int launch_run_text(const int32_t* run_s, const int32_t* run_e, int64_t nruns, int64_t n,
+                    uint8_t* out, int64_t* d_len, int64_t* d_tmp, int64_t* d_partial, hipStream_t s);
+
+// ---- local.hip --------------------------------------------------------------------------------
+constexpr int SEG_L = 1000;      // compression.cpp:375
+constexpr int SEG_REC_CAP = 256; // >= 2 * (1000 / 10) + 1 records per segment
+struct SegStat {
+    int32_t nrec;     // records written
+    int32_t nmatch;   // match records
+    int32_t lit;      // literal bytes
+    int32_t pass;     // 1 = k pass succeeded, 2 = k2 pass succeeded, 0 = no match record
+    int32_t non_n;    // segment holds a byte other than 'N' (compression.cpp:419)
+    int32_t first_p;  // segment-local p of first / last match
+    int32_t last_p;
+    int32_t pad;
+};
+int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT,
+                      int64_t iters, uint32_t* recs, SegStat* stat, hipStream_t s);
+// switch FSM (compression.cpp:395-473): *d_switch = first segment where mism > T2, or -1
+int64_t fsm_chunks(int64_t iters);
+int launch_switch_fsm(const SegStat* stat, int64_t iters, int32_t* d_maps, int32_t* h_maps, int64_t* switch_seg,
+                      hipStream_t s);
+// record text for local mode (delta-encoded, compression.cpp:406-415 + :222-304) + leftover
+int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_t* recs,
+                      const SegStat* stat, uint8_t* out, int64_t* d_len, int64_t* d_tmp_a,
+                      int64_t* d_tmp_b, int64_t* d_partial, hipStream_t s);
+
+// ---- walk.hip ---------------------------------------------------------------------------------
+struct WalkWorkspace;  // defined in walk.hip
+struct WalkResult {
+    int64_t n_matches;
+    int64_t rounds;
+    int64_t chunks;
+};
+size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk);
+// Global pass match_sequences(R', T', 14, 100, true) (compression.cpp:561) and its record text
+// (compression.cpp:564-573 + delta_encode).  `ws` is device memory of walk_workspace_bytes.
+int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m,
+                          int chunk, void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len,
+                          WalkResult* res, hipStream_t s);
+// the raw match list of the last global_match_and_emit (device pointers inside ws)
+int global_matches(void* ws, const int32_t** t, const int32_t** p, const int32_t** l, int64_t* n);
+
+// ---- decomp.hip: see decomp.h

@@ -1,0 +1,169 @@
+// scan.hip -- device-wide exclusive scans (reduce-then-scan, three launches).
+//
+// Used for every compaction offset in the pipeline (FASTA strip, run lists, per-segment and
+// per-match text offsets).  Tile = 256 threads x 16 items; block partials are scanned by one
+// 1024-thread block.  HBM-bound: 8 B read twice + 8 B written per element.
+#include "internal.h"
+
+namespace {
+
+constexpr int ITEMS = 16;
+constexpr int TILE = SCCG_BLOCK * ITEMS;
+
+struct OpSum {
+    static __device__ __forceinline__ int64_t id() { return 0; }
+    static __device__ __forceinline__ int64_t f(int64_t a, int64_t b) { return a + b; }
+};
+struct OpMax {
+    static __device__ __forceinline__ int64_t id() { return INT64_MIN; }
+    static __device__ __forceinline__ int64_t f(int64_t a, int64_t b) { return a > b ? a : b; }
+};
+
+template <class Op>
+__device__ __forceinline__ int64_t wave_incl(int64_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int64_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v = Op::f(v, o);
+    }
+    return v;
+}
+
+// exclusive block scan with arbitrary op; returns exclusive value, *total = block aggregate
+template <class Op>
+__device__ int64_t block_excl(int64_t v, int64_t* tmp /*17*/, int64_t* total) {
+    int64_t incl = wave_incl<Op>(v);
+    const int w = wave_in_block(), lane = lane_id(), nw = (int)(blockDim.x >> 6);
+    int64_t excl_in_wave = __shfl_up(incl, 1, 64);
+    if (lane == 0) excl_in_wave = Op::id();
+    if (lane == 63) tmp[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t s = Op::id();
+        for (int i = 0; i < nw; i++) { int64_t t = tmp[i]; tmp[i] = s; s = Op::f(s, t); }
+        tmp[16] = s;
+    }
+    __syncthreads();
+    int64_t r = Op::f(tmp[w], excl_in_wave);
+    if (total) *total = tmp[16];
+    __syncthreads();
+    return r;
+}
+
+template <class Op>
+__global__ __launch_bounds__(SCCG_BLOCK) void k_tile_reduce(const int64_t* __restrict__ in, int64_t n,
+                                                            int64_t* __restrict__ partial) {
+    __shared__ int64_t tmp[17];
+    const int64_t base = (int64_t)blockIdx.x * TILE;
+    int64_t acc = Op::id();
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        int64_t idx = base + (int64_t)i * SCCG_BLOCK + threadIdx.x;
+        if (idx < n) acc = Op::f(acc, in[idx]);
+    }
+    int64_t tot;
+    block_excl<Op>(acc, tmp, &tot);
+    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+template <class Op>
+__global__ __launch_bounds__(1024) void k_partials_scan(int64_t* __restrict__ partial, int64_t nb,
+                                                        int64_t* __restrict__ total) {
+    __shared__ int64_t tmp[17];
+    int64_t carry = Op::id();
+    for (int64_t base = 0; base < nb; base += 1024) {
+        int64_t idx = base + threadIdx.x;
+        int64_t v = idx < nb ? partial[idx] : Op::id();
+        int64_t tot;
+        int64_t ex = block_excl<Op>(v, tmp, &tot);
+        if (idx < nb) partial[idx] = Op::f(carry, ex);
+        carry = Op::f(carry, tot);
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
+template <class Op>
+__global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(const int64_t* __restrict__ in, int64_t n,
+                                                          const int64_t* __restrict__ partial,
+                                                          int64_t* __restrict__ out) {
+    __shared__ int64_t tmp[17];
+    // each thread owns ITEMS consecutive elements
+    const int64_t base = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * ITEMS;
+    int64_t v[ITEMS];
+    int64_t acc = Op::id();
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        v[i] = (base + i < n) ? in[base + i] : Op::id();
+        acc = Op::f(acc, v[i]);
+    }
+    int64_t ex = block_excl<Op>(acc, tmp, nullptr);
+    int64_t run = Op::f(partial[blockIdx.x], ex);
+#pragma unroll
+    for (int i = 0; i < ITEMS; i++) {
+        if (base + i < n) out[base + i] = run;
+        run = Op::f(run, v[i]);
+    }
+}
+
+template <class Op>
+int scan_impl(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
+              hipStream_t s) {
+    if (n <= 0) {
+        if (d_total) return dev_set_i64(d_total, 1, {0}, s);
+        return 0;
+    }
+    const int64_t nb = (n + TILE - 1) / TILE;
+    hipLaunchKernelGGL(k_tile_reduce<Op>, dim3((unsigned)nb), dim3(SCCG_BLOCK), 0, s, in, n, d_partial);
+    hipLaunchKernelGGL(k_partials_scan<Op>, dim3(1), dim3(1024), 0, s, d_partial, nb, d_total);
+    hipLaunchKernelGGL(k_tile_scan<Op>, dim3((unsigned)nb), dim3(SCCG_BLOCK), 0, s, in, n,
+                       (const int64_t*)d_partial, out);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+struct Vals8 {
+    int64_t v[8];
+};
+__global__ void k_set_i64(int64_t* p, int n, Vals8 v) {
+    if ((int)threadIdx.x < n) p[threadIdx.x] = v.v[threadIdx.x];
+}
+struct Vals8i {
+    int32_t v[8];
+};
+__global__ void k_set_i32(int32_t* p, int n, Vals8i v) {
+    if ((int)threadIdx.x < n) p[threadIdx.x] = v.v[threadIdx.x];
+}
+
+}  // namespace
+
+// Stream-ordered writes of up to 8 scalars: the values travel as kernel arguments, so no host
+// buffer has to outlive the call (a hipMemcpyAsync from a stack temporary would).
+int dev_set_i64(int64_t* p, int n, std::initializer_list<int64_t> vals, hipStream_t s) {
+    Vals8 v{};
+    int i = 0;
+    for (int64_t x : vals) if (i < 8) v.v[i++] = x;
+    hipLaunchKernelGGL(k_set_i64, dim3(1), dim3(64), 0, s, p, n < i ? n : i, v);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+int dev_set_i32(int32_t* p, int n, std::initializer_list<int32_t> vals, hipStream_t s) {
+    Vals8i v{};
+    int i = 0;
+    for (int32_t x : vals) if (i < 8) v.v[i++] = x;
+    hipLaunchKernelGGL(k_set_i32, dim3(1), dim3(64), 0, s, p, n < i ? n : i, v);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int64_t scan_partials_needed(int64_t n) { return (n + TILE - 1) / TILE + 1; }
+
+int dev_excl_sum(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
+                 hipStream_t s) {
+    return scan_impl<OpSum>(in, out, n, d_total, d_partial, s);
+}
+
+int dev_excl_max(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
+                 hipStream_t s) {
+    return scan_impl<OpMax>(in, out, n, d_total, d_partial, s);
+}

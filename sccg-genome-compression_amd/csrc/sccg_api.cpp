@@ -1,0 +1,598 @@
+// sccg_api.cpp -- the C ABI (include/sccg.h): context, device buffers, and the compress /
+// reconstruct pipelines as sequences of HIP kernel launches on one stream.
+//
+// Pipeline (compression.cpp:320-582 without the 7z call):
+//   find header -> strip target / reference FASTA (ingest.hip)
+//   header line, lowercase-run line                            compression.cpp:337-368
+//   local segments k=14, then k=10 for the failures (local.hip) compression.cpp:395-452
+//   switch state machine                                        compression.cpp:454-473
+//   local: ",\n" + segment records + leftover                   compression.cpp:368, :476-481
+//   global: N-run line, N erase, windowed walk (walk.hip)       compression.cpp:484-574
+// delta_encode (:222-304) is folded into the emitters: each "(p," is written as "(p-p_prev,".
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "decomp.h"
+#include "internal.h"
+
+static thread_local char g_hip_err[512];
+
+int sccg_hip_fail(hipError_t e, const char* what, const char* file, int line) {
+    snprintf(g_hip_err, sizeof g_hip_err, "%s:%d: %s -> %s", file, line, what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? SCCG_E_NOMEM : SCCG_E_HIP;
+}
+
+namespace {
+
+enum Slot {
+    B_RFA, B_TFA, B_R, B_T, B_TILE_A, B_TILE_B, B_TILE_LAST, B_TILE_OFF, B_TILE_CARRY, B_SCAL, B_PARTIAL,
+    B_RUN_S, B_RUN_E, B_TMP64, B_RECS, B_STAT, B_MAPS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
+    // decompression
+    B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC,
+    B_COUNT
+};
+
+constexpr int WALK_CHUNK = 16384;
+constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide compares, tails)
+
+}  // namespace
+
+struct sccg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    sccg_stats stats{};
+    void* buf[B_COUNT] = {};
+    size_t cap[B_COUNT] = {};
+    std::vector<int32_t> h_maps;
+
+    int fail(int rc, const char* fmt, ...) {
+        char tmp[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(tmp, sizeof tmp, fmt, ap);
+        va_end(ap);
+        err = tmp;
+        return rc;
+    }
+    int hipfail(int rc) {
+        err = g_hip_err;
+        return rc;
+    }
+    // device buffer of >= bytes (grown on demand, contents not preserved)
+    void* get(int slot, size_t bytes) {
+        bytes = (bytes + DPAD + 255) & ~(size_t)255;
+        if (cap[slot] >= bytes) return buf[slot];
+        if (buf[slot]) (void)hipFree(buf[slot]);
+        buf[slot] = nullptr;
+        cap[slot] = 0;
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        buf[slot] = p;
+        cap[slot] = bytes;
+        return p;
+    }
+};
+
+#define TRY(expr)                                  \
+    do {                                           \
+        int rc_ = (expr);                          \
+        if (rc_) return ctx->hipfail(rc_);         \
+    } while (0)
+#define HIPTRY(expr)                               \
+    do {                                           \
+        hipError_t e_ = (expr);                    \
+        if (e_ != hipSuccess) return ctx->hipfail(sccg_hip_fail(e_, #expr, __FILE__, __LINE__)); \
+    } while (0)
+#define GET(T, var, slot, n)                                                            \
+    T* var = reinterpret_cast<T*>(ctx->get(slot, (size_t)(n) * sizeof(T)));            \
+    if (!var) return ctx->fail(SCCG_E_NOMEM, "device allocation of %zu bytes failed", (size_t)(n) * sizeof(T))
+
+extern "C" {
+
+int sccg_ctx_create(int device, sccg_ctx** out) {
+    if (!out) return SCCG_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SCCG_E_HIP;
+    if (device < 0 || device >= n) return SCCG_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return SCCG_E_HIP;
+    sccg_ctx* c = new sccg_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return SCCG_E_HIP;
+    }
+    *out = c;
+    return SCCG_OK;
+}
+
+void sccg_ctx_destroy(sccg_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (int i = 0; i < B_COUNT; i++)
+        if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* sccg_last_error(const sccg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int sccg_last_stats(const sccg_ctx* ctx, sccg_stats* out) {
+    if (!ctx || !out) return SCCG_E_INVALID;
+    *out = ctx->stats;
+    return SCCG_OK;
+}
+
+void sccg_buf_free(sccg_buf* b) {
+    if (!b) return;
+    free(b->data);
+    b->data = nullptr;
+    b->len = 0;
+}
+
+void sccg_records_free(sccg_records* r) {
+    if (!r) return;
+    free(r->kind); free(r->pos); free(r->len); free(r->t);
+    memset(r, 0, sizeof *r);
+}
+
+size_t sccg_compress_bound(size_t ref_len, size_t tgt_len) {
+    (void)ref_len;
+    return 12 * tgt_len + 4096;
+}
+
+}  // extern "C"
+
+namespace {
+
+int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n) {
+    HIPTRY(hipMemcpyAsync(h, d, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPTRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+// strips one FASTA into `out`, returns the kept length
+int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const int64_t* d_hdr, uint8_t* out,
+          int64_t* d_len, int32_t* d_flags, int64_t* h_len) {
+    const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE + 1;
+    IngestScratch sc;
+    GET(int64_t, ta, B_TILE_A, ntiles);
+    GET(int64_t, tb, B_TILE_B, ntiles);
+    GET(int32_t, tl, B_TILE_LAST, ntiles);
+    GET(int64_t, to, B_TILE_OFF, ntiles);
+    GET(int32_t, tc, B_TILE_CARRY, ntiles);
+    sc.tile_a = ta; sc.tile_b = tb; sc.tile_last = tl; sc.tile_off = to; sc.tile_carry = tc; sc.scalars = nullptr;
+    TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, nullptr, ctx->stream));
+    return d2h_i64(ctx, d_len, h_len, 1);
+}
+
+// run line of `pred` over s[0,n) written at out; returns its length
+int run_line(sccg_ctx* ctx, RunPred pred, const uint8_t* s, int64_t n, uint8_t* out, int64_t* d_sc, int64_t* h_len) {
+    const int64_t maxruns = n / 2 + 2;
+    const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE + 1;
+    GET(int32_t, rs, B_RUN_S, maxruns);
+    GET(int32_t, re, B_RUN_E, maxruns);
+    GET(int64_t, tmp, B_TMP64, (maxruns > ntiles ? maxruns : ntiles));
+    GET(int64_t, part, B_PARTIAL, scan_partials_needed(maxruns > ntiles ? maxruns : ntiles) + 16);
+    TRY(launch_runs(pred, s, n, rs, re, d_sc, tmp, part, ctx->stream));
+    int64_t nruns = 0;
+    TRY(d2h_i64(ctx, d_sc, &nruns, 1));
+    TRY(launch_run_text(rs, re, nruns, n, out, d_sc, tmp, part, ctx->stream));
+    return d2h_i64(ctx, d_sc, h_len, 1);
+}
+
+int put_bytes(sccg_ctx* ctx, uint8_t* dst, const char* s, size_t n) {
+    HIPTRY(hipMemcpyAsync(dst, s, n, hipMemcpyHostToDevice, ctx->stream));
+    HIPTRY(hipStreamSynchronize(ctx->stream));   // s may be a stack temporary
+    return 0;
+}
+
+int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_t* tfa, int64_t tn, uint8_t* out,
+                         int64_t out_cap, int64_t* out_len) {
+    hipStream_t s = ctx->stream;
+    sccg_stats st{};
+    st.switch_segment = -1;
+    GET(int64_t, sc, B_SCAL, 64);
+    GET(uint8_t, T, B_T, tn + 64);
+    GET(uint8_t, R, B_R, rn + 64);
+    int32_t* d_flags = reinterpret_cast<int32_t*>(sc + 32);
+    HIPTRY(hipMemsetAsync(d_flags, 0, sizeof(int32_t), s));
+
+    // ---- ingest (compression.cpp:181-220)
+    TRY(launch_find_header(tfa, tn, sc, s));
+    int64_t hdr[2];
+    TRY(d2h_i64(ctx, sc, hdr, 2));
+    int64_t nT = 0, nR = 0;
+    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, &nT));
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 3, nullptr, &nR));
+    if (nT >= INT32_MAX - 8 || nR >= INT32_MAX - 8)
+        return ctx->fail(SCCG_E_UNSUPPORTED, "sequence longer than the reference's int positions allow");
+    int32_t flags = 0;
+    HIPTRY(hipMemcpyAsync(&flags, d_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    if (flags & 1)
+        return ctx->fail(SCCG_E_UNSUPPORTED,
+                         "target sequence holds '(' bytes: delta_encode's token scan would misparse them "
+                         "(compression.cpp:263-292); not supported yet");
+    st.target_bases = nT;
+    st.reference_bases = nR;
+    const bool has_hdr = hdr[0] < tn;
+    const int64_t hlen = has_hdr ? hdr[1] - hdr[0] : 0;
+    if (out_cap < hlen + 1 + 11 * nT + 64) return ctx->fail(SCCG_E_INVALID, "output capacity too small");
+
+    // ---- header + lowercase line (compression.cpp:337-368)
+    int64_t pos = 0;
+    if (has_hdr) {
+        HIPTRY(hipMemcpyAsync(out, tfa + hdr[0], (size_t)hlen, hipMemcpyDeviceToDevice, s));
+        TRY(put_bytes(ctx, out + hlen, "\n", 1));
+        pos = hlen + 1;
+    }
+    int64_t llen = 0;
+    TRY(run_line(ctx, RUN_LOWER, T, nT, out + pos, sc + 4, &llen));
+    pos += llen;
+    const int64_t lower_end = pos;
+
+    // ---- local segments (compression.cpp:372-474)
+    const int64_t nRs = (nR + SEG_L - 1) / SEG_L, nTs = (nT + SEG_L - 1) / SEG_L;
+    const int64_t iters = nRs < nTs ? nRs : nTs;
+    int64_t sw = -1;
+    GET(uint32_t, recs, B_RECS, (iters > 0 ? iters : 1) * SEG_REC_CAP);
+    GET(SegStat, stat, B_STAT, iters > 0 ? iters : 1);
+    if (iters > 0) {
+        TRY(launch_local_pass(14, 1, 1, R, nR, T, nT, iters, recs, stat, s));
+        TRY(launch_local_pass(10, 2, 1, R, nR, T, nT, iters, recs, stat, s));
+        const int64_t nch = fsm_chunks(iters);
+        GET(int32_t, maps, B_MAPS, nch * 12);
+        ctx->h_maps.resize((size_t)(nch * 12));
+        TRY(launch_switch_fsm(stat, iters, maps, ctx->h_maps.data(), &sw, s));
+    }
+    st.switch_segment = sw;
+    if (sw < 0) {
+        // ---- local: "\n,\n" + records + leftover segments
+        TRY(put_bytes(ctx, out + pos, "\n,\n", 3));
+        pos += 3;
+        GET(int64_t, sa, B_SEG_A, iters + 1);
+        GET(int64_t, sb, B_SEG_B, iters + 1);
+        GET(int64_t, part, B_PARTIAL, scan_partials_needed(iters + 1) + 16);
+        TRY(launch_local_emit(T, nT, iters, recs, stat, out + pos, sc + 5, sa, sb, part, s));
+        int64_t rlen = 0;
+        TRY(d2h_i64(ctx, sc + 5, &rlen, 1));
+        // statistics: match tokens / literal bytes of the record line
+        std::vector<SegStat> hs((size_t)(iters > 0 ? iters : 0));
+        if (iters > 0) {
+            HIPTRY(hipMemcpyAsync(hs.data(), stat, (size_t)iters * sizeof(SegStat), hipMemcpyDeviceToHost, s));
+            HIPTRY(hipStreamSynchronize(s));
+        }
+        int64_t nm = 0, lit = 0;
+        for (auto& x : hs) if (x.pass) { nm += x.nmatch; lit += x.lit; }
+        const int64_t lead = iters * SEG_L < nT ? iters * SEG_L : nT;
+        st.n_matches = nm;
+        st.literal_bases = lit + (nT - lead);
+        pos += rlen;
+    } else {
+        // ---- global (compression.cpp:484-574)
+        st.mode_global = 1;
+        pos = lower_end;
+        TRY(put_bytes(ctx, out + pos, "\n", 1));
+        pos += 1;
+        int64_t nlen = 0;
+        TRY(run_line(ctx, RUN_N, T, nT, out + pos, sc + 6, &nlen));
+        pos += nlen;
+        TRY(put_bytes(ctx, out + pos, "\n", 1));
+        pos += 1;
+        GET(uint8_t, Tp, B_TP, nT + 64);
+        GET(uint8_t, Rp, B_RP, nR + 64);
+        const int64_t ntile = (nT > nR ? nT : nR) / INGEST_TILE + 2;
+        GET(int64_t, tcnt, B_TMP64, ntile);
+        GET(int64_t, part, B_PARTIAL, scan_partials_needed(ntile) + 16);
+        TRY(launch_filter(FILTER_DROP_N_UPPER, T, nT, Tp, sc + 7, tcnt, part, s));
+        TRY(launch_filter(FILTER_DROP_N_UPPER, R, nR, Rp, sc + 8, tcnt, part, s));
+        int64_t np[2];
+        TRY(d2h_i64(ctx, sc + 7, np, 2));
+        const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, WALK_CHUNK);
+        void* ws = ctx->get(B_WALK, wsb);
+        if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
+        WalkResult wr{};
+        int64_t rlen = 0;
+        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, WALK_CHUNK, ws, wsb, out + pos, &rlen, &wr, s));
+        st.n_matches = wr.n_matches;
+        st.walk_rounds = wr.rounds;
+        st.walk_chunks = wr.chunks;
+        pos += rlen;
+    }
+    HIPTRY(hipStreamSynchronize(s));
+    st.record_bytes = pos;
+    ctx->stats = st;
+    *out_len = pos;
+    return SCCG_OK;
+}
+
+// -------------------------------------------------------------------------------------------
+// reconstruction (decompression.cpp)
+// -------------------------------------------------------------------------------------------
+int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_t* rec, int64_t n, uint8_t* out,
+                     int64_t out_cap, int64_t* out_len, bool size_only) {
+    hipStream_t s = ctx->stream;
+    GET(int64_t, sc, B_SCAL, 64);
+    int64_t nl[4];
+    TRY(dc_find_lines(rec, n, sc, s));
+    TRY(d2h_i64(ctx, sc, nl, 4));
+    uint8_t first = 0;
+    if (n > 0) {
+        HIPTRY(hipMemcpyAsync(&first, rec, 1, hipMemcpyDeviceToHost, s));
+        HIPTRY(hipStreamSynchronize(s));
+    }
+    // getline semantics: line i spans [start_i, nl_i); it exists iff start_i < n  (:68-97)
+    int64_t start[4], end[4];
+    start[0] = 0;
+    for (int i = 0; i < 4; i++) {
+        end[i] = nl[i];
+        if (i < 3) start[i + 1] = nl[i] + 1;
+    }
+    if (n <= 0) return ctx->fail(SCCG_E_FORMAT, "empty record file");
+    const bool has_hdr = end[0] > 0 && first == '>';
+    const int li = has_hdr ? 1 : 0;
+    for (int i = 1; i <= li + 2; i++)
+        if (start[i] >= n + (i == 0)) return ctx->fail(SCCG_E_FORMAT, "record file misses line %d", i + 1);
+    const uint8_t* lower = rec + start[li];
+    const int64_t nlower = end[li] - start[li];
+    const uint8_t* nline = rec + start[li + 1];
+    const int64_t nnl = end[li + 1] - start[li + 1];
+    const uint8_t* enc = rec + start[li + 2];
+    const int64_t nenc = end[li + 2] - start[li + 2];
+
+    // ---- reference (decompression.cpp:47-58, 105-110)
+    GET(uint8_t, R, B_R, rn + 64);
+    GET(uint8_t, Rp, B_RP, rn + 64);
+    int64_t nR = 0, nRp = 0;
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 8, nullptr, &nR));
+    bool n_is_comma = false;
+    if (nnl == 1) {
+        uint8_t c = 0;
+        HIPTRY(hipMemcpyAsync(&c, nline, 1, hipMemcpyDeviceToHost, s));
+        HIPTRY(hipStreamSynchronize(s));
+        n_is_comma = c == ',';
+    }
+    {
+        const int64_t ntile = nR / INGEST_TILE + 2;
+        GET(int64_t, tcnt, B_TMP64, ntile);
+        GET(int64_t, part, B_PARTIAL, scan_partials_needed(ntile) + 16);
+        TRY(launch_filter(n_is_comma ? FILTER_UPPER : FILTER_DROP_UPPERN_ONLY, R, nR, Rp, sc + 9, tcnt, part, s));
+        TRY(d2h_i64(ctx, sc + 9, &nRp, 1));
+    }
+
+    // ---- run lines + record line
+    const int64_t nmax = (nlower > nnl ? nlower : nnl) > nenc ? (nlower > nnl ? nlower : nnl) : nenc;
+    GET(int64_t, lp, B_D_LP, nmax + 1);
+    GET(int64_t, flag, B_D_FLAG, nmax + 1);
+    GET(int64_t, dlt, B_D_DLT, nmax + 1);
+    GET(int64_t, part, B_PARTIAL, scan_partials_needed(nmax + 1) + 16);
+    int32_t* d_err = reinterpret_cast<int32_t*>(sc + 40);
+    HIPTRY(hipMemsetAsync(d_err, 0, sizeof(int32_t), s));
+    DcRuns lr{}, nr{};
+    {
+        GET(int32_t, ls, B_D_LS, nlower / 2 + 2);
+        GET(int32_t, ll, B_D_LL, nlower / 2 + 2);
+        GET(int64_t, lc, B_D_LC, nlower / 2 + 2);
+        lr.start = ls; lr.len = ll; lr.cum = lc;
+        TRY(dc_parse_runs(lower, nlower, &lr, lp, flag, dlt, part, d_err, sc + 10, s));
+        GET(int32_t, ns, B_D_NS, nnl / 2 + 2);
+        GET(int32_t, nlr, B_D_NL, nnl / 2 + 2);
+        GET(int64_t, nc, B_D_NC, nnl / 2 + 2);
+        nr.start = ns; nr.len = nlr; nr.cum = nc;
+        TRY(dc_parse_runs(nline, nnl, &nr, lp, flag, dlt, part, d_err, sc + 11, s));
+    }
+    GET(int64_t, contrib, B_D_CONTRIB, nenc + 1);
+    GET(int64_t, doff, B_D_OFF, nenc + 1);
+    GET(int64_t, dsum, B_D_DSUM, nenc + 1);
+    TRY(dc_decode_prepare(enc, nenc, lp, contrib, dlt, doff, dsum, nRp, part, d_err, sc + 12, s));
+    int64_t D = 0;
+    TRY(d2h_i64(ctx, sc + 12, &D, 1));
+    int32_t err = 0;
+    HIPTRY(hipMemcpyAsync(&err, d_err, sizeof err, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    if (err & 1) return ctx->fail(SCCG_E_PARSE, "record text outside the run/token grammar");
+    if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
+    const int64_t nres = D + nr.total;
+    if (nr.n > 0) {
+        int32_t ls_last = 0, ll_last = 0;
+        HIPTRY(hipMemcpyAsync(&ls_last, nr.start + nr.n - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPTRY(hipMemcpyAsync(&ll_last, nr.len + nr.n - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPTRY(hipStreamSynchronize(s));
+        if ((int64_t)ls_last + ll_last > nres) return ctx->fail(SCCG_E_PARSE, "N positions beyond the sequence");
+    }
+    const int64_t hlen = has_hdr ? end[0] : 0;
+    const int64_t total = hlen + 1 + nres + (nres > 0 ? (nres - 1) / 50 : 0) + 1;
+    *out_len = total;
+    if (size_only) return SCCG_OK;
+    if (total > out_cap) return ctx->fail(SCCG_E_NOMEM, "output needs %lld bytes", (long long)total);
+    GET(uint8_t, dec, B_D_DEC, D + 64);
+    TRY(dc_decode_fill(enc, nenc, lp, doff, dsum, dlt, contrib, Rp, dec, s));
+    if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
+    TRY(put_bytes(ctx, out + hlen, "\n", 1));
+    TRY(dc_format(dec, nres, nr, lr, out + hlen + 1, s));
+    TRY(put_bytes(ctx, out + total - 1, "\n", 1));
+    HIPTRY(hipStreamSynchronize(s));
+    ctx->stats.target_bases = nres;
+    ctx->stats.reference_bases = nRp;
+    return SCCG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sccg_compress_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len, const void* d_tgt_fa, size_t tgt_len,
+                         void* d_out, size_t out_cap, size_t* out_len, void* stream) {
+    if (!ctx || !d_out || !out_len || (!d_ref_fa && ref_len) || (!d_tgt_fa && tgt_len)) return SCCG_E_INVALID;
+    HIPTRY(hipSetDevice(ctx->device));
+    hipStream_t saved = ctx->stream;
+    if (stream) ctx->stream = (hipStream_t)stream;
+    int64_t len = 0;
+    int rc = compress_device_impl(ctx, (const uint8_t*)d_ref_fa, (int64_t)ref_len, (const uint8_t*)d_tgt_fa,
+                                  (int64_t)tgt_len, (uint8_t*)d_out, (int64_t)out_cap, &len);
+    ctx->stream = saved;
+    *out_len = (size_t)len;
+    return rc;
+}
+
+int sccg_compress(sccg_ctx* ctx, const char* ref_fa, size_t ref_len, const char* tgt_fa, size_t tgt_len,
+                  sccg_buf* out_text) {
+    if (!ctx || !out_text || (!ref_fa && ref_len) || (!tgt_fa && tgt_len)) return SCCG_E_INVALID;
+    out_text->data = nullptr;
+    out_text->len = 0;
+    HIPTRY(hipSetDevice(ctx->device));
+    uint8_t* drf = reinterpret_cast<uint8_t*>(ctx->get(B_RFA, ref_len + 16));
+    uint8_t* dtf = reinterpret_cast<uint8_t*>(ctx->get(B_TFA, tgt_len + 16));
+    const size_t cap = sccg_compress_bound(ref_len, tgt_len);
+    uint8_t* dout = reinterpret_cast<uint8_t*>(ctx->get(B_OUT, cap));
+    if (!drf || !dtf || !dout) return ctx->fail(SCCG_E_NOMEM, "device allocation failed");
+    if (ref_len) HIPTRY(hipMemcpyAsync(drf, ref_fa, ref_len, hipMemcpyHostToDevice, ctx->stream));
+    if (tgt_len) HIPTRY(hipMemcpyAsync(dtf, tgt_fa, tgt_len, hipMemcpyHostToDevice, ctx->stream));
+    int64_t len = 0;
+    int rc = compress_device_impl(ctx, drf, (int64_t)ref_len, dtf, (int64_t)tgt_len, dout, (int64_t)cap, &len);
+    if (rc) return rc;
+    char* h = (char*)malloc((size_t)len + 1);
+    if (!h) return ctx->fail(SCCG_E_NOMEM, "host allocation failed");
+    if (len) HIPTRY(hipMemcpy(h, dout, (size_t)len, hipMemcpyDeviceToHost));
+    h[len] = 0;
+    out_text->data = h;
+    out_text->len = (size_t)len;
+    return SCCG_OK;
+}
+
+int sccg_reconstruct_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len, const void* d_rec, size_t rec_len,
+                            void* d_out, size_t out_cap, size_t* out_len, void* stream) {
+    if (!ctx || !out_len || (!d_ref_fa && ref_len) || (!d_rec && rec_len)) return SCCG_E_INVALID;
+    HIPTRY(hipSetDevice(ctx->device));
+    hipStream_t saved = ctx->stream;
+    if (stream) ctx->stream = (hipStream_t)stream;
+    int64_t len = 0;
+    int rc = reconstruct_impl(ctx, (const uint8_t*)d_ref_fa, (int64_t)ref_len, (const uint8_t*)d_rec, (int64_t)rec_len,
+                              (uint8_t*)d_out, (int64_t)out_cap, &len, d_out == nullptr);
+    ctx->stream = saved;
+    *out_len = (size_t)len;
+    return rc;
+}
+
+int sccg_reconstruct(sccg_ctx* ctx, const char* ref_fa, size_t ref_len, const char* rec_text, size_t rec_len,
+                     sccg_buf* out_fa) {
+    if (!ctx || !out_fa || (!ref_fa && ref_len) || (!rec_text && rec_len)) return SCCG_E_INVALID;
+    out_fa->data = nullptr;
+    out_fa->len = 0;
+    HIPTRY(hipSetDevice(ctx->device));
+    uint8_t* drf = reinterpret_cast<uint8_t*>(ctx->get(B_RFA, ref_len + 16));
+    uint8_t* drc = reinterpret_cast<uint8_t*>(ctx->get(B_TFA, rec_len + 16));
+    if (!drf || !drc) return ctx->fail(SCCG_E_NOMEM, "device allocation failed");
+    if (ref_len) HIPTRY(hipMemcpyAsync(drf, ref_fa, ref_len, hipMemcpyHostToDevice, ctx->stream));
+    if (rec_len) HIPTRY(hipMemcpyAsync(drc, rec_text, rec_len, hipMemcpyHostToDevice, ctx->stream));
+    int64_t need = 0;
+    int rc = reconstruct_impl(ctx, drf, (int64_t)ref_len, drc, (int64_t)rec_len, nullptr, 0, &need, true);
+    if (rc) return rc;
+    uint8_t* dout = reinterpret_cast<uint8_t*>(ctx->get(B_OUT, (size_t)need + 16));
+    if (!dout) return ctx->fail(SCCG_E_NOMEM, "device allocation failed");
+    int64_t len = 0;
+    rc = reconstruct_impl(ctx, drf, (int64_t)ref_len, drc, (int64_t)rec_len, dout, need + 16, &len, false);
+    if (rc) return rc;
+    char* h = (char*)malloc((size_t)len + 1);
+    if (!h) return ctx->fail(SCCG_E_NOMEM, "host allocation failed");
+    HIPTRY(hipMemcpy(h, dout, (size_t)len, hipMemcpyDeviceToHost));
+    h[len] = 0;
+    out_fa->data = h;
+    out_fa->len = (size_t)len;
+    return SCCG_OK;
+}
+
+// match_sequences seam (compression.cpp:36): local segments or the windowed global walk
+int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, size_t nt, int k, int m, int global,
+               int64_t offset, sccg_records* out) {
+    if (!ctx || !out || (!sr && nr) || (!st && nt)) return SCCG_E_INVALID;
+    memset(out, 0, sizeof *out);
+    HIPTRY(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    std::vector<uint8_t> kind;
+    std::vector<int32_t> pos, len;
+    std::vector<int64_t> tt;
+    auto push = [&](uint8_t kd, int32_t p, int32_t l, int64_t t) {
+        kind.push_back(kd); pos.push_back(p); len.push_back(l); tt.push_back(t);
+    };
+    if (!global) {
+        if (nr > (size_t)SEG_L || nt > (size_t)SEG_L || (k != 14 && k != 10))
+            return ctx->fail(SCCG_E_UNSUPPORTED, "local sccg_match takes |Sr|,|St| <= 1000 and k in {10,14}");
+        GET(uint8_t, R, B_R, nr + 64);
+        GET(uint8_t, T, B_T, nt + 64);
+        GET(uint32_t, recs, B_RECS, SEG_REC_CAP);
+        GET(SegStat, stat, B_STAT, 1);
+        if (nr) HIPTRY(hipMemcpyAsync(R, sr, nr, hipMemcpyHostToDevice, s));
+        if (nt) HIPTRY(hipMemcpyAsync(T, st, nt, hipMemcpyHostToDevice, s));
+        TRY(launch_local_pass(k, 1, 0, R, (int64_t)nr, T, (int64_t)nt, 1, recs, stat, s));
+        SegStat hs;
+        uint32_t hr[SEG_REC_CAP];
+        HIPTRY(hipMemcpyAsync(&hs, stat, sizeof hs, hipMemcpyDeviceToHost, s));
+        HIPTRY(hipMemcpyAsync(hr, recs, sizeof hr, hipMemcpyDeviceToHost, s));
+        HIPTRY(hipStreamSynchronize(s));
+        for (int i = 0; i < hs.nrec; i++) {
+            const uint32_t r = hr[i];
+            if (r >> 31) push(1, (int32_t)((r >> 11) & 0xfffff) + (int32_t)offset, (int32_t)(r & 0x7ff), -1);
+            else push(0, 0, (int32_t)(r & 0x7ff), (int64_t)(r >> 11));
+        }
+        // match records carry no t: recover it from the running position
+        int64_t t = 0;
+        for (size_t i = 0; i < kind.size(); i++) { if (kind[i]) tt[i] = t; t += len[i]; }
+    } else {
+        if (m < 0 || 2 * m + 1 > 256 || k < 1 || k > 15 || nr >= (size_t)INT32_MAX - 8 || nt >= (size_t)INT32_MAX - 8)
+            return ctx->fail(SCCG_E_UNSUPPORTED, "global sccg_match takes 0 <= m <= 127, 1 <= k <= 15");
+        GET(uint8_t, R, B_RP, nr + 64);
+        GET(uint8_t, T, B_TP, nt + 64);
+        if (nr) HIPTRY(hipMemcpyAsync(R, sr, nr, hipMemcpyHostToDevice, s));
+        if (nt) HIPTRY(hipMemcpyAsync(T, st, nt, hipMemcpyHostToDevice, s));
+        const size_t wsb = walk_workspace_bytes((int64_t)nr, (int64_t)nt, k, WALK_CHUNK);
+        void* ws = ctx->get(B_WALK, wsb);
+        GET(uint8_t, txt, B_OUT, 4 * nt + 64);
+        if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace");
+        WalkResult wr{};
+        int64_t tl = 0;
+        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, k, m, WALK_CHUNK, ws, wsb, txt, &tl, &wr, s));
+        const int32_t *dt, *dp, *dl;
+        int64_t nm;
+        global_matches(ws, &dt, &dp, &dl, &nm);
+        std::vector<int32_t> ht((size_t)nm), hp((size_t)nm), hl((size_t)nm);
+        if (nm) {
+            HIPTRY(hipMemcpyAsync(ht.data(), dt, (size_t)nm * 4, hipMemcpyDeviceToHost, s));
+            HIPTRY(hipMemcpyAsync(hp.data(), dp, (size_t)nm * 4, hipMemcpyDeviceToHost, s));
+            HIPTRY(hipMemcpyAsync(hl.data(), dl, (size_t)nm * 4, hipMemcpyDeviceToHost, s));
+        }
+        HIPTRY(hipStreamSynchronize(s));
+        int64_t prev_end = 0;
+        for (int64_t i = 0; i < nm; i++) {
+            if (ht[i] > prev_end) push(0, 0, (int32_t)(ht[i] - prev_end), prev_end);
+            push(1, hp[i] + (int32_t)offset, hl[i], ht[i]);
+            prev_end = ht[i] + hl[i];
+        }
+        if ((int64_t)nt > prev_end) push(0, 0, (int32_t)((int64_t)nt - prev_end), prev_end);
+    }
+    const size_t n = kind.size();
+    out->n = (int64_t)n;
+    out->kind = (uint8_t*)malloc(n ? n : 1);
+    out->pos = (int32_t*)malloc((n ? n : 1) * 4);
+    out->len = (int32_t*)malloc((n ? n : 1) * 4);
+    out->t = (int64_t*)malloc((n ? n : 1) * 8);
+    if (!out->kind || !out->pos || !out->len || !out->t) return ctx->fail(SCCG_E_NOMEM, "host allocation");
+    if (n) {
+        memcpy(out->kind, kind.data(), n);
+        memcpy(out->pos, pos.data(), n * 4);
+        memcpy(out->len, len.data(), n * 4);
+        memcpy(out->t, tt.data(), n * 8);
+    }
+    return SCCG_OK;
+}
+
+}  // extern "C"

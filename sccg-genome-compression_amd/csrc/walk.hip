@@ -1,0 +1,882 @@
+// walk.hip -- global mode: match_sequences(R', T', 14, 100, true) and its record text.
+//
+//   compression.cpp:561  match_sequences(reference_genome, target_genome, k, m, true)
+//   compression.cpp:64-161 greedy walk, :83-101 +-m range gate, :110-138 selection
+//   compression.cpp:564-573 record emission, :222-304 delta_encode
+//
+// The walk is sequential through its state (index, prev_match_end = P).  Two observations make
+// it parallel and exact:
+//   1. Once P != -1 the gate admits only candidates c in [P-m, P+m]; a gated step is therefore a
+//      function of the target k-mer and the 2m+k reference bytes around P, never of the full
+//      k-mer table: an LDS-resident window of <= 201 keys decides both "literal" and the
+//      candidate set (the ungated l1/p1 of :124-129 is only consulted when the gated pick is the
+//      pn2==0 sentinel, i.e. p2 == 0, which needs P <= m -- handled by an exact full scan).
+//   2. Two walks that reach the same (index, P) coincide from then on.  So the target is cut into
+//      chunks; round 1 walks every chunk speculatively from a guessed P (a 32-mer anchor on a
+//      1/16-sampled reference index); later rounds re-walk a chunk from its predecessor's exit
+//      state until it emits a match its previous trajectory also holds (then the rest of the
+//      trajectory is kept).  Rounds repeat until every chunk was walked from its true entry.
+// The first step (P == -1, ungated) and the p2 == 0 escalations run as exact grid-wide scans.
+#include "internal.h"
+
+#include <vector>
+
+namespace {
+
+constexpr int WPB = 4;                 // chunks (waves) per block
+constexpr int WCAP = 256;              // window positions held in LDS (2m+1 <= WCAP)
+constexpr int WBYTES = WCAP + 32;
+constexpr int WTBITS = 9;              // window hash slots
+constexpr int WTSLOTS = 1 << WTBITS;
+constexpr int32_t INVALID = INT32_MIN;
+constexpr int ANCHOR_K = 32;
+constexpr int ANCHOR_STEP = 16;
+constexpr uint64_t A_EMPTY = ~0ull;
+constexpr uint32_t A_UNSET = 0xFFFFFFFEu, A_MULTI = 0xFFFFFFFFu;
+
+enum ChunkKind : int32_t { KIND_SPEC = 0, KIND_FIX = 1, KIND_RESUME = 2 };
+enum ChunkStatus : int32_t { ST_OK = 0, ST_ESC = 1 };
+
+struct WalkPtrs {
+    const uint8_t* R;
+    const uint8_t* T;
+    int32_t nR, nT, k, m, S, C, cap;
+    int32_t* bt[2];
+    int32_t* bp[2];
+    int32_t* bl[2];
+    int32_t* cnt[2];
+    int32_t* cur;
+    int32_t* exitX;
+    int32_t* exitP;
+    int32_t* usedX;
+    int32_t* usedP;
+    int32_t* kind;
+    int32_t* status;
+    int32_t* escX;
+    int32_t* escP;
+    int32_t* escN;
+    int32_t* escQ;
+    int32_t* snapX;
+    int32_t* snapP;
+    int32_t* guess;
+    int32_t* plist;
+    int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP
+    uint64_t* akeys;
+    uint32_t* apos;
+    int32_t abits;
+    unsigned long long* fc;   // full-candidate scan scalars: [0] lmax [1] cnt [2] has0 [3] minkey [4] firsthit [5] firstexo
+    int64_t* flat_off;        // per chunk
+    int32_t* ft;
+    int32_t* fp;
+    int32_t* fl;
+    int64_t* tlen;            // per flat match: text length -> offsets
+    int64_t* partial;
+    int64_t* scal64;          // [0] total matches [1] text bytes
+};
+
+struct WalkLds {
+    uint8_t win[WBYTES];
+    uint8_t tb[64 + 32];
+    uint32_t wkeys[WCAP];
+    uint32_t wtab[WTSLOTS / 2];
+    int32_t cand[WCAP];
+};
+
+__device__ __forceinline__ uint64_t pick_key(int32_t p, int32_t pme) {
+    const int32_t d = p - pme;
+    return ((uint64_t)(uint32_t)(d < 0 ? -d : d) << 32) | (uint32_t)p;
+}
+
+__device__ __forceinline__ uint32_t wt_get(const uint32_t* tab, int slot) {
+    return (tab[slot >> 1] >> ((slot & 1) * 16)) & 0xffffu;
+}
+__device__ __forceinline__ void wt_insert(uint32_t* tab, uint32_t key, uint32_t val) {
+    int slot = (int)slot_hash(key, WTBITS);
+    for (;;) {
+        uint32_t* w = &tab[slot >> 1];
+        const int sh = (slot & 1) * 16;
+        uint32_t old = *w;
+        while (((old >> sh) & 0xffffu) == 0) {
+            const uint32_t prev = atomicCAS(w, old, old | (val << sh));
+            if (prev == old) return;
+            old = prev;
+        }
+        slot = (slot + 1) & (WTSLOTS - 1);
+    }
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int k) {
+    for (int i = 0; i < k; i++) if (a[i] != b[i]) return false;
+    return true;
+}
+
+// 16 bytes at an arbitrary address as 4 little-endian words (5 aligned dword loads)
+__device__ __forceinline__ void load16u(const uint8_t* p, uint32_t (&o)[4]) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t v[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) v[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+}
+
+// longest common extension of R[a..] and T[b..], at most maxlen bytes; whole wave, 1 KiB / step
+__device__ int32_t wave_lce(const uint8_t* __restrict__ R, int32_t a, const uint8_t* __restrict__ T, int32_t b,
+                            int32_t maxlen) {
+    const int lane = lane_id();
+    for (int32_t off = 0; off < maxlen; off += 1024) {
+        const int32_t my = off + 16 * lane;
+        int32_t valid = maxlen - my;
+        int32_t e = INT32_MAX;
+        if (valid > 0) {
+            uint32_t r[4], t[4];
+            load16u(R + a + my, r);
+            load16u(T + b + my, t);
+            int pos = 16;
+#pragma unroll
+            for (int i = 3; i >= 0; i--) {
+                const uint32_t x = r[i] ^ t[i];
+                if (x) pos = 4 * i + (__builtin_ctz(x) >> 3);
+            }
+            if (valid < 16 && pos > valid) pos = valid;
+            if (pos < 16) e = my + pos;
+        }
+        const int32_t m = wave_min(e);
+        if (m != INT32_MAX) return m < maxlen ? m : maxlen;
+    }
+    return maxlen > 0 ? maxlen : 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// window of P: keys of every reference k-mer start in [max(0,P-m), min(nR-k, P+m)]
+// ---------------------------------------------------------------------------------------------
+__device__ void build_window(const WalkPtrs& A, WalkLds& L, int32_t P, int32_t& lo, int32_t& nwin) {
+    const int lane = lane_id();
+    lo = P - A.m < 0 ? 0 : P - A.m;
+    const int32_t hi = (P + A.m < A.nR - A.k) ? P + A.m : A.nR - A.k;
+    nwin = hi - lo + 1;
+    if (nwin < 0) nwin = 0;
+    const int nbytes = nwin + A.k - 1;
+    for (int i = lane; i < WBYTES; i += 64) L.win[i] = (i < nbytes) ? A.R[lo + i] : (uint8_t)0;
+    for (int i = lane; i < WTSLOTS / 2; i += 64) L.wtab[i] = 0;
+    wave_sync();
+    for (int i = lane; i < nwin; i += 64) {
+        const uint32_t key = kmer_key(&L.win[i], A.k);
+        L.wkeys[i] = key;
+        wt_insert(L.wtab, key, (uint32_t)i + 1);
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ bool window_has(const WalkPtrs& A, const WalkLds& L, uint32_t key, const uint8_t* kb) {
+    int slot = (int)slot_hash(key, WTBITS);
+    for (int probes = 0; probes < WTSLOTS; probes++) {
+        const uint32_t v = wt_get(L.wtab, slot);
+        if (!v) return false;
+        const int i = (int)v - 1;
+        if (L.wkeys[i] == key && (key < KEY_EXOTIC || bytes_eq(&L.win[i], kb, A.k))) return true;
+        slot = (slot + 1) & (WTSLOTS - 1);
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------------------------
+// the chunk walk (one wave per chunk)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
+    __shared__ WalkLds lds_all[WPB];
+    const int w = wave_in_block(), lane = lane_id();
+    const int32_t li = (int32_t)blockIdx.x * WPB + w;
+    if (li >= nlist) return;
+    WalkLds& L = lds_all[w];
+    const int32_t j = list[li];
+    const int32_t kind = A.kind[j];
+    const int32_t lo_j = j * A.S;
+    const int32_t hi_j = (lo_j + A.S < A.nT) ? lo_j + A.S : A.nT;
+    const int32_t lastk = A.nT - A.k;
+    const int k = A.k;
+
+    int32_t x, P, n = 0, q = 0, ob, cb = -1, cc = 0;
+    if (kind == KIND_SPEC) {
+        ob = A.cur[j];
+        x = lo_j;
+        P = A.guess[j];
+        if (lane == 0) { A.usedX[j] = lo_j; A.usedP[j] = P; }
+    } else if (kind == KIND_FIX) {
+        cb = A.cur[j];
+        ob = 1 - cb;
+        cc = A.cnt[cb][j];
+        x = A.snapX[j];
+        P = A.snapP[j];
+        if (lane == 0) { A.usedX[j] = x; A.usedP[j] = P; }
+    } else {   // resume after an escalation was resolved on the host
+        cb = A.cur[j];
+        ob = 1 - cb;
+        cc = A.cnt[cb][j];
+        x = A.escX[j];
+        P = A.escP[j];
+        n = A.escN[j];
+        q = A.escQ[j];
+    }
+    if (lane == 0) A.status[j] = ST_OK;
+    if (P == INVALID) {   // speculative chunk without an anchor: nothing to offer
+        if (lane == 0) { A.cnt[ob][j] = 0; A.exitX[j] = INVALID; A.exitP[j] = INVALID; }
+        return;
+    }
+    int32_t* ot = A.bt[ob] + (size_t)j * A.cap;
+    int32_t* op = A.bp[ob] + (size_t)j * A.cap;
+    int32_t* ol = A.bl[ob] + (size_t)j * A.cap;
+    const int32_t* ct = cb >= 0 ? A.bt[cb] + (size_t)j * A.cap : nullptr;
+    const int32_t* cp = cb >= 0 ? A.bp[cb] + (size_t)j * A.cap : nullptr;
+    const int32_t* cl = cb >= 0 ? A.bl[cb] + (size_t)j * A.cap : nullptr;
+
+    int32_t wlo = 0, nwin = 0, wP = INVALID;
+    bool converged = false, escalated = false;
+    const int32_t scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
+    while (x < scan_end) {
+        if (wP != P) { build_window(A, L, P, wlo, nwin); wP = P; }
+        if (nwin <= 0) { x = scan_end; break; }
+        // ---- literal steps: first y in [x, scan_end) whose k-mer is in the window
+        for (int i = lane; i < 64 + 32; i += 64) {
+            const int32_t pos = x + i;
+            L.tb[i] = pos < A.nT ? A.T[pos] : (uint8_t)0;
+        }
+        wave_sync();
+        const int32_t y_l = x + lane;
+        const bool valid = y_l < scan_end;
+        const uint32_t key_l = valid ? kmer_key(&L.tb[lane], k) : 0u;
+        const bool hit = valid && window_has(A, L, key_l, &L.tb[lane]);
+        const unsigned long long hm = __ballot(hit);
+        if (!hm) {
+            x = (x + 64 < scan_end) ? x + 64 : scan_end;
+            wave_sync();
+            continue;
+        }
+        const int hl = first_lane(hm);
+        const int32_t y = x + hl;
+        const uint32_t key = __shfl(key_l, hl, 64);
+        // ---- candidates in the window (compression.cpp:114-130, in-range ones only)
+        int ncand = 0;
+        for (int i0 = 0; i0 < nwin; i0 += 64) {
+            const int i = i0 + lane;
+            const bool c = i < nwin && L.wkeys[i] == key && (key < KEY_EXOTIC || bytes_eq(&L.win[i], &L.tb[hl], k));
+            const unsigned long long cm = __ballot(c);
+            if (c) L.cand[ncand + __popcll(cm & ((1ull << lane) - 1))] = wlo + i;
+            ncand += __popcll(cm);
+        }
+        wave_sync();
+        int32_t bl = 0, bcnt = 0;
+        bool bhas0 = false;
+        uint64_t bkey = ~0ull;
+        for (int ci = 0; ci < ncand; ci++) {
+            const int32_t c = L.cand[ci];
+            int32_t maxlen = A.nR - (c + k);
+            const int32_t mt = A.nT - (y + k);
+            if (mt < maxlen) maxlen = mt;
+            const int32_t l = k + wave_lce(A.R, c + k, A.T, y + k, maxlen);   // extend_alignment
+            if (l > bl) { bl = l; bcnt = 1; bhas0 = (c == 0); bkey = c ? pick_key(c, P) : ~0ull; }
+            else if (l == bl) {
+                bcnt++;
+                if (c == 0) bhas0 = true;
+                else { const uint64_t pk = pick_key(c, P); bkey = pk < bkey ? pk : bkey; }
+            }
+        }
+        uint64_t pk;
+        if (bcnt >= 2 && bhas0) pk = bkey;
+        else { const uint64_t k0 = bhas0 ? pick_key(0, P) : ~0ull; pk = k0 < bkey ? k0 : bkey; }
+        const int32_t p = (int32_t)(uint32_t)pk;
+        if (p == 0) {   // pn2 == 0: the reference falls back to the ungated (pn1, ln1) (:134-138)
+            escalated = true;
+            if (lane == 0) {
+                if (kind == KIND_SPEC) { A.cnt[ob][j] = 0; A.exitX[j] = INVALID; A.exitP[j] = INVALID; }
+                else {
+                    A.status[j] = ST_ESC;
+                    A.escX[j] = y; A.escP[j] = P; A.escN[j] = n; A.escQ[j] = q;
+                    atomicAdd(&A.scal[1], 1);
+                }
+            }
+            break;
+        }
+        if (lane == 0) { ot[n] = y; op[n] = p; ol[n] = bl; }
+        n++;
+        // ---- convergence with the previous trajectory of this chunk
+        if (cb >= 0) {
+            for (;;) {
+                const int32_t qi = q + lane;
+                const bool ge = qi >= cc || ct[qi] >= y;
+                const unsigned long long gm = __ballot(ge);
+                if (gm) { q += first_lane(gm); break; }
+                q += 64;
+            }
+            if (q < cc && ct[q] == y && cp[q] == p && cl[q] == bl) {
+                const int32_t rest = cc - q - 1;
+                for (int i = lane; i < rest; i += 64) {
+                    ot[n + i] = ct[q + 1 + i];
+                    op[n + i] = cp[q + 1 + i];
+                    ol[n + i] = cl[q + 1 + i];
+                }
+                n += rest;
+                converged = true;
+                break;
+            }
+        }
+        P = p + bl - 1;   // compression.cpp:149
+        x = y + bl;       // compression.cpp:159
+        wave_sync();
+    }
+    if (escalated) return;
+    if (lane == 0) {
+        A.cnt[ob][j] = n;
+        if (!converged) { A.exitX[j] = x; A.exitP[j] = P; }
+        if (cb >= 0) A.cur[j] = ob;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// pending chunks: entry state (predecessor's exit) differs from the one their trajectory used
+// ---------------------------------------------------------------------------------------------
+__global__ void k_pending(WalkPtrs A) {
+    for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
+        const int32_t ex = j ? A.exitX[j - 1] : A.scal[2];
+        const int32_t ep = j ? A.exitP[j - 1] : A.scal[3];
+        if (ex == INVALID) continue;
+        if (ex == A.usedX[j] && ep == A.usedP[j]) continue;
+        A.snapX[j] = ex;
+        A.snapP[j] = ep;
+        A.kind[j] = KIND_FIX;
+        A.plist[atomicAdd(&A.scal[0], 1)] = j;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// anchors: 32-mers at every 16th R' position -> position (or MULTI); one probe batch per chunk
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {   // bijective
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return x;
+}
+__device__ __forceinline__ bool code32(const uint8_t* s, uint64_t& code) {
+    uint64_t c = 0;
+    for (int i = 0; i < ANCHOR_K; i++) {
+        const uint32_t b = base2(s[i]);
+        if (b > 3) return false;
+        c = (c << 2) | b;
+    }
+    code = c;
+    return true;
+}
+
+__global__ void k_anchor_clear(uint64_t* keys, uint32_t* pos, int64_t slots) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < slots; i += (int64_t)gridDim.x * blockDim.x) {
+        keys[i] = A_EMPTY;
+        pos[i] = A_UNSET;
+    }
+}
+
+__global__ void k_anchor_build(WalkPtrs A) {
+    const int64_t ns = A.nR >= ANCHOR_K ? ((int64_t)A.nR - ANCHOR_K) / ANCHOR_STEP + 1 : 0;
+    const uint64_t smask = (1ull << A.abits) - 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t p = (int32_t)(i * ANCHOR_STEP);
+        uint64_t code;
+        if (!code32(A.R + p, code)) continue;
+        const uint64_t key = mix64(code);
+        if (key == A_EMPTY) continue;
+        uint64_t slot = key >> (64 - A.abits);
+        for (;;) {
+            const unsigned long long prev = atomicCAS((unsigned long long*)&A.akeys[slot], (unsigned long long)A_EMPTY,
+                                                      (unsigned long long)key);
+            if (prev == A_EMPTY) { atomicCAS(&A.apos[slot], A_UNSET, (uint32_t)p); break; }
+            if (prev == key) { atomicExch(&A.apos[slot], A_MULTI); break; }
+            slot = (slot + 1) & smask;
+        }
+    }
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
+    const int32_t j = (int32_t)blockIdx.x * WPB + wave_in_block();
+    if (j >= A.C) return;
+    const int lane = lane_id();
+    const uint64_t smask = (1ull << A.abits) - 1;
+    int32_t g = INVALID;
+    for (int b = 0; b < 4 && g == INVALID; b++) {
+        const int32_t y = j * A.S + b * 64 + lane;
+        int32_t diag = INVALID;
+        uint64_t code;
+        if (y + ANCHOR_K <= A.nT && code32(A.T + y, code)) {
+            const uint64_t key = mix64(code);
+            uint64_t slot = key >> (64 - A.abits);
+            for (int probes = 0; probes < 64; probes++) {
+                const uint64_t kk = A.akeys[slot];
+                if (kk == A_EMPTY) break;
+                if (kk == key) {
+                    const uint32_t ps = A.apos[slot];
+                    if (ps < A_UNSET) diag = (int32_t)ps - y;
+                    break;
+                }
+                slot = (slot + 1) & smask;
+            }
+        }
+        const unsigned long long m = __ballot(diag != INVALID);
+        if (m) {
+            const int l = first_lane(m);
+            const int32_t d = __shfl(diag, l, 64);
+            int64_t gp = (int64_t)j * A.S - 1 + d;
+            if (gp < 0) gp = 0;
+            if (gp > A.nR - 1) gp = A.nR - 1;
+            g = (int32_t)gp;
+        }
+    }
+    if (lane == 0) A.guess[j] = g;
+}
+
+// ---------------------------------------------------------------------------------------------
+// exact full-reference candidate scans (the ungated first step and the p2 == 0 escalation)
+// ---------------------------------------------------------------------------------------------
+constexpr int FC_PER_T = 64;
+
+__device__ __forceinline__ int32_t serial_ext(const uint8_t* R, int32_t nR, const uint8_t* T, int32_t nT, int32_t c,
+                                              int32_t y, int k) {
+    int32_t l = k;
+    while (c + l < nR && y + l < nT && R[c + l] == T[y + l]) ++l;
+    return l;
+}
+
+// pass 0: max extension over all candidates; pass 1: count / has0 / min pick key at that max
+__global__ void k_fullc(WalkPtrs A, int32_t y, int32_t P, int pass) {
+    const int k = A.k;
+    uint8_t kb[16];
+    for (int i = 0; i < k; i++) kb[i] = A.T[y + i];
+    const uint32_t key = kmer_key(kb, k);
+    const uint32_t lmax = (uint32_t)A.fc[0];
+    const int64_t npos = (int64_t)A.nR - k + 1;
+    const uint32_t MASK = (1u << (2 * k)) - 1u;
+    for (int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * FC_PER_T; p0 < npos;
+         p0 += (int64_t)gridDim.x * blockDim.x * FC_PER_T) {
+        uint32_t code = 0;
+        int lastbad = -1000;
+        for (int i = 0; i < FC_PER_T + k - 1; i++) {
+            const int64_t pos = p0 + i;
+            if (pos >= A.nR) break;
+            uint32_t b = base2(A.R[pos]);
+            if (b > 3) { lastbad = i; b = 0; }
+            code = ((code << 2) | b) & MASK;
+            const int st = i - (k - 1);
+            if (st < 0) continue;
+            const int64_t c = p0 + st;
+            if (c >= npos) break;
+            bool eq;
+            if (key < KEY_EXOTIC) eq = lastbad < st && code == key;
+            else eq = lastbad >= st && bytes_eq(A.R + c, kb, k);
+            if (!eq) continue;
+            const int32_t l = serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, y, k);
+            if (pass == 0) atomicMax(&A.fc[0], (unsigned long long)l);
+            else if ((uint32_t)l == lmax) {
+                atomicAdd(&A.fc[1], 1ull);
+                if (c == 0) atomicOr(&A.fc[2], 1ull);
+                else atomicMin(&A.fc[3], (unsigned long long)pick_key((int32_t)c, P));
+            }
+        }
+    }
+}
+
+// first target position in [x0, x0+nb) whose k-mer occurs anywhere in R' (pure keys), and the
+// first position in the batch holding a non-ACGT k-mer (checked separately, exactly)
+constexpr int PB = 1024;
+constexpr int PBBITS = 11;
+__global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0, int32_t nb) {
+    __shared__ uint32_t hkey[1 << PBBITS];
+    __shared__ uint32_t hidx[1 << PBBITS];
+    const int k = A.k;
+    for (int i = threadIdx.x; i < (1 << PBBITS); i += blockDim.x) { hkey[i] = 0xffffffffu; hidx[i] = 0xffffffffu; }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+        const uint32_t key = kmer_key(A.T + x0 + i, k);
+        if (key >= KEY_EXOTIC) { atomicMin(&A.fc[5], (unsigned long long)(x0 + i)); continue; }
+        int slot = (int)slot_hash(key, PBBITS);
+        for (;;) {
+            const uint32_t prev = atomicCAS(&hkey[slot], 0xffffffffu, key);
+            if (prev == 0xffffffffu || prev == key) { atomicMin(&hidx[slot], (uint32_t)i); break; }
+            slot = (slot + 1) & ((1 << PBBITS) - 1);
+        }
+    }
+    __syncthreads();
+    const int64_t npos = (int64_t)A.nR - k + 1;
+    const uint32_t MASK = (1u << (2 * k)) - 1u;
+    for (int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * FC_PER_T; p0 < npos;
+         p0 += (int64_t)gridDim.x * blockDim.x * FC_PER_T) {
+        uint32_t code = 0;
+        int lastbad = -1000;
+        for (int i = 0; i < FC_PER_T + k - 1; i++) {
+            const int64_t pos = p0 + i;
+            if (pos >= A.nR) break;
+            uint32_t b = base2(A.R[pos]);
+            if (b > 3) { lastbad = i; b = 0; }
+            code = ((code << 2) | b) & MASK;
+            const int st = i - (k - 1);
+            if (st < 0 || lastbad >= st) continue;
+            if (p0 + st >= npos) break;
+            int slot = (int)slot_hash(code, PBBITS);
+            for (;;) {
+                const uint32_t hk = hkey[slot];
+                if (hk == 0xffffffffu) break;
+                if (hk == code) { atomicMin(&A.fc[4], (unsigned long long)(x0 + hidx[slot])); break; }
+                slot = (slot + 1) & ((1 << PBBITS) - 1);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// flatten + record text
+// ---------------------------------------------------------------------------------------------
+__global__ void k_chunk_counts(WalkPtrs A) {
+    for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x))
+        A.flat_off[j] = A.cnt[A.cur[j]][j];
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_flatten(WalkPtrs A, int32_t first) {
+    const int32_t j = (int32_t)blockIdx.x * WPB + wave_in_block();
+    if (j >= A.C) return;
+    const int lane = lane_id();
+    const int32_t b = A.cur[j];
+    const int32_t n = A.cnt[b][j];
+    const int64_t o = A.flat_off[j] + first;
+    const int32_t* t = A.bt[b] + (size_t)j * A.cap;
+    const int32_t* p = A.bp[b] + (size_t)j * A.cap;
+    const int32_t* l = A.bl[b] + (size_t)j * A.cap;
+    for (int i = lane; i < n; i += 64) { A.ft[o + i] = t[i]; A.fp[o + i] = p[i]; A.fl[o + i] = l[i]; }
+}
+
+__global__ void k_match_textlen(WalkPtrs A, int64_t nm) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t pend = i ? A.ft[i - 1] + A.fl[i - 1] : 0;
+        const int32_t pprev = i ? A.fp[i - 1] : 0;
+        const int32_t d = (int32_t)((uint32_t)A.fp[i] - (uint32_t)pprev);
+        A.tlen[i] = (int64_t)(A.ft[i] - pend) + 3 + ndigits_i32(d) + ndigits_i32(A.fl[i]);
+    }
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int64_t nm, uint8_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * WPB + wave_in_block();
+    if (i >= nm) return;
+    const int lane = lane_id();
+    const int32_t pend = i ? A.ft[i - 1] + A.fl[i - 1] : 0;
+    const int32_t t = A.ft[i];
+    uint8_t* o = out + A.tlen[i];
+    for (int32_t q = lane; q < t - pend; q += 64) o[q] = A.T[pend + q];
+    if (lane == 0) {
+        uint8_t* d = o + (t - pend);
+        const int32_t pprev = i ? A.fp[i - 1] : 0;
+        *d++ = '(';
+        d += write_i32(d, (int32_t)((uint32_t)A.fp[i] - (uint32_t)pprev));
+        *d++ = ',';
+        d += write_i32(d, A.fl[i]);
+        *d = ')';
+    }
+}
+
+__global__ void k_copy(const uint8_t* __restrict__ in, int64_t n, uint8_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+struct Carve {
+    char* base;
+    size_t off, cap;
+    template <typename T>
+    T* take(size_t n) {
+        off = (off + 255) & ~(size_t)255;
+        T* p = reinterpret_cast<T*>(base + off);
+        off += n * sizeof(T);
+        return p;
+    }
+};
+
+int anchor_bits(int64_t nR) {
+    int64_t want = 2 * (nR / ANCHOR_STEP + 1);
+    int b = 10;
+    while ((1ll << b) < want && b < 34) b++;
+    return b;
+}
+
+WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int k, int m,
+               int S, size_t* used) {
+    WalkPtrs A{};
+    Carve c{(char*)ws, 0, ws_bytes};
+    A.R = R; A.T = T;
+    A.nR = (int32_t)nR; A.nT = (int32_t)nT; A.k = k; A.m = m; A.S = S;
+    A.C = (int32_t)((nT + S - 1) / S);
+    if (A.C < 1) A.C = 1;
+    A.cap = S / k + 4;
+    const size_t C = (size_t)A.C, cap = (size_t)A.cap;
+    for (int b = 0; b < 2; b++) {
+        A.bt[b] = c.take<int32_t>(C * cap);
+        A.bp[b] = c.take<int32_t>(C * cap);
+        A.bl[b] = c.take<int32_t>(C * cap);
+        A.cnt[b] = c.take<int32_t>(C);
+    }
+    A.cur = c.take<int32_t>(C);
+    A.exitX = c.take<int32_t>(C); A.exitP = c.take<int32_t>(C);
+    A.usedX = c.take<int32_t>(C); A.usedP = c.take<int32_t>(C);
+    A.kind = c.take<int32_t>(C); A.status = c.take<int32_t>(C);
+    A.escX = c.take<int32_t>(C); A.escP = c.take<int32_t>(C); A.escN = c.take<int32_t>(C); A.escQ = c.take<int32_t>(C);
+    A.snapX = c.take<int32_t>(C); A.snapP = c.take<int32_t>(C);
+    A.guess = c.take<int32_t>(C);
+    A.plist = c.take<int32_t>(C);
+    A.scal = c.take<int32_t>(16);
+    A.abits = anchor_bits(nR);
+    A.akeys = c.take<uint64_t>((size_t)1 << A.abits);
+    A.apos = c.take<uint32_t>((size_t)1 << A.abits);
+    A.fc = c.take<unsigned long long>(8);
+    A.flat_off = c.take<int64_t>(C + 1);
+    const size_t maxm = (size_t)(nT / k + 2);
+    A.ft = c.take<int32_t>(maxm); A.fp = c.take<int32_t>(maxm); A.fl = c.take<int32_t>(maxm);
+    A.tlen = c.take<int64_t>(maxm + 1);
+    A.partial = c.take<int64_t>((size_t)scan_partials_needed((int64_t)(maxm > C ? maxm : C) + 1) + 16);
+    A.scal64 = c.take<int64_t>(8);
+    *used = c.off;
+    return A;
+}
+
+struct FullC {
+    int64_t lmax;
+    int32_t p;
+};
+
+constexpr int32_t NEVER = INT32_MIN + 1;   // "no entry used yet": differs from every state
+
+int set_u64(unsigned long long* p, std::initializer_list<int64_t> v, hipStream_t s) {
+    return dev_set_i64(reinterpret_cast<int64_t*>(p), (int)v.size(), v, s);
+}
+
+int run_fullc(WalkPtrs& A, int32_t y, int32_t P, FullC* out, hipStream_t s) {
+    int rc = set_u64(A.fc, {0, 0, 0, -1}, s);
+    if (rc) return rc;
+    const int64_t npos = (int64_t)A.nR - A.k + 1;
+    unsigned g = grid_for(npos > 0 ? npos : 1, 256 * FC_PER_T);
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_fullc, dim3(g), dim3(256), 0, s, A, y, P, 0);
+    hipLaunchKernelGGL(k_fullc, dim3(g), dim3(256), 0, s, A, y, P, 1);
+    SCCG_HIP(hipGetLastError());
+    unsigned long long r[4];
+    SCCG_HIP(hipMemcpyAsync(r, A.fc, sizeof r, hipMemcpyDeviceToHost, s));
+    SCCG_HIP(hipStreamSynchronize(s));
+    out->lmax = (int64_t)r[0];
+    if (r[0] == 0) { out->p = INVALID; return 0; }
+    const uint64_t k0 = (uint64_t)(uint32_t)(P < 0 ? -P : P) << 32;   // pick_key(0, P)
+    uint64_t pk;
+    if (r[1] >= 2 && r[2]) pk = r[3];
+    else pk = (r[2] && k0 < r[3]) ? k0 : r[3];
+    out->p = (int32_t)(uint32_t)pk;
+    return 0;
+}
+
+// host vector -> device, completed before returning (the vector may die right after)
+int h2d_sync(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return 0;
+    SCCG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    SCCG_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+}  // namespace
+
+size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk) {
+    size_t used = 0;
+    carve(nullptr, 0, nullptr, nR, nullptr, nT, k, 100, chunk, &used);
+    return used + 4096;
+}
+
+static thread_local WalkPtrs g_last;
+static thread_local int64_t g_last_n = 0;
+
+int global_matches(void* /*ws*/, const int32_t** t, const int32_t** p, const int32_t** l, int64_t* n) {
+    *t = g_last.ft; *p = g_last.fp; *l = g_last.fl; *n = g_last_n;
+    return 0;
+}
+
+#define RC(expr)                      \
+    do {                              \
+        int rc_ = (expr);             \
+        if (rc_) return rc_;          \
+    } while (0)
+
+int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
+                          void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s) {
+    if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
+    size_t used = 0;
+    WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, &used);
+    if (used > ws_bytes) return SCCG_E_INTERNAL;
+    res->rounds = 0;
+    res->chunks = A.C;
+    res->n_matches = 0;
+    const int32_t lastk = (int32_t)nTp - k;
+
+    // ---- the exact first (ungated) step: first target position with any candidate
+    int32_t first_y = INVALID, first_p = 0, first_l = 0;
+    if (nRp >= k && lastk >= 0) {
+        int32_t x0 = 0;
+        while (x0 <= lastk && first_y == INVALID) {
+            const int32_t nb = (lastk - x0 + 1) < PB ? (lastk - x0 + 1) : PB;
+            RC(set_u64(A.fc + 4, {-1, -1}, s));
+            const int64_t npos = nRp - k + 1;
+            unsigned g = grid_for(npos, 256 * FC_PER_T);
+            if (g > 4096) g = 4096;
+            hipLaunchKernelGGL(k_presence, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, nb);
+            SCCG_HIP(hipGetLastError());
+            unsigned long long r[2];
+            SCCG_HIP(hipMemcpyAsync(r, A.fc + 4, sizeof r, hipMemcpyDeviceToHost, s));
+            SCCG_HIP(hipStreamSynchronize(s));
+            if (r[0] != ~0ull && r[0] < r[1]) { first_y = (int32_t)r[0]; break; }
+            if (r[1] != ~0ull) {
+                FullC f;
+                RC(run_fullc(A, (int32_t)r[1], -1, &f, s));
+                if (f.lmax > 0) { first_y = (int32_t)r[1]; break; }
+                x0 = (int32_t)r[1] + 1;
+                continue;
+            }
+            x0 += nb;
+        }
+        if (first_y != INVALID) {
+            FullC f;
+            RC(run_fullc(A, first_y, -1, &f, s));
+            first_p = f.p;
+            first_l = (int32_t)f.lmax;
+        }
+    }
+    int32_t startX, startP;
+    if (first_y != INVALID) { startX = first_y + first_l; startP = first_p + first_l - 1; }
+    else { startX = lastk + 1 > 0 ? lastk + 1 : 0; startP = INVALID; }
+
+    // ---- init chunk state
+    const size_t C = (size_t)A.C;
+    SCCG_HIP(hipMemsetAsync(A.cur, 0, C * sizeof(int32_t), s));
+    SCCG_HIP(hipMemsetAsync(A.cnt[0], 0, C * sizeof(int32_t), s));
+    SCCG_HIP(hipMemsetAsync(A.cnt[1], 0, C * sizeof(int32_t), s));
+    SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.usedX, NEVER, C, s));
+    SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.usedP, NEVER, C, s));
+    SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.exitX, INVALID, C, s));
+    SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.exitP, INVALID, C, s));
+    RC(dev_set_i32(A.scal, 4, {0, 0, startX, startP}, s));
+
+    if (startP != INVALID && lastk >= 0) {
+        // anchors -> speculative guesses for chunks 1..C-1
+        const int64_t slots = 1ll << A.abits;
+        hipLaunchKernelGGL(k_anchor_clear, dim3(grid_for(slots, 256) > 8192 ? 8192 : grid_for(slots, 256)), dim3(256), 0,
+                           s, A.akeys, A.apos, slots);
+        const int64_t ns = nRp / ANCHOR_STEP + 1;
+        hipLaunchKernelGGL(k_anchor_build, dim3(grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256)), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
+        SCCG_HIP(hipGetLastError());
+        // round 1: chunk 0 exact (as a fix-up with an empty trajectory), chunks >= 1 speculative
+        {
+            std::vector<int32_t> kinds(C, KIND_SPEC), ids(C);
+            kinds[0] = KIND_FIX;
+            for (size_t j = 0; j < C; j++) ids[j] = (int32_t)j;
+            RC(h2d_sync(A.kind, kinds.data(), C * sizeof(int32_t), s));
+            RC(h2d_sync(A.plist, ids.data(), C * sizeof(int32_t), s));
+        }
+        RC(dev_set_i32(A.snapX, 1, {startX}, s));
+        RC(dev_set_i32(A.snapP, 1, {startP}, s));
+        int32_t nlist = A.C;
+        for (int64_t round = 1;; round++) {
+            hipLaunchKernelGGL(k_walk, dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
+            SCCG_HIP(hipGetLastError());
+            res->rounds = round;
+            // resolve escalations of exact walks (pn2 == 0 -> ungated pn1/ln1), then resume them
+            for (;;) {
+                int32_t nesc = 0;
+                SCCG_HIP(hipMemcpyAsync(&nesc, A.scal + 1, sizeof nesc, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipStreamSynchronize(s));
+                if (!nesc) break;
+                std::vector<int32_t> st(C), ex(C), ep(C), en(C), cur(C);
+                SCCG_HIP(hipMemcpyAsync(st.data(), A.status, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(ex.data(), A.escX, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(ep.data(), A.escP, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(en.data(), A.escN, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(cur.data(), A.cur, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipStreamSynchronize(s));
+                std::vector<int32_t> rl;
+                for (size_t j = 0; j < C; j++) {
+                    if (st[j] != ST_ESC) continue;
+                    FullC f;
+                    RC(run_fullc(A, ex[j], ep[j], &f, s));
+                    if (f.lmax <= 0) return SCCG_E_INTERNAL;   // a window candidate exists, so C is non-empty
+                    const int32_t ob = 1 - cur[j];
+                    const size_t at = j * (size_t)A.cap + (size_t)en[j];
+                    RC(dev_set_i32(A.bt[ob] + at, 1, {ex[j]}, s));
+                    RC(dev_set_i32(A.bp[ob] + at, 1, {f.p}, s));
+                    RC(dev_set_i32(A.bl[ob] + at, 1, {(int32_t)f.lmax}, s));
+                    RC(dev_set_i32(A.escX + j, 1, {ex[j] + (int32_t)f.lmax}, s));
+                    RC(dev_set_i32(A.escP + j, 1, {f.p + (int32_t)f.lmax - 1}, s));
+                    RC(dev_set_i32(A.escN + j, 1, {en[j] + 1}, s));
+                    RC(dev_set_i32(A.kind + j, 1, {KIND_RESUME}, s));
+                    rl.push_back((int32_t)j);
+                }
+                RC(dev_set_i32(A.scal + 1, 1, {0}, s));
+                RC(h2d_sync(A.plist, rl.data(), rl.size() * 4, s));
+                hipLaunchKernelGGL(k_walk, dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
+                                   (const int32_t*)A.plist, (int32_t)rl.size());
+                SCCG_HIP(hipGetLastError());
+            }
+            // which chunks were walked from a state that is not their true entry?
+            RC(dev_set_i32(A.scal, 1, {0}, s));
+            hipLaunchKernelGGL(k_pending, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
+            SCCG_HIP(hipGetLastError());
+            SCCG_HIP(hipMemcpyAsync(&nlist, A.scal, sizeof nlist, hipMemcpyDeviceToHost, s));
+            SCCG_HIP(hipStreamSynchronize(s));
+            if (!nlist) break;
+            if (round > 4 * (int64_t)A.C + 16) return SCCG_E_INTERNAL;
+        }
+    }
+
+    // ---- flatten: first match, then every chunk's trajectory
+    const int32_t nfirst = first_y != INVALID ? 1 : 0;
+    hipLaunchKernelGGL(k_chunk_counts, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
+    RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
+    if (nfirst) {
+        RC(dev_set_i32(A.ft, 1, {first_y}, s));
+        RC(dev_set_i32(A.fp, 1, {first_p}, s));
+        RC(dev_set_i32(A.fl, 1, {first_l}, s));
+    }
+    hipLaunchKernelGGL(k_flatten, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, nfirst);
+    SCCG_HIP(hipGetLastError());
+    int64_t nchunkm = 0;
+    SCCG_HIP(hipMemcpyAsync(&nchunkm, A.scal64, sizeof nchunkm, hipMemcpyDeviceToHost, s));
+    SCCG_HIP(hipStreamSynchronize(s));
+    const int64_t nm = nchunkm + nfirst;
+    res->n_matches = nm;
+    g_last = A;
+    g_last_n = nm;
+
+    // ---- record text: literal gap + "(dp,l)" per match, then the tail literal
+    int64_t text = 0;
+    int32_t tail_from = 0;
+    if (nm > 0) {
+        const unsigned g = grid_for(nm, 256) > 4096 ? 4096 : grid_for(nm, 256);
+        hipLaunchKernelGGL(k_match_textlen, dim3(g), dim3(256), 0, s, A, nm);
+        RC(dev_excl_sum(A.tlen, A.tlen, nm, A.scal64 + 1, A.partial, s));
+        hipLaunchKernelGGL(k_match_textwrite, dim3(grid_for(nm, WPB)), dim3(SCCG_BLOCK), 0, s, A, nm, out);
+        SCCG_HIP(hipGetLastError());
+        int32_t lt[2];
+        SCCG_HIP(hipMemcpyAsync(&text, A.scal64 + 1, sizeof text, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipMemcpyAsync(&lt[0], A.ft + nm - 1, 4, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipMemcpyAsync(&lt[1], A.fl + nm - 1, 4, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipStreamSynchronize(s));
+        tail_from = lt[0] + lt[1];
+    }
+    const int64_t tail = nTp - tail_from;
+    if (tail > 0) {
+        const unsigned g = grid_for(tail, 256) > 8192 ? 8192 : grid_for(tail, 256);
+        hipLaunchKernelGGL(k_copy, dim3(g), dim3(256), 0, s, Tp + tail_from, tail, out + text);
+        SCCG_HIP(hipGetLastError());
+    }
+    *out_len = text + (tail > 0 ? tail : 0);
+    return 0;
+}

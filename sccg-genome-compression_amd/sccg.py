@@ -1,0 +1,177 @@
+"""ctypes binding of libsccg.so (include/sccg.h) -- the MI355X SCCG hot path.
+
+Mirrors the reference's two entry points (compression.cpp:320 compress_genome up to 7z,
+decompression.cpp:117 reconstruct_genome + file body) and the match_sequences seam
+(compression.cpp:36).  There is no CPU fallback: if the HIP library or a GPU is missing,
+construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsccg.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "sccg.h")
+
+SCCG_OK = 0
+ERRORS = {1: "SCCG_E_INVALID", 2: "SCCG_E_HIP", 3: "SCCG_E_NOMEM", 4: "SCCG_E_DELTA_STOI",
+          5: "SCCG_E_FORMAT", 6: "SCCG_E_RANGE", 7: "SCCG_E_PARSE", 8: "SCCG_E_UNSUPPORTED",
+          9: "SCCG_E_INTERNAL"}
+
+
+class SccgError(RuntimeError):
+    def __init__(self, rc: int, msg: str = ""):
+        super().__init__(f"{ERRORS.get(rc, rc)}: {msg}")
+        self.rc = rc
+
+
+class Buf(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class Records(ctypes.Structure):
+    _fields_ = [("kind", ctypes.POINTER(ctypes.c_uint8)), ("pos", ctypes.POINTER(ctypes.c_int32)),
+                ("len", ctypes.POINTER(ctypes.c_int32)), ("t", ctypes.POINTER(ctypes.c_int64)),
+                ("n", ctypes.c_int64)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("mode_global", ctypes.c_int), ("switch_segment", ctypes.c_int64),
+                ("target_bases", ctypes.c_int64), ("reference_bases", ctypes.c_int64),
+                ("n_matches", ctypes.c_int64), ("literal_bases", ctypes.c_int64),
+                ("walk_rounds", ctypes.c_int64), ("walk_chunks", ctypes.c_int64),
+                ("record_bytes", ctypes.c_int64)]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+_lib = None
+
+
+def load_library():
+    """Load libsccg.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `make` or __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, sz, c, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int64
+    lib.sccg_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    lib.sccg_ctx_destroy.argtypes = [vp]
+    lib.sccg_last_error.argtypes = [vp]
+    lib.sccg_last_error.restype = ctypes.c_char_p
+    lib.sccg_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    lib.sccg_compress.argtypes = [vp, c, sz, c, sz, ctypes.POINTER(Buf)]
+    lib.sccg_compress_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
+    lib.sccg_compress_bound.argtypes = [sz, sz]
+    lib.sccg_compress_bound.restype = sz
+    lib.sccg_match.argtypes = [vp, c, sz, c, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64,
+                               ctypes.POINTER(Records)]
+    lib.sccg_records_free.argtypes = [ctypes.POINTER(Records)]
+    lib.sccg_reconstruct.argtypes = [vp, c, sz, c, sz, ctypes.POINTER(Buf)]
+    lib.sccg_reconstruct_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
+    lib.sccg_buf_free.argtypes = [ctypes.POINTER(Buf)]
+    _lib = lib
+    return lib
+
+
+def header_functions() -> list[str]:
+    """Every function the C ABI header declares."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|size_t|const char\*)\s+(sccg_\w+)\s*\(", text, re.M)))
+
+
+class Context:
+    """One GPU context (sccg_ctx).  Not re-entrant; one per device."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self.ptr = ctypes.c_void_p()
+        rc = self.lib.sccg_ctx_create(device, ctypes.byref(self.ptr))
+        if rc:
+            raise SccgError(rc, f"sccg_ctx_create(device={device}) failed: no usable GPU")
+
+    def close(self):
+        if self.ptr:
+            self.lib.sccg_ctx_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, rc: int):
+        raise SccgError(rc, self.lib.sccg_last_error(self.ptr).decode(errors="replace"))
+
+    def stats(self) -> dict:
+        st = Stats()
+        self.lib.sccg_last_stats(self.ptr, ctypes.byref(st))
+        return st.as_dict()
+
+    def _take(self, buf: Buf) -> bytes:
+        data = ctypes.string_at(buf.data, buf.len) if buf.data else b""
+        self.lib.sccg_buf_free(ctypes.byref(buf))
+        return data
+
+    def compress(self, ref_fa: bytes, tgt_fa: bytes) -> bytes:
+        """Bytes of compressed_genome.txt (compression.cpp:320-580, without 7z)."""
+        buf = Buf()
+        rc = self.lib.sccg_compress(self.ptr, ref_fa, len(ref_fa), tgt_fa, len(tgt_fa), ctypes.byref(buf))
+        if rc:
+            data = self._take(buf)
+            err = SccgError(rc, self.lib.sccg_last_error(self.ptr).decode(errors="replace"))
+            err.partial = data
+            raise err
+        return self._take(buf)
+
+    def reconstruct(self, record: bytes, ref_fa: bytes) -> bytes:
+        """Bytes of reconstructed_genome.fa (decompression.cpp after 7z)."""
+        buf = Buf()
+        rc = self.lib.sccg_reconstruct(self.ptr, ref_fa, len(ref_fa), record, len(record), ctypes.byref(buf))
+        if rc:
+            self._err(rc)
+        return self._take(buf)
+
+    def compress_device(self, d_ref: int, ref_len: int, d_tgt: int, tgt_len: int, d_out: int, out_cap: int,
+                        stream: int = 0) -> int:
+        """HBM-resident compress: device pointers in, record text written to d_out; returns length."""
+        n = ctypes.c_size_t()
+        rc = self.lib.sccg_compress_device(self.ptr, d_ref, ref_len, d_tgt, tgt_len, d_out, out_cap,
+                                           ctypes.byref(n), stream or None)
+        if rc:
+            self._err(rc)
+        return n.value
+
+    def reconstruct_device(self, d_ref: int, ref_len: int, d_rec: int, rec_len: int, d_out: int, out_cap: int,
+                           stream: int = 0) -> int:
+        n = ctypes.c_size_t()
+        rc = self.lib.sccg_reconstruct_device(self.ptr, d_ref, ref_len, d_rec, rec_len, d_out, out_cap,
+                                              ctypes.byref(n), stream or None)
+        if rc:
+            self._err(rc)
+        return n.value
+
+    def compress_bound(self, ref_len: int, tgt_len: int) -> int:
+        return self.lib.sccg_compress_bound(ref_len, tgt_len)
+
+    def match(self, sr: bytes, st: bytes, k: int, m: int, glob: bool, offset: int = 0):
+        """match_sequences (compression.cpp:36) -> [(kind, p, l, t)] like the oracle's records."""
+        recs = Records()
+        rc = self.lib.sccg_match(self.ptr, sr, len(sr), st, len(st), k, m, int(glob), offset, ctypes.byref(recs))
+        if rc:
+            self._err(rc)
+        out = [(recs.kind[i], recs.pos[i] if recs.kind[i] else 0, recs.len[i], recs.t[i]) for i in range(recs.n)]
+        self.lib.sccg_records_free(ctypes.byref(recs))
+        return out

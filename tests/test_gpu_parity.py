@@ -1,0 +1,140 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's fixtures and the oracle.
+
+* every golden fixture (outputs of the compiled reference) byte-for-byte, compression and
+  decompression, exit-code behaviour included;
+* the larger generator seeds against the reference's sha256 (synth_manifest.json);
+* seeded fuzz pairs against the CPU restatement (oracle/), local and global modes;
+* the match_sequences seam (compression.cpp:36) against the oracle's records;
+* full-size (chr1-shaped) round trip compress -> reconstruct == input FASTA.
+"""
+import hashlib
+import random
+
+import pytest
+
+import fuzzgen
+import goldens
+import oraclelib
+import synthlib
+from pkg import sccg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = sccg.Context(0)
+    yield c
+    c.close()
+
+
+def _gpu_compress(ctx, rfa, tfa):
+    try:
+        return ctx.compress(rfa, tfa), 0
+    except sccg.SccgError as e:
+        return getattr(e, "partial", None), 1
+
+
+def test_golden_compress(ctx, golden_cases):
+    bad = []
+    for c in golden_cases:
+        rec, rc = _gpu_compress(ctx, c["ref_fa"], c["tgt_fa"])
+        if rc != c["compress_rc"] or rec != c["record"]:
+            bad.append(c["name"])
+    assert not bad, bad
+
+
+def test_golden_reconstruct(ctx, golden_cases):
+    bad = []
+    for c in golden_cases:
+        if c["decompress_rc"] is None:
+            continue
+        try:
+            fa, rc = ctx.reconstruct(c["record"], c["ref_fa"]), 0
+        except sccg.SccgError:
+            fa, rc = None, 1
+        if rc != c["decompress_rc"] or (rc == 0 and fa != c["fasta"]):
+            bad.append(c["name"])
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("entry", goldens.synth_manifest(), ids=lambda e: f"{e['profile']}-{e['seed']}")
+def test_synth_manifest(ctx, entry):
+    rfa, tfa = synthlib.synth_pair(entry["profile"], entry["ref_len"], entry["tgt_len"], entry["seed"])
+    rec = ctx.compress(rfa, tfa)
+    assert len(rec) == entry["record_len"]
+    assert hashlib.sha256(rec).hexdigest() == entry["record_sha256"]
+    fa = ctx.reconstruct(rec, rfa)
+    assert hashlib.sha256(fa).hexdigest() == entry["fasta_sha256"]
+
+
+@pytest.mark.parametrize("kind,seed", [("local", s) for s in range(300, 340)] +
+                         [("global", s) for s in range(300, 330)])
+def test_fuzz_vs_oracle(ctx, kind, seed):
+    rfa, tfa = (fuzzgen.local_case if kind == "local" else fuzzgen.global_case)(seed)
+    want = oraclelib.compress(rfa, tfa)
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert rc == 0
+    assert got == want
+    assert ctx.reconstruct(got, rfa) == oraclelib.decompress(want, rfa)
+
+
+def _rand(rng, n, alpha="ACGT"):
+    return "".join(rng.choice(alpha) for _ in range(n)).encode()
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_match_seam_local(ctx, seed):
+    rng = random.Random(seed)
+    n = rng.choice([5, 13, 200, 999, 1000])
+    sr = _rand(rng, n, rng.choice(["ACGT", "AC", "ACGTN", "A"]))
+    st = bytearray(sr[: rng.randint(0, n)] + _rand(rng, rng.randint(0, 1000 - min(n, 1000)) // 2))
+    for i in range(len(st)):
+        if rng.random() < 0.02:
+            st[i] = ord(rng.choice("ACGTNR"))
+    st = bytes(st[:1000])
+    for k in (14, 10):
+        assert ctx.match(sr, st, k, 0, False, 1000 * seed) == oraclelib.match(sr, st, k, 0, False, 1000 * seed)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_match_seam_global(ctx, seed):
+    rng = random.Random(1000 + seed)
+    n = rng.randint(2000, 40000)
+    unit = _rand(rng, rng.randint(10, 200))
+    sr = b"".join(unit if rng.random() < 0.2 else _rand(rng, rng.randint(20, 400)) for _ in range(n // 150))
+    st = bytearray(sr)
+    for i in range(len(st)):
+        if rng.random() < 0.01:
+            st[i] = ord(rng.choice("ACGT"))
+    cut = rng.randint(0, len(st))
+    st = bytes(st[:cut]) + _rand(rng, rng.randint(0, 3000)) + bytes(st[cut + rng.choice([0, 50, 300]):])
+    assert ctx.match(sr, st, 14, 100, True) == oraclelib.match(sr, st, 14, 100, True)
+
+
+def test_synth_medium_vs_oracle(ctx):
+    rfa, tfa = synthlib.synth_pair("hg", 12_000_000, 12_030_000, 77)
+    want = oraclelib.compress(rfa, tfa)
+    assert ctx.compress(rfa, tfa) == want
+    assert ctx.stats()["mode_global"] == 1
+
+
+def test_t2t_vs_oracle(ctx):
+    rfa, tfa = synthlib.synth_pair("t2t", 3_000_000, 3_000_000, 78)
+    assert ctx.compress(rfa, tfa) == oraclelib.compress(rfa, tfa)
+
+
+def test_local_large_vs_oracle(ctx):
+    rfa, tfa = synthlib.synth_pair("local", 10_000_000, 10_000_000, 79)
+    assert ctx.compress(rfa, tfa) == oraclelib.compress(rfa, tfa)
+    assert ctx.stats()["mode_global"] == 0
+
+
+def test_chr1_roundtrip(ctx):
+    """Full BASELINE config size: compress then reconstruct must give back the input FASTA
+    (the generator writes 50-column LF FASTA with a header, so the round trip is byte-exact)."""
+    rfa, tfa = synthlib.synth_pair("hg", 247_249_719, 249_250_621, 1)
+    rec = ctx.compress(rfa, tfa)
+    st = ctx.stats()
+    assert st["mode_global"] == 1 and st["target_bases"] == 249_250_621
+    assert ctx.reconstruct(rec, rfa) == tfa
