@@ -311,7 +311,7 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
                    const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_tok_fill, dim3(grid_for(n, 64 * WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n, d_lp, d_off, d_dsum, d_dlt,
+    PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_fill, dim3(grid_for(n, 64 * WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n, d_lp, d_off, d_dsum, d_dlt,
                        d_contrib, d_R, d_dec);
     SCCG_HIP(hipGetLastError());
     return 0;
@@ -319,7 +319,7 @@ int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int
 
 int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, uint8_t* d_out, hipStream_t s) {
     if (nres <= 0) return 0;
-    hipLaunchKernelGGL(k_format, dim3(grid_for(nres, 256 * OUT_PER_T)), dim3(256), 0, s, d_dec, nres,
+    PROF_LAUNCH(PROF_DC_FORMAT, s, k_format, dim3(grid_for(nres, 256 * OUT_PER_T)), dim3(256), 0, s, d_dec, nres,
                        (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
                        (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, d_out);
     SCCG_HIP(hipGetLastError());

@@ -375,7 +375,7 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
                        sc.tile_a, sc.tile_b, sc.tile_last);
     hipLaunchKernelGGL(k_strip_scan, dim3(1), dim3(1024), 0, s, ntiles, sc.tile_a, sc.tile_b, sc.tile_last,
                        sc.tile_off, sc.tile_carry, d_len);
-    hipLaunchKernelGGL(k_strip_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, buf, n, d_header,
+    PROF_LAUNCH(PROF_STRIP, s, k_strip_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, buf, n, d_header,
                        sc.tile_off, sc.tile_carry, out, d_flags);
     SCCG_HIP(hipGetLastError());
     return 0;
@@ -391,7 +391,7 @@ int launch_filter(FilterMode mode, const uint8_t* in, int64_t n, uint8_t* out, i
     hipLaunchKernelGGL(k_filter_count, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, in, n, d_tile_cnt);
     int rc = dev_excl_sum(d_tile_cnt, d_tile_cnt, ntiles, d_len, d_partial, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_filter_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, in, n,
+    PROF_LAUNCH(PROF_FILTER, s, k_filter_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, in, n,
                        (const int64_t*)d_tile_cnt, out);
     SCCG_HIP(hipGetLastError());
     return 0;
@@ -407,7 +407,7 @@ int launch_runs(RunPred pred, const uint8_t* in, int64_t n, int32_t* rs, int32_t
     hipLaunchKernelGGL(k_runs_count, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, pred, in, n, d_tile_cnt);
     int rc = dev_excl_sum(d_tile_cnt, d_tile_cnt, ntiles, d_nruns, d_partial, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_runs_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, pred, in, n,
+    PROF_LAUNCH(PROF_RUNS, s, k_runs_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, pred, in, n,
                        (const int64_t*)d_tile_cnt, rs, re);
     SCCG_HIP(hipGetLastError());
     return 0;
@@ -423,7 +423,7 @@ int launch_run_text(const int32_t* rs, const int32_t* re, int64_t nruns, int64_t
     hipLaunchKernelGGL(k_run_textlen, dim3(g), dim3(256), 0, s, rs, re, nruns, n, d_tmp);
     int rc = dev_excl_sum(d_tmp, d_tmp, nruns, d_len, d_partial, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_run_textwrite, dim3(g), dim3(256), 0, s, rs, re, nruns, n, (const int64_t*)d_tmp, out);
+    PROF_LAUNCH(PROF_RUNTEXT, s, k_run_textwrite, dim3(g), dim3(256), 0, s, rs, re, nruns, n, (const int64_t*)d_tmp, out);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

@@ -4,6 +4,33 @@
 #include "common.h"
 #include "../../include/sccg.h"
 
+// ---- prof.cpp: per-kernel event timing (each id brackets exactly one kernel launch) -----------
+enum ProfId {
+    PROF_STRIP = 0,      // k_strip_write
+    PROF_RUNS,           // k_runs_write
+    PROF_RUNTEXT,        // k_run_textwrite
+    PROF_LOCAL14,        // k_local_pass<14>
+    PROF_LOCAL10,        // k_local_pass<10>
+    PROF_LOCAL_EMIT,     // k_seg_textwrite
+    PROF_FILTER,         // k_filter_write
+    PROF_ANCHOR,         // k_anchor_build
+    PROF_WALK,           // k_walk
+    PROF_PRESENCE,       // k_presence
+    PROF_FULLC,          // k_fullc
+    PROF_MATCH_EMIT,     // k_match_textwrite
+    PROF_DC_DECODE,      // k_tok_fill
+    PROF_DC_FORMAT,      // k_format
+    PROF_COUNT
+};
+void prof_begin(hipStream_t s, int id);
+void prof_end(hipStream_t s, int id);
+#define PROF_LAUNCH(id, strm, ...)        \
+    do {                                  \
+        prof_begin(strm, id);             \
+        hipLaunchKernelGGL(__VA_ARGS__);  \
+        prof_end(strm, id);               \
+    } while (0)
+
 // ---- scan.hip ---------------------------------------------------------------------------------
 #include <initializer_list>
 int dev_set_i64(int64_t* p, int n, std::initializer_list<int64_t> vals, hipStream_t s);

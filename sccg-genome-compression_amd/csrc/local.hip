@@ -390,9 +390,9 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
     if (iters <= 0) return 0;
     const unsigned g = grid_for(iters, WPB);
     if (k == 14)
-        hipLaunchKernelGGL(k_local_pass<14>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, iters, recs, stat);
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_pass<14>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, iters, recs, stat);
     else if (k == 10)
-        hipLaunchKernelGGL(k_local_pass<10>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, iters, recs, stat);
+        PROF_LAUNCH(PROF_LOCAL10, s, k_local_pass<10>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, iters, recs, stat);
     else
         return SCCG_E_UNSUPPORTED;
     SCCG_HIP(hipGetLastError());
@@ -433,7 +433,7 @@ int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_
                            (const int64_t*)d_tmp_a, d_tmp_b);
         rc = dev_excl_sum(d_tmp_b, d_tmp_b, iters, d_len, d_partial, s);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_seg_textwrite, dim3(grid_for(iters, WPB)), dim3(SCCG_BLOCK), 0, s, stat, iters, recs,
+        PROF_LAUNCH(PROF_LOCAL_EMIT, s, k_seg_textwrite, dim3(grid_for(iters, WPB)), dim3(SCCG_BLOCK), 0, s, stat, iters, recs,
                            (const int64_t*)d_tmp_a, (const int64_t*)d_tmp_b, T, out);
         SCCG_HIP(hipGetLastError());
     } else {

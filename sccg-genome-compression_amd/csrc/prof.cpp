@@ -1,0 +1,118 @@
+// prof.cpp -- optional per-kernel HIP-event timing (sccg_profile / sccg_profile_get).
+//
+// When enabled, the launchers bracket their hot kernels with a pair of events recorded on the
+// stream the kernel runs on, so the measured duration is that launch's device time and agrees
+// with rocprofv3 --kernel-trace for the same kernel.  Disabled (the default) it costs one branch.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+namespace {
+
+struct Pending {
+    int id;
+    hipEvent_t a, b;
+};
+
+struct Registry {
+    std::mutex mu;
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    std::vector<Pending> pending;
+    double ms[PROF_COUNT] = {};
+    int64_t n[PROF_COUNT] = {};
+    hipEvent_t open[PROF_COUNT] = {};
+
+    hipEvent_t take() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void drain() {   // fold completed pairs into the totals
+        for (auto& p : pending) {
+            (void)hipEventSynchronize(p.b);
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) {
+                ms[p.id] += t;
+                n[p.id] += 1;
+            }
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+
+Registry& reg() {
+    static Registry r;
+    return r;
+}
+
+const char* const NAMES[PROF_COUNT] = {
+    "fasta_strip", "run_extract", "run_text", "local_pass_k14", "local_pass_k10", "local_emit", "n_filter",
+    "anchor_build", "walk", "presence_scan", "fullc_scan", "match_emit",
+    "dc_decode", "dc_format",
+};
+
+}  // namespace
+
+void prof_begin(hipStream_t s, int id) {
+    Registry& r = reg();
+    if (!r.on) return;
+    std::lock_guard<std::mutex> g(r.mu);
+    hipEvent_t e = r.take();
+    (void)hipEventRecord(e, s);
+    r.open[id] = e;
+}
+
+void prof_end(hipStream_t s, int id) {
+    Registry& r = reg();
+    if (!r.on) return;
+    std::lock_guard<std::mutex> g(r.mu);
+    if (!r.open[id]) return;
+    hipEvent_t e = r.take();
+    (void)hipEventRecord(e, s);
+    r.pending.push_back({id, r.open[id], e});
+    r.open[id] = nullptr;
+    if (r.pending.size() > 4096) r.drain();
+}
+
+extern "C" {
+
+int sccg_profile(sccg_ctx* /*ctx*/, int enable) {
+    Registry& r = reg();
+    std::lock_guard<std::mutex> g(r.mu);
+    r.drain();
+    r.on = enable != 0;
+    for (int i = 0; i < PROF_COUNT; i++) { r.ms[i] = 0; r.n[i] = 0; r.open[i] = nullptr; }
+    return SCCG_OK;
+}
+
+int sccg_profile_get(sccg_ctx* /*ctx*/, const char* kernel, double* total_ms, int64_t* launches) {
+    if (!kernel || !total_ms || !launches) return SCCG_E_INVALID;
+    Registry& r = reg();
+    std::lock_guard<std::mutex> g(r.mu);
+    r.drain();
+    for (int i = 0; i < PROF_COUNT; i++) {
+        if (!strcmp(NAMES[i], kernel)) {
+            *total_ms = r.ms[i];
+            *launches = r.n[i];
+            return SCCG_OK;
+        }
+    }
+    return SCCG_E_INVALID;
+}
+
+const char* sccg_profile_name(int i) { return (i >= 0 && i < PROF_COUNT) ? NAMES[i] : nullptr; }
+
+}  // extern "C"

@@ -661,8 +661,8 @@ int run_fullc(WalkPtrs& A, int32_t y, int32_t P, FullC* out, hipStream_t s) {
     const int64_t npos = (int64_t)A.nR - A.k + 1;
     unsigned g = grid_for(npos > 0 ? npos : 1, 256 * FC_PER_T);
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(k_fullc, dim3(g), dim3(256), 0, s, A, y, P, 0);
-    hipLaunchKernelGGL(k_fullc, dim3(g), dim3(256), 0, s, A, y, P, 1);
+    PROF_LAUNCH(PROF_FULLC, s, k_fullc, dim3(g), dim3(256), 0, s, A, y, P, 0);
+    PROF_LAUNCH(PROF_FULLC, s, k_fullc, dim3(g), dim3(256), 0, s, A, y, P, 1);
     SCCG_HIP(hipGetLastError());
     unsigned long long r[4];
     SCCG_HIP(hipMemcpyAsync(r, A.fc, sizeof r, hipMemcpyDeviceToHost, s));
@@ -728,7 +728,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             const int64_t npos = nRp - k + 1;
             unsigned g = grid_for(npos, 256 * FC_PER_T);
             if (g > 4096) g = 4096;
-            hipLaunchKernelGGL(k_presence, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, nb);
+            PROF_LAUNCH(PROF_PRESENCE, s, k_presence, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, nb);
             SCCG_HIP(hipGetLastError());
             unsigned long long r[2];
             SCCG_HIP(hipMemcpyAsync(r, A.fc + 4, sizeof r, hipMemcpyDeviceToHost, s));
@@ -771,7 +771,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         hipLaunchKernelGGL(k_anchor_clear, dim3(grid_for(slots, 256) > 8192 ? 8192 : grid_for(slots, 256)), dim3(256), 0,
                            s, A.akeys, A.apos, slots);
         const int64_t ns = nRp / ANCHOR_STEP + 1;
-        hipLaunchKernelGGL(k_anchor_build, dim3(grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256)), dim3(256), 0, s, A);
+        PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build, dim3(grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256)), dim3(256), 0, s, A);
         hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
         SCCG_HIP(hipGetLastError());
         // round 1: chunk 0 exact (as a fix-up with an empty trajectory), chunks >= 1 speculative
@@ -786,7 +786,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         RC(dev_set_i32(A.snapP, 1, {startP}, s));
         int32_t nlist = A.C;
         for (int64_t round = 1;; round++) {
-            hipLaunchKernelGGL(k_walk, dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
+            PROF_LAUNCH(PROF_WALK, s, k_walk, dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
             SCCG_HIP(hipGetLastError());
             res->rounds = round;
             // resolve escalations of exact walks (pn2 == 0 -> ungated pn1/ln1), then resume them
@@ -821,7 +821,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 }
                 RC(dev_set_i32(A.scal + 1, 1, {0}, s));
                 RC(h2d_sync(A.plist, rl.data(), rl.size() * 4, s));
-                hipLaunchKernelGGL(k_walk, dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
+                PROF_LAUNCH(PROF_WALK, s, k_walk, dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
                                    (const int32_t*)A.plist, (int32_t)rl.size());
                 SCCG_HIP(hipGetLastError());
             }
@@ -862,7 +862,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         const unsigned g = grid_for(nm, 256) > 4096 ? 4096 : grid_for(nm, 256);
         hipLaunchKernelGGL(k_match_textlen, dim3(g), dim3(256), 0, s, A, nm);
         RC(dev_excl_sum(A.tlen, A.tlen, nm, A.scal64 + 1, A.partial, s));
-        hipLaunchKernelGGL(k_match_textwrite, dim3(grid_for(nm, WPB)), dim3(SCCG_BLOCK), 0, s, A, nm, out);
+        PROF_LAUNCH(PROF_MATCH_EMIT, s, k_match_textwrite, dim3(grid_for(nm, WPB)), dim3(SCCG_BLOCK), 0, s, A, nm, out);
         SCCG_HIP(hipGetLastError());
         int32_t lt[2];
         SCCG_HIP(hipMemcpyAsync(&text, A.scal64 + 1, sizeof text, hipMemcpyDeviceToHost, s));

@@ -75,6 +75,10 @@ def load_library():
     lib.sccg_reconstruct.argtypes = [vp, c, sz, c, sz, ctypes.POINTER(Buf)]
     lib.sccg_reconstruct_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
     lib.sccg_buf_free.argtypes = [ctypes.POINTER(Buf)]
+    lib.sccg_profile.argtypes = [vp, ctypes.c_int]
+    lib.sccg_profile_get.argtypes = [vp, c, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
+    lib.sccg_profile_name.argtypes = [ctypes.c_int]
+    lib.sccg_profile_name.restype = ctypes.c_char_p
     _lib = lib
     return lib
 
@@ -162,6 +166,23 @@ class Context:
         if rc:
             self._err(rc)
         return n.value
+
+    def profile(self, enable: bool = True) -> None:
+        """Reset and enable (or disable) per-kernel HIP-event timing."""
+        self.lib.sccg_profile(self.ptr, int(enable))
+
+    def profile_get(self) -> dict:
+        """{kernel family: (total_ms, launches)} since the last profile() call."""
+        out, i = {}, 0
+        while True:
+            name = self.lib.sccg_profile_name(i)
+            if not name:
+                return out
+            ms, n = ctypes.c_double(), ctypes.c_int64()
+            self.lib.sccg_profile_get(self.ptr, name, ctypes.byref(ms), ctypes.byref(n))
+            if n.value:
+                out[name.decode()] = (ms.value, n.value)
+            i += 1
 
     def compress_bound(self, ref_len: int, tgt_len: int) -> int:
         return self.lib.sccg_compress_bound(ref_len, tgt_len)
