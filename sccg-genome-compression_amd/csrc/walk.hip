@@ -19,6 +19,8 @@
 // The first step (P == -1, ungated) and the p2 == 0 escalations run as exact grid-wide scans.
 #include "internal.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -59,8 +61,14 @@ struct WalkPtrs {
     int32_t* snapX;
     int32_t* snapP;
     int32_t* guess;
-    int32_t* plist;
-    int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP
+    int32_t* plist;       // chunks walked in the current round
+    int32_t* rlist;       // chunks resumed after an escalation
+    int32_t* newX;        // staged fix-up results (k_commit)
+    int32_t* newP;
+    int32_t* conv;
+    int32_t* changed;
+    int32_t* walked;      // round in which the chunk was last re-walked
+    int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round
     uint64_t* akeys;
     uint32_t* apos;
     int32_t abits;
@@ -204,13 +212,12 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
         x = lo_j;
         P = A.guess[j];
         if (lane == 0) { A.usedX[j] = lo_j; A.usedP[j] = P; }
-    } else if (kind == KIND_FIX) {
+    } else if (kind == KIND_FIX) {   // result is committed (or discarded) by k_commit
         cb = A.cur[j];
         ob = 1 - cb;
         cc = A.cnt[cb][j];
         x = A.snapX[j];
         P = A.snapP[j];
-        if (lane == 0) { A.usedX[j] = x; A.usedP[j] = P; }
     } else {   // resume after an escalation was resolved on the host
         cb = A.cur[j];
         ob = 1 - cb;
@@ -329,8 +336,37 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
     if (escalated) return;
     if (lane == 0) {
         A.cnt[ob][j] = n;
-        if (!converged) { A.exitX[j] = x; A.exitP[j] = P; }
-        if (cb >= 0) A.cur[j] = ob;
+        if (cb < 0) {   // speculative: the trajectory is the chunk's first, take it as is
+            A.exitX[j] = x; A.exitP[j] = P;
+        } else {        // fix-up: staged; k_commit decides
+            const int32_t nx = converged ? A.exitX[j] : x, np = converged ? A.exitP[j] : P;
+            A.newX[j] = nx; A.newP[j] = np;
+            A.conv[j] = converged;
+            A.changed[j] = nx != A.exitX[j] || np != A.exitP[j];
+            A.walked[j] = A.scal[4];
+        }
+        A.status[j] = converged ? 3 : 4;   // diagnostics only (SCCG_DEBUG)
+    }
+}
+
+// Commit the fix-ups of a round.  A re-walk that converged is always taken.  One that did not is
+// taken only if its predecessor's exit did not change in this round: otherwise its entry was a
+// stale (possibly garbage) state and adopting it would push that garbage one chunk further every
+// round.  Discarded chunks stay pending and are re-walked from the corrected entry.  Exactness
+// never depends on this choice -- the loop only ends when every chunk's trajectory was walked from
+// its predecessor's final exit.
+__global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
+    for (int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); i < nlist; i += (int32_t)(gridDim.x * blockDim.x)) {
+        const int32_t j = list[i];
+        if (A.kind[j] == KIND_SPEC || A.status[j] == ST_ESC) continue;
+        const int32_t round = A.scal[4];
+        const bool pred_changed = j > 0 && A.walked[j - 1] == round && A.changed[j - 1];
+        if (!(A.conv[j] || !pred_changed)) continue;
+        A.cur[j] = 1 - A.cur[j];
+        A.exitX[j] = A.newX[j];
+        A.exitP[j] = A.newP[j];
+        A.usedX[j] = A.snapX[j];
+        A.usedP[j] = A.snapP[j];
     }
 }
 
@@ -400,10 +436,13 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
     if (j >= A.C) return;
     const int lane = lane_id();
     const uint64_t smask = (1ull << A.abits) - 1;
-    int32_t g = INVALID;
-    for (int b = 0; b < 4 && g == INVALID; b++) {
+    // probe 256 target positions; each hit on a sampled reference 32-mer votes for a diagonal
+    constexpr int NB = 4;
+    int32_t dg[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
         const int32_t y = j * A.S + b * 64 + lane;
-        int32_t diag = INVALID;
+        dg[b] = INVALID;
         uint64_t code;
         if (y + ANCHOR_K <= A.nT && code32(A.T + y, code)) {
             const uint64_t key = mix64(code);
@@ -413,21 +452,38 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
                 if (kk == A_EMPTY) break;
                 if (kk == key) {
                     const uint32_t ps = A.apos[slot];
-                    if (ps < A_UNSET) diag = (int32_t)ps - y;
+                    if (ps < A_UNSET) dg[b] = (int32_t)ps - y;
                     break;
                 }
                 slot = (slot + 1) & smask;
             }
         }
-        const unsigned long long m = __ballot(diag != INVALID);
-        if (m) {
-            const int l = first_lane(m);
-            const int32_t d = __shfl(diag, l, 64);
-            int64_t gp = (int64_t)j * A.S - 1 + d;
-            if (gp < 0) gp = 0;
-            if (gp > A.nR - 1) gp = A.nR - 1;
-            g = (int32_t)gp;
+    }
+    // earliest diagonal with >= 2 votes (a lone hit is often a repeat copy); else the earliest
+    int32_t g = INVALID, first = INVALID;
+    for (int tries = 0; tries < 8 && g == INVALID; tries++) {
+        int32_t d = INVALID;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const unsigned long long m = __ballot(dg[b] != INVALID);
+            if (m && d == INVALID) d = __shfl(dg[b], first_lane(m), 64);
         }
+        if (d == INVALID) break;
+        if (first == INVALID) first = d;
+        int votes = 0;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            votes += __popcll(__ballot(dg[b] == d));
+            if (dg[b] == d) dg[b] = INVALID;
+        }
+        if (votes >= 2) g = d;
+    }
+    if (g == INVALID) g = first;
+    if (g != INVALID) {
+        int64_t gp = (int64_t)j * A.S - 1 + g;
+        if (gp < 0) gp = 0;
+        if (gp > A.nR - 1) gp = A.nR - 1;
+        g = (int32_t)gp;
     }
     if (lane == 0) A.guess[j] = g;
 }
@@ -629,6 +685,9 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.snapX = c.take<int32_t>(C); A.snapP = c.take<int32_t>(C);
     A.guess = c.take<int32_t>(C);
     A.plist = c.take<int32_t>(C);
+    A.rlist = c.take<int32_t>(C);
+    A.newX = c.take<int32_t>(C); A.newP = c.take<int32_t>(C);
+    A.conv = c.take<int32_t>(C); A.changed = c.take<int32_t>(C); A.walked = c.take<int32_t>(C);
     A.scal = c.take<int32_t>(16);
     A.abits = anchor_bits(nR);
     A.akeys = c.take<uint64_t>((size_t)1 << A.abits);
@@ -683,6 +742,49 @@ int h2d_sync(void* dst, const void* src, size_t bytes, hipStream_t s) {
     SCCG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     SCCG_HIP(hipStreamSynchronize(s));
     return 0;
+}
+
+// Exact walks that hit the pn2 == 0 sentinel stop with status ST_ESC; the reference then takes the
+// ungated (pn1, ln1) over ALL candidates (compression.cpp:124-138): resolve each with the full
+// scan, append that match, and resume the walk behind it.  Rare: needs P <= m.
+int resolve_escalations(WalkPtrs& A, hipStream_t s) {
+    const size_t C = (size_t)A.C;
+    for (;;) {
+        int32_t nesc = 0;
+        SCCG_HIP(hipMemcpyAsync(&nesc, A.scal + 1, sizeof nesc, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipStreamSynchronize(s));
+        if (!nesc) return 0;
+        std::vector<int32_t> st(C), ex(C), ep(C), en(C), cur(C);
+        SCCG_HIP(hipMemcpyAsync(st.data(), A.status, C * 4, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipMemcpyAsync(ex.data(), A.escX, C * 4, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipMemcpyAsync(ep.data(), A.escP, C * 4, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipMemcpyAsync(en.data(), A.escN, C * 4, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipMemcpyAsync(cur.data(), A.cur, C * 4, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipStreamSynchronize(s));
+        std::vector<int32_t> rl;
+        for (size_t j = 0; j < C; j++) {
+            if (st[j] != ST_ESC) continue;
+            FullC f;
+            int rc = run_fullc(A, ex[j], ep[j], &f, s);
+            if (rc) return rc;
+            if (f.lmax <= 0) return SCCG_E_INTERNAL;   // a window candidate exists, so C is non-empty
+            const int32_t ob = 1 - cur[j];
+            const size_t at = j * (size_t)A.cap + (size_t)en[j];
+            if ((rc = dev_set_i32(A.bt[ob] + at, 1, {ex[j]}, s)) || (rc = dev_set_i32(A.bp[ob] + at, 1, {f.p}, s)) ||
+                (rc = dev_set_i32(A.bl[ob] + at, 1, {(int32_t)f.lmax}, s)) ||
+                (rc = dev_set_i32(A.escX + j, 1, {ex[j] + (int32_t)f.lmax}, s)) ||
+                (rc = dev_set_i32(A.escP + j, 1, {f.p + (int32_t)f.lmax - 1}, s)) ||
+                (rc = dev_set_i32(A.escN + j, 1, {en[j] + 1}, s)) || (rc = dev_set_i32(A.kind + j, 1, {KIND_RESUME}, s)))
+                return rc;
+            rl.push_back((int32_t)j);
+        }
+        int rc = dev_set_i32(A.scal + 1, 1, {0}, s);
+        if (rc) return rc;
+        if ((rc = h2d_sync(A.rlist, rl.data(), rl.size() * 4, s))) return rc;
+        PROF_LAUNCH(PROF_WALK, s, k_walk, dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
+                    (const int32_t*)A.rlist, (int32_t)rl.size());
+        SCCG_HIP(hipGetLastError());
+    }
 }
 
 }  // namespace
@@ -785,45 +887,54 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         RC(dev_set_i32(A.snapX, 1, {startX}, s));
         RC(dev_set_i32(A.snapP, 1, {startP}, s));
         int32_t nlist = A.C;
+        const bool dbg = getenv("SCCG_DEBUG") != nullptr;
         for (int64_t round = 1;; round++) {
+            RC(dev_set_i32(A.scal + 4, 1, {(int32_t)round}, s));
             PROF_LAUNCH(PROF_WALK, s, k_walk, dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
             SCCG_HIP(hipGetLastError());
             res->rounds = round;
-            // resolve escalations of exact walks (pn2 == 0 -> ungated pn1/ln1), then resume them
-            for (;;) {
-                int32_t nesc = 0;
-                SCCG_HIP(hipMemcpyAsync(&nesc, A.scal + 1, sizeof nesc, hipMemcpyDeviceToHost, s));
-                SCCG_HIP(hipStreamSynchronize(s));
-                if (!nesc) break;
-                std::vector<int32_t> st(C), ex(C), ep(C), en(C), cur(C);
-                SCCG_HIP(hipMemcpyAsync(st.data(), A.status, C * 4, hipMemcpyDeviceToHost, s));
-                SCCG_HIP(hipMemcpyAsync(ex.data(), A.escX, C * 4, hipMemcpyDeviceToHost, s));
-                SCCG_HIP(hipMemcpyAsync(ep.data(), A.escP, C * 4, hipMemcpyDeviceToHost, s));
-                SCCG_HIP(hipMemcpyAsync(en.data(), A.escN, C * 4, hipMemcpyDeviceToHost, s));
+            RC(resolve_escalations(A, s));
+            hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
+                               (const int32_t*)A.plist, nlist);
+            SCCG_HIP(hipGetLastError());
+            if (dbg && (round <= 6 || round % 1000 == 0)) {
+                std::vector<int32_t> g(C), ex(C), ep(C), ux(C), up(C), cur(C), c0(C), c1(C);
+                SCCG_HIP(hipMemcpyAsync(g.data(), A.guess, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(ex.data(), A.exitX, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(ep.data(), A.exitP, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(ux.data(), A.usedX, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(up.data(), A.usedP, C * 4, hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipMemcpyAsync(cur.data(), A.cur, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(c0.data(), A.cnt[0], C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipMemcpyAsync(c1.data(), A.cnt[1], C * 4, hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipStreamSynchronize(s));
-                std::vector<int32_t> rl;
+                size_t ginv = 0, einv = 0, settled = 0;
                 for (size_t j = 0; j < C; j++) {
-                    if (st[j] != ST_ESC) continue;
-                    FullC f;
-                    RC(run_fullc(A, ex[j], ep[j], &f, s));
-                    if (f.lmax <= 0) return SCCG_E_INTERNAL;   // a window candidate exists, so C is non-empty
-                    const int32_t ob = 1 - cur[j];
-                    const size_t at = j * (size_t)A.cap + (size_t)en[j];
-                    RC(dev_set_i32(A.bt[ob] + at, 1, {ex[j]}, s));
-                    RC(dev_set_i32(A.bp[ob] + at, 1, {f.p}, s));
-                    RC(dev_set_i32(A.bl[ob] + at, 1, {(int32_t)f.lmax}, s));
-                    RC(dev_set_i32(A.escX + j, 1, {ex[j] + (int32_t)f.lmax}, s));
-                    RC(dev_set_i32(A.escP + j, 1, {f.p + (int32_t)f.lmax - 1}, s));
-                    RC(dev_set_i32(A.escN + j, 1, {en[j] + 1}, s));
-                    RC(dev_set_i32(A.kind + j, 1, {KIND_RESUME}, s));
-                    rl.push_back((int32_t)j);
+                    ginv += g[j] == INVALID;
+                    einv += ex[j] == INVALID;
+                    const int32_t px = j ? ex[j - 1] : startX, pp = j ? ep[j - 1] : startP;
+                    settled += (px == ux[j] && pp == up[j]);
                 }
-                RC(dev_set_i32(A.scal + 1, 1, {0}, s));
-                RC(h2d_sync(A.plist, rl.data(), rl.size() * 4, s));
-                PROF_LAUNCH(PROF_WALK, s, k_walk, dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
-                                   (const int32_t*)A.plist, (int32_t)rl.size());
-                SCCG_HIP(hipGetLastError());
+                fprintf(stderr, "[walk] round %lld launched %d: guess INVALID %zu, exit INVALID %zu, settled %zu/%zu\n",
+                        (long long)round, nlist, ginv, einv, settled, C);
+                std::vector<int32_t> stt(C);
+                SCCG_HIP(hipMemcpyAsync(stt.data(), A.status, C * 4, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipStreamSynchronize(s));
+                int shown = 0;
+                for (size_t j = 1; j < C && shown < 6; j++) {
+                    if (ex[j - 1] == ux[j] && ep[j - 1] == up[j]) continue;
+                    shown++;
+                    fprintf(stderr, "  unsettled %zu lo=%d guess=%d used=(%d,%d) pred_exit=(%d,%d) exit=(%d,%d) st=%d cur=%d cnt=%d/%d\n",
+                            j, (int)(j * A.S), g[j], ux[j], up[j], ex[j - 1], ep[j - 1], ex[j], ep[j], stt[j], cur[j], c0[j], c1[j]);
+                    const int32_t b = cur[j];
+                    const int32_t nshow = (b ? c1[j] : c0[j]) < 4 ? (b ? c1[j] : c0[j]) : 4;
+                    std::vector<int32_t> tt(4), pp(4), ll(4);
+                    SCCG_HIP(hipMemcpyAsync(tt.data(), A.bt[b] + j * A.cap, 16, hipMemcpyDeviceToHost, s));
+                    SCCG_HIP(hipMemcpyAsync(pp.data(), A.bp[b] + j * A.cap, 16, hipMemcpyDeviceToHost, s));
+                    SCCG_HIP(hipMemcpyAsync(ll.data(), A.bl[b] + j * A.cap, 16, hipMemcpyDeviceToHost, s));
+                    SCCG_HIP(hipStreamSynchronize(s));
+                    for (int q = 0; q < nshow; q++) fprintf(stderr, "      m%d (%d,%d,%d)\n", q, tt[q], pp[q], ll[q]);
+                }
             }
             // which chunks were walked from a state that is not their true entry?
             RC(dev_set_i32(A.scal, 1, {0}, s));
