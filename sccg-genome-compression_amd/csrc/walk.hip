@@ -19,6 +19,8 @@
 // The first step (P == -1, ungated) and the p2 == 0 escalations run as exact grid-wide scans.
 #include "internal.h"
 
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -35,6 +37,7 @@ constexpr int ANCHOR_K = 32;
 constexpr int ANCHOR_STEP = 16;
 constexpr uint64_t A_EMPTY = ~0ull;
 constexpr uint32_t A_UNSET = 0xFFFFFFFEu, A_MULTI = 0xFFFFFFFFu;
+constexpr int32_t FROZEN_MIN = 4096;   // literal bases at a chunk end that trigger a frozen-P scan
 
 enum ChunkKind : int32_t { KIND_SPEC = 0, KIND_FIX = 1, KIND_RESUME = 2 };
 enum ChunkStatus : int32_t { ST_OK = 0, ST_ESC = 1 };
@@ -68,7 +71,10 @@ struct WalkPtrs {
     int32_t* conv;
     int32_t* changed;
     int32_t* walked;      // round in which the chunk was last re-walked
-    int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round
+    int32_t* frozen;      // fix-up ended in a long literal run at the chunk end
+    int32_t* flist;       // committed frozen chunks of the round
+    int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round,
+                          // [5] frozen count, [6] frozen-scan first hit
     uint64_t* akeys;
     uint32_t* apos;
     int32_t abits;
@@ -190,6 +196,56 @@ __device__ __forceinline__ bool window_has(const WalkPtrs& A, const WalkLds& L, 
     return false;
 }
 
+__device__ __forceinline__ bool window_has_key(const WalkLds& L, uint32_t key) {
+    int slot = (int)slot_hash(key, WTBITS);
+    for (int probes = 0; probes < WTSLOTS; probes++) {
+        const uint32_t v = wt_get(L.wtab, slot);
+        if (!v) return false;
+        if (L.wkeys[v - 1] == key) return true;
+        slot = (slot + 1) & (WTSLOTS - 1);
+    }
+    return false;
+}
+
+// Wide literal scan: first position in [x, end) whose k-mer key occurs in the window (1024
+// positions per wave step: 16 consecutive per lane, rolling 2-bit codes).  Key equality is a
+// superset of byte equality, so every position skipped is certainly a literal step; a returned
+// position is re-checked exactly by the caller.  Returns `end` when there is none.
+constexpr int WIDE = 16;
+__device__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, int32_t x, int32_t end) {
+    const int lane = lane_id(), k = A.k;
+    const uint32_t MASK = (1u << (2 * k)) - 1u;
+    for (int32_t base = x; base < end; base += 64 * WIDE) {
+        const int32_t p0 = base + WIDE * lane;
+        uint32_t w[8];
+        load16u(A.T + p0, *reinterpret_cast<uint32_t(*)[4]>(&w[0]));
+        load16u(A.T + p0 + 16, *reinterpret_cast<uint32_t(*)[4]>(&w[4]));
+        int32_t first = INT32_MAX;
+        uint32_t code = 0;
+        int lastbad = -1000;
+#pragma unroll
+        for (int i = 0; i < WIDE + 15; i++) {
+            const uint8_t c = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+            uint32_t b = base2(c);
+            if (b > 3) { lastbad = i; b = 0; }
+            code = ((code << 2) | b) & MASK;
+            const int st = i - (k - 1);
+            if (st >= 0 && st < WIDE && first == INT32_MAX && p0 + st < end) {
+                uint32_t key = code;
+                if (lastbad >= st) {   // non-ACGT byte inside: hash the k bytes (rare)
+                    uint32_t h = 2166136261u;
+                    for (int q = 0; q < k; q++) { h ^= (uint8_t)(w[(st + q) >> 2] >> (8 * ((st + q) & 3))); h *= 16777619u; }
+                    key = KEY_EXOTIC | (h & 0x7fffffffu);
+                }
+                if (window_has_key(L, key)) first = p0 + st;
+            }
+        }
+        const int32_t m = wave_min(first);
+        if (m != INT32_MAX) return m;
+    }
+    return end;
+}
+
 // ---------------------------------------------------------------------------------------------
 // the chunk walk (one wave per chunk)
 // ---------------------------------------------------------------------------------------------
@@ -240,6 +296,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
     const int32_t* cl = cb >= 0 ? A.bl[cb] + (size_t)j * A.cap : nullptr;
 
     int32_t wlo = 0, nwin = 0, wP = INVALID;
+    int32_t lme = x;   // target index after the last match of this walk (start of the open literal run)
     bool converged = false, escalated = false;
     const int32_t scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
     while (x < scan_end) {
@@ -258,6 +315,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
         const unsigned long long hm = __ballot(hit);
         if (!hm) {
             x = (x + 64 < scan_end) ? x + 64 : scan_end;
+            if (x < scan_end) x = wide_scan(A, L, x, scan_end);
             wave_sync();
             continue;
         }
@@ -329,6 +387,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
                 break;
             }
         }
+        lme = y + bl;
         P = p + bl - 1;   // compression.cpp:149
         x = y + bl;       // compression.cpp:159
         wave_sync();
@@ -344,6 +403,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
             A.conv[j] = converged;
             A.changed[j] = nx != A.exitX[j] || np != A.exitP[j];
             A.walked[j] = A.scal[4];
+            // ended in a long literal run with P frozen at the chunk end: k_frozen_scan territory
+            A.frozen[j] = !converged && x == hi_j && x - lme >= FROZEN_MIN;
         }
         A.status[j] = converged ? 3 : 4;   // diagnostics only (SCCG_DEBUG)
     }
@@ -367,6 +428,45 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
         A.exitP[j] = A.newP[j];
         A.usedX[j] = A.snapX[j];
         A.usedP[j] = A.snapP[j];
+        if (A.frozen[j]) A.flist[atomicAdd(&A.scal[5], 1)] = j;
+    }
+}
+
+// First position in [x0, lastk] whose k-mer key occurs in the window of P, over the whole rest of
+// the target (every wave builds its own copy of the window, then scans a strided share).
+__global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int32_t x0, int32_t P) {
+    __shared__ WalkLds lds_all[WPB];
+    WalkLds& L = lds_all[wave_in_block()];
+    int32_t wlo, nwin;
+    build_window(A, L, P, wlo, nwin);
+    if (nwin <= 0) return;
+    const int32_t end = A.nT - A.k + 1;
+    const int64_t gw = (int64_t)blockIdx.x * WPB + wave_in_block(), G = (int64_t)gridDim.x * WPB;
+    for (int64_t base = x0 + gw * 64 * WIDE; base < end; base += G * 64 * WIDE) {
+        if (base >= (int64_t)__hip_atomic_load(&A.scal[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        const int32_t seg_end = base + 64 * WIDE < end ? (int32_t)(base + 64 * WIDE) : end;
+        const int32_t y = wide_scan(A, L, (int32_t)base, seg_end);
+        if (y < seg_end) {
+            if (lane_id() == 0) atomicMin(&A.scal[6], y);
+            return;
+        }
+    }
+}
+
+// Chunks wholly before the first window hit y after a frozen exit (x0, P) are literal-only: their
+// entry is (min(lo, lastk+1), P), their trajectory empty, their exit (min(hi, lastk+1), P).
+__global__ void k_fill_literal(WalkPtrs A, int32_t j0, int32_t P) {
+    const int32_t y = A.scal[6], lastk1 = A.nT - A.k + 1;
+    for (int32_t j = j0 + (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
+        const int32_t lo = j * A.S, hi = lo + A.S < A.nT ? lo + A.S : A.nT;
+        const int32_t ex = hi < lastk1 ? hi : lastk1;
+        if (ex > y) return;   // chunks are ordered: all later ones reach y too
+        A.cnt[A.cur[j]][j] = 0;
+        A.usedX[j] = lo < lastk1 ? lo : lastk1;
+        A.usedP[j] = P;
+        A.exitX[j] = ex;
+        A.exitP[j] = P;
+        A.changed[j] = 0;
     }
 }
 
@@ -688,6 +788,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.rlist = c.take<int32_t>(C);
     A.newX = c.take<int32_t>(C); A.newP = c.take<int32_t>(C);
     A.conv = c.take<int32_t>(C); A.changed = c.take<int32_t>(C); A.walked = c.take<int32_t>(C);
+    A.frozen = c.take<int32_t>(C); A.flist = c.take<int32_t>(C);
     A.scal = c.take<int32_t>(16);
     A.abits = anchor_bits(nR);
     A.akeys = c.take<uint64_t>((size_t)1 << A.abits);
@@ -785,6 +886,49 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s) {
                     (const int32_t*)A.rlist, (int32_t)rl.size());
         SCCG_HIP(hipGetLastError());
     }
+}
+
+// For every committed fix-up that ended frozen (P unchanged over a long literal run up to its chunk
+// end): one grid-wide scan finds the next window hit after it, and every chunk before that hit is
+// settled as literal-only at once (instead of one chunk per round).
+int frozen_fill(WalkPtrs& A, hipStream_t s) {
+    int32_t nf = 0;
+    SCCG_HIP(hipMemcpyAsync(&nf, A.scal + 5, sizeof nf, hipMemcpyDeviceToHost, s));
+    SCCG_HIP(hipStreamSynchronize(s));
+    if (!nf) return 0;
+    std::vector<int32_t> fl((size_t)nf), ex((size_t)A.C), ep((size_t)A.C);
+    SCCG_HIP(hipMemcpyAsync(fl.data(), A.flist, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
+    SCCG_HIP(hipMemcpyAsync(ex.data(), A.exitX, (size_t)A.C * 4, hipMemcpyDeviceToHost, s));
+    SCCG_HIP(hipMemcpyAsync(ep.data(), A.exitP, (size_t)A.C * 4, hipMemcpyDeviceToHost, s));
+    SCCG_HIP(hipStreamSynchronize(s));
+    std::sort(fl.begin(), fl.end());
+    const int32_t lastk1 = A.nT - A.k + 1;
+    int32_t filled_to = -1;   // chunks <= filled_to were settled by an earlier fill of this round
+    for (int32_t j : fl) {
+        if (j <= filled_to || j + 1 >= A.C) continue;
+        const int32_t x0 = ex[j], P = ep[j];
+        int rc = dev_set_i32(A.scal + 6, 1, {INT32_MAX}, s);
+        if (rc) return rc;
+        const int64_t span = (int64_t)lastk1 - x0;
+        unsigned g = grid_for(span > 0 ? span : 1, WPB * 64 * WIDE);
+        if (g > 1024) g = 1024;
+        hipLaunchKernelGGL(k_frozen_scan, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, P);
+        hipLaunchKernelGGL(k_fill_literal, dim3(grid_for(A.C - j - 1, 256) > 1024 ? 1024 : grid_for(A.C - j - 1, 256)),
+                           dim3(256), 0, s, A, j + 1, P);
+        SCCG_HIP(hipGetLastError());
+        int32_t y = 0;
+        SCCG_HIP(hipMemcpyAsync(&y, A.scal + 6, sizeof y, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipStreamSynchronize(s));
+        // last chunk whose exit min(hi, lastk+1) <= y
+        int32_t last = j;
+        for (int32_t q = j + 1; q < A.C; q++) {
+            const int32_t hi = (q + 1) * A.S < A.nT ? (q + 1) * A.S : A.nT;
+            if ((hi < lastk1 ? hi : lastk1) > y) break;
+            last = q;
+        }
+        filled_to = last;
+    }
+    return 0;
 }
 
 }  // namespace
@@ -894,10 +1038,20 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             SCCG_HIP(hipGetLastError());
             res->rounds = round;
             RC(resolve_escalations(A, s));
+            RC(dev_set_i32(A.scal + 5, 1, {0}, s));
             hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
                                (const int32_t*)A.plist, nlist);
             SCCG_HIP(hipGetLastError());
-            if (dbg && (round <= 6 || round % 1000 == 0)) {
+            RC(frozen_fill(A, s));
+            if (dbg) {
+                SCCG_HIP(hipStreamSynchronize(s));
+                static thread_local auto tprev = std::chrono::steady_clock::now();
+                const auto tnow = std::chrono::steady_clock::now();
+                fprintf(stderr, "[walk] round %lld: %d walked, %.3f ms since last mark\n", (long long)round, nlist,
+                        std::chrono::duration<double, std::milli>(tnow - tprev).count());
+                tprev = tnow;
+            }
+            if (dbg && (round <= 3 || round % 1000 == 0)) {
                 std::vector<int32_t> g(C), ex(C), ep(C), ux(C), up(C), cur(C), c0(C), c1(C);
                 SCCG_HIP(hipMemcpyAsync(g.data(), A.guess, C * 4, hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipMemcpyAsync(ex.data(), A.exitX, C * 4, hipMemcpyDeviceToHost, s));
