@@ -88,12 +88,14 @@ struct SegStat {
     int32_t last_p;
     int32_t pad;
 };
+// segments [seg0, seg_end) of one pass (pass 2 only touches segments pass 1 left without a match)
 int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT,
-                      int64_t iters, uint32_t* recs, SegStat* stat, hipStream_t s);
-// switch FSM (compression.cpp:395-473): *d_switch = first segment where mism > T2, or -1
+                      int64_t seg0, int64_t seg_end, uint32_t* recs, SegStat* stat, hipStream_t s);
+// switch FSM (compression.cpp:395-473) over segments [seg0, seg_end) from counter state *state
+// (min(mismatch, 5); 6 = switched): *switch_seg = first segment where mismatch > T2, or -1
 int64_t fsm_chunks(int64_t iters);
-int launch_switch_fsm(const SegStat* stat, int64_t iters, int32_t* d_maps, int32_t* h_maps, int64_t* switch_seg,
-                      hipStream_t s);
+int launch_switch_fsm(const SegStat* stat, int64_t seg0, int64_t seg_end, int32_t* d_maps, int32_t* h_maps, int* state,
+                      int64_t* switch_seg, hipStream_t s);
 // record text for local mode (delta-encoded, compression.cpp:406-415 + :222-304) + leftover
 int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_t* recs,
                       const SegStat* stat, uint8_t* out, int64_t* d_len, int64_t* d_tmp_a,

@@ -64,12 +64,13 @@ __device__ __forceinline__ uint64_t pick_key(int p, int pme) {
 
 template <int K>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, const uint8_t* __restrict__ R, int64_t nR,
-                                                           const uint8_t* __restrict__ T, int64_t nT, int64_t iters,
-                                                           uint32_t* __restrict__ recs, SegStat* __restrict__ stat) {
+                                                           const uint8_t* __restrict__ T, int64_t nT, int64_t seg0,
+                                                           int64_t seg_end, uint32_t* __restrict__ recs,
+                                                           SegStat* __restrict__ stat) {
     __shared__ SegLds lds_all[WPB];
     const int w = wave_in_block(), lane = lane_id();
-    const int64_t seg = (int64_t)blockIdx.x * WPB + w;
-    if (seg >= iters) return;
+    const int64_t seg = seg0 + (int64_t)blockIdx.x * WPB + w;
+    if (seg >= seg_end) return;
     if (pass == 2 && stat[seg].pass != 0) return;
     SegLds& L = lds_all[w];
     const int64_t base = seg * SEG_L;
@@ -250,11 +251,11 @@ __device__ __forceinline__ int seg_class(const SegStat& s) {
     return s.non_n ? 2 : 3;
 }
 
-__global__ void k_fsm_chunks(const SegStat* __restrict__ stat, int64_t iters, int32_t* __restrict__ maps) {
+__global__ void k_fsm_chunks(const SegStat* __restrict__ stat, int64_t seg0, int64_t seg_end, int32_t* __restrict__ maps) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t s0 = t * FSM_G;
-    if (s0 >= iters) return;
-    const int64_t s1 = s0 + FSM_G < iters ? s0 + FSM_G : iters;
+    const int64_t s0 = seg0 + t * FSM_G;
+    if (s0 >= seg_end) return;
+    const int64_t s1 = s0 + FSM_G < seg_end ? s0 + FSM_G : seg_end;
     int st[6], at[6];
     for (int i = 0; i < 6; i++) { st[i] = i; at[i] = -1; }
     for (int64_t s = s0; s < s1; s++) {
@@ -385,14 +386,16 @@ __global__ void k_copy_upper(const uint8_t* __restrict__ in, int64_t n, uint8_t*
 
 }  // namespace
 
-int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t iters,
-                      uint32_t* recs, SegStat* stat, hipStream_t s) {
-    if (iters <= 0) return 0;
-    const unsigned g = grid_for(iters, WPB);
+int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t seg0,
+                      int64_t seg_end, uint32_t* recs, SegStat* stat, hipStream_t s) {
+    if (seg_end <= seg0) return 0;
+    const unsigned g = grid_for(seg_end - seg0, WPB);
     if (k == 14)
-        PROF_LAUNCH(PROF_LOCAL14, s, k_local_pass<14>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, iters, recs, stat);
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_pass<14>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, seg0,
+                    seg_end, recs, stat);
     else if (k == 10)
-        PROF_LAUNCH(PROF_LOCAL10, s, k_local_pass<10>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, iters, recs, stat);
+        PROF_LAUNCH(PROF_LOCAL10, s, k_local_pass<10>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, seg0,
+                    seg_end, recs, stat);
     else
         return SCCG_E_UNSUPPORTED;
     SCCG_HIP(hipGetLastError());
@@ -401,21 +404,22 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
 
 int64_t fsm_chunks(int64_t iters) { return (iters + FSM_G - 1) / FSM_G; }
 
-int launch_switch_fsm(const SegStat* stat, int64_t iters, int32_t* d_maps, int32_t* h_maps, int64_t* switch_seg,
-                      hipStream_t s) {
+int launch_switch_fsm(const SegStat* stat, int64_t seg0, int64_t seg_end, int32_t* d_maps, int32_t* h_maps, int* state,
+                      int64_t* switch_seg, hipStream_t s) {
     *switch_seg = -1;
-    if (iters <= 0) return 0;
-    const int64_t nch = fsm_chunks(iters);
-    hipLaunchKernelGGL(k_fsm_chunks, dim3(grid_for(nch, 256)), dim3(256), 0, s, stat, iters, d_maps);
+    if (seg_end <= seg0) return 0;
+    const int64_t nch = fsm_chunks(seg_end - seg0);
+    hipLaunchKernelGGL(k_fsm_chunks, dim3(grid_for(nch, 256)), dim3(256), 0, s, stat, seg0, seg_end, d_maps);
     SCCG_HIP(hipGetLastError());
     SCCG_HIP(hipMemcpyAsync(h_maps, d_maps, (size_t)nch * 12 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     SCCG_HIP(hipStreamSynchronize(s));
-    int st = 0;
+    int st = *state;
     for (int64_t c = 0; c < nch; c++) {
         const int m = h_maps[c * 12 + st];
-        if (m == SW) { *switch_seg = c * FSM_G + h_maps[c * 12 + 6 + st]; return 0; }
+        if (m == SW) { *switch_seg = seg0 + c * FSM_G + h_maps[c * 12 + 6 + st]; *state = SW; return 0; }
         st = m;
     }
+    *state = st;
     return 0;
 }
 

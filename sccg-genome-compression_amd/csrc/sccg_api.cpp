@@ -39,6 +39,7 @@ enum Slot {
 };
 
 constexpr int WALK_CHUNK = 16384;
+constexpr int64_t LOCAL_BATCH0 = 8192;   // first local batch (segments); multiple of the FSM chunk
 constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide compares, tails)
 
 }  // namespace
@@ -247,12 +248,19 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     GET(uint32_t, recs, B_RECS, (iters > 0 ? iters : 1) * SEG_REC_CAP);
     GET(SegStat, stat, B_STAT, iters > 0 ? iters : 1);
     if (iters > 0) {
-        TRY(launch_local_pass(14, 1, 1, R, nR, T, nT, iters, recs, stat, s));
-        TRY(launch_local_pass(10, 2, 1, R, nR, T, nT, iters, recs, stat, s));
+        // Segments run in geometrically growing batches, each followed by the switch state
+        // machine: once the counter passes T2 the rest of the local work would be discarded
+        // (compression.cpp:462-473), so it is never launched.
         const int64_t nch = fsm_chunks(iters);
         GET(int32_t, maps, B_MAPS, nch * 12);
         ctx->h_maps.resize((size_t)(nch * 12));
-        TRY(launch_switch_fsm(stat, iters, maps, ctx->h_maps.data(), &sw, s));
+        int fsm_state = 0;
+        for (int64_t b0 = 0, bs = LOCAL_BATCH0; b0 < iters && sw < 0; b0 += bs, bs *= 4) {
+            const int64_t b1 = b0 + bs < iters ? b0 + bs : iters;
+            TRY(launch_local_pass(14, 1, 1, R, nR, T, nT, b0, b1, recs, stat, s));
+            TRY(launch_local_pass(10, 2, 1, R, nR, T, nT, b0, b1, recs, stat, s));
+            TRY(launch_switch_fsm(stat, b0, b1, maps, ctx->h_maps.data(), &fsm_state, &sw, s));
+        }
     }
     st.switch_segment = sw;
     if (sw < 0) {
@@ -533,7 +541,7 @@ int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, s
         GET(SegStat, stat, B_STAT, 1);
         if (nr) HIPTRY(hipMemcpyAsync(R, sr, nr, hipMemcpyHostToDevice, s));
         if (nt) HIPTRY(hipMemcpyAsync(T, st, nt, hipMemcpyHostToDevice, s));
-        TRY(launch_local_pass(k, 1, 0, R, (int64_t)nr, T, (int64_t)nt, 1, recs, stat, s));
+        TRY(launch_local_pass(k, 1, 0, R, (int64_t)nr, T, (int64_t)nt, 0, 1, recs, stat, s));
         SegStat hs;
         uint32_t hr[SEG_REC_CAP];
         HIPTRY(hipMemcpyAsync(&hs, stat, sizeof hs, hipMemcpyDeviceToHost, s));
