@@ -38,17 +38,6 @@ __device__ __forceinline__ bool parse_int(const uint8_t* s, int64_t n, int64_t a
     return true;
 }
 
-__global__ void k_find_from(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ from_slot,
-                            int64_t* __restrict__ res, uint8_t c) {
-    const int64_t from = from_slot ? *from_slot + 1 : 0;
-    const int64_t CH = 1 << 16;
-    const int64_t base = from + (int64_t)blockIdx.x * CH;
-    if (from > n) return;
-    if (base >= (int64_t)__hip_atomic_load((unsigned long long*)res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    for (int64_t i = base + threadIdx.x; i < base + CH && i < n; i += blockDim.x)
-        if (s[i] == c) atomicMin((unsigned long long*)res, (unsigned long long)i);
-}
-
 // positions of '(' / ')' -> value i, else -1 (for a max-scan: last parenthesis at or before i)
 __global__ void k_paren_pos(const uint8_t* __restrict__ s, int64_t n, int64_t* __restrict__ v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -234,14 +223,11 @@ __global__ void k_format(const uint8_t* __restrict__ dec, int64_t nres, const in
 }  // namespace
 
 // =============================================================================================
-int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl /*4*/, hipStream_t s) {
-    int rc = dev_set_i64(d_nl, 4, {n, n, n, n}, s);
-    if (rc) return rc;
-    const unsigned g = grid_for(n > 0 ? n : 1, 1 << 16);
-    for (int i = 0; i < 4; i++)
-        hipLaunchKernelGGL(k_find_from, dim3(g), dim3(256), 0, s, d_rec, n, i ? (const int64_t*)(d_nl + i - 1) : nullptr,
-                           d_nl + i, (uint8_t)'\n');
-    SCCG_HIP(hipGetLastError());
+int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl /*8: 4 results + 4 tickets*/, hipStream_t s) {
+    for (int i = 0; i < 4; i++) {
+        int rc = launch_first_match(d_rec, n, i ? (const int64_t*)(d_nl + i - 1) : nullptr, 1, '\n', d_nl + i, d_nl + 4 + i, s);
+        if (rc) return rc;
+    }
     return 0;
 }
 

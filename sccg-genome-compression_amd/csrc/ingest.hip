@@ -29,24 +29,39 @@ __device__ __forceinline__ void load_bytes(const uint8_t* __restrict__ buf, int6
 // ---------------------------------------------------------------------------------------------
 // header search
 // ---------------------------------------------------------------------------------------------
-constexpr int64_t HDR_CHUNK = 1 << 16;
 
-__global__ void k_find_header(const uint8_t* __restrict__ buf, int64_t n, int64_t* __restrict__ sc) {
-    const int64_t base = (int64_t)blockIdx.x * HDR_CHUNK;
-    if (base >= (int64_t)__hip_atomic_load((unsigned long long*)&sc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    for (int64_t i = base + threadIdx.x; i < base + HDR_CHUNK && i < n; i += blockDim.x) {
-        if (buf[i] == '>' && (i == 0 || buf[i - 1] == '\n'))
-            atomicMin((unsigned long long*)&sc[0], (unsigned long long)i);
+// First position >= from (from = *from_slot + 1, or 0) holding `c` (mode 1) or a '>' that starts a
+// line (mode 0).  Blocks take 16 KiB chunks in increasing order from a ticket and stop as soon as a
+// chunk starts past the best match: a header at the start of the file costs one wave of chunks,
+// not a pass over the whole FASTA.  *res must hold n on entry; *ticket 0.
+constexpr int64_t FM_CHUNK = 16384;
+__global__ __launch_bounds__(SCCG_BLOCK) void k_first_match(const uint8_t* __restrict__ buf, int64_t n,
+                                                            const int64_t* __restrict__ from_slot, int mode, uint8_t c,
+                                                            int64_t* __restrict__ res, unsigned int* __restrict__ ticket) {
+    __shared__ int64_t s_cs;
+    const int64_t from = from_slot ? *from_slot + 1 : 0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const int64_t cs = from + (int64_t)atomicAdd(ticket, 1u) * FM_CHUNK;
+            const int64_t best = (int64_t)__hip_atomic_load((unsigned long long*)res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_cs = (cs >= n || cs >= best) ? -1 : cs;
+        }
+        __syncthreads();
+        const int64_t cs = s_cs;
+        __syncthreads();
+        if (cs < 0) return;
+        const int64_t p0 = cs + (int64_t)threadIdx.x * (FM_CHUNK / SCCG_BLOCK);
+        int64_t hit = INT64_MAX;
+        uint8_t prev = (p0 > 0 && p0 - 1 < n) ? buf[p0 - 1] : (uint8_t)'\n';
+        for (int i = 0; i < FM_CHUNK / SCCG_BLOCK && hit == INT64_MAX; i++) {
+            const int64_t p = p0 + i;
+            if (p >= n) break;
+            const uint8_t b = buf[p];
+            if (mode == 0 ? (b == '>' && (p == 0 || prev == '\n')) : (b == c)) hit = p;
+            prev = b;
+        }
+        if (hit != INT64_MAX) atomicMin((unsigned long long*)res, (unsigned long long)hit);
     }
-}
-
-__global__ void k_find_eol(const uint8_t* __restrict__ buf, int64_t n, int64_t* __restrict__ sc) {
-    const int64_t h = sc[0];
-    if (h >= n) { if (blockIdx.x == 0 && threadIdx.x == 0) sc[1] = n; return; }
-    const int64_t base = h + (int64_t)blockIdx.x * HDR_CHUNK;
-    if (base >= (int64_t)__hip_atomic_load((unsigned long long*)&sc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    for (int64_t i = base + threadIdx.x; i < base + HDR_CHUNK && i < n; i += blockDim.x)
-        if (buf[i] == '\n') atomicMin((unsigned long long*)&sc[1], (unsigned long long)i);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -351,16 +366,25 @@ __global__ void k_run_textwrite(const int32_t* __restrict__ rs, const int32_t* _
 }  // namespace
 
 // =============================================================================================
-int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t s) {
-    int rc = dev_set_i64(d_sc, 2, {n, n}, s);
+int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, int mode, uint8_t c, int64_t* res,
+                       int64_t* ticket_slot, hipStream_t s) {
+    int rc = dev_set_i64(res, 1, {n}, s);
+    if (!rc) rc = dev_set_i64(ticket_slot, 1, {0}, s);
     if (rc) return rc;
     if (n > 0) {
-        const unsigned g = grid_for(n, (int)HDR_CHUNK);
-        hipLaunchKernelGGL(k_find_header, dim3(g), dim3(256), 0, s, buf, n, d_sc);
-        hipLaunchKernelGGL(k_find_eol, dim3(g), dim3(256), 0, s, buf, n, d_sc);
+        hipLaunchKernelGGL(k_first_match, dim3(64), dim3(SCCG_BLOCK), 0, s, buf, n, from_slot, mode, c, res,
+                           reinterpret_cast<unsigned int*>(ticket_slot));
+        SCCG_HIP(hipGetLastError());
     }
-    SCCG_HIP(hipGetLastError());
     return 0;
+}
+
+int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t s) {
+    // d_sc[0] = header start (first '>' at a line start), d_sc[1] = its '\n' (n if none);
+    // d_sc[62], d_sc[63] are the chunk tickets
+    int rc = launch_first_match(buf, n, nullptr, 0, '>', d_sc, d_sc + 62, s);
+    if (!rc) rc = launch_first_match(buf, n, d_sc, 1, '\n', d_sc + 1, d_sc + 63, s);
+    return rc;
 }
 
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,

@@ -59,6 +59,10 @@ struct IngestScratch {
 // Target header: first line starting with '>' (compression.cpp:210); writes [h, he) into
 // scalars[0..1] (h = n when absent).
 int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_scalars, hipStream_t s);
+// *res = first position >= *from_slot + 1 (0 if from_slot is null) holding byte c (mode 1) or a
+// '>' that starts a line (mode 0); n if none.  *ticket_slot is scratch.
+int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, int mode, uint8_t c, int64_t* res,
+                       int64_t* ticket_slot, hipStream_t s);
 // read_genomes_from_files (compression.cpp:193-218): compacts the kept, non-space bytes of `buf`
 // into `out` (original case); *d_len = kept count; in TGT mode lines [h, he) are the header.
 // d_flags (optional) gets bit0 when a kept byte is '('.

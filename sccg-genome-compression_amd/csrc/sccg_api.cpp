@@ -11,6 +11,7 @@
 // delta_encode (:222-304) is folded into the emitters: each "(p," is written as "(p-p_prev,".
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -201,6 +202,16 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     hipStream_t s = ctx->stream;
     sccg_stats st{};
     st.switch_segment = -1;
+    // SCCG_DEBUG: host-side phase clock (synchronises at every mark, diagnostics only)
+    const bool dbg = getenv("SCCG_DEBUG") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!dbg) return;
+        (void)hipStreamSynchronize(s);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[phase] %-14s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     GET(int64_t, sc, B_SCAL, 64);
     GET(uint8_t, T, B_T, tn + 64);
     GET(uint8_t, R, B_R, rn + 64);
@@ -225,6 +236,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
                          "(compression.cpp:263-292); not supported yet");
     st.target_bases = nT;
     st.reference_bases = nR;
+    mark("ingest");
     const bool has_hdr = hdr[0] < tn;
     const int64_t hlen = has_hdr ? hdr[1] - hdr[0] : 0;
     if (out_cap < hlen + 1 + 11 * nT + 64) return ctx->fail(SCCG_E_INVALID, "output capacity too small");
@@ -240,6 +252,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     TRY(run_line(ctx, RUN_LOWER, T, nT, out + pos, sc + 4, &llen));
     pos += llen;
     const int64_t lower_end = pos;
+    mark("lower_line");
 
     // ---- local segments (compression.cpp:372-474)
     const int64_t nRs = (nR + SEG_L - 1) / SEG_L, nTs = (nT + SEG_L - 1) / SEG_L;
@@ -255,7 +268,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         GET(int32_t, maps, B_MAPS, nch * 12);
         ctx->h_maps.resize((size_t)(nch * 12));
         int fsm_state = 0;
-        for (int64_t b0 = 0, bs = LOCAL_BATCH0; b0 < iters && sw < 0; b0 += bs, bs *= 4) {
+        for (int64_t b0 = 0, bs = LOCAL_BATCH0; b0 < iters && sw < 0; b0 += bs, bs *= 2) {
             const int64_t b1 = b0 + bs < iters ? b0 + bs : iters;
             TRY(launch_local_pass(14, 1, 1, R, nR, T, nT, b0, b1, recs, stat, s));
             TRY(launch_local_pass(10, 2, 1, R, nR, T, nT, b0, b1, recs, stat, s));
@@ -263,6 +276,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         }
     }
     st.switch_segment = sw;
+    mark("local");
     if (sw < 0) {
         // ---- local: "\n,\n" + records + leftover segments
         TRY(put_bytes(ctx, out + pos, "\n,\n", 3));
@@ -296,6 +310,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         pos += nlen;
         TRY(put_bytes(ctx, out + pos, "\n", 1));
         pos += 1;
+        mark("n_line");
         GET(uint8_t, Tp, B_TP, nT + 64);
         GET(uint8_t, Rp, B_RP, nR + 64);
         const int64_t ntile = (nT > nR ? nT : nR) / INGEST_TILE + 2;
@@ -305,6 +320,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         TRY(launch_filter(FILTER_DROP_N_UPPER, R, nR, Rp, sc + 8, tcnt, part, s));
         int64_t np[2];
         TRY(d2h_i64(ctx, sc + 7, np, 2));
+        mark("n_erase");
         const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, WALK_CHUNK);
         void* ws = ctx->get(B_WALK, wsb);
         if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
@@ -315,6 +331,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         st.walk_rounds = wr.rounds;
         st.walk_chunks = wr.chunks;
         pos += rlen;
+        mark("global_walk");
     }
     HIPTRY(hipStreamSynchronize(s));
     st.record_bytes = pos;

@@ -996,6 +996,16 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             first_l = (int32_t)f.lmax;
         }
     }
+    const bool dbgp = getenv("SCCG_DEBUG") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!dbgp) return;
+        (void)hipStreamSynchronize(s);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[phase]   walk.%-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
+    mark("first_step");
     int32_t startX, startP;
     if (first_y != INVALID) { startX = first_y + first_l; startP = first_p + first_l - 1; }
     else { startX = lastk + 1 > 0 ? lastk + 1 : 0; startP = INVALID; }
@@ -1030,6 +1040,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         }
         RC(dev_set_i32(A.snapX, 1, {startX}, s));
         RC(dev_set_i32(A.snapP, 1, {startP}, s));
+        mark("anchors");
         int32_t nlist = A.C;
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
         for (int64_t round = 1;; round++) {
@@ -1101,6 +1112,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         }
     }
 
+    mark("rounds");
     // ---- flatten: first match, then every chunk's trajectory
     const int32_t nfirst = first_y != INVALID ? 1 : 0;
     hipLaunchKernelGGL(k_chunk_counts, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
@@ -1143,5 +1155,6 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         SCCG_HIP(hipGetLastError());
     }
     *out_len = text + (tail > 0 ? tail : 0);
+    mark("emit");
     return 0;
 }
