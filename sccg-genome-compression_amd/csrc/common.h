@@ -101,6 +101,10 @@ __device__ __forceinline__ T wave_min(T v) {
     return v;
 }
 __device__ __forceinline__ int first_lane(unsigned long long m) { return m ? __ffsll((long long)m) - 1 : 64; }
+// wave-uniform copies (SGPR): a value every lane agrees on, and lane l's value
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int32_t lane_val(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, l); }
 
 // exclusive block scan (sum) for a 256-thread block; `tmp` = 5 LDS slots
 template <typename T>

@@ -29,7 +29,6 @@ namespace {
 
 constexpr int WPB = 4;                 // chunks (waves) per block
 constexpr int WCAP = 256;              // window positions held in LDS (2m+1 <= WCAP)
-constexpr int WBYTES = WCAP + 32;
 constexpr int WTBITS = 9;              // window hash slots
 constexpr int WTSLOTS = 1 << WTBITS;
 constexpr int32_t INVALID = INT32_MIN;
@@ -86,14 +85,12 @@ struct WalkPtrs {
     int64_t* tlen;            // per flat match: text length -> offsets
     int64_t* partial;
     int64_t* scal64;          // [0] total matches [1] text bytes
+    uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
 };
 
-struct WalkLds {
-    uint8_t win[WBYTES];
-    uint8_t tb[64 + 32];
+struct WalkLds {   // per wave: LDS hash of the window keys (wide literal scans)
     uint32_t wkeys[WCAP];
     uint32_t wtab[WTSLOTS / 2];
-    int32_t cand[WCAP];
 };
 
 __device__ __forceinline__ uint64_t pick_key(int32_t p, int32_t pme) {
@@ -157,43 +154,150 @@ __device__ int32_t wave_lce(const uint8_t* __restrict__ R, int32_t a, const uint
             if (valid < 16 && pos > valid) pos = valid;
             if (pos < 16) e = my + pos;
         }
-        const int32_t m = wave_min(e);
-        if (m != INT32_MAX) return m < maxlen ? m : maxlen;
+        // lanes cover increasing offsets: the first lane that stops holds the extension
+        const unsigned long long sm = __ballot(e != INT32_MAX);
+        if (sm) {
+            const int32_t m = lane_val(e, first_lane(sm));
+            return m < maxlen ? m : maxlen;
+        }
     }
     return maxlen > 0 ? maxlen : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
-// window of P: keys of every reference k-mer start in [max(0,P-m), min(nR-k, P+m)]
+// Walk k-mer keys.  Inside the walk a pure A/C/G/T k-mer's key is its 2-bit codes packed first
+// base LOWEST (bits 2i..2i+1 = base i), so the keys of every k-mer in a run of bytes are shifts of
+// one packed word; a k-mer holding any other byte gets exotic_key() (high bit set, confirmed by a
+// byte compare).  Equal pure keys <=> equal bytes.  Only the walk's own window / target / LDS keys
+// use this convention.
 // ---------------------------------------------------------------------------------------------
-__device__ void build_window(const WalkPtrs& A, WalkLds& L, int32_t P, int32_t& lo, int32_t& nwin) {
-    const int lane = lane_id();
-    lo = P - A.m < 0 ? 0 : P - A.m;
-    const int32_t hi = (P + A.m < A.nR - A.k) ? P + A.m : A.nR - A.k;
-    nwin = hi - lo + 1;
-    if (nwin < 0) nwin = 0;
-    const int nbytes = nwin + A.k - 1;
-    for (int i = lane; i < WBYTES; i += 64) L.win[i] = (i < nbytes) ? A.R[lo + i] : (uint8_t)0;
-    for (int i = lane; i < WTSLOTS / 2; i += 64) L.wtab[i] = 0;
-    wave_sync();
-    for (int i = lane; i < nwin; i += 64) {
-        const uint32_t key = kmer_key(&L.win[i], A.k);
-        L.wkeys[i] = key;
-        wt_insert(L.wtab, key, (uint32_t)i + 1);
+// 4 bytes -> their 2-bit codes in 8 bits (byte i at bits 2i), and `diff` nonzero in exactly the
+// bytes that are not A/C/G/T: code = ((c >> 1) ^ (c >> 2)) & 3 maps A,C,G,T -> 0,1,2,3, and a
+// byte-permute of "ACGT" by the codes rebuilds the byte iff it was one of them.
+__device__ __forceinline__ uint32_t swar_codes(uint32_t w, uint32_t& diff) {
+    const uint32_t c = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
+    diff = __builtin_amdgcn_perm(0x54474341u, 0x54474341u, c) ^ w;
+    const uint32_t p = c | (c >> 6);
+    return (p | (p >> 12)) & 0xffu;
+}
+// bit i set <=> byte i of `diff` is nonzero
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t diff) {
+    const uint32_t nz = ((((diff & 0x7f7f7f7fu) + 0x7f7f7f7fu) | diff) & 0x80808080u) >> 7;
+    return (nz | (nz >> 7) | (nz >> 14) | (nz >> 21)) & 0xfu;
+}
+// ND consecutive words -> packed codes (byte i at bits 2i) and the non-ACGT byte mask
+template <int ND>
+__device__ __forceinline__ void pack_codes(const uint32_t (&w)[ND], uint64_t& code, uint32_t& bad) {
+    uint32_t d[ND], acc = 0;
+    code = 0;
+#pragma unroll
+    for (int i = 0; i < ND; i++) {
+        code |= (uint64_t)swar_codes(w[i], d[i]) << (8 * i);
+        acc |= d[i];
     }
-    wave_sync();
+    bad = 0;
+    if (acc) {   // rare: some byte is not A/C/G/T
+#pragma unroll
+        for (int i = 0; i < ND; i++) bad |= nz_bytes(d[i]) << (4 * i);
+    }
+}
+// ND bytes-worth of words at an arbitrary address (ND+1 aligned dword loads)
+template <int ND>
+__device__ __forceinline__ void loadw(const uint8_t* p, uint32_t (&o)[ND]) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t v[ND + 1];
+#pragma unroll
+    for (int i = 0; i <= ND; i++) v[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < ND; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+}
+// scalar form (any k <= 15)
+__device__ __forceinline__ uint32_t walk_key(const uint8_t* s, int k) {
+    uint32_t code = 0;
+    for (int i = 0; i < k; i++) {
+        const uint32_t b = base2(s[i]);
+        if (b > 3) return exotic_key(s, k);
+        code |= b << (2 * i);
+    }
+    return code;
 }
 
-__device__ __forceinline__ bool window_has(const WalkPtrs& A, const WalkLds& L, uint32_t key, const uint8_t* kb) {
-    int slot = (int)slot_hash(key, WTBITS);
-    for (int probes = 0; probes < WTSLOTS; probes++) {
-        const uint32_t v = wt_get(L.wtab, slot);
-        if (!v) return false;
-        const int i = (int)v - 1;
-        if (L.wkeys[i] == key && (key < KEY_EXOTIC || bytes_eq(&L.win[i], kb, A.k))) return true;
-        slot = (slot + 1) & (WTSLOTS - 1);
+// ---------------------------------------------------------------------------------------------
+// window of P in registers: lane l holds the keys of window indices 4l+q (q < 4), i.e. of the
+// reference k-mers starting at lo+4l+q, lo = max(0, P-m), up to hi = min(nR-k, P+m).
+// 2m+1 <= 4*64 window positions (m = 100: 201).
+// ---------------------------------------------------------------------------------------------
+struct RegWin {
+    int32_t P, lo, n;
+    uint32_t key[4];
+    uint32_t vmask;   // bit q: index 4*lane+q is inside the window
+};
+
+__device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin& W) {
+    const int lane = lane_id(), k = A.k;
+    W.P = P;
+    W.lo = P - A.m < 0 ? 0 : P - A.m;
+    const int32_t hi = (P + A.m < A.nR - k) ? P + A.m : A.nR - k;
+    W.n = hi - W.lo + 1;
+    if (W.n < 0) W.n = 0;
+    W.vmask = 0;
+    W.key[0] = W.key[1] = W.key[2] = W.key[3] = 0;
+    const int i0 = 4 * lane;
+    if (i0 >= W.n) return;
+    uint32_t w[5];   // 20 bytes >= 3 + k
+    loadw<5>(A.R + W.lo + i0, w);
+    uint64_t code;
+    uint32_t bad;
+    pack_codes<5>(w, code, bad);
+    const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        W.key[q] = (bad >> q) & KM ? exotic_key(A.R + W.lo + i0 + q, k) : (uint32_t)(code >> (2 * q)) & MASK;
+        if (i0 + q < W.n) W.vmask |= 1u << q;
     }
-    return false;
+}
+
+// key of the target k-mer at y (one unaligned 16-byte load; k <= 15)
+__device__ __forceinline__ uint32_t target_key(const WalkPtrs& A, int32_t y) {
+    const int k = A.k;
+    uint32_t w[4];
+    loadw<4>(A.T + y, w);
+    uint64_t code;
+    uint32_t bad;
+    pack_codes<4>(w, code, bad);
+    return bad & ((1u << k) - 1u) ? exotic_key(A.T + y, k) : (uint32_t)code & ((1u << (2 * k)) - 1u);
+}
+
+// bit q set: window index 4*lane+q holds exactly the k-mer T[y..y+k) (key kk)
+__device__ __forceinline__ uint32_t win_match(const WalkPtrs& A, const RegWin& W, uint32_t kk, int32_t y) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (((W.vmask >> q) & 1u) && W.key[q] == kk) m |= 1u << q;
+    if (m && kk >= KEY_EXOTIC) {   // hash keys: confirm bytes (rare)
+        const int32_t c0 = W.lo + 4 * lane_id();
+        for (int q = 0; q < 4; q++)
+            if (((m >> q) & 1u) && !bytes_eq(A.R + c0 + q, A.T + y, A.k)) m &= ~(1u << q);
+    }
+    return m;
+}
+
+// LDS hash of the register window's keys (only needed for wide literal scans)
+__device__ void hash_window(const RegWin& W, WalkLds& L) {
+    const int lane = lane_id();
+    for (int i = lane; i < WTSLOTS / 2; i += 64) L.wtab[i] = 0;
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if ((W.vmask >> q) & 1u) {
+            const int i = 4 * lane + q;
+            L.wkeys[i] = W.key[q];
+            wt_insert(L.wtab, W.key[q], (uint32_t)i + 1);
+        }
+    }
+    wave_sync();
 }
 
 __device__ __forceinline__ bool window_has_key(const WalkLds& L, uint32_t key) {
@@ -208,40 +312,29 @@ __device__ __forceinline__ bool window_has_key(const WalkLds& L, uint32_t key) {
 }
 
 // Wide literal scan: first position in [x, end) whose k-mer key occurs in the window (1024
-// positions per wave step: 16 consecutive per lane, rolling 2-bit codes).  Key equality is a
-// superset of byte equality, so every position skipped is certainly a literal step; a returned
-// position is re-checked exactly by the caller.  Returns `end` when there is none.
+// positions per wave step: 16 consecutive per lane, keys by shifting one packed code word).  Key
+// equality is a superset of byte equality, so every position skipped is certainly a literal step;
+// a returned position is re-checked exactly by the caller.  Returns `end` when there is none.
 constexpr int WIDE = 16;
-__device__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, int32_t x, int32_t end) {
+__device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, int32_t x, int32_t end) {
     const int lane = lane_id(), k = A.k;
-    const uint32_t MASK = (1u << (2 * k)) - 1u;
+    const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
     for (int32_t base = x; base < end; base += 64 * WIDE) {
         const int32_t p0 = base + WIDE * lane;
-        uint32_t w[8];
-        load16u(A.T + p0, *reinterpret_cast<uint32_t(*)[4]>(&w[0]));
-        load16u(A.T + p0 + 16, *reinterpret_cast<uint32_t(*)[4]>(&w[4]));
+        uint32_t w[8];   // 32 bytes >= WIDE + k - 1
+        loadw<8>(A.T + p0, w);
+        uint64_t code;
+        uint32_t bad;
+        pack_codes<8>(w, code, bad);
         int32_t first = INT32_MAX;
-        uint32_t code = 0;
-        int lastbad = -1000;
 #pragma unroll
-        for (int i = 0; i < WIDE + 15; i++) {
-            const uint8_t c = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-            uint32_t b = base2(c);
-            if (b > 3) { lastbad = i; b = 0; }
-            code = ((code << 2) | b) & MASK;
-            const int st = i - (k - 1);
-            if (st >= 0 && st < WIDE && first == INT32_MAX && p0 + st < end) {
-                uint32_t key = code;
-                if (lastbad >= st) {   // non-ACGT byte inside: hash the k bytes (rare)
-                    uint32_t h = 2166136261u;
-                    for (int q = 0; q < k; q++) { h ^= (uint8_t)(w[(st + q) >> 2] >> (8 * ((st + q) & 3))); h *= 16777619u; }
-                    key = KEY_EXOTIC | (h & 0x7fffffffu);
-                }
-                if (window_has_key(L, key)) first = p0 + st;
-            }
+        for (int st = 0; st < WIDE; st++) {
+            if (p0 + st >= end) break;
+            const uint32_t key = (bad >> st) & KM ? exotic_key(A.T + p0 + st, k) : (uint32_t)(code >> (2 * st)) & MASK;
+            if (window_has_key(L, key)) { first = p0 + st; break; }
         }
-        const int32_t m = wave_min(first);
-        if (m != INT32_MAX) return m;
+        const unsigned long long hm = __ballot(first != INT32_MAX);   // lanes in position order
+        if (hm) return lane_val(first, first_lane(hm));
     }
     return end;
 }
@@ -249,14 +342,16 @@ __device__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, int32_t x, int
 // ---------------------------------------------------------------------------------------------
 // the chunk walk (one wave per chunk)
 // ---------------------------------------------------------------------------------------------
+constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail
+template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
     __shared__ WalkLds lds_all[WPB];
     const int w = wave_in_block(), lane = lane_id();
     const int32_t li = (int32_t)blockIdx.x * WPB + w;
     if (li >= nlist) return;
     WalkLds& L = lds_all[w];
-    const int32_t j = list[li];
-    const int32_t kind = A.kind[j];
+    const int32_t j = uni(list[li]);
+    const int32_t kind = uni(A.kind[j]);
     const int32_t lo_j = j * A.S;
     const int32_t hi_j = (lo_j + A.S < A.nT) ? lo_j + A.S : A.nT;
     const int32_t lastk = A.nT - A.k;
@@ -264,26 +359,32 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
 
     int32_t x, P, n = 0, q = 0, ob, cb = -1, cc = 0;
     if (kind == KIND_SPEC) {
-        ob = A.cur[j];
+        ob = uni(A.cur[j]);
         x = lo_j;
-        P = A.guess[j];
+        P = uni(A.guess[j]);
         if (lane == 0) { A.usedX[j] = lo_j; A.usedP[j] = P; }
     } else if (kind == KIND_FIX) {   // result is committed (or discarded) by k_commit
-        cb = A.cur[j];
+        cb = uni(A.cur[j]);
         ob = 1 - cb;
-        cc = A.cnt[cb][j];
-        x = A.snapX[j];
-        P = A.snapP[j];
+        cc = uni(A.cnt[cb][j]);
+        x = uni(A.snapX[j]);
+        P = uni(A.snapP[j]);
     } else {   // resume after an escalation was resolved on the host
-        cb = A.cur[j];
+        cb = uni(A.cur[j]);
         ob = 1 - cb;
-        cc = A.cnt[cb][j];
-        x = A.escX[j];
-        P = A.escP[j];
-        n = A.escN[j];
-        q = A.escQ[j];
+        cc = uni(A.cnt[cb][j]);
+        x = uni(A.escX[j]);
+        P = uni(A.escP[j]);
+        n = uni(A.escN[j]);
+        q = uni(A.escQ[j]);
     }
     if (lane == 0) A.status[j] = ST_OK;
+    const uint64_t dbg_t0 = DBG ? wall_clock64() : 0;
+    uint64_t dbg_c[10] = {};   // matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail
+    uint64_t tq = dbg_t0;
+    auto tick = [&](int slot) {
+        if (DBG) { const uint64_t t = wall_clock64(); dbg_c[slot] += t - tq; tq = t; }
+    };
     if (P == INVALID) {   // speculative chunk without an anchor: nothing to offer
         if (lane == 0) { A.cnt[ob][j] = 0; A.exitX[j] = INVALID; A.exitP[j] = INVALID; }
         return;
@@ -295,57 +396,64 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
     const int32_t* cp = cb >= 0 ? A.bp[cb] + (size_t)j * A.cap : nullptr;
     const int32_t* cl = cb >= 0 ? A.bl[cb] + (size_t)j * A.cap : nullptr;
 
-    int32_t wlo = 0, nwin = 0, wP = INVALID;
+    RegWin W;
+    W.P = INVALID;
+    int32_t hashP = INVALID;   // P whose window keys are in the LDS hash (built only for wide scans)
     int32_t lme = x;   // target index after the last match of this walk (start of the open literal run)
     bool converged = false, escalated = false;
     const int32_t scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
     while (x < scan_end) {
-        if (wP != P) { build_window(A, L, P, wlo, nwin); wP = P; }
-        if (nwin <= 0) { x = scan_end; break; }
-        // ---- literal steps: first y in [x, scan_end) whose k-mer is in the window
-        for (int i = lane; i < 64 + 32; i += 64) {
-            const int32_t pos = x + i;
-            L.tb[i] = pos < A.nT ? A.T[pos] : (uint8_t)0;
-        }
-        wave_sync();
+        if (DBG) tick(9);
+        if (W.P != P) { reg_window(A, P, W); if (DBG) dbg_c[3]++; }
+        if (DBG) tick(6);
+        if (W.n <= 0) { x = scan_end; break; }
+        if (DBG) dbg_c[1]++;
+        // ---- literal steps: first y in [x, scan_end) whose k-mer has a candidate in the window
         const int32_t y_l = x + lane;
         const bool valid = y_l < scan_end;
-        const uint32_t key_l = valid ? kmer_key(&L.tb[lane], k) : 0u;
-        const bool hit = valid && window_has(A, L, key_l, &L.tb[lane]);
-        const unsigned long long hm = __ballot(hit);
-        if (!hm) {
+        const uint32_t key_l = valid ? target_key(A, y_l) : 0u;
+        int hl = -1;
+        const int nb = scan_end - x < 64 ? scan_end - x : 64;
+        for (int yy = 0; yy < nb; yy++) {
+            const uint32_t kk = lane_val(key_l, yy);
+            if (__ballot(win_match(A, W, kk, x + yy) != 0)) { hl = yy; break; }
+        }
+        if (hl < 0) {
             x = (x + 64 < scan_end) ? x + 64 : scan_end;
-            if (x < scan_end) x = wide_scan(A, L, x, scan_end);
-            wave_sync();
+            if (x < scan_end) {
+                if (hashP != P) { hash_window(W, L); hashP = P; }
+                x = wide_scan(A, L, x, scan_end);
+                if (DBG) dbg_c[2]++;
+            }
             continue;
         }
-        const int hl = first_lane(hm);
         const int32_t y = x + hl;
-        const uint32_t key = __shfl(key_l, hl, 64);
-        // ---- candidates in the window (compression.cpp:114-130, in-range ones only)
-        int ncand = 0;
-        for (int i0 = 0; i0 < nwin; i0 += 64) {
-            const int i = i0 + lane;
-            const bool c = i < nwin && L.wkeys[i] == key && (key < KEY_EXOTIC || bytes_eq(&L.win[i], &L.tb[hl], k));
-            const unsigned long long cm = __ballot(c);
-            if (c) L.cand[ncand + __popcll(cm & ((1ull << lane) - 1))] = wlo + i;
-            ncand += __popcll(cm);
-        }
-        wave_sync();
+        const uint32_t key = lane_val(key_l, hl);
+        if (DBG) tick(7);
+        // ---- candidates in the window (compression.cpp:114-130, in-range ones only), extended one
+        //      at a time by the whole wave; order-free reduction
+        const uint32_t mine = win_match(A, W, key, y);   // bit q: window index 4*lane+q matches
         int32_t bl = 0, bcnt = 0;
         bool bhas0 = false;
         uint64_t bkey = ~0ull;
-        for (int ci = 0; ci < ncand; ci++) {
-            const int32_t c = L.cand[ci];
-            int32_t maxlen = A.nR - (c + k);
-            const int32_t mt = A.nT - (y + k);
-            if (mt < maxlen) maxlen = mt;
-            const int32_t l = k + wave_lce(A.R, c + k, A.T, y + k, maxlen);   // extend_alignment
-            if (l > bl) { bl = l; bcnt = 1; bhas0 = (c == 0); bkey = c ? pick_key(c, P) : ~0ull; }
-            else if (l == bl) {
-                bcnt++;
-                if (c == 0) bhas0 = true;
-                else { const uint64_t pk = pick_key(c, P); bkey = pk < bkey ? pk : bkey; }
+        int ncand = 0;
+        for (int qq = 0; qq < 4; qq++) {
+            unsigned long long cm = __ballot((mine >> qq) & 1u);
+            while (cm) {
+                const int cl_ = __ffsll((long long)cm) - 1;
+                cm &= cm - 1;
+                const int32_t c = W.lo + 4 * cl_ + qq;
+                int32_t maxlen = A.nR - (c + k);
+                const int32_t mt = A.nT - (y + k);
+                if (mt < maxlen) maxlen = mt;
+                const int32_t l = k + wave_lce(A.R, c + k, A.T, y + k, maxlen);   // extend_alignment
+                ncand++;
+                if (l > bl) { bl = l; bcnt = 1; bhas0 = (c == 0); bkey = c ? pick_key(c, P) : ~0ull; }
+                else if (l == bl) {
+                    bcnt++;
+                    if (c == 0) bhas0 = true;
+                    else { const uint64_t pk = pick_key(c, P); bkey = pk < bkey ? pk : bkey; }
+                }
             }
         }
         uint64_t pk;
@@ -366,6 +474,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
         }
         if (lane == 0) { ot[n] = y; op[n] = p; ol[n] = bl; }
         n++;
+        if (DBG) { dbg_c[0]++; dbg_c[4] += ncand; dbg_c[5] += bl; tick(8); }
         // ---- convergence with the previous trajectory of this chunk
         if (cb >= 0) {
             for (;;) {
@@ -390,9 +499,14 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
         lme = y + bl;
         P = p + bl - 1;   // compression.cpp:149
         x = y + bl;       // compression.cpp:159
-        wave_sync();
     }
     if (escalated) return;
+    if (DBG && lane == 0 && A.scal[4] == 1) {
+        tick(9);
+        uint64_t* d = A.dbg + (size_t)j * DBG_SLOTS;
+        d[0] = wall_clock64() - dbg_t0;
+        for (int i = 0; i < 10; i++) d[1 + i] = dbg_c[i];
+    }
     if (lane == 0) {
         A.cnt[ob][j] = n;
         if (cb < 0) {   // speculative: the trajectory is the chunk's first, take it as is
@@ -437,9 +551,10 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
 __global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int32_t x0, int32_t P) {
     __shared__ WalkLds lds_all[WPB];
     WalkLds& L = lds_all[wave_in_block()];
-    int32_t wlo, nwin;
-    build_window(A, L, P, wlo, nwin);
-    if (nwin <= 0) return;
+    RegWin W;
+    reg_window(A, P, W);
+    if (W.n <= 0) return;
+    hash_window(W, L);
     const int32_t end = A.nT - A.k + 1;
     const int64_t gw = (int64_t)blockIdx.x * WPB + wave_in_block(), G = (int64_t)gridDim.x * WPB;
     for (int64_t base = x0 + gw * 64 * WIDE; base < end; base += G * 64 * WIDE) {
@@ -800,9 +915,14 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.tlen = c.take<int64_t>(maxm + 1);
     A.partial = c.take<int64_t>((size_t)scan_partials_needed((int64_t)(maxm > C ? maxm : C) + 1) + 16);
     A.scal64 = c.take<int64_t>(8);
+    A.dbg = c.take<uint64_t>(C * DBG_SLOTS);
     *used = c.off;
     return A;
 }
+
+// SCCG_DEBUG runs take the instrumented walk
+using WalkKernel = void (*)(WalkPtrs, const int32_t*, int32_t);
+WalkKernel walk_kernel(const WalkPtrs& A) { return A.dbg ? k_walk<true> : k_walk<false>; }
 
 struct FullC {
     int64_t lmax;
@@ -882,7 +1002,7 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s) {
         int rc = dev_set_i32(A.scal + 1, 1, {0}, s);
         if (rc) return rc;
         if ((rc = h2d_sync(A.rlist, rl.data(), rl.size() * 4, s))) return rc;
-        PROF_LAUNCH(PROF_WALK, s, k_walk, dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
+        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
                     (const int32_t*)A.rlist, (int32_t)rl.size());
         SCCG_HIP(hipGetLastError());
     }
@@ -959,6 +1079,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     size_t used = 0;
     WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, &used);
     if (used > ws_bytes) return SCCG_E_INTERNAL;
+    if (!getenv("SCCG_DEBUG")) A.dbg = nullptr;   // per-chunk counters only in diagnostic runs
     res->rounds = 0;
     res->chunks = A.C;
     res->n_matches = 0;
@@ -1045,7 +1166,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
         for (int64_t round = 1;; round++) {
             RC(dev_set_i32(A.scal + 4, 1, {(int32_t)round}, s));
-            PROF_LAUNCH(PROF_WALK, s, k_walk, dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
+            PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
             SCCG_HIP(hipGetLastError());
             res->rounds = round;
             RC(resolve_escalations(A, s));
@@ -1061,6 +1182,37 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 fprintf(stderr, "[walk] round %lld: %d walked, %.3f ms since last mark\n", (long long)round, nlist,
                         std::chrono::duration<double, std::milli>(tnow - tprev).count());
                 tprev = tnow;
+            }
+            if (dbg && round == 1) {   // per-chunk cost profile of the speculative round
+                constexpr size_t DS = DBG_SLOTS;
+                std::vector<uint64_t> d(C * DS);
+                SCCG_HIP(hipMemcpyAsync(d.data(), A.dbg, C * DS * 8, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipStreamSynchronize(s));
+                std::vector<uint64_t> tk(C);
+                uint64_t sum[11] = {};
+                for (size_t j = 0; j < C; j++) {
+                    tk[j] = d[j * DS];
+                    for (int i = 0; i < 11; i++) sum[i] += d[j * DS + i];
+                }
+                std::vector<uint64_t> sorted = tk;
+                std::sort(sorted.begin(), sorted.end());
+                fprintf(stderr, "[walk] r1 chunk ticks(10ns): mean %.0f p50 %llu p90 %llu p99 %llu max %llu | totals: matches %llu "
+                        "batches %llu wides %llu windows %llu cands %llu extbases %llu\n",
+                        (double)sum[0] / C, (unsigned long long)sorted[C / 2], (unsigned long long)sorted[C * 9 / 10],
+                        (unsigned long long)sorted[C * 99 / 100], (unsigned long long)sorted[C - 1],
+                        (unsigned long long)sum[1], (unsigned long long)sum[2], (unsigned long long)sum[3],
+                        (unsigned long long)sum[4], (unsigned long long)sum[5], (unsigned long long)sum[6]);
+                fprintf(stderr, "[walk] r1 step phases (10ns, summed over chunks): window %llu find %llu cand+lce %llu tail %llu\n",
+                        (unsigned long long)sum[7], (unsigned long long)sum[8], (unsigned long long)sum[9], (unsigned long long)sum[10]);
+                std::vector<size_t> idx(C);
+                for (size_t j = 0; j < C; j++) idx[j] = j;
+                std::partial_sort(idx.begin(), idx.begin() + 5, idx.end(), [&](size_t a, size_t b) { return tk[a] > tk[b]; });
+                for (int q = 0; q < 5; q++) {
+                    const uint64_t* e = &d[idx[q] * DS];
+                    fprintf(stderr, "   slow chunk %zu: ticks %llu matches %llu batches %llu wides %llu windows %llu cands %llu ext %llu\n",
+                            idx[q], (unsigned long long)e[0], (unsigned long long)e[1], (unsigned long long)e[2],
+                            (unsigned long long)e[3], (unsigned long long)e[4], (unsigned long long)e[5], (unsigned long long)e[6]);
+                }
             }
             if (dbg && (round <= 3 || round % 1000 == 0)) {
                 std::vector<int32_t> g(C), ex(C), ep(C), ux(C), up(C), cur(C), c0(C), c1(C);
