@@ -59,6 +59,66 @@ __device__ __forceinline__ int write_i32(uint8_t* dst, int32_t v) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Packed ("walk") k-mer keys: a pure A/C/G/T k-mer's key is its 2-bit codes packed first base
+// LOWEST (bits 2i..2i+1 = base i), so the keys of every k-mer in a run of bytes are shifts of one
+// packed word computed 4 bytes at a time (SWAR); a k-mer holding any other byte gets exotic_key()
+// (high bit set, confirmed by a byte compare).  Equal pure keys <=> equal bytes.  Each kernel
+// uses one convention for all the keys it compares (walk, full sweeps, local segments).
+// ---------------------------------------------------------------------------------------------
+// 4 bytes -> their 2-bit codes in 8 bits (byte i at bits 2i), and `diff` nonzero in exactly the
+// bytes that are not A/C/G/T: code = ((c >> 1) ^ (c >> 2)) & 3 maps A,C,G,T -> 0,1,2,3, and a
+// byte-permute of "ACGT" by the codes rebuilds the byte iff it was one of them.
+__device__ __forceinline__ uint32_t swar_codes(uint32_t w, uint32_t& diff) {
+    const uint32_t c = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
+    diff = __builtin_amdgcn_perm(0x54474341u, 0x54474341u, c) ^ w;
+    const uint32_t p = c | (c >> 6);
+    return (p | (p >> 12)) & 0xffu;
+}
+// bit i set <=> byte i of `diff` is nonzero
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t diff) {
+    const uint32_t nz = ((((diff & 0x7f7f7f7fu) + 0x7f7f7f7fu) | diff) & 0x80808080u) >> 7;
+    return (nz | (nz >> 7) | (nz >> 14) | (nz >> 21)) & 0xfu;
+}
+// ND consecutive words -> packed codes (byte i at bits 2i) and the non-ACGT byte mask
+template <int ND>
+__device__ __forceinline__ void pack_codes(const uint32_t (&w)[ND], uint64_t& code, uint32_t& bad) {
+    uint32_t d[ND], acc = 0;
+    code = 0;
+#pragma unroll
+    for (int i = 0; i < ND; i++) {
+        code |= (uint64_t)swar_codes(w[i], d[i]) << (8 * i);
+        acc |= d[i];
+    }
+    bad = 0;
+    if (acc) {   // rare: some byte is not A/C/G/T
+#pragma unroll
+        for (int i = 0; i < ND; i++) bad |= nz_bytes(d[i]) << (4 * i);
+    }
+}
+// ND words from an arbitrary (global or LDS) address: ND+1 aligned dword loads
+template <int ND>
+__device__ __forceinline__ void loadw(const uint8_t* p, uint32_t (&o)[ND]) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t v[ND + 1];
+#pragma unroll
+    for (int i = 0; i <= ND; i++) v[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < ND; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+}
+// scalar form (any k <= 15)
+__device__ __forceinline__ uint32_t walk_key(const uint8_t* s, int k) {
+    uint32_t code = 0;
+    for (int i = 0; i < k; i++) {
+        const uint32_t b = base2(s[i]);
+        if (b > 3) return exotic_key(s, k);
+        code |= b << (2 * i);
+    }
+    return code;
+}
+
+// ---------------------------------------------------------------------------------------------
 // wave64 primitives
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }

@@ -65,35 +65,88 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_first_match(const uint8_t* __res
 }
 
 // ---------------------------------------------------------------------------------------------
-// FASTA strip.  A line's fate is decided by its first byte (REF: '>' lines dropped; TGT: only the
-// header line [h, he) dropped); every isspace byte is dropped.  In REF mode bytes before the first
-// line start of a tile inherit the status of an earlier tile: the per-tile summary keeps those
-// bytes apart (a) from the ones whose status is known (b).
+// FASTA strip (+ optional byte filter in the same pass).  A line's fate is decided by its first
+// byte (REF: '>' lines dropped; TGT: only the header line [h, he) dropped); every isspace byte is
+// dropped.  In REF mode bytes before the first line start of a tile inherit the status of an
+// earlier tile: the per-tile summary keeps those bytes apart (a) from the ones whose status is
+// known (b).  The filter output (N erase + toupper) is the filter applied to the strip output, so
+// it carries the same (a, b) split (fa, fb).
+//
+// Writes are staged: every thread drops its kept bytes into an LDS copy of the tile's output at
+// its block-scan offset, then the block stores the tile's output range with aligned dword stores.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint8_t wb(const uint32_t (&w)[PER_T / 4], int i) { return (uint8_t)(w[i >> 2] >> (8 * (i & 3))); }
+
+__device__ __forceinline__ void load_words(const uint8_t* __restrict__ buf, int64_t n, int64_t off, uint32_t (&w)[PER_T / 4]) {
+    if (off + PER_T <= n && (((uintptr_t)(buf + off)) & 15) == 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(buf + off);
+        const uint4 v0 = p[0], v1 = p[1];
+        w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w; w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < PER_T / 4; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int64_t p = off + 4 * q + i;
+                v |= (uint32_t)(p < n ? buf[p] : (uint8_t)' ') << (8 * i);
+            }
+            w[q] = v;
+        }
+    }
+}
+
+__device__ __forceinline__ bool filter_keep(FilterMode m, uint8_t c) {
+    if (m == FILTER_DROP_N_UPPER) return c != 'N' && c != 'n';
+    if (m == FILTER_DROP_UPPERN_ONLY) return c != 'N';
+    return true;
+}
+
+// Block-cooperative store of the `cnt` bytes staged in LDS (4-byte aligned, cnt + 4 readable)
+// to out[g0, g0 + cnt): head bytes, aligned dword body, tail bytes.
+__device__ __forceinline__ void stage_out(const uint32_t* __restrict__ st4, int cnt, uint8_t* __restrict__ out, int64_t g0) {
+    const uint8_t* st = reinterpret_cast<const uint8_t*>(st4);
+    const int t = (int)threadIdx.x;
+    int head = (int)((4 - (g0 & 3)) & 3);
+    if (head > cnt) head = cnt;
+    if (t < head) out[g0 + t] = st[t];
+    const int nd = (cnt - head) >> 2;
+    uint32_t* o4 = reinterpret_cast<uint32_t*>(out + g0 + head);
+    for (int d = t; d < nd; d += (int)blockDim.x) {
+        const int o = head + 4 * d;
+        o4[d] = __builtin_amdgcn_alignbyte(st4[(o >> 2) + 1], st4[o >> 2], (uint32_t)(o & 3));
+    }
+    const int done = head + 4 * nd;
+    if (t < cnt - done) out[g0 + done + t] = st[done + t];
+}
+
 struct ThreadSum {
-    int32_t a, b;   // kept-if-carry-keeps count, kept count
-    int32_t last;   // status of the last line start in range: -1 none, 0 drop, 1 keep
+    int32_t a, b;     // kept-if-carry-keeps count, kept count
+    int32_t fa, fb;   // the same, counting only bytes the filter keeps
+    int32_t last;     // status of the last line start in range: -1 none, 0 drop, 1 keep
 };
 
-__device__ __forceinline__ ThreadSum thread_summary(IngestMode mode, const uint8_t (&b)[PER_T], uint8_t prev,
-                                                    int64_t off, int64_t n, int64_t h, int64_t he) {
-    ThreadSum r{0, 0, -1};
+__device__ __forceinline__ ThreadSum thread_summary(IngestMode mode, FilterMode fm, const uint32_t (&w)[PER_T / 4],
+                                                    uint8_t prev, int64_t off, int64_t n, int64_t h, int64_t he) {
+    ThreadSum r{0, 0, 0, 0, -1};
     int cur = -1;
 #pragma unroll
     for (int i = 0; i < PER_T; i++) {
         const int64_t pos = off + i;
-        const uint8_t c = b[i];
-        const uint8_t pc = i ? b[i - 1] : prev;
+        const uint8_t c = wb(w, i);
+        const uint8_t pc = i ? wb(w, i - 1) : prev;
+        const bool fk = filter_keep(fm, c);
         if (mode == INGEST_REF) {
             if (pos < n && (pos == 0 || pc == '\n')) cur = (c == '>') ? 0 : 1;
             const bool sp = pos >= n || c_isspace(c);
             if (!sp) {
-                if (cur < 0) r.a++;
-                else r.b += cur;
+                if (cur < 0) { r.a++; r.fa += fk; }
+                else if (cur) { r.b++; r.fb += fk; }
             }
         } else {
             const bool keep = pos < n && !c_isspace(c) && !(pos >= h && pos < he);
             r.b += keep;
+            r.fb += keep && fk;
         }
     }
     r.last = cur;
@@ -119,104 +172,123 @@ __device__ __forceinline__ int32_t block_prior_status(int32_t last, int32_t* tmp
     return ex >= 0 ? ex : carry;
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(IngestMode mode, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(IngestMode mode, FilterMode fm, const uint8_t* __restrict__ buf,
                                                               int64_t n, const int64_t* __restrict__ hdr,
                                                               int64_t* __restrict__ ta, int64_t* __restrict__ tb,
+                                                              int64_t* __restrict__ tfa, int64_t* __restrict__ tfb,
                                                               int32_t* __restrict__ tlast) {
     __shared__ int32_t tmp[8];
-    __shared__ int64_t tmp64[8];
+    __shared__ int32_t tmp32[8];
     const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
-    uint8_t b[PER_T];
-    load_bytes(buf, n, off, b);
+    uint32_t w[PER_T / 4];
+    load_words(buf, n, off, w);
     const uint8_t prev = (off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n';
     const int64_t h = mode == INGEST_TGT ? hdr[0] : 0, he = mode == INGEST_TGT ? hdr[1] : 0;
-    ThreadSum r = thread_summary(mode, b, prev, off, n, h, he);
+    ThreadSum r = thread_summary(mode, fm, w, prev, off, n, h, he);
     const int32_t prior = block_prior_status(r.last, tmp);
     // a-bytes of a thread with a prior line start in the block are resolved now
-    int64_t A = prior < 0 ? r.a : 0;
-    int64_t B = r.b + (prior == 1 ? r.a : 0);
-    int64_t At, Bt;
-    block_excl_add<int64_t>(A, tmp64, &At);
-    block_excl_add<int64_t>(B, tmp64, &Bt);
+    const int32_t A = prior < 0 ? r.a : 0, B = r.b + (prior == 1 ? r.a : 0);
+    const int32_t FA = prior < 0 ? r.fa : 0, FB = r.fb + (prior == 1 ? r.fa : 0);
+    int32_t At, Bt, FAt, FBt;
+    block_excl_add<int32_t>(A, tmp32, &At);
+    block_excl_add<int32_t>(B, tmp32, &Bt);
+    block_excl_add<int32_t>(FA, tmp32, &FAt);
+    block_excl_add<int32_t>(FB, tmp32, &FBt);
     // block last status = prior status of a virtual thread after the last one
-    int32_t mylast = r.last >= 0 ? r.last : prior;
+    const int32_t mylast = r.last >= 0 ? r.last : prior;
     if (threadIdx.x == blockDim.x - 1) {
         ta[blockIdx.x] = At;
         tb[blockIdx.x] = Bt;
+        tfa[blockIdx.x] = FAt;
+        tfb[blockIdx.x] = FBt;
         tlast[blockIdx.x] = mylast;
     }
 }
 
-// one 1024-thread block: compose the tile summaries in order -> per-tile output offset and
-// carry-in status; total kept bytes -> *d_len
+// one 1024-thread block: compose the tile summaries in order -> per-tile output offsets (strip and
+// filter) and carry-in status; totals -> d_len[0], d_len2[0]
 __global__ __launch_bounds__(1024) void k_strip_scan(int64_t ntiles, const int64_t* __restrict__ ta,
-                                                     const int64_t* __restrict__ tb,
-                                                     const int32_t* __restrict__ tlast,
-                                                     int64_t* __restrict__ toff, int32_t* __restrict__ tcarry,
-                                                     int64_t* __restrict__ d_len) {
-    __shared__ int64_t sA[1024], sB[1024];
+                                                     const int64_t* __restrict__ tb, const int64_t* __restrict__ tfa,
+                                                     const int64_t* __restrict__ tfb, const int32_t* __restrict__ tlast,
+                                                     int64_t* __restrict__ toff, int64_t* __restrict__ toff2,
+                                                     int32_t* __restrict__ tcarry, int64_t* __restrict__ d_len,
+                                                     int64_t* __restrict__ d_len2) {
+    __shared__ int64_t sA[1024], sB[1024], sFA[1024], sFB[1024];
     __shared__ int32_t sL[1024];
     const int64_t per = (ntiles + 1023) / 1024;
     const int64_t t0 = (int64_t)threadIdx.x * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
-    int64_t A = 0, B = 0;
+    int64_t A = 0, B = 0, FA = 0, FB = 0;
     int32_t last = -1;
     for (int64_t t = t0; t < t1; t++) {
         const int32_t yl = tlast[t];
-        const int64_t ya = ta[t], yb = tb[t];
+        const int64_t ya = ta[t], yb = tb[t], yfa = tfa[t], yfb = tfb[t];
         B += yb + (last == 1 ? ya : 0);
-        if (last < 0) A += ya;
+        FB += yfb + (last == 1 ? yfa : 0);
+        if (last < 0) { A += ya; FA += yfa; }
         if (yl >= 0) last = yl;
     }
-    sA[threadIdx.x] = A; sB[threadIdx.x] = B; sL[threadIdx.x] = last;
+    sA[threadIdx.x] = A; sB[threadIdx.x] = B; sFA[threadIdx.x] = FA; sFB[threadIdx.x] = FB; sL[threadIdx.x] = last;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int64_t off = 0;
+        int64_t off = 0, off2 = 0;
         int32_t carry = 1;
         for (int i = 0; i < 1024; i++) {
-            const int64_t a = sA[i], b = sB[i];
+            const int64_t a = sA[i], b = sB[i], fa = sFA[i], fb = sFB[i];
             const int32_t l = sL[i];
-            sA[i] = off;        // offset at start of thread i's range
+            sA[i] = off;        // offsets at start of thread i's range
+            sFA[i] = off2;
             sL[i] = carry;      // carry-in status
             off += b + (carry == 1 ? a : 0);
+            off2 += fb + (carry == 1 ? fa : 0);
             if (l >= 0) carry = l;
         }
         *d_len = off;
+        if (d_len2) *d_len2 = off2;
     }
     __syncthreads();
-    int64_t off = sA[threadIdx.x];
+    int64_t off = sA[threadIdx.x], off2 = sFA[threadIdx.x];
     int32_t carry = sL[threadIdx.x];
     for (int64_t t = t0; t < t1; t++) {
         toff[t] = off;
+        toff2[t] = off2;
         tcarry[t] = carry;
         off += tb[t] + (carry == 1 ? ta[t] : 0);
+        off2 += tfb[t] + (carry == 1 ? tfa[t] : 0);
         if (tlast[t] >= 0) carry = tlast[t];
     }
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(IngestMode mode, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(IngestMode mode, FilterMode fm, const uint8_t* __restrict__ buf,
                                                             int64_t n, const int64_t* __restrict__ hdr,
                                                             const int64_t* __restrict__ toff,
+                                                            const int64_t* __restrict__ toff2,
                                                             const int32_t* __restrict__ tcarry,
-                                                            uint8_t* __restrict__ out, int32_t* __restrict__ flags) {
+                                                            uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
+                                                            int32_t* __restrict__ flags) {
     __shared__ int32_t tmp[8];
-    __shared__ int64_t tmp64[8];
+    __shared__ int32_t tmp32[8];
+    __shared__ uint32_t st1[INGEST_TILE / 4 + 2];
+    __shared__ uint32_t st2[INGEST_TILE / 4 + 2];
     const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
-    uint8_t b[PER_T];
-    load_bytes(buf, n, off, b);
+    uint32_t w[PER_T / 4];
+    load_words(buf, n, off, w);
     const uint8_t prev = (off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n';
     const int64_t h = mode == INGEST_TGT ? hdr[0] : 0, he = mode == INGEST_TGT ? hdr[1] : 0;
-    ThreadSum r = thread_summary(mode, b, prev, off, n, h, he);
+    ThreadSum r = thread_summary(mode, fm, w, prev, off, n, h, he);
     int32_t prior = block_prior_status(r.last, tmp);
     if (prior < 0) prior = tcarry[blockIdx.x];
-    const int64_t mine = r.b + (prior == 1 ? r.a : 0);
-    int64_t pos = toff[blockIdx.x] + block_excl_add<int64_t>(mine, tmp64, nullptr);
+    int32_t tot1, tot2;
+    int32_t p1 = block_excl_add<int32_t>(r.b + (prior == 1 ? r.a : 0), tmp32, &tot1);
+    int32_t p2 = out2 ? block_excl_add<int32_t>(r.fb + (prior == 1 ? r.fa : 0), tmp32, &tot2) : 0;
+    uint8_t* s1 = reinterpret_cast<uint8_t*>(st1);
+    uint8_t* s2 = reinterpret_cast<uint8_t*>(st2);
     int cur = prior;
     bool paren = false;
 #pragma unroll
     for (int i = 0; i < PER_T; i++) {
         const int64_t p = off + i;
-        const uint8_t c = b[i];
-        const uint8_t pc = i ? b[i - 1] : prev;
+        const uint8_t c = wb(w, i);
+        const uint8_t pc = i ? wb(w, i - 1) : prev;
         bool keep;
         if (mode == INGEST_REF) {
             if (p < n && (p == 0 || pc == '\n')) cur = (c == '>') ? 0 : 1;
@@ -225,50 +297,15 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(IngestMode mode, con
             keep = p < n && !c_isspace(c) && !(p >= h && p < he);
         }
         if (keep) {
-            out[pos++] = c;
+            s1[p1++] = c;
             paren |= (c == '(');
+            if (out2 && filter_keep(fm, c)) s2[p2++] = c_toupper(c);
         }
     }
-    if (flags && paren) atomicOr(flags, 1);
-}
-
-// ---------------------------------------------------------------------------------------------
-// byte filter (count per tile -> scan -> write)
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool filter_keep(FilterMode m, uint8_t c) {
-    if (m == FILTER_DROP_N_UPPER) return c != 'N' && c != 'n';
-    if (m == FILTER_DROP_UPPERN_ONLY) return c != 'N';
-    return true;
-}
-
-__global__ __launch_bounds__(SCCG_BLOCK) void k_filter_count(FilterMode m, const uint8_t* __restrict__ in,
-                                                             int64_t n, int64_t* __restrict__ cnt) {
-    __shared__ int64_t tmp64[8];
-    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
-    uint8_t b[PER_T];
-    load_bytes(in, n, off, b);
-    int64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < PER_T; i++) c += (off + i < n) && filter_keep(m, b[i]);
-    int64_t tot;
-    block_excl_add<int64_t>(c, tmp64, &tot);
-    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(SCCG_BLOCK) void k_filter_write(FilterMode m, const uint8_t* __restrict__ in,
-                                                             int64_t n, const int64_t* __restrict__ toff,
-                                                             uint8_t* __restrict__ out) {
-    __shared__ int64_t tmp64[8];
-    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
-    uint8_t b[PER_T];
-    load_bytes(in, n, off, b);
-    int64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < PER_T; i++) c += (off + i < n) && filter_keep(m, b[i]);
-    int64_t pos = toff[blockIdx.x] + block_excl_add<int64_t>(c, tmp64, nullptr);
-#pragma unroll
-    for (int i = 0; i < PER_T; i++)
-        if (off + i < n && filter_keep(m, b[i])) out[pos++] = c_toupper(b[i]);
+    if (flags && __ballot(paren) && lane_id() == 0) atomicOr(flags, 1);
+    __syncthreads();
+    stage_out(st1, tot1, out, toff[blockIdx.x]);
+    if (out2) stage_out(st2, tot2, out2, toff2[blockIdx.x]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -388,35 +425,21 @@ int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t
 }
 
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,
-                       int64_t* d_len, int32_t* d_flags, const IngestScratch& sc, int64_t* /*d_partial*/,
-                       hipStream_t s) {
+                       int64_t* d_len, int32_t* d_flags, const IngestScratch& sc, hipStream_t s, FilterMode fmode,
+                       uint8_t* out2, int64_t* d_len2) {
     if (n <= 0) {
         SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));
+        if (d_len2) SCCG_HIP(hipMemsetAsync(d_len2, 0, sizeof(int64_t), s));
         return 0;
     }
+    if (!out2) fmode = FILTER_UPPER;   // second output unused
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
-    hipLaunchKernelGGL(k_strip_summary, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, buf, n, d_header,
-                       sc.tile_a, sc.tile_b, sc.tile_last);
-    hipLaunchKernelGGL(k_strip_scan, dim3(1), dim3(1024), 0, s, ntiles, sc.tile_a, sc.tile_b, sc.tile_last,
-                       sc.tile_off, sc.tile_carry, d_len);
-    PROF_LAUNCH(PROF_STRIP, s, k_strip_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, buf, n, d_header,
-                       sc.tile_off, sc.tile_carry, out, d_flags);
-    SCCG_HIP(hipGetLastError());
-    return 0;
-}
-
-int launch_filter(FilterMode mode, const uint8_t* in, int64_t n, uint8_t* out, int64_t* d_len,
-                  int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s) {
-    if (n <= 0) {
-        SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));
-        return 0;
-    }
-    const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
-    hipLaunchKernelGGL(k_filter_count, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, in, n, d_tile_cnt);
-    int rc = dev_excl_sum(d_tile_cnt, d_tile_cnt, ntiles, d_len, d_partial, s);
-    if (rc) return rc;
-    PROF_LAUNCH(PROF_FILTER, s, k_filter_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, in, n,
-                       (const int64_t*)d_tile_cnt, out);
+    hipLaunchKernelGGL(k_strip_summary, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, fmode, buf, n, d_header,
+                       sc.tile_a, sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last);
+    hipLaunchKernelGGL(k_strip_scan, dim3(1), dim3(1024), 0, s, ntiles, sc.tile_a, sc.tile_b, sc.tile_fa, sc.tile_fb,
+                       sc.tile_last, sc.tile_off, sc.tile_off2, sc.tile_carry, d_len, d_len2);
+    PROF_LAUNCH(PROF_STRIP, s, k_strip_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, fmode, buf, n,
+                d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

@@ -44,14 +44,17 @@ int dev_excl_max(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, i
 // ---- ingest.hip -------------------------------------------------------------------------------
 constexpr int INGEST_TILE = 8192;  // bytes per 256-thread tile (32 per thread)
 enum IngestMode { INGEST_REF = 0, INGEST_TGT = 1 };
-enum FilterMode { FILTER_DROP_N_UPPER = 0, FILTER_DROP_UPPERN_ONLY = 1, FILTER_UPPER = 2 };
+enum FilterMode { FILTER_DROP_N_UPPER = 0, FILTER_DROP_UPPERN_ONLY = 1, FILTER_UPPER = 2 };   // all uppercase
 enum RunPred { RUN_LOWER = 0, RUN_N = 1 };
 
 struct IngestScratch {
     int64_t* tile_a;      // per tile
     int64_t* tile_b;
+    int64_t* tile_fa;
+    int64_t* tile_fb;
     int32_t* tile_last;
     int64_t* tile_off;
+    int64_t* tile_off2;
     int32_t* tile_carry;
     int64_t* scalars;     // [0] header start, [1] header end, [2] out len, [3] flags
 };
@@ -65,13 +68,13 @@ int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, 
                        int64_t* ticket_slot, hipStream_t s);
 // read_genomes_from_files (compression.cpp:193-218): compacts the kept, non-space bytes of `buf`
 // into `out` (original case); *d_len = kept count; in TGT mode lines [h, he) are the header.
-// d_flags (optional) gets bit0 when a kept byte is '('.
+// d_flags (optional) gets bit0 when a kept byte is '('.  With out2, the same pass also writes the
+// kept bytes through the byte filter + case map `fmode` (N erase of compression.cpp:556-557 /
+// decompression.cpp:108-110) into out2, *d_len2 = their count.
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header,
                        uint8_t* out, int64_t* d_len, int32_t* d_flags, const IngestScratch& sc,
-                       int64_t* d_partial, hipStream_t s);
-// byte filter + case map (N erase of compression.cpp:556-557 / decompression.cpp:108-110)
-int launch_filter(FilterMode mode, const uint8_t* in, int64_t n, uint8_t* out, int64_t* d_len,
-                  int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s);
+                       hipStream_t s, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
+                       int64_t* d_len2 = nullptr);
 // maximal runs of a predicate -> start/end (inclusive) arrays; *d_nruns = count
 int launch_runs(RunPred pred, const uint8_t* s_in, int64_t n, int32_t* run_s, int32_t* run_e,
                 int64_t* d_nruns, int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s);

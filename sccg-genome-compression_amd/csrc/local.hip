@@ -4,57 +4,54 @@
 //   match_sequences(r_i, t_i, k, 0, false, i*L)   compression.cpp:36-179 with global=false
 //   extend_alignment       compression.cpp:27-34
 //
-// One wavefront owns one 1000-base segment pair: both segments live in LDS (uppercased on load),
-// the reference segment's k-mers go into an LDS open-addressing table (2048 u16 slots), the
-// target's "has any candidate" bits are precomputed lane-parallel, and the walk itself is a
-// wave-uniform loop that jumps from hit to hit.  Candidates are enumerated 64 table slots at a
-// time, extended lane-parallel and reduced with the order-free form of the reference's selection
-// loop (tested against the oracle).  Segments are independent, so a launch covers
-// every segment; the switch point is found afterwards by a state-machine scan.
+// One wavefront owns one 1000-base segment pair: both segments live in LDS (uppercased on load).
+// The reference segment's k-mers are counting-sorted into 1024 hash buckets (one LDS atomic add
+// per k-mer for its rank in the bucket, a wave scan for the bucket starts, one scatter) -- no
+// probing, no CAS retries, and duplicate k-mers (poly-A, microsatellites) cost nothing extra.
+// The target's "has any candidate" bits are computed lane-parallel from the buckets, and the walk
+// is a wave-uniform loop that jumps from hit to hit.  A hit's candidates (its bucket's entries
+// with the same k-mer) are extended by the whole wave one at a time, or one per lane when there
+// are many, and reduced with the order-free form of the reference's selection loop (SURVEY.md
+// A.4, tested against the oracle).  Segments are independent, so a launch covers every segment;
+// the switch point is found afterwards by a state-machine scan.
 #include "internal.h"
+
+#include <cstdio>
+#include <cstdlib>
 
 namespace {
 
 constexpr int WPB = 4;            // segments (waves) per block
 constexpr int SEGB = 1024 + 16;   // LDS bytes per segment string
-constexpr int TBITS = 11;         // 2048 table slots
-constexpr int TSLOTS = 1 << TBITS;
+constexpr int NBB = 10;           // 1024 k-mer buckets
+constexpr int NB = 1 << NBB;
+constexpr int MANY = 4;           // more candidates than this: extend one per lane
 
 struct SegLds {
     uint8_t r[SEGB];
     uint8_t t[SEGB];
-    uint32_t keys[1000];
-    uint32_t table[TSLOTS / 2];   // two u16 slots per word: value = position + 1, 0 = empty
+    uint32_t skey[1024];          // reference k-mer keys, grouped by bucket
+    uint16_t spos[1024];          // their positions
+    uint32_t bstart[NB + 1];      // bucket b holds entries [bstart[b], bstart[b+1])
     uint64_t hits[16];            // bit p: target k-mer at p has >= 1 candidate
 };
-
-__device__ __forceinline__ uint32_t tab_get(const uint32_t* tab, int slot) {
-    return (tab[slot >> 1] >> ((slot & 1) * 16)) & 0xffffu;
-}
-
-__device__ __forceinline__ void tab_insert(uint32_t* tab, uint32_t key, uint32_t val) {
-    int slot = (int)slot_hash(key, TBITS);
-    for (;;) {
-        uint32_t* w = &tab[slot >> 1];
-        const int sh = (slot & 1) * 16;
-        uint32_t old = *w;
-        while (((old >> sh) & 0xffffu) == 0) {
-            const uint32_t prev = atomicCAS(w, old, old | (val << sh));
-            if (prev == old) return;
-            old = prev;
-        }
-        slot = (slot + 1) & (TSLOTS - 1);
-    }
-}
 
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int k) {
     for (int i = 0; i < k; i++) if (a[i] != b[i]) return false;
     return true;
 }
 
+// packed key (common.h) of the K-mer at s (LDS), scalar
 template <int K>
-__device__ __forceinline__ uint32_t seg_key(const uint8_t* s, int p) {
-    return kmer_key(s + p, K);
+__device__ __forceinline__ uint32_t seg_key(const uint8_t* s) {
+    uint32_t code = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const uint32_t b = base2(s[i]);
+        if (b > 3) return exotic_key(s, K);
+        code |= b << (2 * i);
+    }
+    return code;
 }
 
 __device__ __forceinline__ uint64_t pick_key(int p, int pme) {
@@ -62,7 +59,28 @@ __device__ __forceinline__ uint64_t pick_key(int p, int pme) {
     return ((uint64_t)(uint32_t)(d < 0 ? -d : d) << 32) | (uint32_t)p;
 }
 
+// uppercase 4 bytes (compression.cpp:369-370 toupper)
+__device__ __forceinline__ uint32_t upper4(uint32_t w) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) o |= (uint32_t)c_toupper((uint8_t)(w >> (8 * i))) << (8 * i);
+    return o;
+}
+
+// keys of the 16 K-mers starting at s[0..16) (s 16-byte aligned in LDS; 32 bytes readable)
 template <int K>
+__device__ __forceinline__ void keys16(const uint8_t* s, uint64_t& code, uint32_t& bad) {
+    const uint32_t* w4 = reinterpret_cast<const uint32_t*>(s);
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = w4[i];
+    pack_codes<8>(w, code, bad);
+}
+
+// SCCG_DEBUG: phase ticks (10 ns) summed over segments: load, keys, insert, hits, walk, count
+__device__ unsigned long long g_local_dbg[8];
+
+template <int K, bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, const uint8_t* __restrict__ R, int64_t nR,
                                                            const uint8_t* __restrict__ T, int64_t nT, int64_t seg0,
                                                            int64_t seg_end, uint32_t* __restrict__ recs,
@@ -76,78 +94,99 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
     const int64_t base = seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
     const int nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
+    constexpr uint32_t MASK = (1u << (2 * K)) - 1u, KM = (1u << K) - 1u;
+    uint64_t tq = DBG ? wall_clock64() : 0, tph[5] = {0, 0, 0, 0, 0};
+    auto tick = [&](int i) {
+        if (DBG) { const uint64_t t = wall_clock64(); tph[i] += t - tq; tq = t; }
+    };
 
-    // ---- load both segments, uppercased (compression.cpp:369-370, :386-389)
+    // ---- load both segments, uppercased (compression.cpp:369-370, :386-389); base is a multiple
+    //      of 1000, so the dword loads are aligned; bytes past the segment end read as 0
     bool non_n = false;
-    for (int i = lane; i < SEGB; i += 64) {
-        uint8_t rc = i < nr ? R[base + i] : (uint8_t)0;
-        uint8_t tc = i < nt ? T[base + i] : (uint8_t)0;
-        if (upper) { rc = c_toupper(rc); tc = c_toupper(tc); }
-        L.r[i] = rc;
-        L.t[i] = tc;
-        non_n |= (i < nt && tc != 'N');
+    {
+        const uint32_t* R4 = reinterpret_cast<const uint32_t*>(R + base);
+        const uint32_t* T4 = reinterpret_cast<const uint32_t*>(T + base);
+        uint32_t* r4 = reinterpret_cast<uint32_t*>(L.r);
+        uint32_t* t4 = reinterpret_cast<uint32_t*>(L.t);
+        for (int i = lane; i < SEGB / 4; i += 64) {
+            const int b0 = 4 * i;
+            uint32_t rw = b0 < nr ? R4[i] : 0u, tw = b0 < nt ? T4[i] : 0u;
+            if (nr - b0 < 4) rw &= nr - b0 <= 0 ? 0u : (1u << (8 * (nr - b0))) - 1u;
+            if (nt - b0 < 4) tw &= nt - b0 <= 0 ? 0u : (1u << (8 * (nt - b0))) - 1u;
+            if (upper) { rw = upper4(rw); tw = upper4(tw); }
+            r4[i] = rw;
+            t4[i] = tw;
+#pragma unroll
+            for (int q = 0; q < 4; q++) non_n |= (b0 + q < nt && (uint8_t)(tw >> (8 * q)) != 'N');
+        }
     }
-    for (int i = lane; i < TSLOTS / 2; i += 64) L.table[i] = 0;
     if (lane < 16) L.hits[lane] = 0;
     non_n = __ballot(non_n) != 0;
     wave_sync();
+    tick(0);
 
-    // ---- H: every k-mer of the reference segment (compression.cpp:41-47)
+    // ---- H: every k-mer of the reference segment (compression.cpp:41-47), counting-sorted by
+    //      bucket; lane l owns starts 16l..16l+15
     const int lastr = nr - K;
+    for (int i = lane; i < NB; i += 64) L.bstart[i] = 0;
+    wave_sync();
     {
         const int p0 = lane * 16;
-        uint32_t code = 0;
-        int lastbad = -1000;
-        constexpr uint32_t MASK = (K >= 16) ? 0xffffffffu : ((1u << (2 * K)) - 1u);
-        for (int i = 0; i < 16 + K - 1; i++) {
-            const int pos = p0 + i;
-            const uint8_t c = pos < nr ? L.r[pos] : (uint8_t)0;
-            uint32_t b = base2(c);
-            if (b > 3) { lastbad = i; b = 0; }
-            code = ((code << 2) | b) & MASK;
-            const int st = i - (K - 1);
-            if (st >= 0) {
-                const int p = p0 + st;
-                if (p <= lastr) {
-                    const uint32_t key = lastbad >= st ? exotic_key(&L.r[p], K) : code;
-                    L.keys[p] = key;
-                }
+        uint64_t code;
+        uint32_t bad;
+        keys16<K>(&L.r[p0], code, bad);
+        uint32_t key[16], rank[16];
+#pragma unroll
+        for (int st = 0; st < 16; st++) {
+            const int p = p0 + st;
+            key[st] = (bad >> st) & KM ? exotic_key(&L.r[p], K) : (uint32_t)(code >> (2 * st)) & MASK;
+            if (p <= lastr) rank[st] = atomicAdd(&L.bstart[slot_hash(key[st], NBB)], 1u);
+        }
+        wave_sync();
+        // bucket starts: exclusive scan of the counts (16 buckets per lane)
+        uint32_t c[16], run = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) { c[i] = L.bstart[16 * lane + i]; run += c[i]; }
+        const uint32_t incl = wave_incl_add(run);
+        uint32_t o = incl - run;
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < 16; i++) { L.bstart[16 * lane + i] = o; o += c[i]; }
+        if (lane == 63) L.bstart[NB] = o;
+        wave_sync();
+#pragma unroll
+        for (int st = 0; st < 16; st++) {
+            const int p = p0 + st;
+            if (p <= lastr) {
+                const uint32_t at = L.bstart[slot_hash(key[st], NBB)] + rank[st];
+                L.skey[at] = key[st];
+                L.spos[at] = (uint16_t)p;
             }
         }
     }
     wave_sync();
-    for (int p = lane; p <= lastr; p += 64) tab_insert(L.table, L.keys[p], (uint32_t)p + 1);
-    wave_sync();
+    tick(1);
+    tick(2);
 
     // ---- hit bits for every target k-mer start (compression.cpp:77 "H.find")
     const int lastk = nt - K;
     {
         const int p0 = lane * 16;
         uint32_t mask16 = 0;
-        uint32_t code = 0;
-        int lastbad = -1000;
-        constexpr uint32_t MASK = (K >= 16) ? 0xffffffffu : ((1u << (2 * K)) - 1u);
-        for (int i = 0; i < 16 + K - 1; i++) {
-            const int pos = p0 + i;
-            const uint8_t c = pos < nt ? L.t[pos] : (uint8_t)0;
-            uint32_t b = base2(c);
-            if (b > 3) { lastbad = i; b = 0; }
-            code = ((code << 2) | b) & MASK;
-            const int st = i - (K - 1);
-            if (st >= 0) {
+        if (lastr >= 0) {
+            uint64_t code;
+            uint32_t bad;
+            keys16<K>(&L.t[p0], code, bad);
+            for (int st = 0; st < 16; st++) {
                 const int p = p0 + st;
-                if (p <= lastk && lastr >= 0) {
-                    const uint32_t key = lastbad >= st ? exotic_key(&L.t[p], K) : code;
-                    int slot = (int)slot_hash(key, TBITS);
-                    for (int probes = 0; probes < TSLOTS; probes++) {
-                        const uint32_t v = tab_get(L.table, slot);
-                        if (!v) break;
-                        const int q = (int)v - 1;
-                        if (L.keys[q] == key && (key < KEY_EXOTIC || bytes_eq(&L.r[q], &L.t[p], K))) {
-                            mask16 |= 1u << st;
-                            break;
-                        }
-                        slot = (slot + 1) & (TSLOTS - 1);
+                if (p > lastk) break;
+                const uint32_t key = (bad >> st) & KM ? exotic_key(&L.t[p], K) : (uint32_t)(code >> (2 * st)) & MASK;
+                const uint32_t b = slot_hash(key, NBB);
+                const int e1 = (int)L.bstart[b + 1];
+                for (int e = (int)L.bstart[b]; e < e1; e++) {
+                    if (L.skey[e] == key && (key < KEY_EXOTIC || bytes_eq(&L.r[L.spos[e]], &L.t[p], K))) {
+                        mask16 |= 1u << st;
+                        break;
                     }
                 }
             }
@@ -155,6 +194,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
         reinterpret_cast<uint16_t*>(L.hits)[lane] = (uint16_t)mask16;
     }
     wave_sync();
+    tick(3);
 
     // ---- the greedy walk (compression.cpp:64-161), wave-uniform
     uint32_t* out = recs + seg * SEG_REC_CAP;
@@ -176,40 +216,72 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
             nrec++;
             lit += nxt - idx;
         }
-        const uint32_t key = seg_key<K>(L.t, nxt);
-        const int h0 = (int)slot_hash(key, TBITS);
+        const uint32_t key = seg_key<K>(&L.t[nxt]);
+        const uint32_t bk = slot_hash(key, NBB);
+        const int e0 = (int)L.bstart[bk], e1 = (int)L.bstart[bk + 1];
+        // candidates: the bucket's entries holding this k-mer, 64 entries per step
         int bl = 0, bcnt = 0;
         bool bhas0 = false;
         uint64_t bkey = ~0ull;
-        for (int b0 = 0; b0 < TSLOTS; b0 += 64) {
-            const uint32_t v = tab_get(L.table, (h0 + b0 + lane) & (TSLOTS - 1));
-            const unsigned long long em = __ballot(v == 0);
-            const int fe = first_lane(em);
-            if (lane < fe) {
-                const int q = (int)v - 1;
-                if (L.keys[q] == key && (key < KEY_EXOTIC || bytes_eq(&L.r[q], &L.t[nxt], K))) {
-                    int l = K;   // extend_alignment (compression.cpp:27-34)
-                    while (q + l < nr && nxt + l < nt && L.r[q + l] == L.t[nxt + l]) ++l;
-                    if (l > bl) {
-                        bl = l; bcnt = 1; bhas0 = (q == 0); bkey = q ? pick_key(q, pme) : ~0ull;
-                    } else if (l == bl) {
+        for (int eb = e0; eb < e1; eb += 64) {
+            const int e = eb + lane;
+            int q = -1;
+            if (e < e1 && L.skey[e] == key) {
+                q = L.spos[e];
+                if (key >= KEY_EXOTIC && !bytes_eq(&L.r[q], &L.t[nxt], K)) q = -1;
+            }
+            unsigned long long cm = __ballot(q >= 0);
+            if (__popcll(cm) <= MANY) {
+                while (cm) {   // few candidates: the whole wave extends each
+                    const int cl = __ffsll((long long)cm) - 1;
+                    cm &= cm - 1;
+                    const int qc = lane_val(q, cl);
+                    const int maxl = (nr - qc) < (nt - nxt) ? (nr - qc) : (nt - nxt);
+                    int l = maxl;   // extend_alignment (compression.cpp:27-34)
+                    for (int off = K; off < maxl; off += 64) {
+                        const int i = off + lane;
+                        const unsigned long long sm = __ballot(i >= maxl || L.r[qc + i] != L.t[nxt + i]);
+                        if (sm) { l = off + first_lane(sm); break; }
+                    }
+                    if (l < K) l = K;
+                    if (l > bl) { bl = l; bcnt = 1; bhas0 = (qc == 0); bkey = qc ? pick_key(qc, pme) : ~0ull; }
+                    else if (l == bl) {
                         bcnt++;
-                        if (q == 0) bhas0 = true;
-                        else { const uint64_t pk = pick_key(q, pme); bkey = pk < bkey ? pk : bkey; }
+                        if (qc == 0) bhas0 = true;
+                        else { const uint64_t pk = pick_key(qc, pme); bkey = pk < bkey ? pk : bkey; }
                     }
                 }
+            } else {   // many candidates (repeats): one per lane, 4 bytes per step
+                int l = 0;
+                if (q >= 0) {
+                    const int maxl = (nr - q) < (nt - nxt) ? (nr - q) : (nt - nxt);
+                    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
+                    const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
+                    l = K;
+                    while (l < maxl) {
+                        const int ra = q + l, ta = nxt + l;
+                        const uint32_t rv = __builtin_amdgcn_alignbyte(r4[(ra >> 2) + 1], r4[ra >> 2], (uint32_t)(ra & 3));
+                        const uint32_t tv = __builtin_amdgcn_alignbyte(t4[(ta >> 2) + 1], t4[ta >> 2], (uint32_t)(ta & 3));
+                        const uint32_t x = rv ^ tv;
+                        if (x) { l += __builtin_ctz(x) >> 3; break; }
+                        l += 4;
+                    }
+                    if (l > maxl) l = maxl;
+                }
+                const int lm = wave_max(l);
+                const int cnt = (int)__popcll(__ballot(q >= 0 && l == lm));
+                const bool h0 = __ballot(q == 0 && l == lm) != 0;
+                const uint64_t mk = wave_min((q > 0 && l == lm) ? pick_key(q, pme) : ~0ull);
+                if (lm > bl) { bl = lm; bcnt = cnt; bhas0 = h0; bkey = mk; }
+                else if (lm == bl) { bcnt += cnt; bhas0 |= h0; bkey = mk < bkey ? mk : bkey; }
             }
-            if (em) break;
         }
-        const int Lm = wave_max(bl);
-        const int cnt = wave_sum(bl == Lm ? bcnt : 0);
-        const bool has0 = __ballot(bl == Lm && bhas0) != 0;
-        const uint64_t mk = wave_min(bl == Lm ? bkey : ~0ull);
+        const int Lm = bl;
         uint64_t pk;
-        if (cnt >= 2 && has0) pk = mk;                 // pn==0 sentinel (compression.cpp:118, :125)
+        if (bcnt >= 2 && bhas0) pk = bkey;                 // pn==0 sentinel (compression.cpp:118, :125)
         else {
-            const uint64_t k0 = has0 ? pick_key(0, pme) : ~0ull;
-            pk = k0 < mk ? k0 : mk;
+            const uint64_t k0 = bhas0 ? pick_key(0, pme) : ~0ull;
+            pk = k0 < bkey ? k0 : bkey;
         }
         const int p = (int)(uint32_t)pk;
         if (lane == 0) out[nrec] = 0x80000000u | ((uint32_t)p << 11) | (uint32_t)Lm;
@@ -224,6 +296,14 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
         if (lane == 0) out[nrec] = ((uint32_t)idx << 11) | (uint32_t)(nt - idx);
         nrec++;
         lit += nt - idx;
+    }
+    if (DBG) {
+        tick(4);
+        if (lane == 0) {
+            for (int i = 0; i < 5; i++) atomicAdd(&g_local_dbg[i], (unsigned long long)tph[i]);
+            atomicAdd(&g_local_dbg[5], 1ull);
+            atomicMax(&g_local_dbg[6], (unsigned long long)(tph[0] + tph[1] + tph[2] + tph[3] + tph[4]));
+        }
     }
     if (lane == 0) {
         SegStat s;
@@ -390,15 +470,36 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
                       int64_t seg_end, uint32_t* recs, SegStat* stat, hipStream_t s) {
     if (seg_end <= seg0) return 0;
     const unsigned g = grid_for(seg_end - seg0, WPB);
-    if (k == 14)
-        PROF_LAUNCH(PROF_LOCAL14, s, k_local_pass<14>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, seg0,
-                    seg_end, recs, stat);
+    static const bool dbg = getenv("SCCG_DEBUG") != nullptr;
+    if (dbg) {
+        const unsigned long long z[8] = {};
+        SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
+        SCCG_HIP(hipStreamSynchronize(s));
+    }
+    if (k == 14 && !dbg)
+        PROF_LAUNCH(PROF_LOCAL14, s, (k_local_pass<14, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT,
+                    seg0, seg_end, recs, stat);
+    else if (k == 14)
+        PROF_LAUNCH(PROF_LOCAL14, s, (k_local_pass<14, true>), dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT,
+                    seg0, seg_end, recs, stat);
+    else if (k == 10 && !dbg)
+        PROF_LAUNCH(PROF_LOCAL10, s, (k_local_pass<10, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT,
+                    seg0, seg_end, recs, stat);
     else if (k == 10)
-        PROF_LAUNCH(PROF_LOCAL10, s, k_local_pass<10>, dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT, seg0,
-                    seg_end, recs, stat);
+        PROF_LAUNCH(PROF_LOCAL10, s, (k_local_pass<10, true>), dim3(g), dim3(SCCG_BLOCK), 0, s, pass, upper, R, nR, T, nT,
+                    seg0, seg_end, recs, stat);
     else
         return SCCG_E_UNSUPPORTED;
     SCCG_HIP(hipGetLastError());
+    if (dbg) {
+        unsigned long long d[8];
+        SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipStreamSynchronize(s));
+        const double n = d[5] ? (double)d[5] : 1.0;
+        fprintf(stderr, "[local k=%d pass=%d] %llu segments, per segment (us): load %.2f keys %.2f insert %.2f hits %.2f walk %.2f"
+                " | max segment %.2f\n", k, pass, d[5], d[0] / n / 100, d[1] / n / 100, d[2] / n / 100, d[3] / n / 100,
+                d[4] / n / 100, d[6] / 100.0);
+    }
     return 0;
 }
 

@@ -32,7 +32,8 @@ int sccg_hip_fail(hipError_t e, const char* what, const char* file, int line) {
 namespace {
 
 enum Slot {
-    B_RFA, B_TFA, B_R, B_T, B_TILE_A, B_TILE_B, B_TILE_LAST, B_TILE_OFF, B_TILE_CARRY, B_SCAL, B_PARTIAL,
+    B_RFA, B_TFA, B_R, B_T, B_TILE_A, B_TILE_B, B_TILE_FA, B_TILE_FB, B_TILE_LAST, B_TILE_OFF, B_TILE_OFF2, B_TILE_CARRY,
+    B_SCAL, B_PARTIAL,
     B_RUN_S, B_RUN_E, B_TMP64, B_RECS, B_STAT, B_MAPS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
     // decompression
     B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC,
@@ -161,19 +162,25 @@ int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n) {
     return 0;
 }
 
-// strips one FASTA into `out`, returns the kept length
+// strips one FASTA into `out` (and its filtered copy into out2, when given); returns the kept
+// length(s): h_len[0] strip, h_len[1] filter (d_len[0..1] on the device)
 int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const int64_t* d_hdr, uint8_t* out,
-          int64_t* d_len, int32_t* d_flags, int64_t* h_len) {
+          int64_t* d_len, int32_t* d_flags, int64_t* h_len, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr) {
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE + 1;
     IngestScratch sc;
     GET(int64_t, ta, B_TILE_A, ntiles);
     GET(int64_t, tb, B_TILE_B, ntiles);
+    GET(int64_t, tfa, B_TILE_FA, ntiles);
+    GET(int64_t, tfb, B_TILE_FB, ntiles);
     GET(int32_t, tl, B_TILE_LAST, ntiles);
     GET(int64_t, to, B_TILE_OFF, ntiles);
+    GET(int64_t, to2, B_TILE_OFF2, ntiles);
     GET(int32_t, tc, B_TILE_CARRY, ntiles);
-    sc.tile_a = ta; sc.tile_b = tb; sc.tile_last = tl; sc.tile_off = to; sc.tile_carry = tc; sc.scalars = nullptr;
-    TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, nullptr, ctx->stream));
-    return d2h_i64(ctx, d_len, h_len, 1);
+    sc.tile_a = ta; sc.tile_b = tb; sc.tile_fa = tfa; sc.tile_fb = tfb; sc.tile_last = tl; sc.tile_off = to;
+    sc.tile_off2 = to2; sc.tile_carry = tc; sc.scalars = nullptr;
+    TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, ctx->stream, fmode, out2,
+                           out2 ? d_len + 1 : nullptr));
+    return d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1);
 }
 
 // run line of `pred` over s[0,n) written at out; returns its length
@@ -215,6 +222,10 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     GET(int64_t, sc, B_SCAL, 64);
     GET(uint8_t, T, B_T, tn + 64);
     GET(uint8_t, R, B_R, rn + 64);
+    // N-erased, uppercased copies for the global pass (compression.cpp:523-524, :556-557), written
+    // by the same ingest pass (the local pass may end up not needing them)
+    GET(uint8_t, Tp, B_TP, tn + 64);
+    GET(uint8_t, Rp, B_RP, rn + 64);
     int32_t* d_flags = reinterpret_cast<int32_t*>(sc + 32);
     HIPTRY(hipMemsetAsync(d_flags, 0, sizeof(int32_t), s));
 
@@ -222,9 +233,10 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     TRY(launch_find_header(tfa, tn, sc, s));
     int64_t hdr[2];
     TRY(d2h_i64(ctx, sc, hdr, 2));
-    int64_t nT = 0, nR = 0;
-    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, &nT));
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 3, nullptr, &nR));
+    int64_t lt[2], lr[2];
+    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, lt, FILTER_DROP_N_UPPER, Tp));
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, lr, FILTER_DROP_N_UPPER, Rp));
+    const int64_t nT = lt[0], nR = lr[0];
     if (nT >= INT32_MAX - 8 || nR >= INT32_MAX - 8)
         return ctx->fail(SCCG_E_UNSUPPORTED, "sequence longer than the reference's int positions allow");
     int32_t flags = 0;
@@ -311,16 +323,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         TRY(put_bytes(ctx, out + pos, "\n", 1));
         pos += 1;
         mark("n_line");
-        GET(uint8_t, Tp, B_TP, nT + 64);
-        GET(uint8_t, Rp, B_RP, nR + 64);
-        const int64_t ntile = (nT > nR ? nT : nR) / INGEST_TILE + 2;
-        GET(int64_t, tcnt, B_TMP64, ntile);
-        GET(int64_t, part, B_PARTIAL, scan_partials_needed(ntile) + 16);
-        TRY(launch_filter(FILTER_DROP_N_UPPER, T, nT, Tp, sc + 7, tcnt, part, s));
-        TRY(launch_filter(FILTER_DROP_N_UPPER, R, nR, Rp, sc + 8, tcnt, part, s));
-        int64_t np[2];
-        TRY(d2h_i64(ctx, sc + 7, np, 2));
-        mark("n_erase");
+        const int64_t np[2] = {lt[1], lr[1]};
         const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, WALK_CHUNK);
         void* ws = ctx->get(B_WALK, wsb);
         if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
@@ -377,8 +380,6 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     // ---- reference (decompression.cpp:47-58, 105-110)
     GET(uint8_t, R, B_R, rn + 64);
     GET(uint8_t, Rp, B_RP, rn + 64);
-    int64_t nR = 0, nRp = 0;
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 8, nullptr, &nR));
     bool n_is_comma = false;
     if (nnl == 1) {
         uint8_t c = 0;
@@ -386,13 +387,10 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
         HIPTRY(hipStreamSynchronize(s));
         n_is_comma = c == ',';
     }
-    {
-        const int64_t ntile = nR / INGEST_TILE + 2;
-        GET(int64_t, tcnt, B_TMP64, ntile);
-        GET(int64_t, part, B_PARTIAL, scan_partials_needed(ntile) + 16);
-        TRY(launch_filter(n_is_comma ? FILTER_UPPER : FILTER_DROP_UPPERN_ONLY, R, nR, Rp, sc + 9, tcnt, part, s));
-        TRY(d2h_i64(ctx, sc + 9, &nRp, 1));
-    }
+    int64_t rl[2];
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 8, nullptr, rl,
+              n_is_comma ? FILTER_UPPER : FILTER_DROP_UPPERN_ONLY, Rp));
+    const int64_t nRp = rl[1];
 
     // ---- run lines + record line
     const int64_t nmax = (nlower > nnl ? nlower : nnl) > nenc ? (nlower > nnl ? nlower : nnl) : nenc;

@@ -33,7 +33,7 @@ constexpr int WTBITS = 9;              // window hash slots
 constexpr int WTSLOTS = 1 << WTBITS;
 constexpr int32_t INVALID = INT32_MIN;
 constexpr int ANCHOR_K = 32;
-constexpr int ANCHOR_STEP = 16;
+constexpr int ANCHOR_STEP = 32;
 constexpr uint64_t A_EMPTY = ~0ull;
 constexpr uint32_t A_UNSET = 0xFFFFFFFEu, A_MULTI = 0xFFFFFFFFu;
 constexpr int32_t FROZEN_MIN = 4096;   // literal bases at a chunk end that trigger a frozen-P scan
@@ -88,9 +88,11 @@ struct WalkPtrs {
     uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
 };
 
+constexpr int WFBITS = 12;             // window pre-filter bitmap (4096 bits)
 struct WalkLds {   // per wave: LDS hash of the window keys (wide literal scans)
     uint32_t wkeys[WCAP];
     uint32_t wtab[WTSLOTS / 2];
+    uint32_t wbits[1 << (WFBITS - 5)];
 };
 
 __device__ __forceinline__ uint64_t pick_key(int32_t p, int32_t pme) {
@@ -165,66 +167,6 @@ __device__ int32_t wave_lce(const uint8_t* __restrict__ R, int32_t a, const uint
 }
 
 // ---------------------------------------------------------------------------------------------
-// Walk k-mer keys.  Inside the walk a pure A/C/G/T k-mer's key is its 2-bit codes packed first
-// base LOWEST (bits 2i..2i+1 = base i), so the keys of every k-mer in a run of bytes are shifts of
-// one packed word; a k-mer holding any other byte gets exotic_key() (high bit set, confirmed by a
-// byte compare).  Equal pure keys <=> equal bytes.  Only the walk's own window / target / LDS keys
-// use this convention.
-// ---------------------------------------------------------------------------------------------
-// 4 bytes -> their 2-bit codes in 8 bits (byte i at bits 2i), and `diff` nonzero in exactly the
-// bytes that are not A/C/G/T: code = ((c >> 1) ^ (c >> 2)) & 3 maps A,C,G,T -> 0,1,2,3, and a
-// byte-permute of "ACGT" by the codes rebuilds the byte iff it was one of them.
-__device__ __forceinline__ uint32_t swar_codes(uint32_t w, uint32_t& diff) {
-    const uint32_t c = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
-    diff = __builtin_amdgcn_perm(0x54474341u, 0x54474341u, c) ^ w;
-    const uint32_t p = c | (c >> 6);
-    return (p | (p >> 12)) & 0xffu;
-}
-// bit i set <=> byte i of `diff` is nonzero
-__device__ __forceinline__ uint32_t nz_bytes(uint32_t diff) {
-    const uint32_t nz = ((((diff & 0x7f7f7f7fu) + 0x7f7f7f7fu) | diff) & 0x80808080u) >> 7;
-    return (nz | (nz >> 7) | (nz >> 14) | (nz >> 21)) & 0xfu;
-}
-// ND consecutive words -> packed codes (byte i at bits 2i) and the non-ACGT byte mask
-template <int ND>
-__device__ __forceinline__ void pack_codes(const uint32_t (&w)[ND], uint64_t& code, uint32_t& bad) {
-    uint32_t d[ND], acc = 0;
-    code = 0;
-#pragma unroll
-    for (int i = 0; i < ND; i++) {
-        code |= (uint64_t)swar_codes(w[i], d[i]) << (8 * i);
-        acc |= d[i];
-    }
-    bad = 0;
-    if (acc) {   // rare: some byte is not A/C/G/T
-#pragma unroll
-        for (int i = 0; i < ND; i++) bad |= nz_bytes(d[i]) << (4 * i);
-    }
-}
-// ND bytes-worth of words at an arbitrary address (ND+1 aligned dword loads)
-template <int ND>
-__device__ __forceinline__ void loadw(const uint8_t* p, uint32_t (&o)[ND]) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    uint32_t v[ND + 1];
-#pragma unroll
-    for (int i = 0; i <= ND; i++) v[i] = w[i];
-#pragma unroll
-    for (int i = 0; i < ND; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
-}
-// scalar form (any k <= 15)
-__device__ __forceinline__ uint32_t walk_key(const uint8_t* s, int k) {
-    uint32_t code = 0;
-    for (int i = 0; i < k; i++) {
-        const uint32_t b = base2(s[i]);
-        if (b > 3) return exotic_key(s, k);
-        code |= b << (2 * i);
-    }
-    return code;
-}
-
-// ---------------------------------------------------------------------------------------------
 // window of P in registers: lane l holds the keys of window indices 4l+q (q < 4), i.e. of the
 // reference k-mers starting at lo+4l+q, lo = max(0, P-m), up to hi = min(nR-k, P+m).
 // 2m+1 <= 4*64 window positions (m = 100: 201).
@@ -288,6 +230,7 @@ __device__ __forceinline__ uint32_t win_match(const WalkPtrs& A, const RegWin& W
 __device__ void hash_window(const RegWin& W, WalkLds& L) {
     const int lane = lane_id();
     for (int i = lane; i < WTSLOTS / 2; i += 64) L.wtab[i] = 0;
+    for (int i = lane; i < (1 << (WFBITS - 5)); i += 64) L.wbits[i] = 0;
     wave_sync();
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -295,6 +238,8 @@ __device__ void hash_window(const RegWin& W, WalkLds& L) {
             const int i = 4 * lane + q;
             L.wkeys[i] = W.key[q];
             wt_insert(L.wtab, W.key[q], (uint32_t)i + 1);
+            const uint32_t fb = slot_hash(W.key[q], WFBITS);
+            atomicOr(&L.wbits[fb >> 5], 1u << (fb & 31));
         }
     }
     wave_sync();
@@ -326,12 +271,18 @@ __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L
         uint64_t code;
         uint32_t bad;
         pack_codes<8>(w, code, bad);
+        // bitmap pre-filter for all 16 positions (independent LDS reads), exact probes in order
+        uint32_t key[WIDE], cand = 0;
+#pragma unroll
+        for (int st = 0; st < WIDE; st++) {
+            key[st] = (bad >> st) & KM ? exotic_key(A.T + p0 + st, k) : (uint32_t)(code >> (2 * st)) & MASK;
+            const uint32_t fb = slot_hash(key[st], WFBITS);
+            if (p0 + st < end && ((L.wbits[fb >> 5] >> (fb & 31)) & 1u)) cand |= 1u << st;
+        }
         int32_t first = INT32_MAX;
 #pragma unroll
         for (int st = 0; st < WIDE; st++) {
-            if (p0 + st >= end) break;
-            const uint32_t key = (bad >> st) & KM ? exotic_key(A.T + p0 + st, k) : (uint32_t)(code >> (2 * st)) & MASK;
-            if (window_has_key(L, key)) { first = p0 + st; break; }
+            if (((cand >> st) & 1u) && window_has_key(L, key[st])) { first = p0 + st; break; }
         }
         const unsigned long long hm = __ballot(first != INT32_MAX);   // lanes in position order
         if (hm) return lane_val(first, first_lane(hm));
@@ -608,15 +559,20 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {   // bijective
     x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
     return x;
 }
+// 2-bit code of the 32-mer at s (false if it holds a non-ACGT byte); s 16-byte aligned or not
+template <bool ALIGNED>
 __device__ __forceinline__ bool code32(const uint8_t* s, uint64_t& code) {
-    uint64_t c = 0;
-    for (int i = 0; i < ANCHOR_K; i++) {
-        const uint32_t b = base2(s[i]);
-        if (b > 3) return false;
-        c = (c << 2) | b;
+    uint32_t w[8];
+    if (ALIGNED) {
+        const uint4* p = reinterpret_cast<const uint4*>(s);
+        const uint4 a = p[0], b = p[1];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
+        loadw<8>(s, w);
     }
-    code = c;
-    return true;
+    uint32_t bad;
+    pack_codes<8>(w, code, bad);
+    return bad == 0;
 }
 
 __global__ void k_anchor_clear(uint64_t* keys, uint32_t* pos, int64_t slots) {
@@ -632,7 +588,7 @@ __global__ void k_anchor_build(WalkPtrs A) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t p = (int32_t)(i * ANCHOR_STEP);
         uint64_t code;
-        if (!code32(A.R + p, code)) continue;
+        if (!code32<true>(A.R + p, code)) continue;
         const uint64_t key = mix64(code);
         if (key == A_EMPTY) continue;
         uint64_t slot = key >> (64 - A.abits);
@@ -659,7 +615,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
         const int32_t y = j * A.S + b * 64 + lane;
         dg[b] = INVALID;
         uint64_t code;
-        if (y + ANCHOR_K <= A.nT && code32(A.T + y, code)) {
+        if (y + ANCHOR_K <= A.nT && code32<false>(A.T + y, code)) {
             const uint64_t key = mix64(code);
             uint64_t slot = key >> (64 - A.abits);
             for (int probes = 0; probes < 64; probes++) {
@@ -715,57 +671,89 @@ __device__ __forceinline__ int32_t serial_ext(const uint8_t* R, int32_t nR, cons
     return l;
 }
 
+// Full-reference k-mer sweep: every thread takes FC_PER_T = 64 consecutive start positions, reads
+// their 64 + 16 bytes as five aligned 16-byte loads, tests each position's walk key (and whether
+// the k-mer holds a non-ACGT byte) with `pred`, then calls `hit` for every position that passed
+// (out of the unrolled part).  HBM-bound: R' is read once per sweep.
+template <typename Pred, typename Hit>
+__device__ __forceinline__ void sweep_kmers(const uint8_t* __restrict__ R, int64_t npos, int k, Pred&& pred, Hit&& hit) {
+    const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
+    for (int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * FC_PER_T; p0 < npos;
+         p0 += (int64_t)gridDim.x * blockDim.x * FC_PER_T) {
+        const uint4* src = reinterpret_cast<const uint4*>(R + p0);
+        uint32_t w[20];
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const uint4 v = src[i];
+            w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+        }
+        uint32_t cw[20], dw[20], acc = 0;
+        uint64_t hits = 0;
+#pragma unroll
+        for (int i = 0; i < 20; i++) { cw[i] = swar_codes(w[i], dw[i]); acc |= dw[i]; }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            uint64_t code = 0;
+            uint32_t bad = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) code |= (uint64_t)cw[4 * g + i] << (8 * i);
+            if (acc) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) bad |= nz_bytes(dw[4 * g + i]) << (4 * i);
+            }
+#pragma unroll
+            for (int st = 0; st < 16; st++) {
+                if (pred((uint32_t)(code >> (2 * st)) & MASK, ((bad >> st) & KM) == 0)) hits |= 1ull << (16 * g + st);
+            }
+        }
+        if (p0 + FC_PER_T > npos) hits &= npos - p0 >= 64 ? ~0ull : ((1ull << (npos - p0)) - 1);
+        while (hits) {
+            const int b = __ffsll((long long)hits) - 1;
+            hits &= hits - 1;
+            hit(p0 + b);
+        }
+    }
+}
+
 // pass 0: max extension over all candidates; pass 1: count / has0 / min pick key at that max
 __global__ void k_fullc(WalkPtrs A, int32_t y, int32_t P, int pass) {
     const int k = A.k;
-    uint8_t kb[16];
-    for (int i = 0; i < k; i++) kb[i] = A.T[y + i];
-    const uint32_t key = kmer_key(kb, k);
+    const uint8_t* kb = A.T + y;
+    const uint32_t key = walk_key(kb, k);
     const uint32_t lmax = (uint32_t)A.fc[0];
-    const int64_t npos = (int64_t)A.nR - k + 1;
-    const uint32_t MASK = (1u << (2 * k)) - 1u;
-    for (int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * FC_PER_T; p0 < npos;
-         p0 += (int64_t)gridDim.x * blockDim.x * FC_PER_T) {
-        uint32_t code = 0;
-        int lastbad = -1000;
-        for (int i = 0; i < FC_PER_T + k - 1; i++) {
-            const int64_t pos = p0 + i;
-            if (pos >= A.nR) break;
-            uint32_t b = base2(A.R[pos]);
-            if (b > 3) { lastbad = i; b = 0; }
-            code = ((code << 2) | b) & MASK;
-            const int st = i - (k - 1);
-            if (st < 0) continue;
-            const int64_t c = p0 + st;
-            if (c >= npos) break;
-            bool eq;
-            if (key < KEY_EXOTIC) eq = lastbad < st && code == key;
-            else eq = lastbad >= st && bytes_eq(A.R + c, kb, k);
-            if (!eq) continue;
-            const int32_t l = serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, y, k);
-            if (pass == 0) atomicMax(&A.fc[0], (unsigned long long)l);
-            else if ((uint32_t)l == lmax) {
-                atomicAdd(&A.fc[1], 1ull);
-                if (c == 0) atomicOr(&A.fc[2], 1ull);
-                else atomicMin(&A.fc[3], (unsigned long long)pick_key((int32_t)c, P));
-            }
+    const bool exo = key >= KEY_EXOTIC;
+    sweep_kmers(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) {
+        return exo ? !pure : (pure && code == key);   // exotic: candidates confirmed bytewise below
+    }, [&](int64_t c) {
+        if (exo && !bytes_eq(A.R + c, kb, k)) return;
+        const int32_t l = serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, y, k);
+        if (pass == 0) atomicMax(&A.fc[0], (unsigned long long)l);
+        else if ((uint32_t)l == lmax) {
+            atomicAdd(&A.fc[1], 1ull);
+            if (c == 0) atomicOr(&A.fc[2], 1ull);
+            else atomicMin(&A.fc[3], (unsigned long long)pick_key((int32_t)c, P));
         }
-    }
+    });
 }
 
 // first target position in [x0, x0+nb) whose k-mer occurs anywhere in R' (pure keys), and the
 // first position in the batch holding a non-ACGT k-mer (checked separately, exactly)
 constexpr int PB = 1024;
 constexpr int PBBITS = 11;
+constexpr int PFBITS = 17;   // presence pre-filter: 2^17-bit LDS bitmap of the batch's keys
 __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0, int32_t nb) {
     __shared__ uint32_t hkey[1 << PBBITS];
     __shared__ uint32_t hidx[1 << PBBITS];
+    __shared__ uint32_t bits[1 << (PFBITS - 5)];
     const int k = A.k;
     for (int i = threadIdx.x; i < (1 << PBBITS); i += blockDim.x) { hkey[i] = 0xffffffffu; hidx[i] = 0xffffffffu; }
+    for (int i = threadIdx.x; i < (1 << (PFBITS - 5)); i += blockDim.x) bits[i] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-        const uint32_t key = kmer_key(A.T + x0 + i, k);
+        const uint32_t key = walk_key(A.T + x0 + i, k);
         if (key >= KEY_EXOTIC) { atomicMin(&A.fc[5], (unsigned long long)(x0 + i)); continue; }
+        const uint32_t fb = slot_hash(key, PFBITS);
+        atomicOr(&bits[fb >> 5], 1u << (fb & 31));
         int slot = (int)slot_hash(key, PBBITS);
         for (;;) {
             const uint32_t prev = atomicCAS(&hkey[slot], 0xffffffffu, key);
@@ -774,30 +762,25 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
         }
     }
     __syncthreads();
-    const int64_t npos = (int64_t)A.nR - k + 1;
-    const uint32_t MASK = (1u << (2 * k)) - 1u;
-    for (int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * FC_PER_T; p0 < npos;
-         p0 += (int64_t)gridDim.x * blockDim.x * FC_PER_T) {
-        uint32_t code = 0;
-        int lastbad = -1000;
-        for (int i = 0; i < FC_PER_T + k - 1; i++) {
-            const int64_t pos = p0 + i;
-            if (pos >= A.nR) break;
-            uint32_t b = base2(A.R[pos]);
-            if (b > 3) { lastbad = i; b = 0; }
-            code = ((code << 2) | b) & MASK;
-            const int st = i - (k - 1);
-            if (st < 0 || lastbad >= st) continue;
-            if (p0 + st >= npos) break;
-            int slot = (int)slot_hash(code, PBBITS);
-            for (;;) {
-                const uint32_t hk = hkey[slot];
-                if (hk == 0xffffffffu) break;
-                if (hk == code) { atomicMin(&A.fc[4], (unsigned long long)(x0 + hidx[slot])); break; }
-                slot = (slot + 1) & ((1 << PBBITS) - 1);
-            }
+    // the bitmap test is branch-free per position; the exact probe runs only for bitmap hits
+    sweep_kmers(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) {
+        const uint32_t fb = slot_hash(code, PFBITS);
+        return pure && ((bits[fb >> 5] >> (fb & 31)) & 1u);
+    }, [&](int64_t c) {
+        uint64_t cw = 0;
+        uint32_t bad;
+        uint32_t w[4];
+        loadw<4>(A.R + c, w);
+        pack_codes<4>(w, cw, bad);
+        const uint32_t code = (uint32_t)cw & ((1u << (2 * k)) - 1u);
+        int slot = (int)slot_hash(code, PBBITS);
+        for (;;) {
+            const uint32_t hk = hkey[slot];
+            if (hk == 0xffffffffu) break;
+            if (hk == code) { atomicMin(&A.fc[4], (unsigned long long)(x0 + hidx[slot])); break; }
+            slot = (slot + 1) & ((1 << PBBITS) - 1);
         }
-    }
+    });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1196,6 +1179,12 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 }
                 std::vector<uint64_t> sorted = tk;
                 std::sort(sorted.begin(), sorted.end());
+                {
+                    int dev = 0, khz = 0;
+                    (void)hipGetDevice(&dev);
+                    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+                    fprintf(stderr, "[walk] wall clock rate %d kHz\n", khz);
+                }
                 fprintf(stderr, "[walk] r1 chunk ticks(10ns): mean %.0f p50 %llu p90 %llu p99 %llu max %llu | totals: matches %llu "
                         "batches %llu wides %llu windows %llu cands %llu extbases %llu\n",
                         (double)sum[0] / C, (unsigned long long)sorted[C / 2], (unsigned long long)sorted[C * 9 / 10],
@@ -1209,9 +1198,11 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 std::partial_sort(idx.begin(), idx.begin() + 5, idx.end(), [&](size_t a, size_t b) { return tk[a] > tk[b]; });
                 for (int q = 0; q < 5; q++) {
                     const uint64_t* e = &d[idx[q] * DS];
-                    fprintf(stderr, "   slow chunk %zu: ticks %llu matches %llu batches %llu wides %llu windows %llu cands %llu ext %llu\n",
+                    fprintf(stderr, "   slow chunk %zu: ticks %llu matches %llu batches %llu wides %llu windows %llu cands %llu ext %llu "
+                            "| win %llu find %llu cand %llu tail %llu\n",
                             idx[q], (unsigned long long)e[0], (unsigned long long)e[1], (unsigned long long)e[2],
-                            (unsigned long long)e[3], (unsigned long long)e[4], (unsigned long long)e[5], (unsigned long long)e[6]);
+                            (unsigned long long)e[3], (unsigned long long)e[4], (unsigned long long)e[5], (unsigned long long)e[6],
+                            (unsigned long long)e[7], (unsigned long long)e[8], (unsigned long long)e[9], (unsigned long long)e[10]);
                 }
             }
             if (dbg && (round <= 3 || round % 1000 == 0)) {
