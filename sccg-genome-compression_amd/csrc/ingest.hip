@@ -12,20 +12,6 @@ namespace {
 
 constexpr int PER_T = INGEST_TILE / SCCG_BLOCK;  // 32 bytes per thread
 
-__device__ __forceinline__ void load_bytes(const uint8_t* __restrict__ buf, int64_t n, int64_t off,
-                                           uint8_t (&b)[PER_T]) {
-    if (off + PER_T <= n && (((uintptr_t)(buf + off)) & 15) == 0) {
-        const uint4* p = reinterpret_cast<const uint4*>(buf + off);
-        uint4 v0 = p[0], v1 = p[1];
-        uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-        for (int i = 0; i < PER_T; i++) b[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-    } else {
-#pragma unroll
-        for (int i = 0; i < PER_T; i++) b[i] = (off + i < n) ? buf[off + i] : (uint8_t)' ';
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // header search
 // ---------------------------------------------------------------------------------------------
@@ -102,54 +88,76 @@ __device__ __forceinline__ bool filter_keep(FilterMode m, uint8_t c) {
     return true;
 }
 
-// Block-cooperative store of the `cnt` bytes staged in LDS (4-byte aligned, cnt + 4 readable)
-// to out[g0, g0 + cnt): head bytes, aligned dword body, tail bytes.
+// LDS staging of a tile's output.  Threads write their kept bytes at their block-scan offsets, so
+// lane t writes near byte 32t: a 4-byte skew every 32 bytes (dword index d -> d + d/8) spreads
+// those writes over distinct banks.  A dword-aligned group of 4 logical bytes stays contiguous.
+constexpr int STAGE_WORDS = INGEST_TILE / 4 + INGEST_TILE / 32 + 4;
+__device__ __forceinline__ int stage_at(int a) { return a + ((a >> 5) << 2); }
+__device__ __forceinline__ uint32_t stage_word(const uint32_t* st4, int d) { return st4[d + (d >> 3)]; }
+
+// Block-cooperative store of the `cnt` staged bytes to out[g0, g0 + cnt): head bytes, aligned
+// dword body, tail bytes.
 __device__ __forceinline__ void stage_out(const uint32_t* __restrict__ st4, int cnt, uint8_t* __restrict__ out, int64_t g0) {
     const uint8_t* st = reinterpret_cast<const uint8_t*>(st4);
     const int t = (int)threadIdx.x;
     int head = (int)((4 - (g0 & 3)) & 3);
     if (head > cnt) head = cnt;
-    if (t < head) out[g0 + t] = st[t];
+    if (t < head) out[g0 + t] = st[stage_at(t)];
     const int nd = (cnt - head) >> 2;
     uint32_t* o4 = reinterpret_cast<uint32_t*>(out + g0 + head);
     for (int d = t; d < nd; d += (int)blockDim.x) {
         const int o = head + 4 * d;
-        o4[d] = __builtin_amdgcn_alignbyte(st4[(o >> 2) + 1], st4[o >> 2], (uint32_t)(o & 3));
+        o4[d] = __builtin_amdgcn_alignbyte(stage_word(st4, (o >> 2) + 1), stage_word(st4, o >> 2), (uint32_t)(o & 3));
     }
     const int done = head + 4 * nd;
-    if (t < cnt - done) out[g0 + done + t] = st[done + t];
+    if (t < cnt - done) out[g0 + done + t] = st[stage_at(done + t)];
 }
 
-struct ThreadSum {
-    int32_t a, b;     // kept-if-carry-keeps count, kept count
-    int32_t fa, fb;   // the same, counting only bytes the filter keeps
-    int32_t last;     // status of the last line start in range: -1 none, 0 drop, 1 keep
+// Per-thread byte masks of a 32-byte range (bit i = byte off + i):
+//   known    kept by strip, line status decided inside the range (REF) / always (TGT)
+//   unknown  REF: non-space bytes before the range's first line start (status from earlier)
+//   fk       kept by the byte filter;  par  '(' bytes
+struct StripMasks {
+    uint32_t known, unknown, fk, par;
+    int32_t last;   // status of the last line start in range: -1 none, 0 drop, 1 keep
 };
 
-__device__ __forceinline__ ThreadSum thread_summary(IngestMode mode, FilterMode fm, const uint32_t (&w)[PER_T / 4],
-                                                    uint8_t prev, int64_t off, int64_t n, int64_t h, int64_t he) {
-    ThreadSum r{0, 0, 0, 0, -1};
-    int cur = -1;
+__device__ __forceinline__ StripMasks strip_masks(IngestMode mode, FilterMode fm, const uint32_t (&w)[PER_T / 4],
+                                                  uint8_t prev, int64_t off, int64_t n, int64_t h, int64_t he) {
+    uint32_t ws = 0, nl = 0, gt = 0, fk = 0, par = 0;
 #pragma unroll
     for (int i = 0; i < PER_T; i++) {
-        const int64_t pos = off + i;
         const uint8_t c = wb(w, i);
-        const uint8_t pc = i ? wb(w, i - 1) : prev;
-        const bool fk = filter_keep(fm, c);
-        if (mode == INGEST_REF) {
-            if (pos < n && (pos == 0 || pc == '\n')) cur = (c == '>') ? 0 : 1;
-            const bool sp = pos >= n || c_isspace(c);
-            if (!sp) {
-                if (cur < 0) { r.a++; r.fa += fk; }
-                else if (cur) { r.b++; r.fb += fk; }
-            }
-        } else {
-            const bool keep = pos < n && !c_isspace(c) && !(pos >= h && pos < he);
-            r.b += keep;
-            r.fb += keep && fk;
-        }
+        ws |= (uint32_t)c_isspace(c) << i;
+        nl |= (uint32_t)(c == '\n') << i;
+        gt |= (uint32_t)(c == '>') << i;
+        fk |= (uint32_t)filter_keep(fm, c) << i;
+        par |= (uint32_t)(c == '(') << i;
     }
-    r.last = cur;
+    const int64_t lim = n - off;
+    const uint32_t valid = lim >= 32 ? ~0u : (lim > 0 ? (1u << lim) - 1u : 0u);
+    StripMasks r{0, 0, fk, par, -1};
+    if (mode == INGEST_TGT) {
+        const int64_t lo = h - off < 0 ? 0 : (h - off > 32 ? 32 : h - off);
+        const int64_t hi = he - off < 0 ? 0 : (he - off > 32 ? 32 : he - off);
+        const uint32_t below_hi = hi >= 32 ? ~0u : (1u << hi) - 1u, below_lo = lo >= 32 ? ~0u : (1u << lo) - 1u;
+        r.known = ~ws & valid & ~(below_hi & ~below_lo);
+        return r;
+    }
+    // REF: a line's fate is its first byte; line starts are position 0 and bytes after a '\n'
+    const uint32_t ls = ((nl << 1) | (uint32_t)(off == 0 || prev == '\n')) & valid;
+    const int first = ls ? __builtin_ctz(ls) : 32;
+    r.unknown = ~ws & valid & (first >= 32 ? ~0u : (1u << first) - 1u);
+    uint32_t keep = 0, rem = ls;
+    while (rem) {
+        const int j = __builtin_ctz(rem);
+        rem &= rem - 1;
+        const int nx = rem ? __builtin_ctz(rem) : 32;
+        const int32_t st = !((gt >> j) & 1u);
+        if (st) keep |= (nx >= 32 ? ~0u : (1u << nx) - 1u) & ~((1u << j) - 1u);
+        r.last = st;
+    }
+    r.known = ~ws & valid & keep;
     return r;
 }
 
@@ -184,11 +192,13 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(IngestMode mode, F
     load_words(buf, n, off, w);
     const uint8_t prev = (off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n';
     const int64_t h = mode == INGEST_TGT ? hdr[0] : 0, he = mode == INGEST_TGT ? hdr[1] : 0;
-    ThreadSum r = thread_summary(mode, fm, w, prev, off, n, h, he);
+    const StripMasks r = strip_masks(mode, fm, w, prev, off, n, h, he);
+    const int32_t ra = __popc(r.unknown), rb = __popc(r.known);
+    const int32_t rfa = __popc(r.unknown & r.fk), rfb = __popc(r.known & r.fk);
     const int32_t prior = block_prior_status(r.last, tmp);
     // a-bytes of a thread with a prior line start in the block are resolved now
-    const int32_t A = prior < 0 ? r.a : 0, B = r.b + (prior == 1 ? r.a : 0);
-    const int32_t FA = prior < 0 ? r.fa : 0, FB = r.fb + (prior == 1 ? r.fa : 0);
+    const int32_t A = prior < 0 ? ra : 0, B = rb + (prior == 1 ? ra : 0);
+    const int32_t FA = prior < 0 ? rfa : 0, FB = rfb + (prior == 1 ? rfa : 0);
     int32_t At, Bt, FAt, FBt;
     block_excl_add<int32_t>(A, tmp32, &At);
     block_excl_add<int32_t>(B, tmp32, &Bt);
@@ -267,42 +277,29 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(IngestMode mode, Fil
                                                             int32_t* __restrict__ flags) {
     __shared__ int32_t tmp[8];
     __shared__ int32_t tmp32[8];
-    __shared__ uint32_t st1[INGEST_TILE / 4 + 2];
-    __shared__ uint32_t st2[INGEST_TILE / 4 + 2];
+    __shared__ uint32_t st1[STAGE_WORDS];
+    __shared__ uint32_t st2[STAGE_WORDS];
     const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
     uint32_t w[PER_T / 4];
     load_words(buf, n, off, w);
     const uint8_t prev = (off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n';
     const int64_t h = mode == INGEST_TGT ? hdr[0] : 0, he = mode == INGEST_TGT ? hdr[1] : 0;
-    ThreadSum r = thread_summary(mode, fm, w, prev, off, n, h, he);
+    const StripMasks r = strip_masks(mode, fm, w, prev, off, n, h, he);
     int32_t prior = block_prior_status(r.last, tmp);
     if (prior < 0) prior = tcarry[blockIdx.x];
+    const uint32_t keep = r.known | (prior == 1 ? r.unknown : 0u), fkeep = keep & r.fk;
     int32_t tot1, tot2;
-    int32_t p1 = block_excl_add<int32_t>(r.b + (prior == 1 ? r.a : 0), tmp32, &tot1);
-    int32_t p2 = out2 ? block_excl_add<int32_t>(r.fb + (prior == 1 ? r.fa : 0), tmp32, &tot2) : 0;
+    int32_t p1 = block_excl_add<int32_t>(__popc(keep), tmp32, &tot1);
+    int32_t p2 = out2 ? block_excl_add<int32_t>(__popc(fkeep), tmp32, &tot2) : 0;
     uint8_t* s1 = reinterpret_cast<uint8_t*>(st1);
     uint8_t* s2 = reinterpret_cast<uint8_t*>(st2);
-    int cur = prior;
-    bool paren = false;
 #pragma unroll
     for (int i = 0; i < PER_T; i++) {
-        const int64_t p = off + i;
         const uint8_t c = wb(w, i);
-        const uint8_t pc = i ? wb(w, i - 1) : prev;
-        bool keep;
-        if (mode == INGEST_REF) {
-            if (p < n && (p == 0 || pc == '\n')) cur = (c == '>') ? 0 : 1;
-            keep = p < n && !c_isspace(c) && cur == 1;
-        } else {
-            keep = p < n && !c_isspace(c) && !(p >= h && p < he);
-        }
-        if (keep) {
-            s1[p1++] = c;
-            paren |= (c == '(');
-            if (out2 && filter_keep(fm, c)) s2[p2++] = c_toupper(c);
-        }
+        if ((keep >> i) & 1u) s1[stage_at(p1++)] = c;
+        if (out2 && ((fkeep >> i) & 1u)) s2[stage_at(p2++)] = c_toupper(c);
     }
-    if (flags && __ballot(paren) && lane_id() == 0) atomicOr(flags, 1);
+    if (flags && __ballot((keep & r.par) != 0) && lane_id() == 0) atomicOr(flags, 1);
     __syncthreads();
     stage_out(st1, tot1, out, toff[blockIdx.x]);
     if (out2) stage_out(st2, tot2, out2, toff2[blockIdx.x]);
@@ -315,56 +312,50 @@ __device__ __forceinline__ bool run_pred(RunPred p, uint8_t c) {
     return p == RUN_LOWER ? c_islower(c) : (c == 'N' || c == 'n');
 }
 
+// bit i: pred(byte off + i); bytes past n are not in any run
+__device__ __forceinline__ uint32_t pred_mask(RunPred pr, const uint8_t* __restrict__ in, int64_t n, int64_t off) {
+    uint32_t w[PER_T / 4];
+    load_words(in, n, off, w);   // pads with ' ' (in no run)
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < PER_T; i++) m |= (uint32_t)run_pred(pr, wb(w, i)) << i;
+    return m;
+}
+
 __global__ __launch_bounds__(SCCG_BLOCK) void k_runs_count(RunPred pr, const uint8_t* __restrict__ in, int64_t n,
                                                            int64_t* __restrict__ cnt) {
-    __shared__ int64_t tmp64[8];
+    __shared__ int32_t tmp32[8];
     const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
-    uint8_t b[PER_T];
-    load_bytes(in, n, off, b);
-    bool prev = off > 0 && off - 1 < n && run_pred(pr, in[off - 1]);
-    int64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < PER_T; i++) {
-        const bool cur = off + i < n && run_pred(pr, b[i]);
-        c += cur && !prev;
-        prev = cur;
-    }
-    int64_t tot;
-    block_excl_add<int64_t>(c, tmp64, &tot);
+    const uint32_t m = pred_mask(pr, in, n, off);
+    const uint32_t prev = off > 0 && off - 1 < n && run_pred(pr, in[off - 1]);
+    const uint32_t starts = m & ~((m << 1) | prev);
+    int32_t tot;
+    block_excl_add<int32_t>(__popc(starts), tmp32, &tot);
     if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
 }
 
 __global__ __launch_bounds__(SCCG_BLOCK) void k_runs_write(RunPred pr, const uint8_t* __restrict__ in, int64_t n,
                                                            const int64_t* __restrict__ toff,
                                                            int32_t* __restrict__ rs, int32_t* __restrict__ re) {
-    __shared__ int64_t tmp64[8];
+    __shared__ int32_t tmp32[8];
     const int64_t tile0 = (int64_t)blockIdx.x * INGEST_TILE;
     const int64_t off = tile0 + (int64_t)threadIdx.x * PER_T;
-    uint8_t b[PER_T];
-    load_bytes(in, n, off, b);
-    bool prev = off > 0 && off - 1 < n && run_pred(pr, in[off - 1]);
-    const bool nxt_in = off + PER_T < n && run_pred(pr, in[off + PER_T]);
-    int64_t cs = 0, ce = 0;
-    bool cur[PER_T];
-#pragma unroll
-    for (int i = 0; i < PER_T; i++) cur[i] = off + i < n && run_pred(pr, b[i]);
-#pragma unroll
-    for (int i = 0; i < PER_T; i++) {
-        const bool pv = i ? cur[i - 1] : prev;
-        const bool nx = i + 1 < PER_T ? cur[i + 1] : nxt_in;
-        cs += cur[i] && !pv;
-        ce += cur[i] && !nx;
-    }
+    const uint32_t m = pred_mask(pr, in, n, off);
+    const uint32_t prev = off > 0 && off - 1 < n && run_pred(pr, in[off - 1]);
+    const uint32_t next = off + PER_T < n && run_pred(pr, in[off + PER_T]);
+    uint32_t starts = m & ~((m << 1) | prev);
+    uint32_t ends = m & ~((m >> 1) | (next << 31));
     // runs open across the tile start end inside this tile (or later) but started before it
     const bool open_in = tile0 > 0 && tile0 < n && run_pred(pr, in[tile0 - 1]) && run_pred(pr, in[tile0]);
-    int64_t ps = toff[blockIdx.x] + block_excl_add<int64_t>(cs, tmp64, nullptr);
-    int64_t pe = toff[blockIdx.x] - (open_in ? 1 : 0) + block_excl_add<int64_t>(ce, tmp64, nullptr);
-#pragma unroll
-    for (int i = 0; i < PER_T; i++) {
-        const bool pv = i ? cur[i - 1] : prev;
-        const bool nx = i + 1 < PER_T ? cur[i + 1] : nxt_in;
-        if (cur[i] && !pv) rs[ps++] = (int32_t)(off + i);
-        if (cur[i] && !nx) re[pe++] = (int32_t)(off + i);
+    int64_t ps = toff[blockIdx.x] + block_excl_add<int32_t>(__popc(starts), tmp32, nullptr);
+    int64_t pe = toff[blockIdx.x] - (open_in ? 1 : 0) + block_excl_add<int32_t>(__popc(ends), tmp32, nullptr);
+    while (starts) {
+        rs[ps++] = (int32_t)(off + __ffs((int)starts) - 1);
+        starts &= starts - 1;
+    }
+    while (ends) {
+        re[pe++] = (int32_t)(off + __ffs((int)ends) - 1);
+        ends &= ends - 1;
     }
 }
 

@@ -219,6 +219,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
         const uint32_t key = seg_key<K>(&L.t[nxt]);
         const uint32_t bk = slot_hash(key, NBB);
         const int e0 = (int)L.bstart[bk], e1 = (int)L.bstart[bk + 1];
+        const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
+        const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
         // candidates: the bucket's entries holding this k-mer, 64 entries per step
         int bl = 0, bcnt = 0;
         bool bhas0 = false;
@@ -237,12 +239,22 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
                     cm &= cm - 1;
                     const int qc = lane_val(q, cl);
                     const int maxl = (nr - qc) < (nt - nxt) ? (nr - qc) : (nt - nxt);
-                    int l = maxl;   // extend_alignment (compression.cpp:27-34)
-                    for (int off = K; off < maxl; off += 64) {
-                        const int i = off + lane;
-                        const unsigned long long sm = __ballot(i >= maxl || L.r[qc + i] != L.t[nxt + i]);
-                        if (sm) { l = off + first_lane(sm); break; }
+                    int l = maxl;   // extend_alignment (compression.cpp:27-34): 4 bytes per lane per step
+                    for (int off = K; off < maxl; off += 256) {
+                        const int i = off + 4 * lane;
+                        int e = INT32_MAX;
+                        if (i < maxl) {
+                            const int ra = qc + i, ta = nxt + i;
+                            const uint32_t rv = __builtin_amdgcn_alignbyte(r4[(ra >> 2) + 1], r4[ra >> 2], (uint32_t)(ra & 3));
+                            const uint32_t tv = __builtin_amdgcn_alignbyte(t4[(ta >> 2) + 1], t4[ta >> 2], (uint32_t)(ta & 3));
+                            const uint32_t x = rv ^ tv;
+                            if (x) e = i + (__builtin_ctz(x) >> 3);
+                            else if (maxl - i <= 4) e = maxl;
+                        }
+                        const unsigned long long sm = __ballot(e != INT32_MAX);
+                        if (sm) { l = lane_val(e, first_lane(sm)); break; }
                     }
+                    if (l > maxl) l = maxl;
                     if (l < K) l = K;
                     if (l > bl) { bl = l; bcnt = 1; bhas0 = (qc == 0); bkey = qc ? pick_key(qc, pme) : ~0ull; }
                     else if (l == bl) {
@@ -255,16 +267,19 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
                 int l = 0;
                 if (q >= 0) {
                     const int maxl = (nr - q) < (nt - nxt) ? (nr - q) : (nt - nxt);
-                    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
-                    const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
                     l = K;
-                    while (l < maxl) {
-                        const int ra = q + l, ta = nxt + l;
-                        const uint32_t rv = __builtin_amdgcn_alignbyte(r4[(ra >> 2) + 1], r4[ra >> 2], (uint32_t)(ra & 3));
-                        const uint32_t tv = __builtin_amdgcn_alignbyte(t4[(ta >> 2) + 1], t4[ta >> 2], (uint32_t)(ta & 3));
-                        const uint32_t x = rv ^ tv;
-                        if (x) { l += __builtin_ctz(x) >> 3; break; }
-                        l += 4;
+                    while (l < maxl) {   // 16 bytes per step
+                        uint32_t rv[4], tv[4];
+                        loadw<4>(&L.r[q + l], rv);
+                        loadw<4>(&L.t[nxt + l], tv);
+                        int d = 16;
+#pragma unroll
+                        for (int w = 3; w >= 0; w--) {
+                            const uint32_t x = rv[w] ^ tv[w];
+                            if (x) d = 4 * w + (__builtin_ctz(x) >> 3);
+                        }
+                        l += d;
+                        if (d < 16) break;
                     }
                     if (l > maxl) l = maxl;
                 }

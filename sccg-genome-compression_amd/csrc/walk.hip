@@ -260,29 +260,35 @@ __device__ __forceinline__ bool window_has_key(const WalkLds& L, uint32_t key) {
 // positions per wave step: 16 consecutive per lane, keys by shifting one packed code word).  Key
 // equality is a superset of byte equality, so every position skipped is certainly a literal step;
 // a returned position is re-checked exactly by the caller.  Returns `end` when there is none.
-constexpr int WIDE = 16;
+constexpr int WIDE = 16;   // positions per lane per step (1024 per wave step)
 __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, int32_t x, int32_t end) {
     const int lane = lane_id(), k = A.k;
     const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
+    uint32_t w[8];   // 32 bytes >= WIDE + k - 1; the next step's words are loaded one step ahead
+    loadw<8>(A.T + x + WIDE * lane, w);
     for (int32_t base = x; base < end; base += 64 * WIDE) {
         const int32_t p0 = base + WIDE * lane;
-        uint32_t w[8];   // 32 bytes >= WIDE + k - 1
-        loadw<8>(A.T + p0, w);
         uint64_t code;
         uint32_t bad;
         pack_codes<8>(w, code, bad);
+        if (base + 64 * WIDE < end) loadw<8>(A.T + p0 + 64 * WIDE, w);
         // bitmap pre-filter for all 16 positions (independent LDS reads), exact probes in order
-        uint32_t key[WIDE], cand = 0;
+        uint32_t cand = 0;
 #pragma unroll
         for (int st = 0; st < WIDE; st++) {
-            key[st] = (bad >> st) & KM ? exotic_key(A.T + p0 + st, k) : (uint32_t)(code >> (2 * st)) & MASK;
-            const uint32_t fb = slot_hash(key[st], WFBITS);
-            if (p0 + st < end && ((L.wbits[fb >> 5] >> (fb & 31)) & 1u)) cand |= 1u << st;
+            const uint32_t key = (bad >> st) & KM ? KEY_EXOTIC : (uint32_t)(code >> (2 * st)) & MASK;
+            const uint32_t fb = slot_hash(key, WFBITS);
+            // exotic k-mers always go to the exact check (their key needs the bytes)
+            if (key == KEY_EXOTIC || ((L.wbits[fb >> 5] >> (fb & 31)) & 1u)) cand |= 1u << st;
         }
+        const int32_t lim = end - p0;
+        if (lim < WIDE) cand &= lim > 0 ? (1u << lim) - 1u : 0u;
         int32_t first = INT32_MAX;
-#pragma unroll
-        for (int st = 0; st < WIDE; st++) {
-            if (((cand >> st) & 1u) && window_has_key(L, key[st])) { first = p0 + st; break; }
+        while (cand) {
+            const int st = __ffs((int)cand) - 1;
+            cand &= cand - 1;
+            const uint32_t key = (bad >> st) & KM ? exotic_key(A.T + p0 + st, k) : (uint32_t)(code >> (2 * st)) & MASK;
+            if (window_has_key(L, key)) { first = p0 + st; break; }
         }
         const unsigned long long hm = __ballot(first != INT32_MAX);   // lanes in position order
         if (hm) return lane_val(first, first_lane(hm));
