@@ -215,56 +215,70 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(IngestMode mode, F
     }
 }
 
-// one 1024-thread block: compose the tile summaries in order -> per-tile output offsets (strip and
-// filter) and carry-in status; totals -> d_len[0], d_len2[0]
+// Tile summary monoid: (a, b, fa, fb, last), "X then Y": Y's status-unknown bytes are resolved by
+// X's last line status (kept if 1, dropped if 0, still unknown if X has no line start).
+struct TileSum {
+    int64_t a, b, fa, fb;
+    int32_t last;
+};
+__device__ __forceinline__ TileSum ts_compose(const TileSum& x, const TileSum& y) {
+    TileSum r;
+    r.a = x.a + (x.last < 0 ? y.a : 0);
+    r.b = x.b + y.b + (x.last == 1 ? y.a : 0);
+    r.fa = x.fa + (x.last < 0 ? y.fa : 0);
+    r.fb = x.fb + y.fb + (x.last == 1 ? y.fa : 0);
+    r.last = y.last >= 0 ? y.last : x.last;
+    return r;
+}
+__device__ __forceinline__ TileSum ts_shfl_up(const TileSum& v, int d) {
+    TileSum r;
+    r.a = __shfl_up(v.a, d, 64); r.b = __shfl_up(v.b, d, 64);
+    r.fa = __shfl_up(v.fa, d, 64); r.fb = __shfl_up(v.fb, d, 64);
+    r.last = __shfl_up(v.last, d, 64);
+    return r;
+}
+
+// one 1024-thread block: scan of the tile summaries (each thread composes a run of tiles, then a
+// wave-shuffle + cross-wave scan) -> per-tile output offsets (strip and filter) and carry-in
+// status; the stream starts as if after a kept line (carry 1); totals -> d_len[0], d_len2[0]
 __global__ __launch_bounds__(1024) void k_strip_scan(int64_t ntiles, const int64_t* __restrict__ ta,
                                                      const int64_t* __restrict__ tb, const int64_t* __restrict__ tfa,
                                                      const int64_t* __restrict__ tfb, const int32_t* __restrict__ tlast,
                                                      int64_t* __restrict__ toff, int64_t* __restrict__ toff2,
                                                      int32_t* __restrict__ tcarry, int64_t* __restrict__ d_len,
                                                      int64_t* __restrict__ d_len2) {
-    __shared__ int64_t sA[1024], sB[1024], sFA[1024], sFB[1024];
-    __shared__ int32_t sL[1024];
+    __shared__ TileSum wsum[16];
     const int64_t per = (ntiles + 1023) / 1024;
     const int64_t t0 = (int64_t)threadIdx.x * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
-    int64_t A = 0, B = 0, FA = 0, FB = 0;
-    int32_t last = -1;
-    for (int64_t t = t0; t < t1; t++) {
-        const int32_t yl = tlast[t];
-        const int64_t ya = ta[t], yb = tb[t], yfa = tfa[t], yfb = tfb[t];
-        B += yb + (last == 1 ? ya : 0);
-        FB += yfb + (last == 1 ? yfa : 0);
-        if (last < 0) { A += ya; FA += yfa; }
-        if (yl >= 0) last = yl;
+    const TileSum id{0, 0, 0, 0, -1};
+    TileSum mine = id;
+    for (int64_t t = t0; t < t1; t++) mine = ts_compose(mine, TileSum{ta[t], tb[t], tfa[t], tfb[t], tlast[t]});
+    const int lane = lane_id(), w = (int)(threadIdx.x >> 6);
+    TileSum incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const TileSum o = ts_shfl_up(incl, d);
+        if (lane >= d) incl = ts_compose(o, incl);
     }
-    sA[threadIdx.x] = A; sB[threadIdx.x] = B; sFA[threadIdx.x] = FA; sFB[threadIdx.x] = FB; sL[threadIdx.x] = last;
+    if (lane == 63) wsum[w] = incl;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int64_t off = 0, off2 = 0;
-        int32_t carry = 1;
-        for (int i = 0; i < 1024; i++) {
-            const int64_t a = sA[i], b = sB[i], fa = sFA[i], fb = sFB[i];
-            const int32_t l = sL[i];
-            sA[i] = off;        // offsets at start of thread i's range
-            sFA[i] = off2;
-            sL[i] = carry;      // carry-in status
-            off += b + (carry == 1 ? a : 0);
-            off2 += fb + (carry == 1 ? fa : 0);
-            if (l >= 0) carry = l;
-        }
-        *d_len = off;
-        if (d_len2) *d_len2 = off2;
+        TileSum run = id;
+        for (int i = 0; i < 16; i++) { const TileSum x = wsum[i]; wsum[i] = run; run = ts_compose(run, x); }
     }
     __syncthreads();
-    int64_t off = sA[threadIdx.x], off2 = sFA[threadIdx.x];
-    int32_t carry = sL[threadIdx.x];
+    TileSum ex = ts_shfl_up(incl, 1);
+    if (lane == 0) ex = id;
+    TileSum run = ts_compose(TileSum{0, 0, 0, 0, 1}, ts_compose(wsum[w], ex));
     for (int64_t t = t0; t < t1; t++) {
-        toff[t] = off;
-        toff2[t] = off2;
-        tcarry[t] = carry;
-        off += tb[t] + (carry == 1 ? ta[t] : 0);
-        off2 += tfb[t] + (carry == 1 ? tfa[t] : 0);
-        if (tlast[t] >= 0) carry = tlast[t];
+        toff[t] = run.b;
+        toff2[t] = run.fb;
+        tcarry[t] = run.last;
+        run = ts_compose(run, TileSum{ta[t], tb[t], tfa[t], tfb[t], tlast[t]});
+    }
+    if (threadIdx.x == 1023) {
+        *d_len = run.b;
+        if (d_len2) *d_len2 = run.fb;
     }
 }
 

@@ -78,7 +78,7 @@ __device__ __forceinline__ void keys16(const uint8_t* s, uint64_t& code, uint32_
 }
 
 // SCCG_DEBUG: phase ticks (10 ns) summed over segments: load, keys, insert, hits, walk, count
-__device__ unsigned long long g_local_dbg[8];
+__device__ unsigned long long g_local_dbg[16];
 
 template <int K, bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, const uint8_t* __restrict__ R, int64_t nR,
@@ -317,7 +317,12 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
         if (lane == 0) {
             for (int i = 0; i < 5; i++) atomicAdd(&g_local_dbg[i], (unsigned long long)tph[i]);
             atomicAdd(&g_local_dbg[5], 1ull);
-            atomicMax(&g_local_dbg[6], (unsigned long long)(tph[0] + tph[1] + tph[2] + tph[3] + tph[4]));
+            const unsigned long long tot = tph[0] + tph[1] + tph[2] + tph[3] + tph[4];
+            if (tot > atomicMax(&g_local_dbg[6], tot)) {   // racy snapshot of the slowest segment (diagnostics)
+                for (int i = 0; i < 5; i++) g_local_dbg[8 + i] = tph[i];
+                g_local_dbg[13] = (unsigned long long)seg;
+                g_local_dbg[14] = (unsigned long long)nmatch;
+            }
         }
     }
     if (lane == 0) {
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
 // ---------------------------------------------------------------------------------------------
 // switch state machine: state = min(mismatch counter, 5), 6 = switched (absorbing)
 // ---------------------------------------------------------------------------------------------
-constexpr int FSM_G = 128;   // segments per thread
+constexpr int FSM_G = 16;    // segments per thread (their stats are loaded up front)
 constexpr int SW = 6;
 
 __device__ __forceinline__ int seg_class(const SegStat& s) {
@@ -351,15 +356,20 @@ __global__ void k_fsm_chunks(const SegStat* __restrict__ stat, int64_t seg0, int
     const int64_t s0 = seg0 + t * FSM_G;
     if (s0 >= seg_end) return;
     const int64_t s1 = s0 + FSM_G < seg_end ? s0 + FSM_G : seg_end;
+    int cls[FSM_G];
+#pragma unroll
+    for (int q = 0; q < FSM_G; q++) cls[q] = s0 + q < s1 ? seg_class(stat[s0 + q]) : 0;
     int st[6], at[6];
     for (int i = 0; i < 6; i++) { st[i] = i; at[i] = -1; }
-    for (int64_t s = s0; s < s1; s++) {
-        const int c = seg_class(stat[s]);
+#pragma unroll
+    for (int q = 0; q < FSM_G; q++) {
+        if (s0 + q >= s1) break;
+        const int c = cls[q];
         for (int i = 0; i < 6; i++) {
             if (st[i] == SW) continue;
             if (c == 0 || c == 3) st[i] = 0;
             else if (c == 1) st[i] = st[i] + 1 > 5 ? 5 : st[i] + 1;
-            else { if (st[i] + 1 > 4) { st[i] = SW; at[i] = (int)(s - s0); } else st[i]++; }
+            else { if (st[i] + 1 > 4) { st[i] = SW; at[i] = q; } else st[i]++; }
         }
     }
     for (int i = 0; i < 6; i++) { maps[t * 12 + i] = st[i]; maps[t * 12 + 6 + i] = at[i]; }
@@ -487,7 +497,7 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
     const unsigned g = grid_for(seg_end - seg0, WPB);
     static const bool dbg = getenv("SCCG_DEBUG") != nullptr;
     if (dbg) {
-        const unsigned long long z[8] = {};
+        const unsigned long long z[16] = {};
         SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
         SCCG_HIP(hipStreamSynchronize(s));
     }
@@ -507,13 +517,15 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
         return SCCG_E_UNSUPPORTED;
     SCCG_HIP(hipGetLastError());
     if (dbg) {
-        unsigned long long d[8];
+        unsigned long long d[16];
         SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
         SCCG_HIP(hipStreamSynchronize(s));
         const double n = d[5] ? (double)d[5] : 1.0;
         fprintf(stderr, "[local k=%d pass=%d] %llu segments, per segment (us): load %.2f keys %.2f insert %.2f hits %.2f walk %.2f"
                 " | max segment %.2f\n", k, pass, d[5], d[0] / n / 100, d[1] / n / 100, d[2] / n / 100, d[3] / n / 100,
                 d[4] / n / 100, d[6] / 100.0);
+        fprintf(stderr, "[local]   slowest segment %llu (%llu matches): load %.1f keys %.1f hits %.1f walk %.1f us\n", d[13],
+                d[14], d[8] / 100.0, (d[9] + d[10]) / 100.0, d[11] / 100.0, d[12] / 100.0);
     }
     return 0;
 }

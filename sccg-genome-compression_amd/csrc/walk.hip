@@ -34,8 +34,8 @@ constexpr int WTSLOTS = 1 << WTBITS;
 constexpr int32_t INVALID = INT32_MIN;
 constexpr int ANCHOR_K = 32;
 constexpr int ANCHOR_STEP = 32;
-constexpr uint64_t A_EMPTY = ~0ull;
-constexpr uint32_t A_UNSET = 0xFFFFFFFEu, A_MULTI = 0xFFFFFFFFu;
+constexpr uint64_t A_EMPTY = ~0ull;          // anchor slot: (32-bit fingerprint << 32) | position
+constexpr uint32_t A_MULTI = 0xFFFFFFFFu;    // position of a 32-mer seen more than once
 constexpr int32_t FROZEN_MIN = 4096;   // literal bases at a chunk end that trigger a frozen-P scan
 
 enum ChunkKind : int32_t { KIND_SPEC = 0, KIND_FIX = 1, KIND_RESUME = 2 };
@@ -74,8 +74,7 @@ struct WalkPtrs {
     int32_t* flist;       // committed frozen chunks of the round
     int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round,
                           // [5] frozen count, [6] frozen-scan first hit
-    uint64_t* akeys;
-    uint32_t* apos;
+    uint64_t* atab;
     int32_t abits;
     unsigned long long* fc;   // full-candidate scan scalars: [0] lmax [1] cnt [2] has0 [3] minkey [4] firsthit [5] firstexo
     int64_t* flat_off;        // per chunk
@@ -88,7 +87,8 @@ struct WalkPtrs {
     uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
 };
 
-constexpr int WFBITS = 12;             // window pre-filter bitmap (4096 bits)
+constexpr int WFBITS = 14;             // window pre-filter: 16384-bit Bloom filter, 2 hashes
+__device__ __forceinline__ uint32_t wf_h2(uint32_t key) { return (key * 0x85EBCA77u) >> (32 - WFBITS); }
 struct WalkLds {   // per wave: LDS hash of the window keys (wide literal scans)
     uint32_t wkeys[WCAP];
     uint32_t wtab[WTSLOTS / 2];
@@ -238,8 +238,9 @@ __device__ void hash_window(const RegWin& W, WalkLds& L) {
             const int i = 4 * lane + q;
             L.wkeys[i] = W.key[q];
             wt_insert(L.wtab, W.key[q], (uint32_t)i + 1);
-            const uint32_t fb = slot_hash(W.key[q], WFBITS);
+            const uint32_t fb = slot_hash(W.key[q], WFBITS), fb2 = wf_h2(W.key[q]);
             atomicOr(&L.wbits[fb >> 5], 1u << (fb & 31));
+            atomicOr(&L.wbits[fb2 >> 5], 1u << (fb2 & 31));
         }
     }
     wave_sync();
@@ -277,9 +278,10 @@ __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L
 #pragma unroll
         for (int st = 0; st < WIDE; st++) {
             const uint32_t key = (bad >> st) & KM ? KEY_EXOTIC : (uint32_t)(code >> (2 * st)) & MASK;
-            const uint32_t fb = slot_hash(key, WFBITS);
+            const uint32_t fb = slot_hash(key, WFBITS), fb2 = wf_h2(key);
             // exotic k-mers always go to the exact check (their key needs the bytes)
-            if (key == KEY_EXOTIC || ((L.wbits[fb >> 5] >> (fb & 31)) & 1u)) cand |= 1u << st;
+            if (key == KEY_EXOTIC || ((L.wbits[fb >> 5] >> (fb & 31)) & (L.wbits[fb2 >> 5] >> (fb2 & 31)) & 1u))
+                cand |= 1u << st;
         }
         const int32_t lim = end - p0;
         if (lim < WIDE) cand &= lim > 0 ? (1u << lim) - 1u : 0u;
@@ -559,7 +561,9 @@ __global__ void k_pending(WalkPtrs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// anchors: 32-mers at every 16th R' position -> position (or MULTI); one probe batch per chunk
+// anchors: 32-mers at every 32nd R' position -> position (or MULTI); one probe batch per chunk.
+// A slot holds a 32-bit fingerprint of the 32-mer's hash (the other hash bits pick the home slot)
+// and the position; a fingerprint clash only costs a wrong guess, never a wrong result.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {   // bijective
     x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
@@ -581,11 +585,9 @@ __device__ __forceinline__ bool code32(const uint8_t* s, uint64_t& code) {
     return bad == 0;
 }
 
-__global__ void k_anchor_clear(uint64_t* keys, uint32_t* pos, int64_t slots) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < slots; i += (int64_t)gridDim.x * blockDim.x) {
-        keys[i] = A_EMPTY;
-        pos[i] = A_UNSET;
-    }
+__device__ __forceinline__ uint32_t anchor_fp(uint64_t key) {
+    const uint32_t f = (uint32_t)key;
+    return f == 0xFFFFFFFFu ? 0xFFFFFFFEu : f;   // never forms A_EMPTY
 }
 
 __global__ void k_anchor_build(WalkPtrs A) {
@@ -596,13 +598,13 @@ __global__ void k_anchor_build(WalkPtrs A) {
         uint64_t code;
         if (!code32<true>(A.R + p, code)) continue;
         const uint64_t key = mix64(code);
-        if (key == A_EMPTY) continue;
+        const uint32_t fp = anchor_fp(key);
+        const unsigned long long ent = ((unsigned long long)fp << 32) | (uint32_t)p;
         uint64_t slot = key >> (64 - A.abits);
         for (;;) {
-            const unsigned long long prev = atomicCAS((unsigned long long*)&A.akeys[slot], (unsigned long long)A_EMPTY,
-                                                      (unsigned long long)key);
-            if (prev == A_EMPTY) { atomicCAS(&A.apos[slot], A_UNSET, (uint32_t)p); break; }
-            if (prev == key) { atomicExch(&A.apos[slot], A_MULTI); break; }
+            const unsigned long long prev = atomicCAS((unsigned long long*)&A.atab[slot], (unsigned long long)A_EMPTY, ent);
+            if (prev == A_EMPTY) break;
+            if ((uint32_t)(prev >> 32) == fp) { atomicOr((unsigned long long*)&A.atab[slot], (unsigned long long)A_MULTI); break; }
             slot = (slot + 1) & smask;
         }
     }
@@ -623,13 +625,14 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
         uint64_t code;
         if (y + ANCHOR_K <= A.nT && code32<false>(A.T + y, code)) {
             const uint64_t key = mix64(code);
+            const uint32_t fp = anchor_fp(key);
             uint64_t slot = key >> (64 - A.abits);
             for (int probes = 0; probes < 64; probes++) {
-                const uint64_t kk = A.akeys[slot];
-                if (kk == A_EMPTY) break;
-                if (kk == key) {
-                    const uint32_t ps = A.apos[slot];
-                    if (ps < A_UNSET) dg[b] = (int32_t)ps - y;
+                const uint64_t v = A.atab[slot];
+                if (v == A_EMPTY) break;
+                if ((uint32_t)(v >> 32) == fp) {
+                    const uint32_t ps = (uint32_t)v;
+                    if (ps != A_MULTI) dg[b] = (int32_t)ps - y;
                     break;
                 }
                 slot = (slot + 1) & smask;
@@ -756,7 +759,11 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
     for (int i = threadIdx.x; i < (1 << (PFBITS - 5)); i += blockDim.x) bits[i] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-        const uint32_t key = walk_key(A.T + x0 + i, k);
+        uint32_t w[4], bad;
+        uint64_t cw;
+        loadw<4>(A.T + x0 + i, w);
+        pack_codes<4>(w, cw, bad);
+        const uint32_t key = bad & ((1u << k) - 1u) ? exotic_key(A.T + x0 + i, k) : (uint32_t)cw & ((1u << (2 * k)) - 1u);
         if (key >= KEY_EXOTIC) { atomicMin(&A.fc[5], (unsigned long long)(x0 + i)); continue; }
         const uint32_t fb = slot_hash(key, PFBITS);
         atomicOr(&bits[fb >> 5], 1u << (fb & 31));
@@ -895,8 +902,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.frozen = c.take<int32_t>(C); A.flist = c.take<int32_t>(C);
     A.scal = c.take<int32_t>(16);
     A.abits = anchor_bits(nR);
-    A.akeys = c.take<uint64_t>((size_t)1 << A.abits);
-    A.apos = c.take<uint32_t>((size_t)1 << A.abits);
+    A.atab = c.take<uint64_t>((size_t)1 << A.abits);
     A.fc = c.take<unsigned long long>(8);
     A.flat_off = c.take<int64_t>(C + 1);
     const size_t maxm = (size_t)(nT / k + 2);
@@ -1083,7 +1089,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             RC(set_u64(A.fc + 4, {-1, -1}, s));
             const int64_t npos = nRp - k + 1;
             unsigned g = grid_for(npos, 256 * FC_PER_T);
-            if (g > 4096) g = 4096;
+            if (g > 1024) g = 1024;   // every block first builds the batch's LDS tables
             PROF_LAUNCH(PROF_PRESENCE, s, k_presence, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, nb);
             SCCG_HIP(hipGetLastError());
             unsigned long long r[2];
@@ -1134,8 +1140,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     if (startP != INVALID && lastk >= 0) {
         // anchors -> speculative guesses for chunks 1..C-1
         const int64_t slots = 1ll << A.abits;
-        hipLaunchKernelGGL(k_anchor_clear, dim3(grid_for(slots, 256) > 8192 ? 8192 : grid_for(slots, 256)), dim3(256), 0,
-                           s, A.akeys, A.apos, slots);
+        SCCG_HIP(hipMemsetAsync(A.atab, 0xFF, (size_t)slots * sizeof(uint64_t), s));   // all A_EMPTY
         const int64_t ns = nRp / ANCHOR_STEP + 1;
         PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build, dim3(grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256)), dim3(256), 0, s, A);
         hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
