@@ -238,23 +238,15 @@ __device__ __forceinline__ TileSum ts_shfl_up(const TileSum& v, int d) {
     return r;
 }
 
-// one 1024-thread block: scan of the tile summaries (each thread composes a run of tiles, then a
-// wave-shuffle + cross-wave scan) -> per-tile output offsets (strip and filter) and carry-in
-// status; the stream starts as if after a kept line (carry 1); totals -> d_len[0], d_len2[0]
-__global__ __launch_bounds__(1024) void k_strip_scan(int64_t ntiles, const int64_t* __restrict__ ta,
-                                                     const int64_t* __restrict__ tb, const int64_t* __restrict__ tfa,
-                                                     const int64_t* __restrict__ tfb, const int32_t* __restrict__ tlast,
-                                                     int64_t* __restrict__ toff, int64_t* __restrict__ toff2,
-                                                     int32_t* __restrict__ tcarry, int64_t* __restrict__ d_len,
-                                                     int64_t* __restrict__ d_len2) {
-    __shared__ TileSum wsum[16];
-    const int64_t per = (ntiles + 1023) / 1024;
-    const int64_t t0 = (int64_t)threadIdx.x * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
+// Scan of the tile summaries in three launches.  (1) one thread per tile, 1024 tiles per block:
+// block-local exclusive prefix, written over the tile's own summary, and the block total;
+// (2) one block: exclusive prefix of the block totals; (3) per tile: stream prefix = "carry 1"
+// then block prefix then local prefix -> output offsets (strip and filter) and carry-in status.
+constexpr int SCAN_B = 1024;
+__device__ __forceinline__ TileSum block_scan_tiles(TileSum v, TileSum* wsum, TileSum* total) {
     const TileSum id{0, 0, 0, 0, -1};
-    TileSum mine = id;
-    for (int64_t t = t0; t < t1; t++) mine = ts_compose(mine, TileSum{ta[t], tb[t], tfa[t], tfb[t], tlast[t]});
-    const int lane = lane_id(), w = (int)(threadIdx.x >> 6);
-    TileSum incl = mine;
+    const int lane = lane_id(), w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
+    TileSum incl = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const TileSum o = ts_shfl_up(incl, d);
@@ -264,21 +256,53 @@ __global__ __launch_bounds__(1024) void k_strip_scan(int64_t ntiles, const int64
     __syncthreads();
     if (threadIdx.x == 0) {
         TileSum run = id;
-        for (int i = 0; i < 16; i++) { const TileSum x = wsum[i]; wsum[i] = run; run = ts_compose(run, x); }
+        for (int i = 0; i < nw; i++) { const TileSum x = wsum[i]; wsum[i] = run; run = ts_compose(run, x); }
+        wsum[16] = run;
     }
     __syncthreads();
     TileSum ex = ts_shfl_up(incl, 1);
     if (lane == 0) ex = id;
-    TileSum run = ts_compose(TileSum{0, 0, 0, 0, 1}, ts_compose(wsum[w], ex));
-    for (int64_t t = t0; t < t1; t++) {
-        toff[t] = run.b;
-        toff2[t] = run.fb;
-        tcarry[t] = run.last;
-        run = ts_compose(run, TileSum{ta[t], tb[t], tfa[t], tfb[t], tlast[t]});
+    if (total) *total = wsum[16];
+    return ts_compose(wsum[w], ex);
+}
+
+__global__ __launch_bounds__(SCAN_B) void k_strip_scan_local(int64_t ntiles, int64_t* __restrict__ ta, int64_t* __restrict__ tb,
+                                                          int64_t* __restrict__ tfa, int64_t* __restrict__ tfb,
+                                                          int32_t* __restrict__ tlast, TileSum* __restrict__ btot) {
+    __shared__ TileSum wsum[17];
+    const int64_t t = (int64_t)blockIdx.x * SCAN_B + threadIdx.x;
+    const TileSum v = t < ntiles ? TileSum{ta[t], tb[t], tfa[t], tfb[t], tlast[t]} : TileSum{0, 0, 0, 0, -1};
+    TileSum tot;
+    const TileSum ex = block_scan_tiles(v, wsum, &tot);
+    if (t < ntiles) { ta[t] = ex.a; tb[t] = ex.b; tfa[t] = ex.fa; tfb[t] = ex.fb; tlast[t] = ex.last; }
+    if (threadIdx.x == 0) btot[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_B) void k_strip_scan_blocks(int64_t nblk, TileSum* __restrict__ btot) {
+    __shared__ TileSum wsum[17];
+    const TileSum v = (int64_t)threadIdx.x < nblk ? btot[threadIdx.x] : TileSum{0, 0, 0, 0, -1};
+    TileSum tot;
+    const TileSum ex = block_scan_tiles(v, wsum, &tot);
+    if ((int64_t)threadIdx.x < nblk) btot[threadIdx.x] = ex;
+    if (threadIdx.x == 0) btot[SCAN_B] = tot;
+}
+
+__global__ void k_strip_scan_apply(int64_t ntiles, const int64_t* __restrict__ ta, const int64_t* __restrict__ tb,
+                                   const int64_t* __restrict__ tfa, const int64_t* __restrict__ tfb,
+                                   const int32_t* __restrict__ tlast, const TileSum* __restrict__ btot,
+                                   int64_t* __restrict__ toff, int64_t* __restrict__ toff2, int32_t* __restrict__ tcarry,
+                                   int64_t* __restrict__ d_len, int64_t* __restrict__ d_len2) {
+    const TileSum start{0, 0, 0, 0, 1};   // the stream starts as if after a kept line
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += (int64_t)gridDim.x * blockDim.x) {
+        const TileSum r = ts_compose(ts_compose(start, btot[t / SCAN_B]), TileSum{ta[t], tb[t], tfa[t], tfb[t], tlast[t]});
+        toff[t] = r.b;
+        toff2[t] = r.fb;
+        tcarry[t] = r.last;
     }
-    if (threadIdx.x == 1023) {
-        *d_len = run.b;
-        if (d_len2) *d_len2 = run.fb;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const TileSum r = ts_compose(start, btot[SCAN_B]);
+        *d_len = r.b;
+        if (d_len2) *d_len2 = r.fb;
     }
 }
 
@@ -441,8 +465,15 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
     hipLaunchKernelGGL(k_strip_summary, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, fmode, buf, n, d_header,
                        sc.tile_a, sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last);
-    hipLaunchKernelGGL(k_strip_scan, dim3(1), dim3(1024), 0, s, ntiles, sc.tile_a, sc.tile_b, sc.tile_fa, sc.tile_fb,
-                       sc.tile_last, sc.tile_off, sc.tile_off2, sc.tile_carry, d_len, d_len2);
+    const int64_t nblk = (ntiles + SCAN_B - 1) / SCAN_B;
+    if (nblk > SCAN_B) return SCCG_E_UNSUPPORTED;   // > 8 GiB of FASTA
+    TileSum* btot = reinterpret_cast<TileSum*>(sc.block_sums);
+    hipLaunchKernelGGL(k_strip_scan_local, dim3((unsigned)nblk), dim3(SCAN_B), 0, s, ntiles, sc.tile_a, sc.tile_b,
+                       sc.tile_fa, sc.tile_fb, sc.tile_last, btot);
+    hipLaunchKernelGGL(k_strip_scan_blocks, dim3(1), dim3(SCAN_B), 0, s, nblk, btot);
+    hipLaunchKernelGGL(k_strip_scan_apply, dim3(grid_for(ntiles, 256)), dim3(256), 0, s, ntiles, sc.tile_a, sc.tile_b,
+                       sc.tile_fa, sc.tile_fb, sc.tile_last, btot, sc.tile_off, sc.tile_off2, sc.tile_carry, d_len,
+                       d_len2);
     PROF_LAUNCH(PROF_STRIP, s, k_strip_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, fmode, buf, n,
                 d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
     SCCG_HIP(hipGetLastError());

@@ -56,6 +56,7 @@ struct IngestScratch {
     int64_t* tile_off;
     int64_t* tile_off2;
     int32_t* tile_carry;
+    void* block_sums;     // (1024 + 1) x 40 bytes
     int64_t* scalars;     // [0] header start, [1] header end, [2] out len, [3] flags
 };
 

@@ -32,7 +32,7 @@ int sccg_hip_fail(hipError_t e, const char* what, const char* file, int line) {
 namespace {
 
 enum Slot {
-    B_RFA, B_TFA, B_R, B_T, B_TILE_A, B_TILE_B, B_TILE_FA, B_TILE_FB, B_TILE_LAST, B_TILE_OFF, B_TILE_OFF2, B_TILE_CARRY,
+    B_RFA, B_TFA, B_R, B_T, B_TILE_A, B_TILE_B, B_TILE_FA, B_TILE_FB, B_TILE_LAST, B_TILE_OFF, B_TILE_OFF2, B_TILE_CARRY, B_TILE_BSUM,
     B_SCAL, B_PARTIAL,
     B_RUN_S, B_RUN_E, B_TMP64, B_RECS, B_STAT, B_MAPS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
     // decompression
@@ -176,8 +176,9 @@ int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const in
     GET(int64_t, to, B_TILE_OFF, ntiles);
     GET(int64_t, to2, B_TILE_OFF2, ntiles);
     GET(int32_t, tc, B_TILE_CARRY, ntiles);
+    GET(int64_t, bs, B_TILE_BSUM, 1025 * 5);
     sc.tile_a = ta; sc.tile_b = tb; sc.tile_fa = tfa; sc.tile_fb = tfb; sc.tile_last = tl; sc.tile_off = to;
-    sc.tile_off2 = to2; sc.tile_carry = tc; sc.scalars = nullptr;
+    sc.tile_off2 = to2; sc.tile_carry = tc; sc.block_sums = bs; sc.scalars = nullptr;
     TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, ctx->stream, fmode, out2,
                            out2 ? d_len + 1 : nullptr));
     return d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1);

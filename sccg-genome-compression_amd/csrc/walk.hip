@@ -77,6 +77,8 @@ struct WalkPtrs {
     uint64_t* atab;
     int32_t abits;
     unsigned long long* fc;   // full-candidate scan scalars: [0] lmax [1] cnt [2] has0 [3] minkey [4] firsthit [5] firstexo
+                              // [8..11] the same four for the batch's first position (k_presence + k_cand_reduce)
+    unsigned long long* fcb;  // per presence block: 4 candidate statistics
     int64_t* flat_off;        // per chunk
     int32_t* ft;
     int32_t* fp;
@@ -749,12 +751,41 @@ __global__ void k_fullc(WalkPtrs A, int32_t y, int32_t P, int pass) {
 // first position in the batch holding a non-ACGT k-mer (checked separately, exactly)
 constexpr int PB = 1024;
 constexpr int PBBITS = 11;
+constexpr int PRESENCE_GRID = 1024;   // blocks of a presence sweep (each first builds the batch's LDS tables)
 constexpr int PFBITS = 17;   // presence pre-filter: 2^17-bit LDS bitmap of the batch's keys
+
+// candidate statistics of one target position (compression.cpp:114-130 over ALL candidates):
+// longest extension, how many reach it, whether position 0 does, least pick key among the others
+struct CandBest {
+    uint32_t l, cnt, has0;
+    uint64_t minkey;
+};
+__device__ __forceinline__ CandBest cb_merge(const CandBest& a, const CandBest& b) {
+    if (a.l > b.l) return a;
+    if (b.l > a.l) return b;
+    return CandBest{a.l, a.cnt + b.cnt, a.has0 | b.has0, a.minkey < b.minkey ? a.minkey : b.minkey};
+}
+__device__ __forceinline__ CandBest cb_shfl_xor(const CandBest& v, int d) {
+    return CandBest{(uint32_t)__shfl_xor((int)v.l, d, 64), (uint32_t)__shfl_xor((int)v.cnt, d, 64),
+                    (uint32_t)__shfl_xor((int)v.has0, d, 64), (uint64_t)__shfl_xor((unsigned long long)v.minkey, d, 64)};
+}
+__device__ __forceinline__ CandBest cb_wave(CandBest v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = cb_merge(v, cb_shfl_xor(v, d));
+    return v;
+}
+
+// Besides the first batch position with any candidate, the sweep gathers the candidate statistics
+// of the batch's FIRST position x0 (the usual answer), so the ungated first step needs no second
+// pass: per-block results in fcb, combined by k_cand_reduce into fc[8..11].
 __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0, int32_t nb) {
     __shared__ uint32_t hkey[1 << PBBITS];
     __shared__ uint32_t hidx[1 << PBBITS];
     __shared__ uint32_t bits[1 << (PFBITS - 5)];
+    __shared__ CandBest wbest[SCCG_BLOCK / 64];
     const int k = A.k;
+    const uint32_t key0 = walk_key(A.T + x0, k);   // exotic: no statistics (host falls back)
+    CandBest best{0, 0, 0, ~0ull};
     for (int i = threadIdx.x; i < (1 << PBBITS); i += blockDim.x) { hkey[i] = 0xffffffffu; hidx[i] = 0xffffffffu; }
     for (int i = threadIdx.x; i < (1 << (PFBITS - 5)); i += blockDim.x) bits[i] = 0;
     __syncthreads();
@@ -786,6 +817,10 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
         loadw<4>(A.R + c, w);
         pack_codes<4>(w, cw, bad);
         const uint32_t code = (uint32_t)cw & ((1u << (2 * k)) - 1u);
+        if (code == key0) {
+            const uint32_t l = (uint32_t)serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, x0, k);
+            best = cb_merge(best, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key((int32_t)c, -1) : ~0ull});
+        }
         int slot = (int)slot_hash(code, PBBITS);
         for (;;) {
             const uint32_t hk = hkey[slot];
@@ -794,6 +829,30 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
             slot = (slot + 1) & ((1 << PBBITS) - 1);
         }
     });
+    best = cb_wave(best);
+    if (lane_id() == 0) wbest[wave_in_block()] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < SCCG_BLOCK / 64; i++) best = cb_merge(best, wbest[i]);
+        unsigned long long* o = A.fcb + 4 * blockIdx.x;
+        o[0] = best.l; o[1] = best.cnt; o[2] = best.has0; o[3] = best.minkey;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_cand_reduce(WalkPtrs A, int nblk) {
+    __shared__ CandBest wbest[16];
+    CandBest v{0, 0, 0, ~0ull};
+    for (int b = (int)threadIdx.x; b < nblk; b += (int)blockDim.x) {
+        const unsigned long long* o = A.fcb + 4 * b;
+        v = cb_merge(v, CandBest{(uint32_t)o[0], (uint32_t)o[1], (uint32_t)o[2], o[3]});
+    }
+    v = cb_wave(v);
+    if (lane_id() == 0) wbest[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); i++) v = cb_merge(v, wbest[i]);
+        A.fc[8] = v.l; A.fc[9] = v.cnt; A.fc[10] = v.has0; A.fc[11] = v.minkey;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -903,7 +962,8 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.scal = c.take<int32_t>(16);
     A.abits = anchor_bits(nR);
     A.atab = c.take<uint64_t>((size_t)1 << A.abits);
-    A.fc = c.take<unsigned long long>(8);
+    A.fc = c.take<unsigned long long>(16);
+    A.fcb = c.take<unsigned long long>(4 * PRESENCE_GRID);
     A.flat_off = c.take<int64_t>(C + 1);
     const size_t maxm = (size_t)(nT / k + 2);
     A.ft = c.take<int32_t>(maxm); A.fp = c.take<int32_t>(maxm); A.fl = c.take<int32_t>(maxm);
@@ -1084,18 +1144,28 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     int32_t first_y = INVALID, first_p = 0, first_l = 0;
     if (nRp >= k && lastk >= 0) {
         int32_t x0 = 0;
+        unsigned long long r[8];   // fc[4..11]: first hit, first exotic, statistics of the batch's x0
         while (x0 <= lastk && first_y == INVALID) {
             const int32_t nb = (lastk - x0 + 1) < PB ? (lastk - x0 + 1) : PB;
             RC(set_u64(A.fc + 4, {-1, -1}, s));
             const int64_t npos = nRp - k + 1;
             unsigned g = grid_for(npos, 256 * FC_PER_T);
-            if (g > 1024) g = 1024;   // every block first builds the batch's LDS tables
+            if (g > PRESENCE_GRID) g = PRESENCE_GRID;
             PROF_LAUNCH(PROF_PRESENCE, s, k_presence, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, nb);
+            hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)g);
             SCCG_HIP(hipGetLastError());
-            unsigned long long r[2];
             SCCG_HIP(hipMemcpyAsync(r, A.fc + 4, sizeof r, hipMemcpyDeviceToHost, s));
             SCCG_HIP(hipStreamSynchronize(s));
-            if (r[0] != ~0ull && r[0] < r[1]) { first_y = (int32_t)r[0]; break; }
+            if (r[0] != ~0ull && r[0] < r[1]) {
+                first_y = (int32_t)r[0];
+                if (first_y == x0 && r[4] > 0) {   // statistics gathered by the same sweep
+                    const uint64_t k0 = 1ull << 32;   // pick_key(0, -1)
+                    const uint64_t pk = (r[5] >= 2 && r[6]) ? r[7] : ((r[6] && k0 < r[7]) ? k0 : r[7]);
+                    first_p = (int32_t)(uint32_t)pk;
+                    first_l = (int32_t)r[4];
+                }
+                break;
+            }
             if (r[1] != ~0ull) {
                 FullC f;
                 RC(run_fullc(A, (int32_t)r[1], -1, &f, s));
@@ -1105,7 +1175,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             }
             x0 += nb;
         }
-        if (first_y != INVALID) {
+        if (first_y != INVALID && first_l == 0) {
             FullC f;
             RC(run_fullc(A, first_y, -1, &f, s));
             first_p = f.p;
