@@ -35,6 +35,8 @@ void prof_end(hipStream_t s, int id);
 #include <initializer_list>
 int dev_set_i64(int64_t* p, int n, std::initializer_list<int64_t> vals, hipStream_t s);
 int dev_set_i32(int32_t* p, int n, std::initializer_list<int32_t> vals, hipStream_t s);
+// stream-ordered write of up to 16 bytes (copied into the kernel arguments)
+int dev_put_bytes(uint8_t* p, const char* bytes, int n, hipStream_t s);
 int64_t scan_partials_needed(int64_t n);
 int dev_excl_sum(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
                  hipStream_t s);

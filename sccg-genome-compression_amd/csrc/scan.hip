@@ -135,7 +135,23 @@ __global__ void k_set_i32(int32_t* p, int n, Vals8i v) {
     if ((int)threadIdx.x < n) p[threadIdx.x] = v.v[threadIdx.x];
 }
 
+struct Bytes16 {
+    uint8_t v[16];
+};
+__global__ void k_set_u8(uint8_t* p, int n, Bytes16 v) {
+    if ((int)threadIdx.x < n) p[threadIdx.x] = v.v[threadIdx.x];
+}
+
 }  // namespace
+
+int dev_put_bytes(uint8_t* p, const char* bytes, int n, hipStream_t s) {
+    Bytes16 v{};
+    if (n > 16) return SCCG_E_INTERNAL;
+    for (int i = 0; i < n; i++) v.v[i] = (uint8_t)bytes[i];
+    hipLaunchKernelGGL(k_set_u8, dim3(1), dim3(64), 0, s, p, n, v);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
 
 // Stream-ordered writes of up to 8 scalars: the values travel as kernel arguments, so no host
 // buffer has to outlive the call (a hipMemcpyAsync from a stack temporary would).

@@ -34,7 +34,7 @@ namespace {
 enum Slot {
     B_RFA, B_TFA, B_R, B_T, B_TILE_A, B_TILE_B, B_TILE_FA, B_TILE_FB, B_TILE_LAST, B_TILE_OFF, B_TILE_OFF2, B_TILE_CARRY, B_TILE_BSUM,
     B_SCAL, B_PARTIAL,
-    B_RUN_S, B_RUN_E, B_TMP64, B_RECS, B_STAT, B_MAPS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
+    B_RUN_S, B_RUN_E, B_TMP64, B_RUN_SN, B_RUN_EN, B_TMP64N, B_NLINE, B_RECS, B_STAT, B_MAPS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
     // decompression
     B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC,
     B_COUNT
@@ -181,28 +181,34 @@ int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const in
     sc.tile_off2 = to2; sc.tile_carry = tc; sc.block_sums = bs; sc.scalars = nullptr;
     TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, ctx->stream, fmode, out2,
                            out2 ? d_len + 1 : nullptr));
-    return d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1);
+    return h_len ? d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1) : 0;   // h_len null: the caller reads d_len later
 }
 
-// run line of `pred` over s[0,n) written at out; returns its length
-int run_line(sccg_ctx* ctx, RunPred pred, const uint8_t* s, int64_t n, uint8_t* out, int64_t* d_sc, int64_t* h_len) {
+// Both run lines of the stripped target (compression.cpp:341-368 lowercase, :495-522 N) in two
+// syncs: run extraction for both predicates, one read of both run counts, run text for both, one
+// read of both text lengths.  The lowercase line goes to out_lower, the N line to out_n.
+int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower, uint8_t** out_n, int64_t* d_sc,
+              int64_t* h_lens) {
+    hipStream_t s = ctx->stream;
     const int64_t maxruns = n / 2 + 2;
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE + 1;
-    GET(int32_t, rs, B_RUN_S, maxruns);
-    GET(int32_t, re, B_RUN_E, maxruns);
-    GET(int64_t, tmp, B_TMP64, (maxruns > ntiles ? maxruns : ntiles));
-    GET(int64_t, part, B_PARTIAL, scan_partials_needed(maxruns > ntiles ? maxruns : ntiles) + 16);
-    TRY(launch_runs(pred, s, n, rs, re, d_sc, tmp, part, ctx->stream));
-    int64_t nruns = 0;
-    TRY(d2h_i64(ctx, d_sc, &nruns, 1));
-    TRY(launch_run_text(rs, re, nruns, n, out, d_sc, tmp, part, ctx->stream));
-    return d2h_i64(ctx, d_sc, h_len, 1);
-}
-
-int put_bytes(sccg_ctx* ctx, uint8_t* dst, const char* s, size_t n) {
-    HIPTRY(hipMemcpyAsync(dst, s, n, hipMemcpyHostToDevice, ctx->stream));
-    HIPTRY(hipStreamSynchronize(ctx->stream));   // s may be a stack temporary
-    return 0;
+    const int64_t ntmp = maxruns > ntiles ? maxruns : ntiles;
+    GET(int32_t, rs_l, B_RUN_S, maxruns);
+    GET(int32_t, re_l, B_RUN_E, maxruns);
+    GET(int64_t, tmp_l, B_TMP64, ntmp);
+    GET(int32_t, rs_n, B_RUN_SN, maxruns);
+    GET(int32_t, re_n, B_RUN_EN, maxruns);
+    GET(int64_t, tmp_n, B_TMP64N, ntmp);
+    GET(int64_t, part, B_PARTIAL, scan_partials_needed(ntmp) + 16);
+    TRY(launch_runs(RUN_LOWER, s_in, n, rs_l, re_l, d_sc, tmp_l, part, s));
+    TRY(launch_runs(RUN_N, s_in, n, rs_n, re_n, d_sc + 1, tmp_n, part, s));
+    int64_t nruns[2];
+    TRY(d2h_i64(ctx, d_sc, nruns, 2));
+    TRY(launch_run_text(rs_l, re_l, nruns[0], n, out_lower, d_sc + 2, tmp_l, part, s));
+    GET(uint8_t, nline, B_NLINE, 24 * nruns[1] + 16);   // <= 23 text bytes per run
+    *out_n = nline;
+    TRY(launch_run_text(rs_n, re_n, nruns[1], n, nline, d_sc + 3, tmp_n, part, s));
+    return d2h_i64(ctx, d_sc + 2, h_lens, 2);
 }
 
 int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_t* tfa, int64_t tn, uint8_t* out,
@@ -231,18 +237,19 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     HIPTRY(hipMemsetAsync(d_flags, 0, sizeof(int32_t), s));
 
     // ---- ingest (compression.cpp:181-220)
+    // header search and both strips run back to back; one sync reads every length (sc[0..9])
     TRY(launch_find_header(tfa, tn, sc, s));
-    int64_t hdr[2];
-    TRY(d2h_i64(ctx, sc, hdr, 2));
-    int64_t lt[2], lr[2];
-    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, lt, FILTER_DROP_N_UPPER, Tp));
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, lr, FILTER_DROP_N_UPPER, Rp));
+    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp));
+    int64_t hsc[10];
+    int32_t flags = 0;
+    HIPTRY(hipMemcpyAsync(hsc, sc, sizeof hsc, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(&flags, d_flags, sizeof flags, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    const int64_t hdr[2] = {hsc[0], hsc[1]}, lt[2] = {hsc[2], hsc[3]}, lr[2] = {hsc[7], hsc[8]};
     const int64_t nT = lt[0], nR = lr[0];
     if (nT >= INT32_MAX - 8 || nR >= INT32_MAX - 8)
         return ctx->fail(SCCG_E_UNSUPPORTED, "sequence longer than the reference's int positions allow");
-    int32_t flags = 0;
-    HIPTRY(hipMemcpyAsync(&flags, d_flags, sizeof flags, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipStreamSynchronize(s));
     if (flags & 1)
         return ctx->fail(SCCG_E_UNSUPPORTED,
                          "target sequence holds '(' bytes: delta_encode's token scan would misparse them "
@@ -258,11 +265,14 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     int64_t pos = 0;
     if (has_hdr) {
         HIPTRY(hipMemcpyAsync(out, tfa + hdr[0], (size_t)hlen, hipMemcpyDeviceToDevice, s));
-        TRY(put_bytes(ctx, out + hlen, "\n", 1));
+        TRY(dev_put_bytes(out + hlen, "\n", 1, s));
         pos = hlen + 1;
     }
-    int64_t llen = 0;
-    TRY(run_line(ctx, RUN_LOWER, T, nT, out + pos, sc + 4, &llen));
+    // both run lines now (the N line is kept aside until the mode is known)
+    uint8_t* nline = nullptr;
+    int64_t rl_len[2];
+    TRY(run_lines(ctx, T, nT, out + pos, &nline, sc + 10, rl_len));
+    const int64_t llen = rl_len[0];
     pos += llen;
     const int64_t lower_end = pos;
     mark("lower_line");
@@ -292,7 +302,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     mark("local");
     if (sw < 0) {
         // ---- local: "\n,\n" + records + leftover segments
-        TRY(put_bytes(ctx, out + pos, "\n,\n", 3));
+        TRY(dev_put_bytes(out + pos, "\n,\n", 3, s));
         pos += 3;
         GET(int64_t, sa, B_SEG_A, iters + 1);
         GET(int64_t, sb, B_SEG_B, iters + 1);
@@ -316,12 +326,12 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         // ---- global (compression.cpp:484-574)
         st.mode_global = 1;
         pos = lower_end;
-        TRY(put_bytes(ctx, out + pos, "\n", 1));
+        TRY(dev_put_bytes(out + pos, "\n", 1, s));
         pos += 1;
-        int64_t nlen = 0;
-        TRY(run_line(ctx, RUN_N, T, nT, out + pos, sc + 6, &nlen));
+        const int64_t nlen = rl_len[1];
+        if (nlen) HIPTRY(hipMemcpyAsync(out + pos, nline, (size_t)nlen, hipMemcpyDeviceToDevice, s));
         pos += nlen;
-        TRY(put_bytes(ctx, out + pos, "\n", 1));
+        TRY(dev_put_bytes(out + pos, "\n", 1, s));
         pos += 1;
         mark("n_line");
         const int64_t np[2] = {lt[1], lr[1]};
@@ -441,9 +451,9 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     GET(uint8_t, dec, B_D_DEC, D + 64);
     TRY(dc_decode_fill(enc, nenc, lp, doff, dsum, dlt, contrib, Rp, dec, s));
     if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
-    TRY(put_bytes(ctx, out + hlen, "\n", 1));
+    TRY(dev_put_bytes(out + hlen, "\n", 1, s));
     TRY(dc_format(dec, nres, nr, lr, out + hlen + 1, s));
-    TRY(put_bytes(ctx, out + total - 1, "\n", 1));
+    TRY(dev_put_bytes(out + total - 1, "\n", 1, s));
     HIPTRY(hipStreamSynchronize(s));
     ctx->stats.target_bases = nres;
     ctx->stats.reference_bases = nRp;

@@ -546,6 +546,14 @@ __global__ void k_fill_literal(WalkPtrs A, int32_t j0, int32_t P) {
     }
 }
 
+// round 1: every chunk, chunk 0 exact (a fix-up with an empty trajectory), the others speculative
+__global__ void k_round1_init(WalkPtrs A) {
+    for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
+        A.kind[j] = j ? KIND_SPEC : KIND_FIX;
+        A.plist[j] = j;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // pending chunks: entry state (predecessor's exit) differs from the one their trajectory used
 // ---------------------------------------------------------------------------------------------
@@ -689,33 +697,39 @@ __device__ __forceinline__ int32_t serial_ext(const uint8_t* R, int32_t nR, cons
 template <typename Pred, typename Hit>
 __device__ __forceinline__ void sweep_kmers(const uint8_t* __restrict__ R, int64_t npos, int k, Pred&& pred, Hit&& hit) {
     const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
-    for (int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * FC_PER_T; p0 < npos;
-         p0 += (int64_t)gridDim.x * blockDim.x * FC_PER_T) {
-        const uint4* src = reinterpret_cast<const uint4*>(R + p0);
-        uint32_t w[20];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * FC_PER_T;
+    for (int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * FC_PER_T; p0 < npos; p0 += stride) {
+        uint32_t cw[20], acc = 0;
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(R + p0);
+            uint32_t w[20];
 #pragma unroll
-        for (int i = 0; i < 5; i++) {
-            const uint4 v = src[i];
-            w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+            for (int i = 0; i < 5; i++) {
+                const uint4 v = src[i];
+                w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+            }
+#pragma unroll
+            for (int i = 0; i < 20; i++) { uint32_t d; cw[i] = swar_codes(w[i], d); acc |= d; }
         }
-        uint32_t cw[20], dw[20], acc = 0;
         uint64_t hits = 0;
-#pragma unroll
-        for (int i = 0; i < 20; i++) { cw[i] = swar_codes(w[i], dw[i]); acc |= dw[i]; }
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             uint64_t code = 0;
             uint32_t bad = 0;
 #pragma unroll
             for (int i = 0; i < 8; i++) code |= (uint64_t)cw[4 * g + i] << (8 * i);
-            if (acc) {
+            if (acc) {   // rare: some byte is not A/C/G/T -- re-read the group's words
+                const uint4* gp = reinterpret_cast<const uint4*>(R + p0 + 16 * g);
+                const uint4 v0 = gp[0], v1 = gp[1];
+                const uint32_t gw[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-                for (int i = 0; i < 8; i++) bad |= nz_bytes(dw[4 * g + i]) << (4 * i);
+                for (int i = 0; i < 8; i++) { uint32_t d; swar_codes(gw[i], d); bad |= nz_bytes(d) << (4 * i); }
             }
+            uint32_t m16 = 0;   // built high position first: shifts by one, no per-bit constants
 #pragma unroll
-            for (int st = 0; st < 16; st++) {
-                if (pred((uint32_t)(code >> (2 * st)) & MASK, ((bad >> st) & KM) == 0)) hits |= 1ull << (16 * g + st);
-            }
+            for (int st = 15; st >= 0; st--)
+                m16 = (m16 << 1) | (uint32_t)pred((uint32_t)(code >> (2 * st)) & MASK, ((bad >> st) & KM) == 0);
+            hits |= (uint64_t)m16 << (16 * g);
         }
         if (p0 + FC_PER_T > npos) hits &= npos - p0 >= 64 ? ~0ull : ((1ull << (npos - p0)) - 1);
         while (hits) {
@@ -1023,8 +1037,9 @@ int h2d_sync(void* dst, const void* src, size_t bytes, hipStream_t s) {
 // Exact walks that hit the pn2 == 0 sentinel stop with status ST_ESC; the reference then takes the
 // ungated (pn1, ln1) over ALL candidates (compression.cpp:124-138): resolve each with the full
 // scan, append that match, and resume the walk behind it.  Rare: needs P <= m.
-int resolve_escalations(WalkPtrs& A, hipStream_t s) {
+int resolve_escalations(WalkPtrs& A, hipStream_t s, std::vector<int32_t>* resumed) {
     const size_t C = (size_t)A.C;
+    std::vector<char> seen(C, 0);
     for (;;) {
         int32_t nesc = 0;
         SCCG_HIP(hipMemcpyAsync(&nesc, A.scal + 1, sizeof nesc, hipMemcpyDeviceToHost, s));
@@ -1053,6 +1068,7 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s) {
                 (rc = dev_set_i32(A.escN + j, 1, {en[j] + 1}, s)) || (rc = dev_set_i32(A.kind + j, 1, {KIND_RESUME}, s)))
                 return rc;
             rl.push_back((int32_t)j);
+            if (!seen[j]) { seen[j] = 1; resumed->push_back((int32_t)j); }
         }
         int rc = dev_set_i32(A.scal + 1, 1, {0}, s);
         if (rc) return rc;
@@ -1216,13 +1232,8 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
         SCCG_HIP(hipGetLastError());
         // round 1: chunk 0 exact (as a fix-up with an empty trajectory), chunks >= 1 speculative
-        {
-            std::vector<int32_t> kinds(C, KIND_SPEC), ids(C);
-            kinds[0] = KIND_FIX;
-            for (size_t j = 0; j < C; j++) ids[j] = (int32_t)j;
-            RC(h2d_sync(A.kind, kinds.data(), C * sizeof(int32_t), s));
-            RC(h2d_sync(A.plist, ids.data(), C * sizeof(int32_t), s));
-        }
+        hipLaunchKernelGGL(k_round1_init, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
+        SCCG_HIP(hipGetLastError());
         RC(dev_set_i32(A.snapX, 1, {startX}, s));
         RC(dev_set_i32(A.snapP, 1, {startP}, s));
         mark("anchors");
@@ -1233,12 +1244,38 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
             SCCG_HIP(hipGetLastError());
             res->rounds = round;
-            RC(resolve_escalations(A, s));
+            // Commit and find the next round's pending chunks without waiting for the host; the
+            // rare escalated (pn2 == 0) and frozen chunks are handled after the round's one sync.
             RC(dev_set_i32(A.scal + 5, 1, {0}, s));
             hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
                                (const int32_t*)A.plist, nlist);
             SCCG_HIP(hipGetLastError());
-            RC(frozen_fill(A, s));
+            auto find_pending = [&]() -> int {
+                RC(dev_set_i32(A.scal, 1, {0}, s));
+                hipLaunchKernelGGL(k_pending, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
+                SCCG_HIP(hipGetLastError());
+                return 0;
+            };
+            RC(find_pending());
+            int32_t rs[6];
+            SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
+            SCCG_HIP(hipStreamSynchronize(s));
+            if (rs[1] || rs[5]) {
+                if (rs[1]) {   // escalations: resolve on the host, resume, commit the resumed chunks
+                    std::vector<int32_t> resumed;
+                    RC(resolve_escalations(A, s, &resumed));
+                    RC(h2d_sync(A.rlist, resumed.data(), resumed.size() * 4, s));
+                    const int32_t nr = (int32_t)resumed.size();
+                    hipLaunchKernelGGL(k_commit, dim3(grid_for(nr, 256) > 4096 ? 4096 : grid_for(nr, 256)), dim3(256), 0, s, A,
+                                       (const int32_t*)A.rlist, nr);
+                    SCCG_HIP(hipGetLastError());
+                }
+                RC(frozen_fill(A, s));
+                RC(find_pending());
+                SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipStreamSynchronize(s));
+            }
+            nlist = rs[0];
             if (dbg) {
                 SCCG_HIP(hipStreamSynchronize(s));
                 static thread_local auto tprev = std::chrono::steady_clock::now();
@@ -1325,12 +1362,6 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                     for (int q = 0; q < nshow; q++) fprintf(stderr, "      m%d (%d,%d,%d)\n", q, tt[q], pp[q], ll[q]);
                 }
             }
-            // which chunks were walked from a state that is not their true entry?
-            RC(dev_set_i32(A.scal, 1, {0}, s));
-            hipLaunchKernelGGL(k_pending, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
-            SCCG_HIP(hipGetLastError());
-            SCCG_HIP(hipMemcpyAsync(&nlist, A.scal, sizeof nlist, hipMemcpyDeviceToHost, s));
-            SCCG_HIP(hipStreamSynchronize(s));
             if (!nlist) break;
             if (round > 4 * (int64_t)A.C + 16) return SCCG_E_INTERNAL;
         }
