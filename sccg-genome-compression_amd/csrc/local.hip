@@ -22,17 +22,17 @@
 namespace {
 
 constexpr int WPB = 4;            // segments (waves) per block
-constexpr int SEGB = 1024 + 16;   // LDS bytes per segment string
-constexpr int NBB = 10;           // 1024 k-mer buckets
+constexpr int SEGB = 1024;        // LDS bytes per segment string (1000 + zero padding)
+constexpr int NBB = 9;            // 512 k-mer buckets
 constexpr int NB = 1 << NBB;
 constexpr int MANY = 4;           // more candidates than this: extend one per lane
 
 struct SegLds {
     uint8_t r[SEGB];
     uint8_t t[SEGB];
-    uint32_t skey[1024];          // reference k-mer keys, grouped by bucket
+    uint32_t skey[1024];          // reference k-mer keys, grouped by bucket (first: the bucket counters)
     uint16_t spos[1024];          // their positions
-    uint32_t bstart[NB + 1];      // bucket b holds entries [bstart[b], bstart[b+1])
+    uint16_t bstart[NB + 1];      // bucket b holds entries [bstart[b], bstart[b+1])
     uint64_t hits[16];            // bit p: target k-mer at p has >= 1 candidate
 };
 
@@ -128,31 +128,35 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
     // ---- H: every k-mer of the reference segment (compression.cpp:41-47), counting-sorted by
     //      bucket; lane l owns starts 16l..16l+15
     const int lastr = nr - K;
-    for (int i = lane; i < NB; i += 64) L.bstart[i] = 0;
+    uint32_t* cnt = L.skey;   // bucket counters live where the keys go later
+    for (int i = lane; i < NB; i += 64) cnt[i] = 0;
     wave_sync();
     {
         const int p0 = lane * 16;
-        uint64_t code;
-        uint32_t bad;
-        keys16<K>(&L.r[p0], code, bad);
+        uint64_t code = 0;
+        uint32_t bad = 0;
+        if (p0 <= lastr) keys16<K>(&L.r[p0], code, bad);   // lanes past lastr own no k-mer
         uint32_t key[16], rank[16];
 #pragma unroll
         for (int st = 0; st < 16; st++) {
             const int p = p0 + st;
-            key[st] = (bad >> st) & KM ? exotic_key(&L.r[p], K) : (uint32_t)(code >> (2 * st)) & MASK;
-            if (p <= lastr) rank[st] = atomicAdd(&L.bstart[slot_hash(key[st], NBB)], 1u);
+            key[st] = 0;
+            if (p <= lastr) {
+                key[st] = (bad >> st) & KM ? exotic_key(&L.r[p], K) : (uint32_t)(code >> (2 * st)) & MASK;
+                rank[st] = atomicAdd(&cnt[slot_hash(key[st], NBB)], 1u);
+            }
         }
         wave_sync();
-        // bucket starts: exclusive scan of the counts (16 buckets per lane)
-        uint32_t c[16], run = 0;
+        // bucket starts: exclusive scan of the counts (NB / 64 buckets per lane)
+        constexpr int BPL = NB / 64;
+        uint32_t c[BPL], run = 0;
 #pragma unroll
-        for (int i = 0; i < 16; i++) { c[i] = L.bstart[16 * lane + i]; run += c[i]; }
+        for (int i = 0; i < BPL; i++) { c[i] = cnt[BPL * lane + i]; run += c[i]; }
         const uint32_t incl = wave_incl_add(run);
         uint32_t o = incl - run;
-        wave_sync();
 #pragma unroll
-        for (int i = 0; i < 16; i++) { L.bstart[16 * lane + i] = o; o += c[i]; }
-        if (lane == 63) L.bstart[NB] = o;
+        for (int i = 0; i < BPL; i++) { L.bstart[BPL * lane + i] = (uint16_t)o; o += c[i]; }
+        if (lane == 63) L.bstart[NB] = (uint16_t)o;
         wave_sync();
 #pragma unroll
         for (int st = 0; st < 16; st++) {
@@ -174,9 +178,9 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
         const int p0 = lane * 16;
         uint32_t mask16 = 0;
         if (lastr >= 0) {
-            uint64_t code;
-            uint32_t bad;
-            keys16<K>(&L.t[p0], code, bad);
+            uint64_t code = 0;
+            uint32_t bad = 0;
+            if (p0 <= lastk) keys16<K>(&L.t[p0], code, bad);
             for (int st = 0; st < 16; st++) {
                 const int p = p0 + st;
                 if (p > lastk) break;

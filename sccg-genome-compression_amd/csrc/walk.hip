@@ -34,8 +34,7 @@ constexpr int WTSLOTS = 1 << WTBITS;
 constexpr int32_t INVALID = INT32_MIN;
 constexpr int ANCHOR_K = 32;
 constexpr int ANCHOR_STEP = 32;
-constexpr uint64_t A_EMPTY = ~0ull;          // anchor slot: (32-bit fingerprint << 32) | position
-constexpr uint32_t A_MULTI = 0xFFFFFFFFu;    // position of a 32-mer seen more than once
+constexpr uint32_t A_MULTI = 0xFFFFFFFFu;    // anchor position of a 32-mer seen more than once
 constexpr int32_t FROZEN_MIN = 4096;   // literal bases at a chunk end that trigger a frozen-P scan
 
 enum ChunkKind : int32_t { KIND_SPEC = 0, KIND_FIX = 1, KIND_RESUME = 2 };
@@ -75,6 +74,7 @@ struct WalkPtrs {
     int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round,
                           // [5] frozen count, [6] frozen-scan first hit
     uint64_t* atab;
+    uint32_t agen;            // anchor tag generation (one per call)
     int32_t abits;
     unsigned long long* fc;   // full-candidate scan scalars: [0] lmax [1] cnt [2] has0 [3] minkey [4] firsthit [5] firstexo
                               // [8..11] the same four for the batch's first position (k_presence + k_cand_reduce)
@@ -572,8 +572,12 @@ __global__ void k_pending(WalkPtrs A) {
 
 // ---------------------------------------------------------------------------------------------
 // anchors: 32-mers at every 32nd R' position -> position (or MULTI); one probe batch per chunk.
-// A slot holds a 32-bit fingerprint of the 32-mer's hash (the other hash bits pick the home slot)
-// and the position; a fingerprint clash only costs a wrong guess, never a wrong result.
+// Direct-mapped table, plain stores: a slot (picked by the top hash bits) holds a 32-bit tag --
+// other hash bits XOR the call's generation, so stale slots from earlier calls never match and
+// the table is never cleared -- and a position.  Pass 1 stores every sample; pass 2 marks a slot
+// MULTI when it holds the same tag with another position (a repeated 32-mer).  A sample that
+// loses its slot to a different 32-mer is simply missing.  Anchors only seed speculation: a
+// wrong or missing one costs a re-walk, never a wrong result.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {   // bijective
     x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
@@ -595,27 +599,24 @@ __device__ __forceinline__ bool code32(const uint8_t* s, uint64_t& code) {
     return bad == 0;
 }
 
-__device__ __forceinline__ uint32_t anchor_fp(uint64_t key) {
-    const uint32_t f = (uint32_t)key;
-    return f == 0xFFFFFFFFu ? 0xFFFFFFFEu : f;   // never forms A_EMPTY
-}
+__device__ __forceinline__ uint32_t anchor_tag(uint64_t key, uint32_t gen) { return (uint32_t)key ^ gen; }
 
+// pass 1 (mark = false): store every sample; pass 2 (mark = true): flag repeated 32-mers
+template <bool MARK>
 __global__ void k_anchor_build(WalkPtrs A) {
     const int64_t ns = A.nR >= ANCHOR_K ? ((int64_t)A.nR - ANCHOR_K) / ANCHOR_STEP + 1 : 0;
-    const uint64_t smask = (1ull << A.abits) - 1;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t p = (int32_t)(i * ANCHOR_STEP);
         uint64_t code;
         if (!code32<true>(A.R + p, code)) continue;
         const uint64_t key = mix64(code);
-        const uint32_t fp = anchor_fp(key);
-        const unsigned long long ent = ((unsigned long long)fp << 32) | (uint32_t)p;
-        uint64_t slot = key >> (64 - A.abits);
-        for (;;) {
-            const unsigned long long prev = atomicCAS((unsigned long long*)&A.atab[slot], (unsigned long long)A_EMPTY, ent);
-            if (prev == A_EMPTY) break;
-            if ((uint32_t)(prev >> 32) == fp) { atomicOr((unsigned long long*)&A.atab[slot], (unsigned long long)A_MULTI); break; }
-            slot = (slot + 1) & smask;
+        const uint32_t tag = anchor_tag(key, A.agen);
+        uint64_t* slot = &A.atab[key >> (64 - A.abits)];
+        if (!MARK) {
+            *slot = ((uint64_t)tag << 32) | (uint32_t)p;
+        } else {
+            const uint64_t v = *slot;
+            if ((uint32_t)(v >> 32) == tag && (uint32_t)v != (uint32_t)p) *slot = ((uint64_t)tag << 32) | A_MULTI;
         }
     }
 }
@@ -624,7 +625,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
     const int32_t j = (int32_t)blockIdx.x * WPB + wave_in_block();
     if (j >= A.C) return;
     const int lane = lane_id();
-    const uint64_t smask = (1ull << A.abits) - 1;
     // probe 256 target positions; each hit on a sampled reference 32-mer votes for a diagonal
     constexpr int NB = 4;
     int32_t dg[NB];
@@ -635,23 +635,15 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
         uint64_t code;
         if (y + ANCHOR_K <= A.nT && code32<false>(A.T + y, code)) {
             const uint64_t key = mix64(code);
-            const uint32_t fp = anchor_fp(key);
-            uint64_t slot = key >> (64 - A.abits);
-            for (int probes = 0; probes < 64; probes++) {
-                const uint64_t v = A.atab[slot];
-                if (v == A_EMPTY) break;
-                if ((uint32_t)(v >> 32) == fp) {
-                    const uint32_t ps = (uint32_t)v;
-                    if (ps != A_MULTI) dg[b] = (int32_t)ps - y;
-                    break;
-                }
-                slot = (slot + 1) & smask;
-            }
+            const uint64_t v = A.atab[key >> (64 - A.abits)];
+            if ((uint32_t)(v >> 32) == anchor_tag(key, A.agen) && (uint32_t)v != A_MULTI) dg[b] = (int32_t)(uint32_t)v - y;
         }
     }
-    // earliest diagonal with >= 2 votes (a lone hit is often a repeat copy); else the earliest
+    // the diagonal with the most votes (>= 2; a lone hit is often a repeat copy), ties to the
+    // earliest; else the earliest
     int32_t g = INVALID, first = INVALID;
-    for (int tries = 0; tries < 8 && g == INVALID; tries++) {
+    int gv = 1;
+    for (int tries = 0; tries < 8; tries++) {
         int32_t d = INVALID;
 #pragma unroll
         for (int b = 0; b < NB; b++) {
@@ -666,7 +658,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
             votes += __popcll(__ballot(dg[b] == d));
             if (dg[b] == d) dg[b] = INVALID;
         }
-        if (votes >= 2) g = d;
+        if (votes > gv) { g = d; gv = votes; }
     }
     if (g == INVALID) g = first;
     if (g != INVALID) {
@@ -939,7 +931,7 @@ struct Carve {
 };
 
 int anchor_bits(int64_t nR) {
-    int64_t want = 2 * (nR / ANCHOR_STEP + 1);
+    int64_t want = 4 * (nR / ANCHOR_STEP + 1);   // load <= 1/4: few samples lose their slot
     int b = 10;
     while ((1ll << b) < want && b < 34) b++;
     return b;
@@ -1226,9 +1218,18 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     if (startP != INVALID && lastk >= 0) {
         // anchors -> speculative guesses for chunks 1..C-1
         const int64_t slots = 1ll << A.abits;
-        SCCG_HIP(hipMemsetAsync(A.atab, 0xFF, (size_t)slots * sizeof(uint64_t), s));   // all A_EMPTY
+        // a fresh workspace is cleared once; afterwards every call's generation retires old slots
+        static thread_local const void* ws_seen = nullptr;
+        static thread_local uint32_t gen = 0;
+        if (ws != ws_seen) {
+            SCCG_HIP(hipMemsetAsync(A.atab, 0, (size_t)slots * sizeof(uint64_t), s));
+            ws_seen = ws;
+        }
+        A.agen = 0x9E3779B9u * ++gen;
         const int64_t ns = nRp / ANCHOR_STEP + 1;
-        PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build, dim3(grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256)), dim3(256), 0, s, A);
+        const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
+        PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
         hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
         SCCG_HIP(hipGetLastError());
         // round 1: chunk 0 exact (as a fix-up with an empty trajectory), chunks >= 1 speculative
