@@ -117,6 +117,18 @@ __device__ __forceinline__ void stage_out(const uint32_t* __restrict__ st4, int 
 //   known    kept by strip, line status decided inside the range (REF) / always (TGT)
 //   unknown  REF: non-space bytes before the range's first line start (status from earlier)
 //   fk       kept by the byte filter;  par  '(' bytes
+// SWAR byte tests on 4 bytes: bit 7 of each byte set where the test holds
+__device__ __forceinline__ uint32_t sw_lt(uint32_t x, uint32_t n) {   // byte < n, n <= 128
+    return ~(((x & 0x7F7F7F7Fu) + (0x80u - n) * 0x01010101u) | x) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t sw_eq(uint32_t x, uint32_t c) { return sw_lt(x ^ (c * 0x01010101u), 1); }
+__device__ __forceinline__ uint32_t sw_bits(uint32_t hm) { return ((hm >> 7) * 0x01020408u) >> 24; }   // -> 4 bits
+// toupper of 4 bytes
+__device__ __forceinline__ uint32_t sw_upper(uint32_t x) {
+    const uint32_t lower = sw_lt(x, 'z' + 1) & ~sw_lt(x, 'a');
+    return x - (lower >> 2);
+}
+
 struct StripMasks {
     uint32_t known, unknown, fk, par;
     int32_t last;   // status of the last line start in range: -1 none, 0 drop, 1 keep
@@ -124,15 +136,21 @@ struct StripMasks {
 
 __device__ __forceinline__ StripMasks strip_masks(IngestMode mode, FilterMode fm, const uint32_t (&w)[PER_T / 4],
                                                   uint8_t prev, int64_t off, int64_t n, int64_t h, int64_t he) {
+    // byte classes four at a time (SWAR); flags gathered into one bit per byte
     uint32_t ws = 0, nl = 0, gt = 0, fk = 0, par = 0;
 #pragma unroll
-    for (int i = 0; i < PER_T; i++) {
-        const uint8_t c = wb(w, i);
-        ws |= (uint32_t)c_isspace(c) << i;
-        nl |= (uint32_t)(c == '\n') << i;
-        gt |= (uint32_t)(c == '>') << i;
-        fk |= (uint32_t)filter_keep(fm, c) << i;
-        par |= (uint32_t)(c == '(') << i;
+    for (int q = 0; q < PER_T / 4; q++) {
+        const uint32_t x = w[q];
+        const int sh = 4 * q;
+        ws |= sw_bits(sw_eq(x, ' ') | (sw_lt(x, 14) & ~sw_lt(x, 9))) << sh;   // isspace: ' ', \t..\r
+        if (mode == INGEST_REF) {
+            nl |= sw_bits(sw_eq(x, '\n')) << sh;
+            gt |= sw_bits(sw_eq(x, '>')) << sh;
+        }
+        const uint32_t nn = fm == FILTER_DROP_N_UPPER ? (sw_eq(x, 'N') | sw_eq(x, 'n'))
+                                                      : (fm == FILTER_DROP_UPPERN_ONLY ? sw_eq(x, 'N') : 0u);
+        fk |= (sw_bits(nn) ^ 0xfu) << sh;
+        par |= sw_bits(sw_eq(x, '(')) << sh;
     }
     const int64_t lim = n - off;
     const uint32_t valid = lim >= 32 ? ~0u : (lim > 0 ? (1u << lim) - 1u : 0u);
@@ -315,8 +333,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(IngestMode mode, Fil
                                                             int32_t* __restrict__ flags) {
     __shared__ int32_t tmp[8];
     __shared__ int32_t tmp32[8];
-    __shared__ uint32_t st1[STAGE_WORDS];
-    __shared__ uint32_t st2[STAGE_WORDS];
+    __shared__ uint32_t st1[STAGE_WORDS + SCCG_BLOCK];   // + one dummy word per thread
+    __shared__ uint32_t st2[STAGE_WORDS + SCCG_BLOCK];
     const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
     uint32_t w[PER_T / 4];
     load_words(buf, n, off, w);
@@ -331,11 +349,17 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(IngestMode mode, Fil
     int32_t p2 = out2 ? block_excl_add<int32_t>(__popc(fkeep), tmp32, &tot2) : 0;
     uint8_t* s1 = reinterpret_cast<uint8_t*>(st1);
     uint8_t* s2 = reinterpret_cast<uint8_t*>(st2);
+    // every byte is stored (a dropped byte into this lane's own dummy word), its slot from a
+    // prefix popcount of the keep mask: no per-byte branch
+    uint32_t uw[PER_T / 4];
+#pragma unroll
+    for (int q = 0; q < PER_T / 4; q++) uw[q] = sw_upper(w[q]);
+    const int dummy = 4 * (STAGE_WORDS + (int)threadIdx.x);
 #pragma unroll
     for (int i = 0; i < PER_T; i++) {
-        const uint8_t c = wb(w, i);
-        if ((keep >> i) & 1u) s1[stage_at(p1++)] = c;
-        if (out2 && ((fkeep >> i) & 1u)) s2[stage_at(p2++)] = c_toupper(c);
+        const uint32_t below = (1u << i) - 1u;
+        s1[(keep >> i) & 1u ? stage_at(p1 + __popc(keep & below)) : dummy] = wb(w, i);
+        if (out2) s2[(fkeep >> i) & 1u ? stage_at(p2 + __popc(fkeep & below)) : dummy] = wb(uw, i);
     }
     if (flags && __ballot((keep & r.par) != 0) && lane_id() == 0) atomicOr(flags, 1);
     __syncthreads();
