@@ -374,51 +374,69 @@ __device__ __forceinline__ bool run_pred(RunPred p, uint8_t c) {
     return p == RUN_LOWER ? c_islower(c) : (c == 'N' || c == 'n');
 }
 
-// bit i: pred(byte off + i); bytes past n are not in any run
-__device__ __forceinline__ uint32_t pred_mask(RunPred pr, const uint8_t* __restrict__ in, int64_t n, int64_t off) {
+// bit i: pred(byte off + i) for both predicates (SWAR); bytes past n are not in any run
+__device__ __forceinline__ void pred_masks(const uint8_t* __restrict__ in, int64_t n, int64_t off, uint32_t& ml,
+                                           uint32_t& mn) {
     uint32_t w[PER_T / 4];
     load_words(in, n, off, w);   // pads with ' ' (in no run)
-    uint32_t m = 0;
+    ml = 0;
+    mn = 0;
 #pragma unroll
-    for (int i = 0; i < PER_T; i++) m |= (uint32_t)run_pred(pr, wb(w, i)) << i;
-    return m;
+    for (int q = 0; q < PER_T / 4; q++) {
+        const uint32_t x = w[q];
+        ml |= sw_bits(sw_lt(x, 'z' + 1) & ~sw_lt(x, 'a')) << (4 * q);
+        mn |= sw_bits(sw_eq(x, 'N') | sw_eq(x, 'n')) << (4 * q);
+    }
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_runs_count(RunPred pr, const uint8_t* __restrict__ in, int64_t n,
-                                                           int64_t* __restrict__ cnt) {
+// Both run lines' predicates in one pass (counts of two predicates packed in one 32-bit block
+// scan: a tile holds at most 4096 runs of each).
+__global__ __launch_bounds__(SCCG_BLOCK) void k_runs_count(const uint8_t* __restrict__ in, int64_t n,
+                                                           int64_t* __restrict__ cnt_l, int64_t* __restrict__ cnt_n) {
     __shared__ int32_t tmp32[8];
     const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
-    const uint32_t m = pred_mask(pr, in, n, off);
-    const uint32_t prev = off > 0 && off - 1 < n && run_pred(pr, in[off - 1]);
-    const uint32_t starts = m & ~((m << 1) | prev);
+    uint32_t ml, mn;
+    pred_masks(in, n, off, ml, mn);
+    const bool in_prev = off > 0 && off - 1 < n;
+    const uint32_t pl = in_prev && run_pred(RUN_LOWER, in[off - 1]), pn = in_prev && run_pred(RUN_N, in[off - 1]);
+    const int32_t c = __popc(ml & ~((ml << 1) | pl)) | (__popc(mn & ~((mn << 1) | pn)) << 16);
     int32_t tot;
-    block_excl_add<int32_t>(__popc(starts), tmp32, &tot);
-    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+    block_excl_add<int32_t>(c, tmp32, &tot);
+    if (threadIdx.x == 0) { cnt_l[blockIdx.x] = tot & 0xffff; cnt_n[blockIdx.x] = tot >> 16; }
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_runs_write(RunPred pr, const uint8_t* __restrict__ in, int64_t n,
-                                                           const int64_t* __restrict__ toff,
-                                                           int32_t* __restrict__ rs, int32_t* __restrict__ re) {
+__device__ __forceinline__ void put_positions(uint32_t bits, int64_t off, int32_t* __restrict__ dst, int64_t at) {
+    while (bits) {
+        dst[at++] = (int32_t)(off + __ffs((int)bits) - 1);
+        bits &= bits - 1;
+    }
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_runs_write(const uint8_t* __restrict__ in, int64_t n,
+                                                           const int64_t* __restrict__ toff_l,
+                                                           const int64_t* __restrict__ toff_n, int32_t* __restrict__ rs_l,
+                                                           int32_t* __restrict__ re_l, int32_t* __restrict__ rs_n,
+                                                           int32_t* __restrict__ re_n) {
     __shared__ int32_t tmp32[8];
     const int64_t tile0 = (int64_t)blockIdx.x * INGEST_TILE;
     const int64_t off = tile0 + (int64_t)threadIdx.x * PER_T;
-    const uint32_t m = pred_mask(pr, in, n, off);
-    const uint32_t prev = off > 0 && off - 1 < n && run_pred(pr, in[off - 1]);
-    const uint32_t next = off + PER_T < n && run_pred(pr, in[off + PER_T]);
-    uint32_t starts = m & ~((m << 1) | prev);
-    uint32_t ends = m & ~((m >> 1) | (next << 31));
+    uint32_t ml, mn;
+    pred_masks(in, n, off, ml, mn);
+    const bool in_prev = off > 0 && off - 1 < n, in_next = off + PER_T < n;
+    const uint32_t pl = in_prev && run_pred(RUN_LOWER, in[off - 1]), pn = in_prev && run_pred(RUN_N, in[off - 1]);
+    const uint32_t nl = in_next && run_pred(RUN_LOWER, in[off + PER_T]), nn = in_next && run_pred(RUN_N, in[off + PER_T]);
+    const uint32_t sl = ml & ~((ml << 1) | pl), el = ml & ~((ml >> 1) | (nl << 31));
+    const uint32_t sn = mn & ~((mn << 1) | pn), en = mn & ~((mn >> 1) | (nn << 31));
     // runs open across the tile start end inside this tile (or later) but started before it
-    const bool open_in = tile0 > 0 && tile0 < n && run_pred(pr, in[tile0 - 1]) && run_pred(pr, in[tile0]);
-    int64_t ps = toff[blockIdx.x] + block_excl_add<int32_t>(__popc(starts), tmp32, nullptr);
-    int64_t pe = toff[blockIdx.x] - (open_in ? 1 : 0) + block_excl_add<int32_t>(__popc(ends), tmp32, nullptr);
-    while (starts) {
-        rs[ps++] = (int32_t)(off + __ffs((int)starts) - 1);
-        starts &= starts - 1;
-    }
-    while (ends) {
-        re[pe++] = (int32_t)(off + __ffs((int)ends) - 1);
-        ends &= ends - 1;
-    }
+    const bool t_in = tile0 > 0 && tile0 < n;
+    const bool open_l = t_in && run_pred(RUN_LOWER, in[tile0 - 1]) && run_pred(RUN_LOWER, in[tile0]);
+    const bool open_n = t_in && run_pred(RUN_N, in[tile0 - 1]) && run_pred(RUN_N, in[tile0]);
+    const int32_t xs = block_excl_add<int32_t>(__popc(sl) | (__popc(sn) << 16), tmp32, nullptr);
+    const int32_t xe = block_excl_add<int32_t>(__popc(el) | (__popc(en) << 16), tmp32, nullptr);
+    put_positions(sl, off, rs_l, toff_l[blockIdx.x] + (xs & 0xffff));
+    put_positions(el, off, re_l, toff_l[blockIdx.x] - (open_l ? 1 : 0) + (xe & 0xffff));
+    put_positions(sn, off, rs_n, toff_n[blockIdx.x] + (xs >> 16));
+    put_positions(en, off, re_n, toff_n[blockIdx.x] - (open_n ? 1 : 0) + (xe >> 16));
 }
 
 // text of one run: "d," | "(d,len)" | final singleton "d" (compression.cpp:351-366)
@@ -504,18 +522,19 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     return 0;
 }
 
-int launch_runs(RunPred pred, const uint8_t* in, int64_t n, int32_t* rs, int32_t* re, int64_t* d_nruns,
-                int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s) {
+int launch_runs2(const uint8_t* in, int64_t n, int32_t* rs_l, int32_t* re_l, int32_t* rs_n, int32_t* re_n,
+                 int64_t* d_nruns, int64_t* d_cnt_l, int64_t* d_cnt_n, int64_t* d_partial, hipStream_t s) {
     if (n <= 0) {
-        SCCG_HIP(hipMemsetAsync(d_nruns, 0, sizeof(int64_t), s));
+        SCCG_HIP(hipMemsetAsync(d_nruns, 0, 2 * sizeof(int64_t), s));
         return 0;
     }
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
-    hipLaunchKernelGGL(k_runs_count, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, pred, in, n, d_tile_cnt);
-    int rc = dev_excl_sum(d_tile_cnt, d_tile_cnt, ntiles, d_nruns, d_partial, s);
+    hipLaunchKernelGGL(k_runs_count, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, in, n, d_cnt_l, d_cnt_n);
+    int rc = dev_excl_sum(d_cnt_l, d_cnt_l, ntiles, d_nruns, d_partial, s);
+    if (!rc) rc = dev_excl_sum(d_cnt_n, d_cnt_n, ntiles, d_nruns + 1, d_partial, s);
     if (rc) return rc;
-    PROF_LAUNCH(PROF_RUNS, s, k_runs_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, pred, in, n,
-                       (const int64_t*)d_tile_cnt, rs, re);
+    PROF_LAUNCH(PROF_RUNS, s, k_runs_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, in, n,
+                (const int64_t*)d_cnt_l, (const int64_t*)d_cnt_n, rs_l, re_l, rs_n, re_n);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

@@ -78,9 +78,10 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
                        uint8_t* out, int64_t* d_len, int32_t* d_flags, const IngestScratch& sc,
                        hipStream_t s, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
                        int64_t* d_len2 = nullptr);
-// maximal runs of a predicate -> start/end (inclusive) arrays; *d_nruns = count
-int launch_runs(RunPred pred, const uint8_t* s_in, int64_t n, int32_t* run_s, int32_t* run_e,
-                int64_t* d_nruns, int64_t* d_tile_cnt, int64_t* d_partial, hipStream_t s);
+// maximal runs of lowercase bytes (rs_l/re_l) and of N/n bytes (rs_n/re_n), start/end inclusive,
+// in one pass; d_nruns[0..1] = their counts
+int launch_runs2(const uint8_t* s_in, int64_t n, int32_t* rs_l, int32_t* re_l, int32_t* rs_n, int32_t* re_n,
+                 int64_t* d_nruns, int64_t* d_cnt_l, int64_t* d_cnt_n, int64_t* d_partial, hipStream_t s);
 // run line text (compression.cpp:341-368): writes it to out, *d_len = bytes
 int launch_run_text(const int32_t* run_s, const int32_t* run_e, int64_t nruns, int64_t n,
                     uint8_t* out, int64_t* d_len, int64_t* d_tmp, int64_t* d_partial, hipStream_t s);

@@ -200,8 +200,7 @@ int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower,
     GET(int32_t, re_n, B_RUN_EN, maxruns);
     GET(int64_t, tmp_n, B_TMP64N, ntmp);
     GET(int64_t, part, B_PARTIAL, scan_partials_needed(ntmp) + 16);
-    TRY(launch_runs(RUN_LOWER, s_in, n, rs_l, re_l, d_sc, tmp_l, part, s));
-    TRY(launch_runs(RUN_N, s_in, n, rs_n, re_n, d_sc + 1, tmp_n, part, s));
+    TRY(launch_runs2(s_in, n, rs_l, re_l, rs_n, re_n, d_sc, tmp_l, tmp_n, part, s));
     int64_t nruns[2];
     TRY(d2h_i64(ctx, d_sc, nruns, 2));
     TRY(launch_run_text(rs_l, re_l, nruns[0], n, out_lower, d_sc + 2, tmp_l, part, s));
