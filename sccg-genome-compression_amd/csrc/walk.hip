@@ -71,6 +71,7 @@ struct WalkPtrs {
     int32_t* walked;      // round in which the chunk was last re-walked
     int32_t* frozen;      // fix-up ended in a long literal run at the chunk end
     int32_t* flist;       // committed frozen chunks of the round
+    int32_t* fy;          // per listed frozen chunk: first window hit after its exit (k_frozen_scan)
     int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round,
                           // [5] frozen count, [6] frozen-scan first hit
     uint64_t* atab;
@@ -507,10 +508,18 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
     }
 }
 
-// First position in [x0, lastk] whose k-mer key occurs in the window of P, over the whole rest of
-// the target (every wave builds its own copy of the window, then scans a strided share).
-__global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int32_t x0, int32_t P) {
+// Frozen chunks (committed fix-ups that ended in a long literal run with P unchanged up to their
+// chunk end; k_commit lists them): for each of the first FROZEN_MAX, the first position after its
+// exit whose k-mer key occurs in its window of P, over the whole rest of the target (grid.y picks
+// the frozen chunk; every wave builds its own copy of the window and scans a strided share).
+constexpr int FROZEN_MAX = 256;    // frozen chunks handled per batch (grid.y)
+constexpr int FROZEN_FIRST = 16;   // the batch launched blind, before the round's sync
+__global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int fbase) {
     __shared__ WalkLds lds_all[WPB];
+    const int fi = (int)blockIdx.y, f = fbase + fi;
+    if (f >= A.scal[5]) return;
+    const int32_t j = A.flist[f];
+    const int32_t x0 = A.exitX[j], P = A.exitP[j];
     WalkLds& L = lds_all[wave_in_block()];
     RegWin W;
     reg_window(A, P, W);
@@ -519,30 +528,65 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int32_t 
     const int32_t end = A.nT - A.k + 1;
     const int64_t gw = (int64_t)blockIdx.x * WPB + wave_in_block(), G = (int64_t)gridDim.x * WPB;
     for (int64_t base = x0 + gw * 64 * WIDE; base < end; base += G * 64 * WIDE) {
-        if (base >= (int64_t)__hip_atomic_load(&A.scal[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        if (base >= (int64_t)__hip_atomic_load(&A.fy[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
         const int32_t seg_end = base + 64 * WIDE < end ? (int32_t)(base + 64 * WIDE) : end;
         const int32_t y = wide_scan(A, L, (int32_t)base, seg_end);
         if (y < seg_end) {
-            if (lane_id() == 0) atomicMin(&A.scal[6], y);
+            if (lane_id() == 0) atomicMin(&A.fy[fi], y);
             return;
         }
     }
 }
 
-// Chunks wholly before the first window hit y after a frozen exit (x0, P) are literal-only: their
-// entry is (min(lo, lastk+1), P), their trajectory empty, their exit (min(hi, lastk+1), P).
-__global__ void k_fill_literal(WalkPtrs A, int32_t j0, int32_t P) {
-    const int32_t y = A.scal[6], lastk1 = A.nT - A.k + 1;
-    for (int32_t j = j0 + (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
-        const int32_t lo = j * A.S, hi = lo + A.S < A.nT ? lo + A.S : A.nT;
-        const int32_t ex = hi < lastk1 ? hi : lastk1;
-        if (ex > y) return;   // chunks are ordered: all later ones reach y too
-        A.cnt[A.cur[j]][j] = 0;
-        A.usedX[j] = lo < lastk1 ? lo : lastk1;
-        A.usedP[j] = P;
-        A.exitX[j] = ex;
-        A.exitP[j] = P;
-        A.changed[j] = 0;
+// One wave: in chunk order, every frozen chunk of the batch not already covered settles the chunks
+// wholly before its first window hit y as literal-only: entry (min(lo, lastk+1), P), empty
+// trajectory, exit (min(hi, lastk+1), P) -- instead of one chunk per round.  Each fill is
+// consistent on its own (no hit before y), so batches may come in any order; the pending check
+// accepts a filled chunk only when it matches its predecessor's exit.
+__global__ void k_frozen_apply(WalkPtrs A, int fbase, int fcap) {
+    __shared__ int32_t sj[FROZEN_MAX], sy[FROZEN_MAX];
+    const int lane = lane_id();
+    int nf = A.scal[5] - fbase;
+    if (nf > fcap) nf = fcap;
+    if (nf <= 0) return;
+    if (lane == 0) {   // insertion sort by chunk
+        for (int f = 0; f < nf; f++) {
+            const int32_t j = A.flist[fbase + f], y = A.fy[f];
+            int i = f;
+            while (i > 0 && sj[i - 1] > j) { sj[i] = sj[i - 1]; sy[i] = sy[i - 1]; i--; }
+            sj[i] = j; sy[i] = y;
+        }
+    }
+    wave_sync();
+    const int32_t lastk1 = A.nT - A.k + 1;
+    int32_t filled_to = -1;
+    for (int f = 0; f < nf; f++) {
+        const int32_t j = sj[f], y = sy[f];
+        if (j <= filled_to || j + 1 >= A.C) continue;
+        const int32_t P = A.exitP[j];
+        int32_t last = j;
+        for (int32_t q0 = j + 1; q0 < A.C; q0 += 64) {
+            const int32_t q = q0 + lane;
+            bool fill = false;
+            if (q < A.C) {
+                const int32_t lo = q * A.S, hi = lo + A.S < A.nT ? lo + A.S : A.nT;
+                const int32_t ex = hi < lastk1 ? hi : lastk1;
+                fill = ex <= y;
+                if (fill) {
+                    A.cnt[A.cur[q]][q] = 0;
+                    A.usedX[q] = lo < lastk1 ? lo : lastk1;
+                    A.usedP[q] = P;
+                    A.exitX[q] = ex;
+                    A.exitP[q] = P;
+                    A.changed[q] = 0;
+                }
+            }
+            const unsigned long long fm = __ballot(fill);   // chunks are ordered: a prefix fills
+            if (fm) last = q0 + 63 - __clzll((long long)fm);
+            if (fm != ~0ull) break;
+        }
+        filled_to = last;
+        wave_sync();
     }
 }
 
@@ -965,6 +1009,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.newX = c.take<int32_t>(C); A.newP = c.take<int32_t>(C);
     A.conv = c.take<int32_t>(C); A.changed = c.take<int32_t>(C); A.walked = c.take<int32_t>(C);
     A.frozen = c.take<int32_t>(C); A.flist = c.take<int32_t>(C);
+    A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);
     A.abits = anchor_bits(nR);
     A.atab = c.take<uint64_t>((size_t)1 << A.abits);
@@ -1069,49 +1114,6 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s, std::vector<int32_t>* resume
                     (const int32_t*)A.rlist, (int32_t)rl.size());
         SCCG_HIP(hipGetLastError());
     }
-}
-
-// For every committed fix-up that ended frozen (P unchanged over a long literal run up to its chunk
-// end): one grid-wide scan finds the next window hit after it, and every chunk before that hit is
-// settled as literal-only at once (instead of one chunk per round).
-int frozen_fill(WalkPtrs& A, hipStream_t s) {
-    int32_t nf = 0;
-    SCCG_HIP(hipMemcpyAsync(&nf, A.scal + 5, sizeof nf, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipStreamSynchronize(s));
-    if (!nf) return 0;
-    std::vector<int32_t> fl((size_t)nf), ex((size_t)A.C), ep((size_t)A.C);
-    SCCG_HIP(hipMemcpyAsync(fl.data(), A.flist, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipMemcpyAsync(ex.data(), A.exitX, (size_t)A.C * 4, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipMemcpyAsync(ep.data(), A.exitP, (size_t)A.C * 4, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipStreamSynchronize(s));
-    std::sort(fl.begin(), fl.end());
-    const int32_t lastk1 = A.nT - A.k + 1;
-    int32_t filled_to = -1;   // chunks <= filled_to were settled by an earlier fill of this round
-    for (int32_t j : fl) {
-        if (j <= filled_to || j + 1 >= A.C) continue;
-        const int32_t x0 = ex[j], P = ep[j];
-        int rc = dev_set_i32(A.scal + 6, 1, {INT32_MAX}, s);
-        if (rc) return rc;
-        const int64_t span = (int64_t)lastk1 - x0;
-        unsigned g = grid_for(span > 0 ? span : 1, WPB * 64 * WIDE);
-        if (g > 1024) g = 1024;
-        hipLaunchKernelGGL(k_frozen_scan, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, P);
-        hipLaunchKernelGGL(k_fill_literal, dim3(grid_for(A.C - j - 1, 256) > 1024 ? 1024 : grid_for(A.C - j - 1, 256)),
-                           dim3(256), 0, s, A, j + 1, P);
-        SCCG_HIP(hipGetLastError());
-        int32_t y = 0;
-        SCCG_HIP(hipMemcpyAsync(&y, A.scal + 6, sizeof y, hipMemcpyDeviceToHost, s));
-        SCCG_HIP(hipStreamSynchronize(s));
-        // last chunk whose exit min(hi, lastk+1) <= y
-        int32_t last = j;
-        for (int32_t q = j + 1; q < A.C; q++) {
-            const int32_t hi = (q + 1) * A.S < A.nT ? (q + 1) * A.S : A.nT;
-            if ((hi < lastk1 ? hi : lastk1) > y) break;
-            last = q;
-        }
-        filled_to = last;
-    }
-    return 0;
 }
 
 }  // namespace
@@ -1251,6 +1253,14 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
                                (const int32_t*)A.plist, nlist);
             SCCG_HIP(hipGetLastError());
+            auto frozen_fill = [&](int fbase, int fcap) -> int {   // device side; no-op past the list
+                SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.fy, INT32_MAX, fcap, s));
+                hipLaunchKernelGGL(k_frozen_scan, dim3(256, fcap), dim3(SCCG_BLOCK), 0, s, A, fbase);
+                hipLaunchKernelGGL(k_frozen_apply, dim3(1), dim3(64), 0, s, A, fbase, fcap);
+                SCCG_HIP(hipGetLastError());
+                return 0;
+            };
+            RC(frozen_fill(0, FROZEN_FIRST));
             auto find_pending = [&]() -> int {
                 RC(dev_set_i32(A.scal, 1, {0}, s));
                 hipLaunchKernelGGL(k_pending, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
@@ -1261,17 +1271,26 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             int32_t rs[6];
             SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
             SCCG_HIP(hipStreamSynchronize(s));
-            if (rs[1] || rs[5]) {
-                if (rs[1]) {   // escalations: resolve on the host, resume, commit the resumed chunks
+            if (rs[5] > FROZEN_FIRST) {   // more frozen chunks than the blind batch covered
+                for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_fill(fb, FROZEN_MAX));
+                RC(find_pending());
+                SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipStreamSynchronize(s));
+            }
+            if (rs[1]) {
+                {   // escalations: resolve on the host, resume, commit the resumed chunks
                     std::vector<int32_t> resumed;
                     RC(resolve_escalations(A, s, &resumed));
                     RC(h2d_sync(A.rlist, resumed.data(), resumed.size() * 4, s));
                     const int32_t nr = (int32_t)resumed.size();
+                    RC(dev_set_i32(A.scal + 5, 1, {0}, s));   // frozen list of the resumed chunks
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(nr, 256) > 4096 ? 4096 : grid_for(nr, 256)), dim3(256), 0, s, A,
                                        (const int32_t*)A.rlist, nr);
                     SCCG_HIP(hipGetLastError());
                 }
-                RC(frozen_fill(A, s));
+                SCCG_HIP(hipMemcpyAsync(&rs[5], A.scal + 5, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+                SCCG_HIP(hipStreamSynchronize(s));
+                for (int fb = 0; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_fill(fb, FROZEN_MAX));
                 RC(find_pending());
                 SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipStreamSynchronize(s));
