@@ -489,10 +489,15 @@ int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, 
 
 int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t s) {
     // d_sc[0] = header start (first '>' at a line start), d_sc[1] = its '\n' (n if none);
-    // d_sc[62], d_sc[63] are the chunk tickets
-    int rc = launch_first_match(buf, n, nullptr, 0, '>', d_sc, d_sc + 62, s);
-    if (!rc) rc = launch_first_match(buf, n, d_sc, 1, '\n', d_sc + 1, d_sc + 63, s);
-    return rc;
+    // d_sc[2], d_sc[3] are the chunk tickets (free for the caller afterwards); one init launch
+    int rc = dev_set_i64(d_sc, 4, {n, n, 0, 0}, s);
+    if (rc || n <= 0) return rc;
+    hipLaunchKernelGGL(k_first_match, dim3(64), dim3(SCCG_BLOCK), 0, s, buf, n, (const int64_t*)nullptr, 0, (uint8_t)'>',
+                       d_sc, reinterpret_cast<unsigned int*>(d_sc + 2));
+    hipLaunchKernelGGL(k_first_match, dim3(64), dim3(SCCG_BLOCK), 0, s, buf, n, (const int64_t*)d_sc, 1, (uint8_t)'\n',
+                       d_sc + 1, reinterpret_cast<unsigned int*>(d_sc + 3));
+    SCCG_HIP(hipGetLastError());
+    return 0;
 }
 
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,

@@ -106,11 +106,35 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(const int64_t* __restr
     }
 }
 
+// small inputs (<= 32 Ki elements): one 1024-thread block, one launch
+constexpr int SMALL_PER = 32;
+template <class Op>
+__global__ __launch_bounds__(1024) void k_small_scan(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ out,
+                                                     int64_t* __restrict__ total) {
+    __shared__ int64_t tmp[17];
+    const int64_t per = (n + 1023) / 1024, base = (int64_t)threadIdx.x * per;
+    int64_t acc = Op::id();
+    for (int64_t i = 0; i < per && base + i < n; i++) acc = Op::f(acc, in[base + i]);
+    int64_t tot;
+    int64_t run = block_excl<Op>(acc, tmp, &tot);
+    for (int64_t i = 0; i < per && base + i < n; i++) {   // second read hits the cache (in may alias out)
+        const int64_t x = in[base + i];
+        out[base + i] = run;
+        run = Op::f(run, x);
+    }
+    if (threadIdx.x == 0 && total) *total = tot;
+}
+
 template <class Op>
 int scan_impl(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
               hipStream_t s) {
     if (n <= 0) {
         if (d_total) return dev_set_i64(d_total, 1, {0}, s);
+        return 0;
+    }
+    if (n <= 1024 * SMALL_PER) {
+        hipLaunchKernelGGL(k_small_scan<Op>, dim3(1), dim3(1024), 0, s, in, n, out, d_total);
+        SCCG_HIP(hipGetLastError());
         return 0;
     }
     const int64_t nb = (n + TILE - 1) / TILE;

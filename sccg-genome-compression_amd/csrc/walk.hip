@@ -36,6 +36,8 @@ constexpr int ANCHOR_K = 32;
 constexpr int ANCHOR_STEP = 32;
 constexpr uint32_t A_MULTI = 0xFFFFFFFFu;    // anchor position of a 32-mer seen more than once
 constexpr int32_t FROZEN_MIN = 4096;   // literal bases at a chunk end that trigger a frozen-P scan
+constexpr int FROZEN_MAX = 256;        // frozen chunks handled per batch (grid.y of k_frozen_scan)
+constexpr int FROZEN_FIRST = 16;       // the batch launched blind, before the round's sync
 
 enum ChunkKind : int32_t { KIND_SPEC = 0, KIND_FIX = 1, KIND_RESUME = 2 };
 enum ChunkStatus : int32_t { ST_OK = 0, ST_ESC = 1 };
@@ -76,6 +78,7 @@ struct WalkPtrs {
                           // [5] frozen count, [6] frozen-scan first hit
     uint64_t* atab;
     uint32_t agen;            // anchor tag generation (one per call)
+    int32_t round;            // walk round of the launch (kernel argument copy)
     int32_t abits;
     unsigned long long* fc;   // full-candidate scan scalars: [0] lmax [1] cnt [2] has0 [3] minkey [4] firsthit [5] firstexo
                               // [8..11] the same four for the batch's first position (k_presence + k_cand_reduce)
@@ -341,6 +344,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
         q = uni(A.escQ[j]);
     }
     if (lane == 0) A.status[j] = ST_OK;
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.scal[5] = 0;   // frozen list of this round's commit
     const uint64_t dbg_t0 = DBG ? wall_clock64() : 0;
     uint64_t dbg_c[10] = {};   // matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail
     uint64_t tq = dbg_t0;
@@ -463,7 +467,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
         x = y + bl;       // compression.cpp:159
     }
     if (escalated) return;
-    if (DBG && lane == 0 && A.scal[4] == 1) {
+    if (DBG && lane == 0 && A.round == 1) {
         tick(9);
         uint64_t* d = A.dbg + (size_t)j * DBG_SLOTS;
         d[0] = wall_clock64() - dbg_t0;
@@ -478,7 +482,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
             A.newX[j] = nx; A.newP[j] = np;
             A.conv[j] = converged;
             A.changed[j] = nx != A.exitX[j] || np != A.exitP[j];
-            A.walked[j] = A.scal[4];
+            A.walked[j] = A.round;
             // ended in a long literal run with P frozen at the chunk end: k_frozen_scan territory
             A.frozen[j] = !converged && x == hi_j && x - lme >= FROZEN_MIN;
         }
@@ -493,10 +497,11 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
 // never depends on this choice -- the loop only ends when every chunk's trajectory was walked from
 // its predecessor's final exit.
 __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
+    if (blockIdx.x == 0 && threadIdx.x < FROZEN_MAX) A.fy[threadIdx.x] = INT32_MAX;   // for k_frozen_scan
     for (int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); i < nlist; i += (int32_t)(gridDim.x * blockDim.x)) {
         const int32_t j = list[i];
         if (A.kind[j] == KIND_SPEC || A.status[j] == ST_ESC) continue;
-        const int32_t round = A.scal[4];
+        const int32_t round = A.round;
         const bool pred_changed = j > 0 && A.walked[j - 1] == round && A.changed[j - 1];
         if (!(A.conv[j] || !pred_changed)) continue;
         A.cur[j] = 1 - A.cur[j];
@@ -512,8 +517,6 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
 // chunk end; k_commit lists them): for each of the first FROZEN_MAX, the first position after its
 // exit whose k-mer key occurs in its window of P, over the whole rest of the target (grid.y picks
 // the frozen chunk; every wave builds its own copy of the window and scans a strided share).
-constexpr int FROZEN_MAX = 256;    // frozen chunks handled per batch (grid.y)
-constexpr int FROZEN_FIRST = 16;   // the batch launched blind, before the round's sync
 __global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int fbase) {
     __shared__ WalkLds lds_all[WPB];
     const int fi = (int)blockIdx.y, f = fbase + fi;
@@ -543,8 +546,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int fbas
 // trajectory, exit (min(hi, lastk+1), P) -- instead of one chunk per round.  Each fill is
 // consistent on its own (no hit before y), so batches may come in any order; the pending check
 // accepts a filled chunk only when it matches its predecessor's exit.
-__global__ void k_frozen_apply(WalkPtrs A, int fbase, int fcap) {
-    __shared__ int32_t sj[FROZEN_MAX], sy[FROZEN_MAX];
+__device__ void frozen_apply_wave(const WalkPtrs& A, int fbase, int fcap, int32_t* sj, int32_t* sy) {
     const int lane = lane_id();
     int nf = A.scal[5] - fbase;
     if (nf > fcap) nf = fcap;
@@ -598,11 +600,14 @@ __global__ void k_round1_init(WalkPtrs A) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// pending chunks: entry state (predecessor's exit) differs from the one their trajectory used
-// ---------------------------------------------------------------------------------------------
-__global__ void k_pending(WalkPtrs A) {
-    for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
+// The end of a round in one block: the frozen fills of a batch (wave 0), then the chunks whose
+// entry state (predecessor's exit) differs from the one their trajectory used -> plist, scal[0].
+__global__ __launch_bounds__(1024) void k_round_tail(WalkPtrs A, int fbase, int fcap) {
+    __shared__ int32_t sj[FROZEN_MAX], sy[FROZEN_MAX];
+    if (threadIdx.x < 64 && fcap > 0) frozen_apply_wave(A, fbase, fcap, sj, sy);
+    if (threadIdx.x == 0) A.scal[0] = 0;
+    __syncthreads();
+    for (int32_t j = (int32_t)threadIdx.x; j < A.C; j += (int32_t)blockDim.x) {
         const int32_t ex = j ? A.exitX[j - 1] : A.scal[2];
         const int32_t ep = j ? A.exitP[j - 1] : A.scal[3];
         if (ex == INVALID) continue;
@@ -1243,37 +1248,28 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         int32_t nlist = A.C;
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
         for (int64_t round = 1;; round++) {
-            RC(dev_set_i32(A.scal + 4, 1, {(int32_t)round}, s));
+            A.round = (int32_t)round;   // every kernel of the round gets it by value
             PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
             SCCG_HIP(hipGetLastError());
             res->rounds = round;
-            // Commit and find the next round's pending chunks without waiting for the host; the
-            // rare escalated (pn2 == 0) and frozen chunks are handled after the round's one sync.
-            RC(dev_set_i32(A.scal + 5, 1, {0}, s));
+            // Commit, fill the first frozen runs and find the next round's pending chunks without
+            // waiting for the host; more frozen chunks and the rare escalated (pn2 == 0) ones are
+            // handled after the round's one sync.
             hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
                                (const int32_t*)A.plist, nlist);
-            SCCG_HIP(hipGetLastError());
-            auto frozen_fill = [&](int fbase, int fcap) -> int {   // device side; no-op past the list
-                SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.fy, INT32_MAX, fcap, s));
-                hipLaunchKernelGGL(k_frozen_scan, dim3(256, fcap), dim3(SCCG_BLOCK), 0, s, A, fbase);
-                hipLaunchKernelGGL(k_frozen_apply, dim3(1), dim3(64), 0, s, A, fbase, fcap);
+            auto frozen_batch = [&](int fbase, int fcap, bool init_fy) -> int {   // no-op past the list
+                if (init_fy) SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.fy, INT32_MAX, fcap, s));
+                if (fcap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fcap), dim3(SCCG_BLOCK), 0, s, A, fbase);
+                hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(1024), 0, s, A, fbase, fcap);   // + pending
                 SCCG_HIP(hipGetLastError());
                 return 0;
             };
-            RC(frozen_fill(0, FROZEN_FIRST));
-            auto find_pending = [&]() -> int {
-                RC(dev_set_i32(A.scal, 1, {0}, s));
-                hipLaunchKernelGGL(k_pending, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
-                SCCG_HIP(hipGetLastError());
-                return 0;
-            };
-            RC(find_pending());
+            RC(frozen_batch(0, FROZEN_FIRST, false));   // fy was set by k_commit
             int32_t rs[6];
             SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
             SCCG_HIP(hipStreamSynchronize(s));
             if (rs[5] > FROZEN_FIRST) {   // more frozen chunks than the blind batch covered
-                for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_fill(fb, FROZEN_MAX));
-                RC(find_pending());
+                for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, true));
                 SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipStreamSynchronize(s));
             }
@@ -1290,8 +1286,8 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 }
                 SCCG_HIP(hipMemcpyAsync(&rs[5], A.scal + 5, sizeof(int32_t), hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipStreamSynchronize(s));
-                for (int fb = 0; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_fill(fb, FROZEN_MAX));
-                RC(find_pending());
+                if (rs[5] == 0) RC(frozen_batch(0, 0, false));   // pending only
+                for (int fb = 0; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, fb > 0));
                 SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipStreamSynchronize(s));
             }
