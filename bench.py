@@ -48,7 +48,7 @@ def algorithmic_bytes(kernel: str, shape: dict) -> float | None:
     nT, nR = shape["target_bases"], shape["reference_bases"]
     if kernel == "fasta_strip":       # read the FASTA, write the kept bytes (target and reference launch)
         return (shape["tgt_fa"] + nT + shape["ref_fa"] + nR) / 2.0
-    if kernel == "local_pass_k14":    # both segment strings once + records and stats
+    if kernel == "local_segments":    # both segment strings once + records and stats
         lead = min(nR, nT)
         return 2.0 * lead + (lead / 1000.0) * (1024 + 32)
     if kernel == "walk":              # every target base once + the matched reference bases once

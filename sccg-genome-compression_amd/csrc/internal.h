@@ -9,7 +9,7 @@ enum ProfId {
     PROF_STRIP = 0,      // k_strip_write
     PROF_RUNS,           // k_runs_write
     PROF_RUNTEXT,        // k_run_textwrite
-    PROF_LOCAL14,        // k_local_pass<14>
+    PROF_LOCAL14,        // k_local_all (compress) / k_local_pass<14>
     PROF_LOCAL10,        // k_local_pass<10>
     PROF_LOCAL_EMIT,     // k_seg_textwrite
     PROF_FILTER,         // k_filter_write
@@ -100,13 +100,15 @@ struct SegStat {
     int32_t pad;
 };
 // segments [seg0, seg_end) of one pass (pass 2 only touches segments pass 1 left without a match)
-int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT,
-                      int64_t seg0, int64_t seg_end, uint32_t* recs, SegStat* stat, hipStream_t s);
+int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t seg0,
+                      int64_t seg_end, uint32_t* recs, SegStat* stat, hipStream_t s);
 // switch FSM (compression.cpp:395-473) over segments [seg0, seg_end) from counter state *state
 // (min(mismatch, 5); 6 = switched): *switch_seg = first segment where mismatch > T2, or -1
-int64_t fsm_chunks(int64_t iters);
-int launch_switch_fsm(const SegStat* stat, int64_t seg0, int64_t seg_end, int32_t* d_maps, int32_t* h_maps, int* state,
-                      int64_t* switch_seg, hipStream_t s);
+// every local segment of a compress (k = 14, then k2 = 10 without a match) and the switch point:
+// ctl = {unused 0, early-exit bound INT32_MAX, switch segment INT32_MAX (= none), 0} on
+// entry; cls: per-segment classes tagged with gen (never cleared: zero-filled once, gen >= 1)
+int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t nseg, uint32_t* recs,
+                     SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s);
 // record text for local mode (delta-encoded, compression.cpp:406-415 + :222-304) + leftover
 int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_t* recs,
                       const SegStat* stat, uint8_t* out, int64_t* d_len, int64_t* d_tmp_a,

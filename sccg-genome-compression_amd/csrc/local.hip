@@ -80,17 +80,13 @@ __device__ __forceinline__ void keys16(const uint8_t* s, uint64_t& code, uint32_
 // SCCG_DEBUG: phase ticks (10 ns) summed over segments: load, keys, insert, hits, walk, count
 __device__ unsigned long long g_local_dbg[16];
 
+// One segment with one k (pass 1: k = 14, pass 2: k2 = 10 on a segment pass 1 left without a match,
+// keeping pass 1's non-N flag); returns its statistics (wave-uniform), the records are in recs.
 template <int K, bool DBG>
-__global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, const uint8_t* __restrict__ R, int64_t nR,
-                                                           const uint8_t* __restrict__ T, int64_t nT, int64_t seg0,
-                                                           int64_t seg_end, uint32_t* __restrict__ recs,
-                                                           SegStat* __restrict__ stat) {
-    __shared__ SegLds lds_all[WPB];
-    const int w = wave_in_block(), lane = lane_id();
-    const int64_t seg = seg0 + (int64_t)blockIdx.x * WPB + w;
-    if (seg >= seg_end) return;
-    if (pass == 2 && stat[seg].pass != 0) return;
-    SegLds& L = lds_all[w];
+__device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pass, int non_n_prev, int upper,
+                                                 const uint8_t* __restrict__ R, int64_t nR, const uint8_t* __restrict__ T,
+                                                 int64_t nT, uint32_t* __restrict__ recs) {
+    const int lane = lane_id();
     const int64_t base = seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
     const int nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
@@ -329,54 +325,108 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
             }
         }
     }
-    if (lane == 0) {
-        SegStat s;
-        s.nrec = nrec;
-        s.nmatch = nmatch;
-        s.lit = lit;
-        s.pass = nmatch ? pass : 0;
-        s.non_n = pass == 1 ? (int)non_n : stat[seg].non_n;
-        s.first_p = firstp;
-        s.last_p = lastp;
-        s.pad = nt;
-        stat[seg] = s;
+    SegStat s;
+    s.nrec = nrec;
+    s.nmatch = nmatch;
+    s.lit = lit;
+    s.pass = nmatch ? pass : 0;
+    s.non_n = pass == 1 ? (int)non_n : non_n_prev;
+    s.first_p = firstp;
+    s.last_p = lastp;
+    s.pad = nt;
+    return s;
+}
+
+// Segments [seg0, seg_end) with one k, a wave per segment (grid-stride).
+template <int K, bool DBG>
+__global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, const uint8_t* __restrict__ R, int64_t nR,
+                                                           const uint8_t* __restrict__ T, int64_t nT, int64_t seg0,
+                                                           int64_t seg_end, uint32_t* __restrict__ recs,
+                                                           SegStat* __restrict__ stat) {
+    __shared__ SegLds lds_all[WPB];
+    const int w = wave_in_block();
+    const int64_t G = (int64_t)gridDim.x * WPB;
+    for (int64_t seg = seg0 + (int64_t)blockIdx.x * WPB + w; seg < seg_end; seg += G) {
+        if (pass == 2 && stat[seg].pass != 0) continue;
+        const SegStat st = local_segment<K, DBG>(lds_all[w], seg, pass, pass == 2 ? stat[seg].non_n : 0, upper, R, nR, T,
+                                                 nT, recs);
+        if (lane_id() == 0) stat[seg] = st;
+        wave_sync();   // the next segment reuses this wave's LDS
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// switch state machine: state = min(mismatch counter, 5), 6 = switched (absorbing)
+// All local segments in one launch (compress).  The grid is the resident capacity and wave i takes
+// segments i, i + G, ... (so the front of processed segments advances in order); each runs k = 14
+// and, without a match, k2 = 10 (compression.cpp:372-474).
+// The switch state machine (compression.cpp:462-473) is a window predicate: its counter before
+// segment e is the number of consecutive class-1/2 segments just before e (class 0/3 resets it),
+// so the switch happens at the first e of class 2 whose 4 predecessors are all class 1 or 2.
+// A wave publishes its segment's class (tagged with the call's generation, so the array is never
+// cleared) and checks the 5 windows holding it; a complete window with that shape lowers ctl[1],
+// and segments past ctl[1] are never started: their work would be discarded.  The class traffic is
+// relaxed agent-scope atomics (no cache maintenance; a window two waves complete at once may go
+// unseen, which only delays the exit): k_switch_final recomputes the first switch from the
+// published classes after the launch (all segments up to it were computed).
 // ---------------------------------------------------------------------------------------------
-constexpr int FSM_G = 16;    // segments per thread (their stats are loaded up front)
-constexpr int SW = 6;
-
 __device__ __forceinline__ int seg_class(const SegStat& s) {
     // 0 good, 1 success-but-bad (mism++ without check), 2 failed non-N (mism++ + check), 3 failed all-N
     if (s.pass) return (2 * s.lit > s.pad && s.non_n) ? 1 : 0;   // (float)lit/len > 0.5f
     return s.non_n ? 2 : 3;
 }
+__device__ __forceinline__ bool mism(int c) { return c == 1 || c == 2; }
 
-__global__ void k_fsm_chunks(const SegStat* __restrict__ stat, int64_t seg0, int64_t seg_end, int32_t* __restrict__ maps) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t s0 = seg0 + t * FSM_G;
-    if (s0 >= seg_end) return;
-    const int64_t s1 = s0 + FSM_G < seg_end ? s0 + FSM_G : seg_end;
-    int cls[FSM_G];
-#pragma unroll
-    for (int q = 0; q < FSM_G; q++) cls[q] = s0 + q < s1 ? seg_class(stat[s0 + q]) : 0;
-    int st[6], at[6];
-    for (int i = 0; i < 6; i++) { st[i] = i; at[i] = -1; }
-#pragma unroll
-    for (int q = 0; q < FSM_G; q++) {
-        if (s0 + q >= s1) break;
-        const int c = cls[q];
-        for (int i = 0; i < 6; i++) {
-            if (st[i] == SW) continue;
-            if (c == 0 || c == 3) st[i] = 0;
-            else if (c == 1) st[i] = st[i] + 1 > 5 ? 5 : st[i] + 1;
-            else { if (st[i] + 1 > 4) { st[i] = SW; at[i] = q; } else st[i]++; }
+template <bool DBG>
+__global__ __launch_bounds__(SCCG_BLOCK) void k_local_all(const uint8_t* __restrict__ R, int64_t nR,
+                                                          const uint8_t* __restrict__ T, int64_t nT, int32_t nseg,
+                                                          uint32_t* __restrict__ recs, SegStat* __restrict__ stat,
+                                                          int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl) {
+    __shared__ SegLds lds_all[WPB];
+    const int w = wave_in_block(), lane = lane_id();
+    SegLds& L = lds_all[w];
+    const int32_t G = (int32_t)gridDim.x * WPB;
+    for (int32_t seg = (int32_t)blockIdx.x * WPB + w; seg < nseg; seg += G) {
+        if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
+        SegStat st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs);
+        if (!st.pass) {
+            wave_sync();
+            st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs);
         }
+        if (lane == 0) stat[seg] = st;
+        const int c = seg_class(st);
+        if (lane == 0) __hip_atomic_store(&cls[seg], (gen << 2) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // classes of seg-4 .. seg+4 (lane i holds seg-4+i; -1 = not published in this call)
+        const int32_t idx = seg - 4 + lane;
+        int v = -1;
+        if (lane < 9 && lane != 4 && idx >= 0 && idx < nseg) {
+            const int32_t t = __hip_atomic_load(&cls[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = (t >> 2) == gen ? (t & 3) : -1;
+        }
+        if (lane == 4) v = c;
+        int k[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) k[i] = lane_val(v, i);
+        int32_t hit = INT32_MAX;
+#pragma unroll
+        for (int m = 8; m >= 4; m--)   // window ending at seg - 4 + m
+            if (k[m] == 2 && mism(k[m - 1]) && mism(k[m - 2]) && mism(k[m - 3]) && mism(k[m - 4]) && seg - 4 + m >= 4)
+                hit = seg - 4 + m;
+        if (hit != INT32_MAX && lane == 0)
+            __hip_atomic_fetch_min(&ctl[1], hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wave_sync();   // the next segment reuses this wave's LDS
     }
-    for (int i = 0; i < 6; i++) { maps[t * 12 + i] = st[i]; maps[t * 12 + 6 + i] = at[i]; }
+}
+
+__global__ void k_switch_final(const int32_t* __restrict__ cls, int32_t gen, int32_t nseg, int32_t* __restrict__ ctl) {
+    const int32_t e = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x) + 4;
+    if (e >= nseg) return;
+    int k[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        const int32_t t = cls[e - 4 + i];
+        k[i] = (t >> 2) == gen ? (t & 3) : -1;
+    }
+    if (k[4] == 2 && mism(k[0]) && mism(k[1]) && mism(k[2]) && mism(k[3])) atomicMin(&ctl[2], e);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -498,7 +548,8 @@ __global__ void k_copy_upper(const uint8_t* __restrict__ in, int64_t n, uint8_t*
 int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t seg0,
                       int64_t seg_end, uint32_t* recs, SegStat* stat, hipStream_t s) {
     if (seg_end <= seg0) return 0;
-    const unsigned g = grid_for(seg_end - seg0, WPB);
+    unsigned g = grid_for(seg_end - seg0, WPB);
+    if (g > 4096) g = 4096;
     static const bool dbg = getenv("SCCG_DEBUG") != nullptr;
     if (dbg) {
         const unsigned long long z[16] = {};
@@ -534,24 +585,41 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
     return 0;
 }
 
-int64_t fsm_chunks(int64_t iters) { return (iters + FSM_G - 1) / FSM_G; }
-
-int launch_switch_fsm(const SegStat* stat, int64_t seg0, int64_t seg_end, int32_t* d_maps, int32_t* h_maps, int* state,
-                      int64_t* switch_seg, hipStream_t s) {
-    *switch_seg = -1;
-    if (seg_end <= seg0) return 0;
-    const int64_t nch = fsm_chunks(seg_end - seg0);
-    hipLaunchKernelGGL(k_fsm_chunks, dim3(grid_for(nch, 256)), dim3(256), 0, s, stat, seg0, seg_end, d_maps);
-    SCCG_HIP(hipGetLastError());
-    SCCG_HIP(hipMemcpyAsync(h_maps, d_maps, (size_t)nch * 12 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipStreamSynchronize(s));
-    int st = *state;
-    for (int64_t c = 0; c < nch; c++) {
-        const int m = h_maps[c * 12 + st];
-        if (m == SW) { *switch_seg = seg0 + c * FSM_G + h_maps[c * 12 + 6 + st]; *state = SW; return 0; }
-        st = m;
+int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t nseg, uint32_t* recs,
+                     SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s) {
+    if (nseg <= 0) return 0;
+    if (nseg >= INT32_MAX / 2) return SCCG_E_UNSUPPORTED;
+    // resident capacity: the grid drains the counter, extra blocks would only find it exhausted
+    static const unsigned cap = [] {
+        int dev = 0, cus = 256, per = 4;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_local_all<false>, SCCG_BLOCK, 0) != hipSuccess || per < 1)
+            per = 4;
+        return (unsigned)(cus * per);
+    }();
+    unsigned g = grid_for(nseg, WPB);
+    if (g > cap) g = cap;
+    static const bool dbg = getenv("SCCG_DEBUG") != nullptr;
+    if (dbg) {
+        const unsigned long long z[16] = {};
+        SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, nR, T, nT, (int32_t)nseg, recs,
+                    stat, cls, gen, ctl);
+        unsigned long long d[16];
+        SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipStreamSynchronize(s));
+        const double n = d[5] ? (double)d[5] : 1.0;
+        fprintf(stderr, "[local all] %llu segment passes, per pass (us): load %.2f keys %.2f insert %.2f hits %.2f walk %.2f"
+                " | max %.2f\n", d[5], d[0] / n / 100, d[1] / n / 100, d[2] / n / 100, d[3] / n / 100, d[4] / n / 100,
+                d[6] / 100.0);
+    } else {
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, nR, T, nT, (int32_t)nseg, recs,
+                    stat, cls, gen, ctl);
     }
-    *state = st;
+    if (nseg > 4)
+        hipLaunchKernelGGL(k_switch_final, dim3(grid_for(nseg - 4, 256)), dim3(256), 0, s, (const int32_t*)cls, gen,
+                           (int32_t)nseg, ctl);
+    SCCG_HIP(hipGetLastError());
     return 0;
 }
 

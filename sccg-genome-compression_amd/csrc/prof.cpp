@@ -59,7 +59,7 @@ Registry& reg() {
 }
 
 const char* const NAMES[PROF_COUNT] = {
-    "fasta_strip", "run_extract", "run_text", "local_pass_k14", "local_pass_k10", "local_emit", "n_filter",
+    "fasta_strip", "run_extract", "run_text", "local_segments", "local_pass_k10", "local_emit", "n_filter",
     "anchor_build", "walk", "presence_scan", "fullc_scan", "match_emit",
     "dc_decode", "dc_format",
 };

@@ -106,21 +106,26 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(const int64_t* __restr
     }
 }
 
-// small inputs (<= 32 Ki elements): one 1024-thread block, one launch
-constexpr int SMALL_PER = 32;
+// small inputs (<= 8 Ki elements): one 1024-thread block, one launch; a thread's (<= 8) loads are
+// issued together
+constexpr int SMALL_PER = 8;
 template <class Op>
 __global__ __launch_bounds__(1024) void k_small_scan(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ out,
                                                      int64_t* __restrict__ total) {
     __shared__ int64_t tmp[17];
     const int64_t per = (n + 1023) / 1024, base = (int64_t)threadIdx.x * per;
+    int64_t v[SMALL_PER];
     int64_t acc = Op::id();
-    for (int64_t i = 0; i < per && base + i < n; i++) acc = Op::f(acc, in[base + i]);
+#pragma unroll
+    for (int i = 0; i < SMALL_PER; i++) v[i] = (i < per && base + i < n) ? in[base + i] : Op::id();
+#pragma unroll
+    for (int i = 0; i < SMALL_PER; i++) acc = Op::f(acc, v[i]);
     int64_t tot;
     int64_t run = block_excl<Op>(acc, tmp, &tot);
-    for (int64_t i = 0; i < per && base + i < n; i++) {   // second read hits the cache (in may alias out)
-        const int64_t x = in[base + i];
-        out[base + i] = run;
-        run = Op::f(run, x);
+#pragma unroll
+    for (int i = 0; i < SMALL_PER; i++) {
+        if (i < per && base + i < n) out[base + i] = run;
+        run = Op::f(run, v[i]);
     }
     if (threadIdx.x == 0 && total) *total = tot;
 }

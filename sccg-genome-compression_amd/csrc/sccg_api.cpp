@@ -34,14 +34,13 @@ namespace {
 enum Slot {
     B_RFA, B_TFA, B_R, B_T, B_TILE_A, B_TILE_B, B_TILE_FA, B_TILE_FB, B_TILE_LAST, B_TILE_OFF, B_TILE_OFF2, B_TILE_CARRY, B_TILE_BSUM,
     B_SCAL, B_PARTIAL,
-    B_RUN_S, B_RUN_E, B_TMP64, B_RUN_SN, B_RUN_EN, B_TMP64N, B_NLINE, B_RECS, B_STAT, B_MAPS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
+    B_RUN_S, B_RUN_E, B_TMP64, B_RUN_SN, B_RUN_EN, B_TMP64N, B_NLINE, B_RECS, B_STAT, B_SEGCLS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
     // decompression
     B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC,
     B_COUNT
 };
 
 constexpr int WALK_CHUNK = 16384;
-constexpr int64_t LOCAL_BATCH0 = 8192;   // first local batch (segments); multiple of the FSM chunk
 constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide compares, tails)
 
 }  // namespace
@@ -53,7 +52,9 @@ struct sccg_ctx {
     sccg_stats stats{};
     void* buf[B_COUNT] = {};
     size_t cap[B_COUNT] = {};
-    std::vector<int32_t> h_maps;
+    void* cls_buf = nullptr;   // local segment classes: buffer the generation tags refer to
+    size_t cls_cap = 0;
+    int32_t cls_gen = 0;
 
     int fail(int rc, const char* fmt, ...) {
         char tmp[512];
@@ -283,19 +284,22 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     GET(uint32_t, recs, B_RECS, (iters > 0 ? iters : 1) * SEG_REC_CAP);
     GET(SegStat, stat, B_STAT, iters > 0 ? iters : 1);
     if (iters > 0) {
-        // Segments run in geometrically growing batches, each followed by the switch state
-        // machine: once the counter passes T2 the rest of the local work would be discarded
-        // (compression.cpp:462-473), so it is never launched.
-        const int64_t nch = fsm_chunks(iters);
-        GET(int32_t, maps, B_MAPS, nch * 12);
-        ctx->h_maps.resize((size_t)(nch * 12));
-        int fsm_state = 0;
-        for (int64_t b0 = 0, bs = LOCAL_BATCH0; b0 < iters && sw < 0; b0 += bs, bs *= 2) {
-            const int64_t b1 = b0 + bs < iters ? b0 + bs : iters;
-            TRY(launch_local_pass(14, 1, 1, R, nR, T, nT, b0, b1, recs, stat, s));
-            TRY(launch_local_pass(10, 2, 1, R, nR, T, nT, b0, b1, recs, stat, s));
-            TRY(launch_switch_fsm(stat, b0, b1, maps, ctx->h_maps.data(), &fsm_state, &sw, s));
+        // one launch over every segment; segments past a detected switch are never started
+        GET(int32_t, cls, B_SEGCLS, iters);
+        if (cls != ctx->cls_buf || ctx->cap[B_SEGCLS] != ctx->cls_cap || ctx->cls_gen >= (1 << 28)) {
+            // new buffer (or tags about to wrap): zero it once, so no stale tag can match
+            HIPTRY(hipMemsetAsync(cls, 0, ctx->cap[B_SEGCLS], s));
+            ctx->cls_buf = cls;
+            ctx->cls_cap = ctx->cap[B_SEGCLS];
+            ctx->cls_gen = 0;
         }
+        const int32_t gen = ++ctx->cls_gen;
+        int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
+        TRY(dev_set_i64(sc + 20, 2, {(int64_t)INT32_MAX << 32, (int64_t)INT32_MAX}, s));
+        TRY(launch_local_all(R, nR, T, nT, iters, recs, stat, cls, gen, ctl, s));
+        int64_t h_sw = 0;
+        TRY(d2h_i64(ctx, sc + 21, &h_sw, 1));   // ctl[2] | ctl[3] << 32
+        sw = h_sw >= INT32_MAX ? -1 : h_sw;
     }
     st.switch_segment = sw;
     mark("local");

@@ -592,11 +592,26 @@ __device__ void frozen_apply_wave(const WalkPtrs& A, int fbase, int fcap, int32_
     }
 }
 
-// round 1: every chunk, chunk 0 exact (a fix-up with an empty trajectory), the others speculative
-__global__ void k_round1_init(WalkPtrs A) {
+// Chunk state before round 1: no trajectory, no exit, never walked; round 1 takes every chunk,
+// chunk 0 exact (a fix-up from the first match's end, with an empty trajectory), the others
+// speculative.
+constexpr int32_t NEVER = INT32_MIN + 1;   // "no entry used yet": differs from every state
+__global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
     for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
+        A.cur[j] = 0;
+        A.cnt[0][j] = 0;
+        A.cnt[1][j] = 0;
+        A.usedX[j] = NEVER;
+        A.usedP[j] = NEVER;
+        A.exitX[j] = INVALID;
+        A.exitP[j] = INVALID;
         A.kind[j] = j ? KIND_SPEC : KIND_FIX;
         A.plist[j] = j;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        A.scal[0] = 0; A.scal[1] = 0; A.scal[2] = startX; A.scal[3] = startP;
+        A.snapX[0] = startX;
+        A.snapP[0] = startP;
     }
 }
 
@@ -1040,8 +1055,6 @@ struct FullC {
     int32_t p;
 };
 
-constexpr int32_t NEVER = INT32_MIN + 1;   // "no entry used yet": differs from every state
-
 int set_u64(unsigned long long* p, std::initializer_list<int64_t> v, hipStream_t s) {
     return dev_set_i64(reinterpret_cast<int64_t*>(p), (int)v.size(), v, s);
 }
@@ -1213,14 +1226,9 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
 
     // ---- init chunk state
     const size_t C = (size_t)A.C;
-    SCCG_HIP(hipMemsetAsync(A.cur, 0, C * sizeof(int32_t), s));
-    SCCG_HIP(hipMemsetAsync(A.cnt[0], 0, C * sizeof(int32_t), s));
-    SCCG_HIP(hipMemsetAsync(A.cnt[1], 0, C * sizeof(int32_t), s));
-    SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.usedX, NEVER, C, s));
-    SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.usedP, NEVER, C, s));
-    SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.exitX, INVALID, C, s));
-    SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.exitP, INVALID, C, s));
-    RC(dev_set_i32(A.scal, 4, {0, 0, startX, startP}, s));
+    hipLaunchKernelGGL(k_walk_init, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
+                       startX, startP);
+    SCCG_HIP(hipGetLastError());
 
     if (startP != INVALID && lastk >= 0) {
         // anchors -> speculative guesses for chunks 1..C-1
@@ -1239,11 +1247,6 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
         hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
         SCCG_HIP(hipGetLastError());
-        // round 1: chunk 0 exact (as a fix-up with an empty trajectory), chunks >= 1 speculative
-        hipLaunchKernelGGL(k_round1_init, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
-        SCCG_HIP(hipGetLastError());
-        RC(dev_set_i32(A.snapX, 1, {startX}, s));
-        RC(dev_set_i32(A.snapP, 1, {startP}, s));
         mark("anchors");
         int32_t nlist = A.C;
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;

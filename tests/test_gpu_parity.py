@@ -152,3 +152,53 @@ def test_chr1_roundtrip(ctx):
     st = ctx.stats()
     assert st["mode_global"] == 1 and st["target_bases"] == 249_250_621
     assert ctx.reconstruct(rec, rfa) == tfa
+
+
+def _switch_case(seed: int, nseg: int = 2400):
+    """Segment-kind patterns for the local->global switch (compression.cpp:462-473): identical
+    segments (good), unrelated random ones (failed or mostly literal), half-copied ones (matched
+    but > 50 % literal), all-N ones (failed, all N: resets the counter) and poly-A ones (failed,
+    not N), in bursts of 1-3, with a planted 5-burst ending in a failure at a seed-dependent
+    segment (or none)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    r = acgt[rng.integers(0, 4, nseg * 1000)]
+    t = r.copy()
+    kinds = np.zeros(nseg, dtype=np.int8)   # 0 copy, 1 random, 2 half, 3 N, 4 poly-A (fails)
+    i = 0
+    while i < nseg:
+        i += int(rng.integers(2, 40))
+        n = int(rng.integers(1, 4))   # bursts too short to switch on their own ...
+        kinds[i:i + n] = rng.choice([1, 2, 3, 4], size=min(n, max(0, nseg - i)))
+        i += n
+    plant = [None, 4, 5, 9, 63, 64, 65, 1000, 4095, nseg - 1][seed % 10]
+    if plant is not None and plant < nseg:
+        kinds[max(0, plant - 4):plant + 1] = rng.choice([1, 2, 4], size=min(plant + 1, 5))   # ... but this one
+        kinds[plant] = 4
+    for s, k in enumerate(kinds):
+        seg = slice(s * 1000, (s + 1) * 1000)
+        if k == 1:
+            t[seg] = acgt[rng.integers(0, 4, 1000)]
+        elif k == 2:
+            t[s * 1000 + 400:(s + 1) * 1000] = acgt[rng.integers(0, 4, 600)]
+        elif k == 3:
+            t[seg] = ord("N")
+        elif k == 4:
+            t[seg] = ord("A")
+    fa = lambda name, x: b">" + name + b"\n" + b"\n".join(x[j:j + 60].tobytes() for j in range(0, len(x), 60)) + b"\n"
+    return fa(b"r", r), fa(b"t", t)
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_switch_window_vs_oracle(ctx, seed):
+    """The fused local kernel's switch detection against the oracle's state machine."""
+    rfa, tfa = _switch_case(seed)
+    want = oraclelib.compress(rfa, tfa)
+    mode_global, sw = oraclelib.last_mode()
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert rc == 0
+    st = ctx.stats()
+    assert bool(st["mode_global"]) == mode_global
+    assert st["switch_segment"] == (sw if mode_global else -1)
+    assert got == want
