@@ -253,8 +253,11 @@ int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64
                        (const int64_t*)d_flag, d_dlt, r->len, d_err);
     SCCG_HIP(hipGetLastError());
     int64_t nr = 0;
-    SCCG_HIP(hipMemcpyAsync(&nr, d_count, sizeof nr, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipStreamSynchronize(s));
+    {
+        const RbItem it{d_count, &nr, (int)sizeof nr};
+        rc = dev_readback(&it, 1, s);
+        if (rc) return rc;
+    }
     r->n = nr;
     if (nr == 0) return 0;
     // exclusive sum of deltas into d_flag (free now), then starts
@@ -268,9 +271,8 @@ int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64
     SCCG_HIP(hipGetLastError());
     rc = dev_excl_sum(r->cum, r->cum, nr, d_count, d_partial, s);
     if (rc) return rc;
-    SCCG_HIP(hipMemcpyAsync(&r->total, d_count, sizeof r->total, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipStreamSynchronize(s));
-    return 0;
+    const RbItem it{d_count, &r->total, (int)sizeof r->total};
+    return dev_readback(&it, 1, s);
 }
 
 int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,

@@ -11,6 +11,7 @@
 namespace {
 
 constexpr int PER_T = INGEST_TILE / SCCG_BLOCK;  // 32 bytes per thread
+constexpr int WPB = SCCG_BLOCK / 64;             // wave tiles per block
 
 // ---------------------------------------------------------------------------------------------
 // header search
@@ -58,19 +59,26 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_first_match(const uint8_t* __res
 // known (b).  The filter output (N erase + toupper) is the filter applied to the strip output, so
 // it carries the same (a, b) split (fa, fb).
 //
-// Writes are staged: every thread drops its kept bytes into an LDS copy of the tile's output at
-// its block-scan offset, then the block stores the tile's output range with aligned dword stores.
+// A tile is one wave's 4 KiB (64 bytes per lane): summary and write need wave operations only, no
+// workgroup barrier, so every wave streams on its own.  Writes are staged: every lane drops its
+// kept bytes into the wave's LDS copy of the tile's output at its wave-scan offset, then the wave
+// stores the tile's output range with aligned dword stores.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint8_t wb(const uint32_t (&w)[PER_T / 4], int i) { return (uint8_t)(w[i >> 2] >> (8 * (i & 3))); }
+template <int NW>
+__device__ __forceinline__ uint8_t wb(const uint32_t (&w)[NW], int i) { return (uint8_t)(w[i >> 2] >> (8 * (i & 3))); }
 
-__device__ __forceinline__ void load_words(const uint8_t* __restrict__ buf, int64_t n, int64_t off, uint32_t (&w)[PER_T / 4]) {
-    if (off + PER_T <= n && (((uintptr_t)(buf + off)) & 15) == 0) {
+template <int NW>
+__device__ __forceinline__ void load_words(const uint8_t* __restrict__ buf, int64_t n, int64_t off, uint32_t (&w)[NW]) {
+    if (off + 4 * NW <= n && (((uintptr_t)(buf + off)) & 15) == 0) {
         const uint4* p = reinterpret_cast<const uint4*>(buf + off);
-        const uint4 v0 = p[0], v1 = p[1];
-        w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w; w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
+#pragma unroll
+        for (int q = 0; q < NW / 4; q++) {
+            const uint4 v = p[q];
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        }
     } else {
 #pragma unroll
-        for (int q = 0; q < PER_T / 4; q++) {
+        for (int q = 0; q < NW; q++) {
             uint32_t v = 0;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -88,35 +96,6 @@ __device__ __forceinline__ bool filter_keep(FilterMode m, uint8_t c) {
     return true;
 }
 
-// LDS staging of a tile's output.  Threads write their kept bytes at their block-scan offsets, so
-// lane t writes near byte 32t: a 4-byte skew every 32 bytes (dword index d -> d + d/8) spreads
-// those writes over distinct banks.  A dword-aligned group of 4 logical bytes stays contiguous.
-constexpr int STAGE_WORDS = INGEST_TILE / 4 + INGEST_TILE / 32 + 4;
-__device__ __forceinline__ int stage_at(int a) { return a + ((a >> 5) << 2); }
-__device__ __forceinline__ uint32_t stage_word(const uint32_t* st4, int d) { return st4[d + (d >> 3)]; }
-
-// Block-cooperative store of the `cnt` staged bytes to out[g0, g0 + cnt): head bytes, aligned
-// dword body, tail bytes.
-__device__ __forceinline__ void stage_out(const uint32_t* __restrict__ st4, int cnt, uint8_t* __restrict__ out, int64_t g0) {
-    const uint8_t* st = reinterpret_cast<const uint8_t*>(st4);
-    const int t = (int)threadIdx.x;
-    int head = (int)((4 - (g0 & 3)) & 3);
-    if (head > cnt) head = cnt;
-    if (t < head) out[g0 + t] = st[stage_at(t)];
-    const int nd = (cnt - head) >> 2;
-    uint32_t* o4 = reinterpret_cast<uint32_t*>(out + g0 + head);
-    for (int d = t; d < nd; d += (int)blockDim.x) {
-        const int o = head + 4 * d;
-        o4[d] = __builtin_amdgcn_alignbyte(stage_word(st4, (o >> 2) + 1), stage_word(st4, o >> 2), (uint32_t)(o & 3));
-    }
-    const int done = head + 4 * nd;
-    if (t < cnt - done) out[g0 + done + t] = st[stage_at(done + t)];
-}
-
-// Per-thread byte masks of a 32-byte range (bit i = byte off + i):
-//   known    kept by strip, line status decided inside the range (REF) / always (TGT)
-//   unknown  REF: non-space bytes before the range's first line start (status from earlier)
-//   fk       kept by the byte filter;  par  '(' bytes
 // SWAR byte tests on 4 bytes: bit 7 of each byte set where the test holds
 __device__ __forceinline__ uint32_t sw_lt(uint32_t x, uint32_t n) {   // byte < n, n <= 128
     return ~(((x & 0x7F7F7F7Fu) + (0x80u - n) * 0x01010101u) | x) & 0x80808080u;
@@ -129,107 +108,148 @@ __device__ __forceinline__ uint32_t sw_upper(uint32_t x) {
     return x - (lower >> 2);
 }
 
+constexpr int SL = 64;                 // strip bytes per lane
+constexpr int SNW = SL / 4;            // words per lane
+constexpr int STRIP_WTILE = 64 * SL;   // bytes per wave tile
+static_assert(STRIP_WTILE == STRIP_TILE, "tile size shared with the host");
+
+// LDS staging of a wave tile's output.  Lane t writes near byte 64t: a one-dword skew every 64
+// bytes (dword d -> d + d/16) makes the lane stride 17 dwords, so those writes hit distinct banks.
+// A dword-aligned group of 4 logical bytes stays contiguous.
+constexpr int STAGE_WORDS = STRIP_WTILE / 4 + STRIP_WTILE / 64 + 4;
+__device__ __forceinline__ int stage_at(int a) { return a + ((a >> 6) << 2); }
+__device__ __forceinline__ uint32_t stage_word(const uint32_t* st4, int d) { return st4[d + (d >> 4)]; }
+
+// Wave store of the `cnt` staged bytes to out[g0, g0 + cnt): head bytes, aligned dword body, tail.
+__device__ __forceinline__ void stage_out(const uint32_t* __restrict__ st4, int cnt, uint8_t* __restrict__ out, int64_t g0) {
+    const uint8_t* st = reinterpret_cast<const uint8_t*>(st4);
+    const int t = lane_id();
+    int head = (int)((4 - (g0 & 3)) & 3);
+    if (head > cnt) head = cnt;
+    if (t < head) out[g0 + t] = st[stage_at(t)];
+    const int nd = (cnt - head) >> 2;
+    uint32_t* o4 = reinterpret_cast<uint32_t*>(out + g0 + head);
+    for (int d = t; d < nd; d += 64) {
+        const int o = head + 4 * d;
+        o4[d] = __builtin_amdgcn_alignbyte(stage_word(st4, (o >> 2) + 1), stage_word(st4, o >> 2), (uint32_t)(o & 3));
+    }
+    const int done = head + 4 * nd;
+    if (t < cnt - done) out[g0 + done + t] = st[stage_at(done + t)];
+}
+
+// Per-lane byte masks of a 64-byte range (bit i = byte off + i):
+//   known    kept by strip, line status decided inside the range (REF) / always (TGT)
+//   unknown  REF: non-space bytes before the range's first line start (status from earlier)
+//   fk       kept by the byte filter;  par  '(' bytes
 struct StripMasks {
-    uint32_t known, unknown, fk, par;
+    uint64_t known, unknown, fk, par;
     int32_t last;   // status of the last line start in range: -1 none, 0 drop, 1 keep
 };
 
-__device__ __forceinline__ StripMasks strip_masks(IngestMode mode, FilterMode fm, const uint32_t (&w)[PER_T / 4],
-                                                  uint8_t prev, int64_t off, int64_t n, int64_t h, int64_t he) {
+__device__ __forceinline__ uint64_t below64(int k) { return k >= 64 ? ~0ull : (1ull << k) - 1ull; }
+
+template <IngestMode MODE>
+__device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t (&w)[SNW], uint8_t prev, int64_t off,
+                                                  int64_t n, int64_t h, int64_t he) {
     // byte classes four at a time (SWAR); flags gathered into one bit per byte
-    uint32_t ws = 0, nl = 0, gt = 0, fk = 0, par = 0;
+    const uint32_t dn_up = fm != FILTER_UPPER ? 0x80808080u : 0u, dn_lo = fm == FILTER_DROP_N_UPPER ? 0x80808080u : 0u;
+    uint64_t ws = 0, nl = 0, gt = 0, fk = 0, par = 0;
 #pragma unroll
-    for (int q = 0; q < PER_T / 4; q++) {
+    for (int q = 0; q < SNW; q++) {
         const uint32_t x = w[q];
         const int sh = 4 * q;
-        ws |= sw_bits(sw_eq(x, ' ') | (sw_lt(x, 14) & ~sw_lt(x, 9))) << sh;   // isspace: ' ', \t..\r
-        if (mode == INGEST_REF) {
-            nl |= sw_bits(sw_eq(x, '\n')) << sh;
-            gt |= sw_bits(sw_eq(x, '>')) << sh;
+        ws |= (uint64_t)sw_bits(sw_eq(x, ' ') | (sw_lt(x, 14) & ~sw_lt(x, 9))) << sh;   // isspace: ' ', \t..\r
+        if (MODE == INGEST_REF) {
+            nl |= (uint64_t)sw_bits(sw_eq(x, '\n')) << sh;
+            gt |= (uint64_t)sw_bits(sw_eq(x, '>')) << sh;
         }
-        const uint32_t nn = fm == FILTER_DROP_N_UPPER ? (sw_eq(x, 'N') | sw_eq(x, 'n'))
-                                                      : (fm == FILTER_DROP_UPPERN_ONLY ? sw_eq(x, 'N') : 0u);
-        fk |= (sw_bits(nn) ^ 0xfu) << sh;
-        par |= sw_bits(sw_eq(x, '(')) << sh;
+        const uint32_t nn = (sw_eq(x, 'N') & dn_up) | (sw_eq(x, 'n') & dn_lo);
+        fk |= (uint64_t)(sw_bits(nn) ^ 0xfu) << sh;
+        par |= (uint64_t)sw_bits(sw_eq(x, '(')) << sh;
     }
     const int64_t lim = n - off;
-    const uint32_t valid = lim >= 32 ? ~0u : (lim > 0 ? (1u << lim) - 1u : 0u);
+    const uint64_t valid = lim >= 64 ? ~0ull : (lim > 0 ? (1ull << lim) - 1ull : 0ull);
     StripMasks r{0, 0, fk, par, -1};
-    if (mode == INGEST_TGT) {
-        const int64_t lo = h - off < 0 ? 0 : (h - off > 32 ? 32 : h - off);
-        const int64_t hi = he - off < 0 ? 0 : (he - off > 32 ? 32 : he - off);
-        const uint32_t below_hi = hi >= 32 ? ~0u : (1u << hi) - 1u, below_lo = lo >= 32 ? ~0u : (1u << lo) - 1u;
-        r.known = ~ws & valid & ~(below_hi & ~below_lo);
+    if (MODE == INGEST_TGT) {
+        const int64_t lo = h - off < 0 ? 0 : (h - off > 64 ? 64 : h - off);
+        const int64_t hi = he - off < 0 ? 0 : (he - off > 64 ? 64 : he - off);
+        r.known = ~ws & valid & ~(below64((int)hi) & ~below64((int)lo));
         return r;
     }
     // REF: a line's fate is its first byte; line starts are position 0 and bytes after a '\n'
-    const uint32_t ls = ((nl << 1) | (uint32_t)(off == 0 || prev == '\n')) & valid;
-    const int first = ls ? __builtin_ctz(ls) : 32;
-    r.unknown = ~ws & valid & (first >= 32 ? ~0u : (1u << first) - 1u);
-    uint32_t keep = 0, rem = ls;
+    const uint64_t ls = ((nl << 1) | (uint64_t)(off == 0 || prev == '\n')) & valid;
+    const int first = ls ? __builtin_ctzll(ls) : 64;
+    r.unknown = ~ws & valid & below64(first);
+    uint64_t keep = 0, rem = ls;
     while (rem) {
-        const int j = __builtin_ctz(rem);
+        const int j = __builtin_ctzll(rem);
         rem &= rem - 1;
-        const int nx = rem ? __builtin_ctz(rem) : 32;
-        const int32_t st = !((gt >> j) & 1u);
-        if (st) keep |= (nx >= 32 ? ~0u : (1u << nx) - 1u) & ~((1u << j) - 1u);
+        const int nx = rem ? __builtin_ctzll(rem) : 64;
+        const int32_t st = !((gt >> j) & 1ull);
+        if (st) keep |= below64(nx) & ~below64(j);
         r.last = st;
     }
     r.known = ~ws & valid & keep;
     return r;
 }
 
-// last-non-null status of the threads before this one in the block (exclusive), -1 if none
-__device__ __forceinline__ int32_t block_prior_status(int32_t last, int32_t* tmp) {
-    const int lane = lane_id(), w = wave_in_block();
-    int32_t v = last;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        int32_t o = __shfl_up(v, d, 64);
-        if (lane >= d && v < 0) v = o;
+// A wave's tile: its words, the byte before it (lane 0's 'prev'), the masks, and each lane's prior
+// line status inside the wave (-1: no line start in the lanes before it).
+template <IngestMode MODE>
+__device__ __forceinline__ StripMasks strip_tile(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n, int64_t h,
+                                                 int64_t he, int64_t off, uint32_t (&w)[SNW], int32_t& prior,
+                                                 uint64_t& lsm) {
+    const int lane = lane_id();
+    load_words<SNW>(buf, n, off, w);
+    uint8_t prev = '\n';
+    if (MODE == INGEST_REF) {
+        const uint32_t up = (uint32_t)__shfl_up((int)w[SNW - 1], 1, 64) >> 24;
+        prev = lane ? (uint8_t)up : ((off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n');
     }
-    int32_t ex = __shfl_up(v, 1, 64);
-    if (lane == 0) ex = -1;
-    if (lane == 63) tmp[w] = v;
-    __syncthreads();
-    int32_t carry = -1;
-    for (int i = 0; i < w; i++) if (tmp[i] >= 0) carry = tmp[i];
-    __syncthreads();
-    return ex >= 0 ? ex : carry;
+    const StripMasks r = strip_masks<MODE>(fm, w, prev, off, n, h, he);
+    prior = -1;
+    lsm = 0;
+    if (MODE == INGEST_REF) {
+        lsm = __ballot(r.last >= 0);
+        const uint64_t m = lsm & below64(lane);
+        const int src = m ? 63 - __builtin_clzll(m) : 0;
+        const int32_t v = __shfl(r.last, src, 64);
+        prior = m ? v : -1;
+    }
+    return r;
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(IngestMode mode, FilterMode fm, const uint8_t* __restrict__ buf,
-                                                              int64_t n, const int64_t* __restrict__ hdr,
-                                                              int64_t* __restrict__ ta, int64_t* __restrict__ tb,
-                                                              int64_t* __restrict__ tfa, int64_t* __restrict__ tfb,
-                                                              int32_t* __restrict__ tlast) {
-    __shared__ int32_t tmp[8];
-    __shared__ int32_t tmp32[8];
-    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
-    uint32_t w[PER_T / 4];
-    load_words(buf, n, off, w);
-    const uint8_t prev = (off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n';
-    const int64_t h = mode == INGEST_TGT ? hdr[0] : 0, he = mode == INGEST_TGT ? hdr[1] : 0;
-    const StripMasks r = strip_masks(mode, fm, w, prev, off, n, h, he);
-    const int32_t ra = __popc(r.unknown), rb = __popc(r.known);
-    const int32_t rfa = __popc(r.unknown & r.fk), rfb = __popc(r.known & r.fk);
-    const int32_t prior = block_prior_status(r.last, tmp);
-    // a-bytes of a thread with a prior line start in the block are resolved now
-    const int32_t A = prior < 0 ? ra : 0, B = rb + (prior == 1 ? ra : 0);
-    const int32_t FA = prior < 0 ? rfa : 0, FB = rfb + (prior == 1 ? rfa : 0);
-    int32_t At, Bt, FAt, FBt;
-    block_excl_add<int32_t>(A, tmp32, &At);
-    block_excl_add<int32_t>(B, tmp32, &Bt);
-    block_excl_add<int32_t>(FA, tmp32, &FAt);
-    block_excl_add<int32_t>(FB, tmp32, &FBt);
-    // block last status = prior status of a virtual thread after the last one
-    const int32_t mylast = r.last >= 0 ? r.last : prior;
-    if (threadIdx.x == blockDim.x - 1) {
-        ta[blockIdx.x] = At;
-        tb[blockIdx.x] = Bt;
-        tfa[blockIdx.x] = FAt;
-        tfb[blockIdx.x] = FBt;
-        tlast[blockIdx.x] = mylast;
+template <IngestMode MODE>
+__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n,
+                                                              const int64_t* __restrict__ hdr, int64_t* __restrict__ ta,
+                                                              int64_t* __restrict__ tb, int64_t* __restrict__ tfa,
+                                                              int64_t* __restrict__ tfb, int32_t* __restrict__ tlast) {
+    const int64_t tile = (int64_t)blockIdx.x * WPB + wave_in_block();
+    if (tile * STRIP_WTILE >= n) return;
+    const int lane = lane_id();
+    const int64_t off = tile * STRIP_WTILE + (int64_t)lane * SL;
+    const int64_t h = MODE == INGEST_TGT ? hdr[0] : 0, he = MODE == INGEST_TGT ? hdr[1] : 0;
+    uint32_t w[SNW];
+    int32_t prior;
+    uint64_t lsm;
+    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm);
+    // a-bytes of a lane with a prior line start in the wave are resolved now
+    const uint64_t ra = (uint64_t)__popcll(r.unknown), rb = (uint64_t)__popcll(r.known);
+    const uint64_t rfa = (uint64_t)__popcll(r.unknown & r.fk), rfb = (uint64_t)__popcll(r.known & r.fk);
+    const uint64_t A = prior < 0 ? ra : 0, B = rb + (prior == 1 ? ra : 0);
+    const uint64_t FA = prior < 0 ? rfa : 0, FB = rfb + (prior == 1 ? rfa : 0);
+    const uint64_t tot = wave_sum<uint64_t>(A | (B << 16) | (FA << 32) | (FB << 48));   // <= 4096 each
+    if (lane == 0) {
+        ta[tile] = (int64_t)(tot & 0xffff);
+        tb[tile] = (int64_t)((tot >> 16) & 0xffff);
+        tfa[tile] = (int64_t)((tot >> 32) & 0xffff);
+        tfb[tile] = (int64_t)(tot >> 48);
+    }
+    if (MODE == INGEST_REF) {
+        const int32_t last = lsm ? __shfl(r.last, 63 - __builtin_clzll(lsm), 64) : -1;
+        if (lane == 0) tlast[tile] = last;
+    } else if (lane == 0) {
+        tlast[tile] = -1;
     }
 }
 
@@ -324,47 +344,56 @@ __global__ void k_strip_scan_apply(int64_t ntiles, const int64_t* __restrict__ t
     }
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(IngestMode mode, FilterMode fm, const uint8_t* __restrict__ buf,
-                                                            int64_t n, const int64_t* __restrict__ hdr,
+template <IngestMode MODE>
+__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n,
+                                                            const int64_t* __restrict__ hdr,
                                                             const int64_t* __restrict__ toff,
                                                             const int64_t* __restrict__ toff2,
                                                             const int32_t* __restrict__ tcarry,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
                                                             int32_t* __restrict__ flags) {
-    __shared__ int32_t tmp[8];
-    __shared__ int32_t tmp32[8];
-    __shared__ uint32_t st1[STAGE_WORDS + SCCG_BLOCK];   // + one dummy word per thread
-    __shared__ uint32_t st2[STAGE_WORDS + SCCG_BLOCK];
-    const int64_t off = (int64_t)blockIdx.x * INGEST_TILE + (int64_t)threadIdx.x * PER_T;
-    uint32_t w[PER_T / 4];
-    load_words(buf, n, off, w);
-    const uint8_t prev = (off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n';
-    const int64_t h = mode == INGEST_TGT ? hdr[0] : 0, he = mode == INGEST_TGT ? hdr[1] : 0;
-    const StripMasks r = strip_masks(mode, fm, w, prev, off, n, h, he);
-    int32_t prior = block_prior_status(r.last, tmp);
-    if (prior < 0) prior = tcarry[blockIdx.x];
-    const uint32_t keep = r.known | (prior == 1 ? r.unknown : 0u), fkeep = keep & r.fk;
-    int32_t tot1, tot2;
-    int32_t p1 = block_excl_add<int32_t>(__popc(keep), tmp32, &tot1);
-    int32_t p2 = out2 ? block_excl_add<int32_t>(__popc(fkeep), tmp32, &tot2) : 0;
-    uint8_t* s1 = reinterpret_cast<uint8_t*>(st1);
-    uint8_t* s2 = reinterpret_cast<uint8_t*>(st2);
-    // every byte is stored (a dropped byte into this lane's own dummy word), its slot from a
-    // prefix popcount of the keep mask: no per-byte branch
-    uint32_t uw[PER_T / 4];
+    __shared__ uint32_t stage_all[WPB][STAGE_WORDS + 64];   // + one dummy word per lane
+    const int64_t tile = (int64_t)blockIdx.x * WPB + wave_in_block();
+    if (tile * STRIP_WTILE >= n) return;
+    const int lane = lane_id();
+    uint32_t* st4 = stage_all[wave_in_block()];
+    uint8_t* s1 = reinterpret_cast<uint8_t*>(st4);
+    const int64_t off = tile * STRIP_WTILE + (int64_t)lane * SL;
+    const int64_t h = MODE == INGEST_TGT ? hdr[0] : 0, he = MODE == INGEST_TGT ? hdr[1] : 0;
+    uint32_t w[SNW];
+    int32_t prior;
+    uint64_t lsm;
+    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm);
+    if (MODE == INGEST_REF && prior < 0) prior = tcarry[tile];
+    const uint64_t keep = r.known | (prior == 1 ? r.unknown : 0ull), fkeep = keep & r.fk;
+    const uint32_t c = (uint32_t)__popcll(keep) | ((uint32_t)__popcll(fkeep) << 16);
+    const uint32_t incl = wave_incl_add<uint32_t>(c), tot = lane_val(incl, 63);
+    const uint32_t ex = incl - c;
+    // every byte is stored (a dropped byte into this lane's own dummy word), at a running slot:
+    // no per-byte branch
+    const int dummy = 4 * (STAGE_WORDS + lane);
+    int q = (int)(ex & 0xffff);
 #pragma unroll
-    for (int q = 0; q < PER_T / 4; q++) uw[q] = sw_upper(w[q]);
-    const int dummy = 4 * (STAGE_WORDS + (int)threadIdx.x);
-#pragma unroll
-    for (int i = 0; i < PER_T; i++) {
-        const uint32_t below = (1u << i) - 1u;
-        s1[(keep >> i) & 1u ? stage_at(p1 + __popc(keep & below)) : dummy] = wb(w, i);
-        if (out2) s2[(fkeep >> i) & 1u ? stage_at(p2 + __popc(fkeep & below)) : dummy] = wb(uw, i);
+    for (int i = 0; i < SL; i++) {
+        const int k = (int)((keep >> i) & 1ull);
+        s1[k ? stage_at(q) : dummy] = wb(w, i);
+        q += k;
     }
-    if (flags && __ballot((keep & r.par) != 0) && lane_id() == 0) atomicOr(flags, 1);
-    __syncthreads();
-    stage_out(st1, tot1, out, toff[blockIdx.x]);
-    if (out2) stage_out(st2, tot2, out2, toff2[blockIdx.x]);
+    if (flags && __ballot((keep & r.par) != 0) && lane == 0) atomicOr(flags, 1);
+    wave_sync();
+    stage_out(st4, (int)(tot & 0xffff), out, toff[tile]);
+    if (out2) {
+        wave_sync();
+        q = (int)(ex >> 16);
+#pragma unroll
+        for (int i = 0; i < SL; i++) {
+            const int k = (int)((fkeep >> i) & 1ull);
+            s1[k ? stage_at(q) : dummy] = (uint8_t)(sw_upper(w[i >> 2]) >> (8 * (i & 3)));
+            q += k;
+        }
+        wave_sync();
+        stage_out(st4, (int)(tot >> 16), out2, toff2[tile]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -509,11 +538,16 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
         return 0;
     }
     if (!out2) fmode = FILTER_UPPER;   // second output unused
-    const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
-    hipLaunchKernelGGL(k_strip_summary, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, fmode, buf, n, d_header,
-                       sc.tile_a, sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last);
+    const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE;
+    const unsigned g = grid_for(ntiles, WPB);
+    if (mode == INGEST_TGT)
+        hipLaunchKernelGGL(k_strip_summary<INGEST_TGT>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header, sc.tile_a,
+                           sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last);
+    else
+        hipLaunchKernelGGL(k_strip_summary<INGEST_REF>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header, sc.tile_a,
+                           sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last);
     const int64_t nblk = (ntiles + SCAN_B - 1) / SCAN_B;
-    if (nblk > SCAN_B) return SCCG_E_UNSUPPORTED;   // > 8 GiB of FASTA
+    if (nblk > SCAN_B) return SCCG_E_UNSUPPORTED;   // > 4 GiB of FASTA
     TileSum* btot = reinterpret_cast<TileSum*>(sc.block_sums);
     hipLaunchKernelGGL(k_strip_scan_local, dim3((unsigned)nblk), dim3(SCAN_B), 0, s, ntiles, sc.tile_a, sc.tile_b,
                        sc.tile_fa, sc.tile_fb, sc.tile_last, btot);
@@ -521,8 +555,12 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     hipLaunchKernelGGL(k_strip_scan_apply, dim3(grid_for(ntiles, 256)), dim3(256), 0, s, ntiles, sc.tile_a, sc.tile_b,
                        sc.tile_fa, sc.tile_fb, sc.tile_last, btot, sc.tile_off, sc.tile_off2, sc.tile_carry, d_len,
                        d_len2);
-    PROF_LAUNCH(PROF_STRIP, s, k_strip_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, mode, fmode, buf, n,
-                d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
+    if (mode == INGEST_TGT)
+        PROF_LAUNCH(PROF_STRIP, s, k_strip_write<INGEST_TGT>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
+    else
+        PROF_LAUNCH(PROF_STRIP, s, k_strip_write<INGEST_REF>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

@@ -33,6 +33,14 @@ void prof_end(hipStream_t s, int id);
 
 // ---- scan.hip ---------------------------------------------------------------------------------
 #include <initializer_list>
+// Blocking read of up to 8 small device values (<= 4 KiB in all) behind the work queued on s,
+// through pinned host memory and a spin on a sequence number (see scan.hip).
+struct RbItem {
+    const void* src;   // device
+    void* dst;         // host
+    int bytes;
+};
+int dev_readback(const RbItem* items, int n, hipStream_t s);
 int dev_set_i64(int64_t* p, int n, std::initializer_list<int64_t> vals, hipStream_t s);
 int dev_set_i32(int32_t* p, int n, std::initializer_list<int32_t> vals, hipStream_t s);
 // stream-ordered write of up to 16 bytes (copied into the kernel arguments)
@@ -44,7 +52,8 @@ int dev_excl_max(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, i
                  hipStream_t s);
 
 // ---- ingest.hip -------------------------------------------------------------------------------
-constexpr int INGEST_TILE = 8192;  // bytes per 256-thread tile (32 per thread)
+constexpr int INGEST_TILE = 8192;  // run extraction: bytes per 256-thread tile (32 per thread)
+constexpr int STRIP_TILE = 4096;   // FASTA strip: bytes per wave tile (64 per lane)
 enum IngestMode { INGEST_REF = 0, INGEST_TGT = 1 };
 enum FilterMode { FILTER_DROP_N_UPPER = 0, FILTER_DROP_UPPERN_ONLY = 1, FILTER_UPPER = 2 };   // all uppercase
 enum RunPred { RUN_LOWER = 0, RUN_N = 1 };

@@ -645,8 +645,11 @@ int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_
     }
     // leftover target segments (compression.cpp:476-481) go after the segment text
     int64_t seg_text = 0;
-    SCCG_HIP(hipMemcpyAsync(&seg_text, d_len, sizeof seg_text, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipStreamSynchronize(s));
+    {
+        const RbItem it{d_len, &seg_text, (int)sizeof seg_text};
+        const int rc = dev_readback(&it, 1, s);
+        if (rc) return rc;
+    }
     const int64_t rest = nT - lead_len;
     if (rest > 0) {
         const unsigned g = grid_for(rest, 256) > 8192 ? 8192 : grid_for(rest, 256);

@@ -5,6 +5,8 @@
 // 1024-thread block.  HBM-bound: 8 B read twice + 8 B written per element.
 #include "internal.h"
 
+#include <cstring>
+
 namespace {
 
 constexpr int ITEMS = 16;
@@ -211,4 +213,91 @@ int dev_excl_sum(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, i
 int dev_excl_max(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
                  hipStream_t s) {
     return scan_impl<OpMax>(in, out, n, d_total, d_partial, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Low-latency readback of a few small device values.  One single-wave kernel copies them into
+// pinned, fine-grained host memory and then publishes a sequence number there with a system-scope
+// release; the host spins on that number.  Compared with hipMemcpyAsync + hipStreamSynchronize
+// this has no copy-engine command and no interrupt wake-up on the host's critical path (a
+// stream-synchronise round trip costs 20-45 us between kernels here, the spin a few).
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int RB_MAX = 8;
+constexpr int RB_BYTES = 4096 - 64;
+struct RbArgs {
+    const uint8_t* src[RB_MAX];
+    int32_t off[RB_MAX];
+    int32_t bytes[RB_MAX];
+    int32_t n;
+};
+__global__ void k_readback(RbArgs a, uint8_t* __restrict__ host, unsigned long long* flag, unsigned long long seq) {
+    for (int i = 0; i < a.n; i++) {
+        const uint8_t* src = a.src[i];
+        uint8_t* dst = host + a.off[i];
+        const int nb = a.bytes[i];
+        if ((((uintptr_t)src) & 3) == 0 && (nb & 3) == 0) {
+            for (int b = (int)threadIdx.x; b < nb / 4; b += (int)blockDim.x)
+                reinterpret_cast<uint32_t*>(dst)[b] = reinterpret_cast<const uint32_t*>(src)[b];
+        } else {
+            for (int b = (int)threadIdx.x; b < nb; b += (int)blockDim.x) dst[b] = src[b];
+        }
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+struct RbHost {
+    uint8_t* buf = nullptr;   // [0, 64): flag; [64, 4096): data
+    uint8_t* dbuf = nullptr;  // device view
+    unsigned long long seq = 0;
+};
+thread_local RbHost g_rb;
+}  // namespace
+
+int dev_readback(const RbItem* items, int n, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (n > RB_MAX) return SCCG_E_INVALID;
+    if (!g_rb.buf) {
+        void* p = nullptr;
+        SCCG_HIP(hipHostMalloc(&p, 4096, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+        void* dp = nullptr;
+        SCCG_HIP(hipHostGetDevicePointer(&dp, p, 0));
+        g_rb.buf = static_cast<uint8_t*>(p);
+        g_rb.dbuf = static_cast<uint8_t*>(dp);
+        *reinterpret_cast<volatile unsigned long long*>(g_rb.buf) = 0;
+    }
+    RbArgs a{};
+    int off = 0;
+    for (int i = 0; i < n; i++) {
+        if (items[i].bytes < 0 || off + items[i].bytes > RB_BYTES) return SCCG_E_INVALID;
+        a.src[i] = static_cast<const uint8_t*>(items[i].src);
+        a.off[i] = off;
+        a.bytes[i] = items[i].bytes;
+        off += (items[i].bytes + 7) & ~7;
+    }
+    a.n = n;
+    const unsigned long long seq = ++g_rb.seq;
+    unsigned long long* flag = reinterpret_cast<unsigned long long*>(g_rb.buf);
+    hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, s, a, g_rb.dbuf + 64,
+                       reinterpret_cast<unsigned long long*>(g_rb.dbuf), seq);
+    SCCG_HIP(hipGetLastError());
+    for (uint64_t it = 1;; it++) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
+        if ((it & 4095) == 0) {
+            // the stream failed, or drained without the flag arriving: fall back to a full wait
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipErrorNotReady) {
+                SCCG_HIP(e == hipSuccess ? hipStreamSynchronize(s) : e);
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+                    return sccg_hip_fail(hipErrorUnknown, "readback flag not raised by a finished stream", __FILE__,
+                                         __LINE__);
+                }
+                break;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    for (int i = 0; i < n; i++) memcpy(items[i].dst, g_rb.buf + 64 + a.off[i], (size_t)items[i].bytes);
+    return 0;
 }

@@ -158,8 +158,8 @@ size_t sccg_compress_bound(size_t ref_len, size_t tgt_len) {
 namespace {
 
 int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n) {
-    HIPTRY(hipMemcpyAsync(h, d, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    HIPTRY(hipStreamSynchronize(ctx->stream));
+    const RbItem it{d, h, n * (int)sizeof(int64_t)};
+    TRY(dev_readback(&it, 1, ctx->stream));
     return 0;
 }
 
@@ -167,7 +167,7 @@ int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n) {
 // length(s): h_len[0] strip, h_len[1] filter (d_len[0..1] on the device)
 int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const int64_t* d_hdr, uint8_t* out,
           int64_t* d_len, int32_t* d_flags, int64_t* h_len, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr) {
-    const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE + 1;
+    const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE + 1;
     IngestScratch sc;
     GET(int64_t, ta, B_TILE_A, ntiles);
     GET(int64_t, tb, B_TILE_B, ntiles);
@@ -243,9 +243,10 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp));
     int64_t hsc[10];
     int32_t flags = 0;
-    HIPTRY(hipMemcpyAsync(hsc, sc, sizeof hsc, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipMemcpyAsync(&flags, d_flags, sizeof flags, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipStreamSynchronize(s));
+    {
+        const RbItem it[2] = {{sc, hsc, (int)sizeof hsc}, {d_flags, &flags, (int)sizeof flags}};
+        TRY(dev_readback(it, 2, s));
+    }
     const int64_t hdr[2] = {hsc[0], hsc[1]}, lt[2] = {hsc[2], hsc[3]}, lr[2] = {hsc[7], hsc[8]};
     const int64_t nT = lt[0], nR = lr[0];
     if (nT >= INT32_MAX - 8 || nR >= INT32_MAX - 8)
@@ -366,11 +367,10 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     GET(int64_t, sc, B_SCAL, 64);
     int64_t nl[4];
     TRY(dc_find_lines(rec, n, sc, s));
-    TRY(d2h_i64(ctx, sc, nl, 4));
     uint8_t first = 0;
-    if (n > 0) {
-        HIPTRY(hipMemcpyAsync(&first, rec, 1, hipMemcpyDeviceToHost, s));
-        HIPTRY(hipStreamSynchronize(s));
+    {
+        const RbItem it[2] = {{sc, nl, (int)sizeof nl}, {rec, &first, n > 0 ? 1 : 0}};
+        TRY(dev_readback(it, 2, s));
     }
     // getline semantics: line i spans [start_i, nl_i); it exists iff start_i < n  (:68-97)
     int64_t start[4], end[4];
@@ -397,8 +397,8 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     bool n_is_comma = false;
     if (nnl == 1) {
         uint8_t c = 0;
-        HIPTRY(hipMemcpyAsync(&c, nline, 1, hipMemcpyDeviceToHost, s));
-        HIPTRY(hipStreamSynchronize(s));
+        const RbItem it{nline, &c, 1};
+        TRY(dev_readback(&it, 1, s));
         n_is_comma = c == ',';
     }
     int64_t rl[2];
@@ -432,18 +432,18 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     GET(int64_t, dsum, B_D_DSUM, nenc + 1);
     TRY(dc_decode_prepare(enc, nenc, lp, contrib, dlt, doff, dsum, nRp, part, d_err, sc + 12, s));
     int64_t D = 0;
-    TRY(d2h_i64(ctx, sc + 12, &D, 1));
     int32_t err = 0;
-    HIPTRY(hipMemcpyAsync(&err, d_err, sizeof err, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipStreamSynchronize(s));
+    {
+        const RbItem it[2] = {{sc + 12, &D, (int)sizeof D}, {d_err, &err, (int)sizeof err}};
+        TRY(dev_readback(it, 2, s));
+    }
     if (err & 1) return ctx->fail(SCCG_E_PARSE, "record text outside the run/token grammar");
     if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
     const int64_t nres = D + nr.total;
     if (nr.n > 0) {
         int32_t ls_last = 0, ll_last = 0;
-        HIPTRY(hipMemcpyAsync(&ls_last, nr.start + nr.n - 1, 4, hipMemcpyDeviceToHost, s));
-        HIPTRY(hipMemcpyAsync(&ll_last, nr.len + nr.n - 1, 4, hipMemcpyDeviceToHost, s));
-        HIPTRY(hipStreamSynchronize(s));
+        const RbItem it[2] = {{nr.start + nr.n - 1, &ls_last, 4}, {nr.len + nr.n - 1, &ll_last, 4}};
+        TRY(dev_readback(it, 2, s));
         if ((int64_t)ls_last + ll_last > nres) return ctx->fail(SCCG_E_PARSE, "N positions beyond the sequence");
     }
     const int64_t hlen = has_hdr ? end[0] : 0;

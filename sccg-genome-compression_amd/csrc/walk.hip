@@ -1069,8 +1069,11 @@ int run_fullc(WalkPtrs& A, int32_t y, int32_t P, FullC* out, hipStream_t s) {
     PROF_LAUNCH(PROF_FULLC, s, k_fullc, dim3(g), dim3(256), 0, s, A, y, P, 1);
     SCCG_HIP(hipGetLastError());
     unsigned long long r[4];
-    SCCG_HIP(hipMemcpyAsync(r, A.fc, sizeof r, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipStreamSynchronize(s));
+    {
+        const RbItem it{A.fc, r, (int)sizeof r};
+        const int rc = dev_readback(&it, 1, s);
+        if (rc) return rc;
+    }
     out->lmax = (int64_t)r[0];
     if (r[0] == 0) { out->p = INVALID; return 0; }
     const uint64_t k0 = (uint64_t)(uint32_t)(P < 0 ? -P : P) << 32;   // pick_key(0, P)
@@ -1182,8 +1185,10 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             PROF_LAUNCH(PROF_PRESENCE, s, k_presence, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, nb);
             hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)g);
             SCCG_HIP(hipGetLastError());
-            SCCG_HIP(hipMemcpyAsync(r, A.fc + 4, sizeof r, hipMemcpyDeviceToHost, s));
-            SCCG_HIP(hipStreamSynchronize(s));
+            {
+                const RbItem it{A.fc + 4, r, (int)sizeof r};
+                RC(dev_readback(&it, 1, s));
+            }
             if (r[0] != ~0ull && r[0] < r[1]) {
                 first_y = (int32_t)r[0];
                 if (first_y == x0 && r[4] > 0) {   // statistics gathered by the same sweep
@@ -1269,12 +1274,11 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             };
             RC(frozen_batch(0, FROZEN_FIRST, false));   // fy was set by k_commit
             int32_t rs[6];
-            SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
-            SCCG_HIP(hipStreamSynchronize(s));
+            const RbItem rs_item{A.scal, rs, (int)sizeof rs};
+            RC(dev_readback(&rs_item, 1, s));
             if (rs[5] > FROZEN_FIRST) {   // more frozen chunks than the blind batch covered
                 for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, true));
-                SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
-                SCCG_HIP(hipStreamSynchronize(s));
+                RC(dev_readback(&rs_item, 1, s));
             }
             if (rs[1]) {
                 {   // escalations: resolve on the host, resume, commit the resumed chunks
@@ -1287,12 +1291,13 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                                        (const int32_t*)A.rlist, nr);
                     SCCG_HIP(hipGetLastError());
                 }
-                SCCG_HIP(hipMemcpyAsync(&rs[5], A.scal + 5, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-                SCCG_HIP(hipStreamSynchronize(s));
+                {
+                    const RbItem it{A.scal + 5, &rs[5], (int)sizeof(int32_t)};
+                    RC(dev_readback(&it, 1, s));
+                }
                 if (rs[5] == 0) RC(frozen_batch(0, 0, false));   // pending only
                 for (int fb = 0; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, fb > 0));
-                SCCG_HIP(hipMemcpyAsync(rs, A.scal, sizeof rs, hipMemcpyDeviceToHost, s));
-                SCCG_HIP(hipStreamSynchronize(s));
+                RC(dev_readback(&rs_item, 1, s));
             }
             nlist = rs[0];
             if (dbg) {
@@ -1399,8 +1404,10 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     hipLaunchKernelGGL(k_flatten, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, nfirst);
     SCCG_HIP(hipGetLastError());
     int64_t nchunkm = 0;
-    SCCG_HIP(hipMemcpyAsync(&nchunkm, A.scal64, sizeof nchunkm, hipMemcpyDeviceToHost, s));
-    SCCG_HIP(hipStreamSynchronize(s));
+    {
+        const RbItem it{A.scal64, &nchunkm, (int)sizeof nchunkm};
+        RC(dev_readback(&it, 1, s));
+    }
     const int64_t nm = nchunkm + nfirst;
     res->n_matches = nm;
     g_last = A;
@@ -1416,10 +1423,8 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         PROF_LAUNCH(PROF_MATCH_EMIT, s, k_match_textwrite, dim3(grid_for(nm, WPB)), dim3(SCCG_BLOCK), 0, s, A, nm, out);
         SCCG_HIP(hipGetLastError());
         int32_t lt[2];
-        SCCG_HIP(hipMemcpyAsync(&text, A.scal64 + 1, sizeof text, hipMemcpyDeviceToHost, s));
-        SCCG_HIP(hipMemcpyAsync(&lt[0], A.ft + nm - 1, 4, hipMemcpyDeviceToHost, s));
-        SCCG_HIP(hipMemcpyAsync(&lt[1], A.fl + nm - 1, 4, hipMemcpyDeviceToHost, s));
-        SCCG_HIP(hipStreamSynchronize(s));
+        const RbItem it[3] = {{A.scal64 + 1, &text, (int)sizeof text}, {A.ft + nm - 1, &lt[0], 4}, {A.fl + nm - 1, &lt[1], 4}};
+        RC(dev_readback(it, 3, s));
         tail_from = lt[0] + lt[1];
     }
     const int64_t tail = nTp - tail_from;
