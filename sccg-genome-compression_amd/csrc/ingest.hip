@@ -113,12 +113,15 @@ constexpr int SNW = SL / 4;            // words per lane
 constexpr int STRIP_WTILE = 64 * SL;   // bytes per wave tile
 static_assert(STRIP_WTILE == STRIP_TILE, "tile size shared with the host");
 
-// LDS staging of a wave tile's output.  Lane t writes near byte 64t: a one-dword skew every 64
-// bytes (dword d -> d + d/16) makes the lane stride 17 dwords, so those writes hit distinct banks.
-// A dword-aligned group of 4 logical bytes stays contiguous.
-constexpr int STAGE_WORDS = STRIP_WTILE / 4 + STRIP_WTILE / 64 + 4;
-__device__ __forceinline__ int stage_at(int a) { return a + ((a >> 6) << 2); }
-__device__ __forceinline__ uint32_t stage_word(const uint32_t* st4, int d) { return st4[d + (d >> 4)]; }
+// LDS staging of a wave tile's output, in output order.  Each lane compacts its 64 bytes a word
+// at a time: v_perm packs a word's kept bytes to the low end (selector from a 16-entry table by
+// the word's 4-bit keep mask) into a 64-bit accumulator aligned to the stage's dwords, and every
+// completed dword is stored with an aligned ds_write_b32 (unaligned LDS stores stall).  A lane's
+// first dword may start with bytes of earlier lanes (written as garbage here) and its last bytes
+// may share a dword with later lanes: after all dword stores, every lane stores its final partial
+// dword byte by byte, which also repairs the garbage that later lanes put there.
+constexpr int STAGE_WORDS = STRIP_WTILE / 4 + 2;
+__device__ __forceinline__ uint32_t stage_word(const uint32_t* st4, int d) { return st4[d]; }
 
 // Wave store of the `cnt` staged bytes to out[g0, g0 + cnt): head bytes, aligned dword body, tail.
 __device__ __forceinline__ void stage_out(const uint32_t* __restrict__ st4, int cnt, uint8_t* __restrict__ out, int64_t g0) {
@@ -126,7 +129,7 @@ __device__ __forceinline__ void stage_out(const uint32_t* __restrict__ st4, int 
     const int t = lane_id();
     int head = (int)((4 - (g0 & 3)) & 3);
     if (head > cnt) head = cnt;
-    if (t < head) out[g0 + t] = st[stage_at(t)];
+    if (t < head) out[g0 + t] = st[t];
     const int nd = (cnt - head) >> 2;
     uint32_t* o4 = reinterpret_cast<uint32_t*>(out + g0 + head);
     for (int d = t; d < nd; d += 64) {
@@ -134,7 +137,51 @@ __device__ __forceinline__ void stage_out(const uint32_t* __restrict__ st4, int 
         o4[d] = __builtin_amdgcn_alignbyte(stage_word(st4, (o >> 2) + 1), stage_word(st4, o >> 2), (uint32_t)(o & 3));
     }
     const int done = head + 4 * nd;
-    if (t < cnt - done) out[g0 + done + t] = st[stage_at(done + t)];
+    if (t < cnt - done) out[g0 + done + t] = st[done + t];
+}
+
+// v_perm selectors: kept bytes of a word (4-bit mask) to the low end, zeros above (0x0c)
+__device__ __forceinline__ uint32_t compact_sel(uint32_t m) {
+    uint32_t sel = 0x0c0c0c0cu;
+    int k = 0;
+    for (int i = 0; i < 4; i++)
+        if ((m >> i) & 1u) { sel = (sel & ~(0xffu << (8 * k))) | ((uint32_t)i << (8 * k)); k++; }
+    return sel;
+}
+
+// Stage the bytes of w (uppercased if UP) selected by keep at byte q0 of st (the lane's output
+// offset in the tile).
+template <bool UP>
+__device__ __forceinline__ void stage_lane(uint8_t* __restrict__ st, const uint32_t* __restrict__ tab,
+                                           const uint32_t (&w)[SNW], uint64_t keep, int q0) {
+    const int mis = q0 & 3;
+    uint32_t* const a0 = reinterpret_cast<uint32_t*>(st + (q0 - mis));
+    uint32_t* a4 = a0;
+    uint64_t acc = 0;
+    int an = mis;   // bytes in acc (the first `mis` belong to earlier lanes)
+#pragma unroll
+    for (int h = 0; h < SNW; h += 8) {
+        uint32_t sel[8];   // selectors first: a table read behind the stage writes would wait for them
+#pragma unroll
+        for (int j = 0; j < 8; j++) sel[j] = tab[(uint32_t)(keep >> (4 * (h + j))) & 0xfu];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t m = (uint32_t)(keep >> (4 * (h + j))) & 0xfu;
+            const uint32_t x = UP ? sw_upper(w[h + j]) : w[h + j];
+            acc |= (uint64_t)__builtin_amdgcn_perm(0u, x, sel[j]) << (8 * an);
+            an += __builtin_popcount(m);
+            if (an >= 4) {
+                *a4++ = (uint32_t)acc;
+                acc >>= 32;
+                an -= 4;
+            }
+        }
+    }
+    wave_sync();
+    uint8_t* tb = reinterpret_cast<uint8_t*>(a4);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+        if (i < an && (a4 != a0 || i >= mis)) tb[i] = (uint8_t)(acc >> (8 * i));
 }
 
 // Per-lane byte masks of a 64-byte range (bit i = byte off + i):
@@ -352,7 +399,10 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
                                                             const int32_t* __restrict__ tcarry,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
                                                             int32_t* __restrict__ flags) {
-    __shared__ uint32_t stage_all[WPB][STAGE_WORDS + 64];   // + one dummy word per lane
+    __shared__ uint32_t stage_all[WPB][STAGE_WORDS];
+    __shared__ uint32_t tab[16];
+    if (threadIdx.x < 16) tab[threadIdx.x] = compact_sel(threadIdx.x);
+    __syncthreads();
     const int64_t tile = (int64_t)blockIdx.x * WPB + wave_in_block();
     if (tile * STRIP_WTILE >= n) return;
     const int lane = lane_id();
@@ -369,28 +419,13 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
     const uint32_t c = (uint32_t)__popcll(keep) | ((uint32_t)__popcll(fkeep) << 16);
     const uint32_t incl = wave_incl_add<uint32_t>(c), tot = lane_val(incl, 63);
     const uint32_t ex = incl - c;
-    // every byte is stored (a dropped byte into this lane's own dummy word), at a running slot:
-    // no per-byte branch
-    const int dummy = 4 * (STAGE_WORDS + lane);
-    int q = (int)(ex & 0xffff);
-#pragma unroll
-    for (int i = 0; i < SL; i++) {
-        const int k = (int)((keep >> i) & 1ull);
-        s1[k ? stage_at(q) : dummy] = wb(w, i);
-        q += k;
-    }
     if (flags && __ballot((keep & r.par) != 0) && lane == 0) atomicOr(flags, 1);
+    stage_lane<false>(s1, tab, w, keep, (int)(ex & 0xffff));
     wave_sync();
     stage_out(st4, (int)(tot & 0xffff), out, toff[tile]);
     if (out2) {
         wave_sync();
-        q = (int)(ex >> 16);
-#pragma unroll
-        for (int i = 0; i < SL; i++) {
-            const int k = (int)((fkeep >> i) & 1ull);
-            s1[k ? stage_at(q) : dummy] = (uint8_t)(sw_upper(w[i >> 2]) >> (8 * (i & 3)));
-            q += k;
-        }
+        stage_lane<true>(s1, tab, w, fkeep, (int)(ex >> 16));
         wave_sync();
         stage_out(st4, (int)(tot >> 16), out2, toff2[tile]);
     }
