@@ -227,14 +227,20 @@ __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t 
     const uint64_t ls = ((nl << 1) | (uint64_t)(off == 0 || prev == '\n')) & valid;
     const int first = ls ? __builtin_ctzll(ls) : 64;
     r.unknown = ~ws & valid & below64(first);
-    uint64_t keep = 0, rem = ls;
-    while (rem) {
-        const int j = __builtin_ctzll(rem);
-        rem &= rem - 1;
-        const int nx = rem ? __builtin_ctzll(rem) : 64;
-        const int32_t st = !((gt >> j) & 1ull);
-        if (st) keep |= below64(nx) & ~below64(j);
-        r.last = st;
+    uint64_t keep = 0;
+    if ((gt & ls) == 0) {   // no '>' line here: everything from the first line start on is kept
+        keep = ~below64(first);
+        r.last = ls ? 1 : -1;
+    } else {
+        uint64_t rem = ls;
+        while (rem) {
+            const int j = __builtin_ctzll(rem);
+            rem &= rem - 1;
+            const int nx = rem ? __builtin_ctzll(rem) : 64;
+            const int32_t st = !((gt >> j) & 1ull);
+            if (st) keep |= below64(nx) & ~below64(j);
+            r.last = st;
+        }
     }
     r.known = ~ws & valid & keep;
     return r;

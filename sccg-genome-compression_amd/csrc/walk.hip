@@ -909,7 +909,34 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
     }
 }
 
-__global__ __launch_bounds__(1024) void k_cand_reduce(WalkPtrs A, int nblk) {
+// The usual first step: does the target's first k-mer (x0) occur in R' at all, and the candidate
+// statistics if so.  One key, no tables: a plain compare per reference position, so this sweep
+// runs at streaming speed; k_presence (the general batch search) runs only when it finds nothing.
+__global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
+    __shared__ CandBest wbest[SCCG_BLOCK / 64];
+    const int k = A.k;
+    const uint32_t key0 = walk_key(A.T + x0, k);
+    CandBest best{0, 0, 0, ~0ull};
+    if (key0 < KEY_EXOTIC) {   // exotic: no statistics, the caller falls back to k_presence
+        sweep_kmers(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) { return pure && code == key0; },
+                    [&](int64_t c) {
+                        const uint32_t l = (uint32_t)serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, x0, k);
+                        best = cb_merge(best, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key((int32_t)c, -1) : ~0ull});
+                    });
+    }
+    best = cb_wave(best);
+    if (lane_id() == 0) wbest[wave_in_block()] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < SCCG_BLOCK / 64; i++) best = cb_merge(best, wbest[i]);
+        unsigned long long* o = A.fcb + 4 * blockIdx.x;
+        o[0] = best.l; o[1] = best.cnt; o[2] = best.has0; o[3] = best.minkey;
+    }
+}
+
+// fc[8..11] = statistics merged over the sweep's blocks; with x0 >= 0 (after k_key0) also
+// fc[4] = x0 when x0's k-mer has a candidate, fc[5] = none
+__global__ __launch_bounds__(1024) void k_cand_reduce(WalkPtrs A, int nblk, int32_t x0) {
     __shared__ CandBest wbest[16];
     CandBest v{0, 0, 0, ~0ull};
     for (int b = (int)threadIdx.x; b < nblk; b += (int)blockDim.x) {
@@ -922,6 +949,7 @@ __global__ __launch_bounds__(1024) void k_cand_reduce(WalkPtrs A, int nblk) {
     if (threadIdx.x == 0) {
         for (int i = 1; i < (int)(blockDim.x >> 6); i++) v = cb_merge(v, wbest[i]);
         A.fc[8] = v.l; A.fc[9] = v.cnt; A.fc[10] = v.has0; A.fc[11] = v.minkey;
+        if (x0 >= 0) { A.fc[4] = v.cnt ? (unsigned long long)x0 : ~0ull; A.fc[5] = ~0ull; }
     }
 }
 
@@ -1171,19 +1199,64 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     res->n_matches = 0;
     const int32_t lastk = (int32_t)nTp - k;
 
+    // ---- anchors -> speculative guesses for chunks 1..C-1 (queued first: they do not depend on
+    //      the first step, so the GPU builds them while the host waits for it)
+    const bool dbgp = getenv("SCCG_DEBUG") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!dbgp) return;
+        (void)hipStreamSynchronize(s);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[phase]   walk.%-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
+    const bool walkable = nRp >= k && lastk >= 0;
+    const unsigned gsweep = grid_for(nRp - k + 1 > 0 ? nRp - k + 1 : 1, 256 * FC_PER_T) > PRESENCE_GRID
+                                ? PRESENCE_GRID : grid_for(nRp - k + 1 > 0 ? nRp - k + 1 : 1, 256 * FC_PER_T);
+    if (walkable) {
+        // the usual first step first: x0 = 0's own k-mer (statistics land in fc[4..11])
+        hipLaunchKernelGGL(k_key0, dim3(gsweep), dim3(SCCG_BLOCK), 0, s, A, 0);
+        hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)gsweep, 0);
+        SCCG_HIP(hipGetLastError());
+        const int64_t slots = 1ll << A.abits;
+        // a fresh workspace is cleared once; afterwards every call's generation retires old slots
+        static thread_local const void* ws_seen = nullptr;
+        static thread_local uint32_t gen = 0;
+        if (ws != ws_seen) {
+            SCCG_HIP(hipMemsetAsync(A.atab, 0, (size_t)slots * sizeof(uint64_t), s));
+            ws_seen = ws;
+        }
+        A.agen = 0x9E3779B9u * ++gen;
+        const int64_t ns = nRp / ANCHOR_STEP + 1;
+        const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
+        PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
+        SCCG_HIP(hipGetLastError());
+    }
+
     // ---- the exact first (ungated) step: first target position with any candidate
     int32_t first_y = INVALID, first_p = 0, first_l = 0;
-    if (nRp >= k && lastk >= 0) {
+    if (walkable) {
         int32_t x0 = 0;
         unsigned long long r[8];   // fc[4..11]: first hit, first exotic, statistics of the batch's x0
+        {
+            const RbItem it{A.fc + 4, r, (int)sizeof r};
+            RC(dev_readback(&it, 1, s));
+        }
+        if (r[0] == 0 && r[4] > 0) {   // x0 = 0 has candidates (k_key0)
+            first_y = 0;
+            const uint64_t k0 = 1ull << 32;   // pick_key(0, -1)
+            const uint64_t pk = (r[5] >= 2 && r[6]) ? r[7] : ((r[6] && k0 < r[7]) ? k0 : r[7]);
+            first_p = (int32_t)(uint32_t)pk;
+            first_l = (int32_t)r[4];
+        }
         while (x0 <= lastk && first_y == INVALID) {
             const int32_t nb = (lastk - x0 + 1) < PB ? (lastk - x0 + 1) : PB;
             RC(set_u64(A.fc + 4, {-1, -1}, s));
-            const int64_t npos = nRp - k + 1;
-            unsigned g = grid_for(npos, 256 * FC_PER_T);
-            if (g > PRESENCE_GRID) g = PRESENCE_GRID;
+            const unsigned g = gsweep;
             PROF_LAUNCH(PROF_PRESENCE, s, k_presence, dim3(g), dim3(SCCG_BLOCK), 0, s, A, x0, nb);
-            hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)g);
+            hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)g, -1);
             SCCG_HIP(hipGetLastError());
             {
                 const RbItem it{A.fc + 4, r, (int)sizeof r};
@@ -1215,15 +1288,6 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             first_l = (int32_t)f.lmax;
         }
     }
-    const bool dbgp = getenv("SCCG_DEBUG") != nullptr;
-    auto t_last = std::chrono::steady_clock::now();
-    auto mark = [&](const char* what) {
-        if (!dbgp) return;
-        (void)hipStreamSynchronize(s);
-        const auto t = std::chrono::steady_clock::now();
-        fprintf(stderr, "[phase]   walk.%-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
-        t_last = t;
-    };
     mark("first_step");
     int32_t startX, startP;
     if (first_y != INVALID) { startX = first_y + first_l; startP = first_p + first_l - 1; }
@@ -1236,22 +1300,6 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     SCCG_HIP(hipGetLastError());
 
     if (startP != INVALID && lastk >= 0) {
-        // anchors -> speculative guesses for chunks 1..C-1
-        const int64_t slots = 1ll << A.abits;
-        // a fresh workspace is cleared once; afterwards every call's generation retires old slots
-        static thread_local const void* ws_seen = nullptr;
-        static thread_local uint32_t gen = 0;
-        if (ws != ws_seen) {
-            SCCG_HIP(hipMemsetAsync(A.atab, 0, (size_t)slots * sizeof(uint64_t), s));
-            ws_seen = ws;
-        }
-        A.agen = 0x9E3779B9u * ++gen;
-        const int64_t ns = nRp / ANCHOR_STEP + 1;
-        const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
-        PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
-        hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
-        hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
-        SCCG_HIP(hipGetLastError());
         mark("anchors");
         int32_t nlist = A.C;
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
