@@ -9,7 +9,7 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
 SRCS     := $(PKG)/csrc/scan.hip $(PKG)/csrc/ingest.hip $(PKG)/csrc/local.hip $(PKG)/csrc/walk.hip \
-            $(PKG)/csrc/decomp.hip $(PKG)/csrc/sccg_api.cpp $(PKG)/csrc/prof.cpp
+            $(PKG)/csrc/decomp.hip $(PKG)/csrc/delta.hip $(PKG)/csrc/sccg_api.cpp $(PKG)/csrc/prof.cpp
 HDRS     := $(wildcard $(PKG)/csrc/*.h) include/sccg.h
 OBJDIR   := $(PKG)/build
 OBJS     := $(patsubst $(PKG)/csrc/%,$(OBJDIR)/%.o,$(SRCS))

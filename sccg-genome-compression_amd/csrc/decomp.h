@@ -12,6 +12,9 @@ struct DcRuns {
 
 // positions of the first four '\n' of the record text (n when absent) -> d_nl[0..3]
 int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl, hipStream_t s);
+// exclusive max-scan of parenthesis positions: d_lp[i] = last '(' or ')' strictly before i
+// (negative when none)
+int dc_last_paren(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_partial, hipStream_t s);
 // parse a lowercase / N run line (decompression.cpp:126-207) into r (arrays pre-allocated with
 // capacity n/2+1); d_err bit0 set on text outside the grammar
 int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,

@@ -119,9 +119,10 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
 int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t nseg, uint32_t* recs,
                      SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s);
 // record text for local mode (delta-encoded, compression.cpp:406-415 + :222-304) + leftover
+// (abs_p: "(p," with absolute p instead, the text before delta_encode)
 int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_t* recs,
                       const SegStat* stat, uint8_t* out, int64_t* d_len, int64_t* d_tmp_a,
-                      int64_t* d_tmp_b, int64_t* d_partial, hipStream_t s);
+                      int64_t* d_tmp_b, int64_t* d_partial, hipStream_t s, bool abs_p = false);
 
 // ---- walk.hip ---------------------------------------------------------------------------------
 struct WalkWorkspace;  // defined in walk.hip
@@ -133,10 +134,19 @@ struct WalkResult {
 size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk);
 // Global pass match_sequences(R', T', 14, 100, true) (compression.cpp:561) and its record text
 // (compression.cpp:564-573 + delta_encode).  `ws` is device memory of walk_workspace_bytes.
+// (abs_p: absolute p on the record line, the text before delta_encode)
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m,
                           int chunk, void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len,
-                          WalkResult* res, hipStream_t s);
+                          WalkResult* res, hipStream_t s, bool abs_p = false);
 // the raw match list of the last global_match_and_emit (device pointers inside ws)
 int global_matches(void* ws, const int32_t** t, const int32_t** p, const int32_t** l, int64_t* n);
+
+// ---- delta.hip --------------------------------------------------------------------------------
+// delta_encode (compression.cpp:222-304) over a record line X[0, n) written with ABSOLUTE p, with
+// the reference's own token scan (needed when literal bytes hold '('; see delta.hip).  On a stoi
+// failure *stoi_fail is set and out = X (the reference keeps the un-delta'd text).
+size_t delta_workspace_bytes(int64_t n);
+int delta_encode_dev(const uint8_t* X, int64_t n, uint8_t* out, int64_t out_cap, int64_t* out_len,
+                     bool* stoi_fail, void* ws, hipStream_t s);
 
 // ---- decomp.hip: see decomp.h

@@ -447,7 +447,7 @@ __device__ __forceinline__ int32_t prev_abs_p(const SegStat* stat, const int64_t
 __global__ __launch_bounds__(SCCG_BLOCK) void k_seg_textlen(const SegStat* __restrict__ stat, int64_t iters,
                                                             const uint32_t* __restrict__ recs,
                                                             const int64_t* __restrict__ prevseg,
-                                                            int64_t* __restrict__ len) {
+                                                            int64_t* __restrict__ len, int abs_p) {
     const int64_t s = (int64_t)blockIdx.x * WPB + wave_in_block();
     if (s >= iters) return;
     const int lane = lane_id();
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_seg_textlen(const SegStat* __res
             const unsigned long long before = mm & ((1ull << lane) - 1);
             const int src = before ? 63 - __clzll((long long)before) : -1;
             const int32_t pp = __shfl(pabs, src < 0 ? 0 : src, 64);
-            const int32_t my_prev = src >= 0 ? pp : prev;
+            const int32_t my_prev = abs_p ? 0 : src >= 0 ? pp : prev;
             int64_t l = 0;
             if (i < st.nrec) {
                 if (is_m) l = 3 + ndigits_i32((int32_t)((uint32_t)pabs - (uint32_t)my_prev)) + ndigits_i32((int32_t)(rec & 0x7ff));
@@ -485,7 +485,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_seg_textwrite(const SegStat* __r
                                                               const int64_t* __restrict__ prevseg,
                                                               const int64_t* __restrict__ off,
                                                               const uint8_t* __restrict__ T,
-                                                              uint8_t* __restrict__ out) {
+                                                              uint8_t* __restrict__ out, int abs_p) {
     __shared__ int64_t roff[WPB][64];
     const int w = wave_in_block();
     const int64_t s = (int64_t)blockIdx.x * WPB + w;
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_seg_textwrite(const SegStat* __r
         const unsigned long long before = mm & ((1ull << lane) - 1);
         const int src = before ? 63 - __clzll((long long)before) : -1;
         const int32_t pp = __shfl(pabs, src < 0 ? 0 : src, 64);
-        const int32_t my_prev = src >= 0 ? pp : prev;
+        const int32_t my_prev = abs_p ? 0 : src >= 0 ? pp : prev;
         const int32_t delta = (int32_t)((uint32_t)pabs - (uint32_t)my_prev);
         int64_t l = 0;
         if (i < st.nrec) l = is_m ? 3 + ndigits_i32(delta) + ndigits_i32((int32_t)(rec & 0x7ff)) : (rec & 0x7ff);
@@ -625,7 +625,7 @@ int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT,
 
 int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_t* recs, const SegStat* stat,
                       uint8_t* out, int64_t* d_len, int64_t* d_tmp_a, int64_t* d_tmp_b, int64_t* d_partial,
-                      hipStream_t s) {
+                      hipStream_t s, bool abs_p) {
     // d_tmp_a: prev-match segment index, d_tmp_b: per-segment text length -> offsets
     const int64_t lead_len = iters * SEG_L < nT ? iters * SEG_L : nT;
     if (iters > 0) {
@@ -634,11 +634,11 @@ int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_
         int rc = dev_excl_max(d_tmp_a, d_tmp_a, iters, nullptr, d_partial, s);
         if (rc) return rc;
         hipLaunchKernelGGL(k_seg_textlen, dim3(grid_for(iters, WPB)), dim3(SCCG_BLOCK), 0, s, stat, iters, recs,
-                           (const int64_t*)d_tmp_a, d_tmp_b);
+                           (const int64_t*)d_tmp_a, d_tmp_b, (int)abs_p);
         rc = dev_excl_sum(d_tmp_b, d_tmp_b, iters, d_len, d_partial, s);
         if (rc) return rc;
         PROF_LAUNCH(PROF_LOCAL_EMIT, s, k_seg_textwrite, dim3(grid_for(iters, WPB)), dim3(SCCG_BLOCK), 0, s, stat, iters, recs,
-                           (const int64_t*)d_tmp_a, (const int64_t*)d_tmp_b, T, out);
+                           (const int64_t*)d_tmp_a, (const int64_t*)d_tmp_b, T, out, (int)abs_p);
         SCCG_HIP(hipGetLastError());
     } else {
         SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));

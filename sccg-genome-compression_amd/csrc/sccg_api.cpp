@@ -9,6 +9,8 @@
 //   local: ",\n" + segment records + leftover                   compression.cpp:368, :476-481
 //   global: N-run line, N erase, windowed walk (walk.hip)       compression.cpp:484-574
 // delta_encode (:222-304) is folded into the emitters: each "(p," is written as "(p-p_prev,".
+// When the target holds '(' bytes, literals can fool delta_encode's token scan; then the record
+// line is written with absolute p (the text before delta_encode) and delta.hip runs that scan.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -37,6 +39,8 @@ enum Slot {
     B_RUN_S, B_RUN_E, B_TMP64, B_RUN_SN, B_RUN_EN, B_TMP64N, B_NLINE, B_RECS, B_STAT, B_SEGCLS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
     // decompression
     B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC,
+    // delta_encode's own token scan (targets holding '(')
+    B_DX, B_DELTA,
     B_COUNT
 };
 
@@ -211,6 +215,14 @@ int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower,
     return d2h_i64(ctx, d_sc + 2, h_lens, 2);
 }
 
+// delta_encode's token scan over an absolute-p record line X (delta.hip)
+int paren_delta(sccg_ctx* ctx, const uint8_t* X, int64_t n, uint8_t* out, int64_t cap, int64_t* len, bool* stoi_fail) {
+    void* ws = ctx->get(B_DELTA, delta_workspace_bytes(n));
+    if (!ws) return ctx->fail(SCCG_E_NOMEM, "delta workspace of %zu bytes", delta_workspace_bytes(n));
+    TRY(delta_encode_dev(X, n, out, cap, len, stoi_fail, ws, ctx->stream));
+    return 0;
+}
+
 int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_t* tfa, int64_t tn, uint8_t* out,
                          int64_t out_cap, int64_t* out_len) {
     hipStream_t s = ctx->stream;
@@ -251,10 +263,9 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     const int64_t nT = lt[0], nR = lr[0];
     if (nT >= INT32_MAX - 8 || nR >= INT32_MAX - 8)
         return ctx->fail(SCCG_E_UNSUPPORTED, "sequence longer than the reference's int positions allow");
-    if (flags & 1)
-        return ctx->fail(SCCG_E_UNSUPPORTED,
-                         "target sequence holds '(' bytes: delta_encode's token scan would misparse them "
-                         "(compression.cpp:263-292); not supported yet");
+    // a '(' among the target bytes can reach the record line as a literal (see delta.hip)
+    const bool paren = (flags & 1) != 0;
+    bool stoi_fail = false;
     st.target_bases = nT;
     st.reference_bases = nR;
     mark("ingest");
@@ -311,9 +322,15 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         GET(int64_t, sa, B_SEG_A, iters + 1);
         GET(int64_t, sb, B_SEG_B, iters + 1);
         GET(int64_t, part, B_PARTIAL, scan_partials_needed(iters + 1) + 16);
-        TRY(launch_local_emit(T, nT, iters, recs, stat, out + pos, sc + 5, sa, sb, part, s));
+        uint8_t* X = out + pos;
+        if (paren) {
+            GET(uint8_t, xb, B_DX, out_cap - pos);
+            X = xb;
+        }
+        TRY(launch_local_emit(T, nT, iters, recs, stat, X, sc + 5, sa, sb, part, s, paren));
         int64_t rlen = 0;
         TRY(d2h_i64(ctx, sc + 5, &rlen, 1));
+        if (paren) TRY(paren_delta(ctx, X, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
         // statistics: match tokens / literal bytes of the record line
         std::vector<SegStat> hs((size_t)(iters > 0 ? iters : 0));
         if (iters > 0) {
@@ -344,7 +361,13 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
         WalkResult wr{};
         int64_t rlen = 0;
-        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, WALK_CHUNK, ws, wsb, out + pos, &rlen, &wr, s));
+        uint8_t* X = out + pos;
+        if (paren) {
+            GET(uint8_t, xb, B_DX, out_cap - pos);
+            X = xb;
+        }
+        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, WALK_CHUNK, ws, wsb, X, &rlen, &wr, s, paren));
+        if (paren) TRY(paren_delta(ctx, X, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
         st.n_matches = wr.n_matches;
         st.walk_rounds = wr.rounds;
         st.walk_chunks = wr.chunks;
@@ -355,6 +378,8 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     st.record_bytes = pos;
     ctx->stats = st;
     *out_len = pos;
+    if (stoi_fail)   // compression.cpp:279 throws: the file keeps the absolute text, main returns 1
+        return ctx->fail(SCCG_E_DELTA_STOI, "delta_encode: stoi fails on a token of the record line");
     return SCCG_OK;
 }
 
@@ -496,14 +521,14 @@ int sccg_compress(sccg_ctx* ctx, const char* ref_fa, size_t ref_len, const char*
     if (tgt_len) HIPTRY(hipMemcpyAsync(dtf, tgt_fa, tgt_len, hipMemcpyHostToDevice, ctx->stream));
     int64_t len = 0;
     int rc = compress_device_impl(ctx, drf, (int64_t)ref_len, dtf, (int64_t)tgt_len, dout, (int64_t)cap, &len);
-    if (rc) return rc;
+    if (rc && rc != SCCG_E_DELTA_STOI) return rc;   // DELTA_STOI still returns the file's text
     char* h = (char*)malloc((size_t)len + 1);
     if (!h) return ctx->fail(SCCG_E_NOMEM, "host allocation failed");
     if (len) HIPTRY(hipMemcpy(h, dout, (size_t)len, hipMemcpyDeviceToHost));
     h[len] = 0;
     out_text->data = h;
     out_text->len = (size_t)len;
-    return SCCG_OK;
+    return rc;
 }
 
 int sccg_reconstruct_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len, const void* d_rec, size_t rec_len,

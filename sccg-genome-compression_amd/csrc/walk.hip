@@ -974,16 +974,18 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_flatten(WalkPtrs A, int32_t firs
     for (int i = lane; i < n; i += 64) { A.ft[o + i] = t[i]; A.fp[o + i] = p[i]; A.fl[o + i] = l[i]; }
 }
 
-__global__ void k_match_textlen(WalkPtrs A, int64_t nm) {
+// abs_p: absolute p (the text compress_genome writes before delta_encode, compression.cpp:567)
+__global__ void k_match_textlen(WalkPtrs A, int64_t nm, int abs_p) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t pend = i ? A.ft[i - 1] + A.fl[i - 1] : 0;
-        const int32_t pprev = i ? A.fp[i - 1] : 0;
+        const int32_t pprev = i && !abs_p ? A.fp[i - 1] : 0;
         const int32_t d = (int32_t)((uint32_t)A.fp[i] - (uint32_t)pprev);
         A.tlen[i] = (int64_t)(A.ft[i] - pend) + 3 + ndigits_i32(d) + ndigits_i32(A.fl[i]);
     }
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int64_t nm, uint8_t* __restrict__ out) {
+__global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int64_t nm, uint8_t* __restrict__ out,
+                                                                int abs_p) {
     const int64_t i = (int64_t)blockIdx.x * WPB + wave_in_block();
     if (i >= nm) return;
     const int lane = lane_id();
@@ -993,7 +995,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int6
     for (int32_t q = lane; q < t - pend; q += 64) o[q] = A.T[pend + q];
     if (lane == 0) {
         uint8_t* d = o + (t - pend);
-        const int32_t pprev = i ? A.fp[i - 1] : 0;
+        const int32_t pprev = i && !abs_p ? A.fp[i - 1] : 0;
         *d++ = '(';
         d += write_i32(d, (int32_t)((uint32_t)A.fp[i] - (uint32_t)pprev));
         *d++ = ',';
@@ -1188,7 +1190,8 @@ int global_matches(void* /*ws*/, const int32_t** t, const int32_t** p, const int
     } while (0)
 
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
-                          void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s) {
+                          void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
+                          bool abs_p) {
     if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
     size_t used = 0;
     WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, &used);
@@ -1466,9 +1469,9 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     int32_t tail_from = 0;
     if (nm > 0) {
         const unsigned g = grid_for(nm, 256) > 4096 ? 4096 : grid_for(nm, 256);
-        hipLaunchKernelGGL(k_match_textlen, dim3(g), dim3(256), 0, s, A, nm);
+        hipLaunchKernelGGL(k_match_textlen, dim3(g), dim3(256), 0, s, A, nm, (int)abs_p);
         RC(dev_excl_sum(A.tlen, A.tlen, nm, A.scal64 + 1, A.partial, s));
-        PROF_LAUNCH(PROF_MATCH_EMIT, s, k_match_textwrite, dim3(grid_for(nm, WPB)), dim3(SCCG_BLOCK), 0, s, A, nm, out);
+        PROF_LAUNCH(PROF_MATCH_EMIT, s, k_match_textwrite, dim3(grid_for(nm, WPB)), dim3(SCCG_BLOCK), 0, s, A, nm, out, (int)abs_p);
         SCCG_HIP(hipGetLastError());
         int32_t lt[2];
         const RbItem it[3] = {{A.scal64 + 1, &text, (int)sizeof text}, {A.ft + nm - 1, &lt[0], 4}, {A.fl + nm - 1, &lt[1], 4}};

@@ -178,3 +178,41 @@ def quirk_cases() -> dict[str, tuple[bytes, bytes]]:
     cases["e_polyA_repeats"] = (to_fasta(("A" * 60 + rand_seq(rng, 40)) * 40),
                                 to_fasta(mutate(rng, ("A" * 60 + rand_seq(rng, 40)) * 45), ">t"))
     return cases
+
+
+# literal pieces every '(' of which converts under stoi (the record stays parseable) ...
+SAFE_PIECES = [")", ",", "(12,", "(-5,", "(+7,", "(0000000000007,", "(2147483647,", "(-2147483648,",
+               "(ACGT)", "()", "(1)", ",3)", "9", "-", "))", "(0,"]
+# ... and ones that make it throw (out of int range, nothing to convert)
+BAD_PIECES = ["(", "(99999999999,", "(2147483648,", "(,", "(A5,", "(("]
+
+
+def paren_case(seed: int) -> tuple[bytes, bytes]:
+    """Targets holding '(' ')' ',' digits and signs among the bases: literal bytes that
+    delta_encode's own token scan (compression.cpp:262-293) pairs with the real "(p,l)" tokens.
+    Local and global shapes; some make its stoi throw (the reference then exits 1)."""
+    rng = random.Random(50_000 + seed)
+    if seed % 2:
+        rfa, tfa = global_case(seed)
+    else:
+        rfa, tfa = local_case(seed % 24 if seed % 4 else 6)
+    lines = tfa.split(b"\n")
+    out = []
+    rate = rng.choice([0.002, 0.01, 0.05])
+    pieces = [["(", ")", ","], SAFE_PIECES, SAFE_PIECES * 20 + BAD_PIECES][seed % 3]
+    for ln in lines:
+        if ln.startswith(b">") or not ln:
+            out.append(ln)
+            continue
+        b = bytearray()
+        for c in ln:
+            if rng.random() < rate:
+                b += rng.choice(pieces).encode()
+            b.append(c)
+        out.append(bytes(b))
+    tfa = b"\n".join(out)
+    if seed % 5 == 0:
+        tfa += b"(" if tfa.endswith(b"\n") else b"\n("   # an opener without a closer at the end
+    if seed % 7 == 0:
+        tfa = tfa.replace(b"\n", b"(5,\n", 3)              # pieces at line ends / header
+    return rfa, tfa

@@ -2,7 +2,7 @@
 """Regenerate the golden fixtures from the REAL reference (oracle/_ref, built from
 /root/reference by `make -C oracle ref`).  Run in the build container only:
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--force]     (--force: rewrite existing fixtures too)
 
 Writes
   tests/golden/cases/<name>.json.gz   inputs + the reference's outputs and exit codes
@@ -34,6 +34,7 @@ STUB = os.path.join(REPO, "oracle", "stub7z")
 
 N_LOCAL = 24
 N_GLOBAL = 12
+N_PAREN = 16   # targets whose literals hold '(' ')' ',' (delta_encode's own token scan)
 SYNTH_SEEDS = [  # (profile, ref_len, tgt_len, seed)
     ("hg", 300_000, 301_000, 1),
     ("hg", 2_000_000, 2_003_000, 2),
@@ -78,10 +79,15 @@ def main() -> None:
         cases[f"local_{i:02d}"] = fuzzgen.local_case(i)
     for i in range(N_GLOBAL):
         cases[f"global_{i:02d}"] = fuzzgen.global_case(i)
+    for i in range(N_PAREN):
+        cases[f"paren_{i:02d}"] = fuzzgen.paren_case(i)
     cases.update(fuzzgen.quirk_cases())
     outdir = os.path.join(HERE, "cases")
     os.makedirs(outdir, exist_ok=True)
+    force = "--force" in sys.argv
     for name, (rfa, tfa) in sorted(cases.items()):
+        if not force and os.path.exists(os.path.join(outdir, name + ".json.gz")):
+            continue   # fixtures are deterministic; keep the committed files byte-stable
         res = run_reference(rfa, tfa)
         doc = {"name": name, "ref_fa": b64(rfa), "tgt_fa": b64(tfa),
                "compress_rc": res["compress_rc"], "record": b64(res["record"]),

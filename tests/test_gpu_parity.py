@@ -202,3 +202,41 @@ def test_switch_window_vs_oracle(ctx, seed):
     assert bool(st["mode_global"]) == mode_global
     assert st["switch_segment"] == (sw if mode_global else -1)
     assert got == want
+
+
+@pytest.mark.parametrize("seed", range(16, 64))
+def test_paren_vs_oracle(ctx, seed):
+    """Targets whose literals hold '(' ')' ',' digits: delta_encode's own token scan
+    (compression.cpp:262-293, delta.hip), including its stoi failures (rc 1, absolute text)."""
+    rfa, tfa = fuzzgen.paren_case(seed)
+    try:
+        want, wrc = oraclelib.compress(rfa, tfa), 0
+    except oraclelib.OracleError as e:
+        want, wrc = e.partial, 1
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert (rc, got) == (wrc, want)
+    if rc == 0:
+        assert _gpu_reconstruct(ctx, got, rfa) == _oracle_reconstruct(want, rfa)
+
+
+@pytest.mark.parametrize("pieces", ["safe", "mixed"])
+def test_paren_large_vs_oracle(ctx, pieces):
+    """Multi-tile scans of the paren path: a 3 Mb global-mode pair with punctuation literals."""
+    import numpy as np
+    rfa, tfa = synthlib.synth_pair("hg", 3_000_000, 3_010_000, 91)
+    rng = np.random.default_rng(5 if pieces == "safe" else 6)
+    pool = fuzzgen.SAFE_PIECES if pieces == "safe" else fuzzgen.SAFE_PIECES * 200 + fuzzgen.BAD_PIECES
+    lines = tfa.split(b"\n")
+    for j in rng.integers(1, len(lines) - 1, 3000):
+        ln = lines[j]
+        if ln and not ln.startswith(b">"):
+            c = int(rng.integers(0, len(ln)))
+            lines[j] = ln[:c] + pool[int(rng.integers(0, len(pool)))].encode() + ln[c:]
+    tfa = b"\n".join(lines)
+    try:
+        want, wrc = oraclelib.compress(rfa, tfa), 0
+    except oraclelib.OracleError as e:
+        want, wrc = e.partial, 1
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert rc == wrc
+    assert got == want
