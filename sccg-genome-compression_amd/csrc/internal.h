@@ -134,6 +134,12 @@ struct WalkResult {
 size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk);
 // Global pass match_sequences(R', T', 14, 100, true) (compression.cpp:561) and its record text
 // (compression.cpp:564-573 + delta_encode).  `ws` is device memory of walk_workspace_bytes.
+// Queues the walk's input-only work (first-step key sweep, anchor index, chunk guesses) on s with
+// no host sync; a later global_match_and_emit with the same ws and inputs skips it (the caller
+// orders its stream after s).
+int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
+                   size_t ws_bytes, hipStream_t s);
+void global_prepare_reset();   // forget a preparation that will not be used
 // (abs_p: absolute p on the record line, the text before delta_encode)
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m,
                           int chunk, void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len,

@@ -44,7 +44,16 @@ enum Slot {
     B_COUNT
 };
 
-constexpr int WALK_CHUNK = 16384;
+constexpr int WALK_CHUNK_DEFAULT = 16384;
+// target bases per speculative walk chunk (SCCG_WALK_CHUNK overrides it for tuning runs)
+int walk_chunk() {
+    static const int v = [] {
+        const char* e = getenv("SCCG_WALK_CHUNK");
+        const int c = e ? atoi(e) : 0;
+        return c >= 1024 && c <= (1 << 20) ? c : WALK_CHUNK_DEFAULT;
+    }();
+    return v;
+}
 constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide compares, tails)
 
 }  // namespace
@@ -52,6 +61,8 @@ constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide com
 struct sccg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;       // second stream: work that overlaps the local pass
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     sccg_stats stats{};
     void* buf[B_COUNT] = {};
@@ -113,7 +124,10 @@ int sccg_ctx_create(int device, sccg_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return SCCG_E_HIP;
     sccg_ctx* c = new sccg_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SCCG_E_HIP;
     }
@@ -125,8 +139,12 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(ctx->side);
     for (int i = 0; i < B_COUNT; i++)
         if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
+    (void)hipEventDestroy(ctx->ev_fork);
+    (void)hipEventDestroy(ctx->ev_join);
+    (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -161,9 +179,9 @@ size_t sccg_compress_bound(size_t ref_len, size_t tgt_len) {
 
 namespace {
 
-int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n) {
+int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n, hipStream_t s = nullptr) {
     const RbItem it{d, h, n * (int)sizeof(int64_t)};
-    TRY(dev_readback(&it, 1, ctx->stream));
+    TRY(dev_readback(&it, 1, s ? s : ctx->stream));
     return 0;
 }
 
@@ -193,8 +211,7 @@ int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const in
 // syncs: run extraction for both predicates, one read of both run counts, run text for both, one
 // read of both text lengths.  The lowercase line goes to out_lower, the N line to out_n.
 int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower, uint8_t** out_n, int64_t* d_sc,
-              int64_t* h_lens) {
-    hipStream_t s = ctx->stream;
+              int64_t* h_lens, hipStream_t s) {
     const int64_t maxruns = n / 2 + 2;
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE + 1;
     const int64_t ntmp = maxruns > ntiles ? maxruns : ntiles;
@@ -207,12 +224,12 @@ int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower,
     GET(int64_t, part, B_PARTIAL, scan_partials_needed(ntmp) + 16);
     TRY(launch_runs2(s_in, n, rs_l, re_l, rs_n, re_n, d_sc, tmp_l, tmp_n, part, s));
     int64_t nruns[2];
-    TRY(d2h_i64(ctx, d_sc, nruns, 2));
+    TRY(d2h_i64(ctx, d_sc, nruns, 2, s));
     TRY(launch_run_text(rs_l, re_l, nruns[0], n, out_lower, d_sc + 2, tmp_l, part, s));
     GET(uint8_t, nline, B_NLINE, 24 * nruns[1] + 16);   // <= 23 text bytes per run
     *out_n = nline;
     TRY(launch_run_text(rs_n, re_n, nruns[1], n, nline, d_sc + 3, tmp_n, part, s));
-    return d2h_i64(ctx, d_sc + 2, h_lens, 2);
+    return d2h_i64(ctx, d_sc + 2, h_lens, 2, s);
 }
 
 // delta_encode's token scan over an absolute-p record line X (delta.hip)
@@ -273,23 +290,14 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     const int64_t hlen = has_hdr ? hdr[1] - hdr[0] : 0;
     if (out_cap < hlen + 1 + 11 * nT + 64) return ctx->fail(SCCG_E_INVALID, "output capacity too small");
 
-    // ---- header + lowercase line (compression.cpp:337-368)
-    int64_t pos = 0;
-    if (has_hdr) {
-        HIPTRY(hipMemcpyAsync(out, tfa + hdr[0], (size_t)hlen, hipMemcpyDeviceToDevice, s));
-        TRY(dev_put_bytes(out + hlen, "\n", 1, s));
-        pos = hlen + 1;
-    }
-    // both run lines now (the N line is kept aside until the mode is known)
-    uint8_t* nline = nullptr;
-    int64_t rl_len[2];
-    TRY(run_lines(ctx, T, nT, out + pos, &nline, sc + 10, rl_len));
-    const int64_t llen = rl_len[0];
-    pos += llen;
-    const int64_t lower_end = pos;
-    mark("lower_line");
+    // ---- fork.  The local pass (compression.cpp:372-474, main stream) is latency-bound; the
+    //      header + run lines and the global walk's input-only preparation (first-step sweep,
+    //      anchor index) only read T/R/T'/R', so they run beside it on the side stream.
+    hipStream_t s2 = ctx->side;
+    HIPTRY(hipEventRecord(ctx->ev_fork, s));
+    HIPTRY(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
 
-    // ---- local segments (compression.cpp:372-474)
+    // ---- local segments (main stream; the switch point is read after the side work is queued)
     const int64_t nRs = (nR + SEG_L - 1) / SEG_L, nTs = (nT + SEG_L - 1) / SEG_L;
     const int64_t iters = nRs < nTs ? nRs : nTs;
     int64_t sw = -1;
@@ -309,13 +317,42 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
         TRY(dev_set_i64(sc + 20, 2, {(int64_t)INT32_MAX << 32, (int64_t)INT32_MAX}, s));
         TRY(launch_local_all(R, nR, T, nT, iters, recs, stat, cls, gen, ctl, s));
+    }
+
+    // ---- header + lowercase line (compression.cpp:337-368), side stream
+    int64_t pos = 0;
+    if (has_hdr) {
+        HIPTRY(hipMemcpyAsync(out, tfa + hdr[0], (size_t)hlen, hipMemcpyDeviceToDevice, s2));
+        TRY(dev_put_bytes(out + hlen, "\n", 1, s2));
+        pos = hlen + 1;
+    }
+    // both run lines now (the N line is kept aside until the mode is known)
+    uint8_t* nline = nullptr;
+    int64_t rl_len[2];
+    TRY(run_lines(ctx, T, nT, out + pos, &nline, sc + 10, rl_len, s2));
+    const int64_t llen = rl_len[0];
+    pos += llen;
+    const int64_t lower_end = pos;
+
+    // ---- the global walk's preparation, side stream (wasted only if the pass stays local)
+    const int64_t np[2] = {lt[1], lr[1]};
+    const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, walk_chunk());
+    void* ws = ctx->get(B_WALK, wsb);
+    if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
+    TRY(global_prepare(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(), ws, wsb, s2));
+    HIPTRY(hipEventRecord(ctx->ev_join, s2));
+
+    // ---- join: the switch point, then everything after it runs behind the side work
+    if (iters > 0) {
         int64_t h_sw = 0;
         TRY(d2h_i64(ctx, sc + 21, &h_sw, 1));   // ctl[2] | ctl[3] << 32
         sw = h_sw >= INT32_MAX ? -1 : h_sw;
     }
+    HIPTRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
     st.switch_segment = sw;
     mark("local");
     if (sw < 0) {
+        global_prepare_reset();
         // ---- local: "\n,\n" + records + leftover segments
         TRY(dev_put_bytes(out + pos, "\n,\n", 3, s));
         pos += 3;
@@ -355,10 +392,6 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         TRY(dev_put_bytes(out + pos, "\n", 1, s));
         pos += 1;
         mark("n_line");
-        const int64_t np[2] = {lt[1], lr[1]};
-        const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, WALK_CHUNK);
-        void* ws = ctx->get(B_WALK, wsb);
-        if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
         WalkResult wr{};
         int64_t rlen = 0;
         uint8_t* X = out + pos;
@@ -366,7 +399,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
             GET(uint8_t, xb, B_DX, out_cap - pos);
             X = xb;
         }
-        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, WALK_CHUNK, ws, wsb, X, &rlen, &wr, s, paren));
+        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(), ws, wsb, X, &rlen, &wr, s, paren));
         if (paren) TRY(paren_delta(ctx, X, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
         st.n_matches = wr.n_matches;
         st.walk_rounds = wr.rounds;
@@ -612,17 +645,18 @@ int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, s
     } else {
         if (m < 0 || 2 * m + 1 > 256 || k < 1 || k > 15 || nr >= (size_t)INT32_MAX - 8 || nt >= (size_t)INT32_MAX - 8)
             return ctx->fail(SCCG_E_UNSUPPORTED, "global sccg_match takes 0 <= m <= 127, 1 <= k <= 15");
+        global_prepare_reset();   // buffers shared with compress: never reuse its preparation
         GET(uint8_t, R, B_RP, nr + 64);
         GET(uint8_t, T, B_TP, nt + 64);
         if (nr) HIPTRY(hipMemcpyAsync(R, sr, nr, hipMemcpyHostToDevice, s));
         if (nt) HIPTRY(hipMemcpyAsync(T, st, nt, hipMemcpyHostToDevice, s));
-        const size_t wsb = walk_workspace_bytes((int64_t)nr, (int64_t)nt, k, WALK_CHUNK);
+        const size_t wsb = walk_workspace_bytes((int64_t)nr, (int64_t)nt, k, walk_chunk());
         void* ws = ctx->get(B_WALK, wsb);
         GET(uint8_t, txt, B_OUT, 4 * nt + 64);
         if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace");
         WalkResult wr{};
         int64_t tl = 0;
-        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, k, m, WALK_CHUNK, ws, wsb, txt, &tl, &wr, s));
+        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, k, m, walk_chunk(), ws, wsb, txt, &tl, &wr, s));
         const int32_t *dt, *dp, *dl;
         int64_t nm;
         global_matches(ws, &dt, &dp, &dl, &nm);

@@ -40,7 +40,16 @@ constexpr int FROZEN_MAX = 256;        // frozen chunks handled per batch (grid.
 constexpr int FROZEN_FIRST = 16;       // the batch launched blind, before the round's sync
 
 enum ChunkKind : int32_t { KIND_SPEC = 0, KIND_FIX = 1, KIND_RESUME = 2 };
-enum ChunkStatus : int32_t { ST_OK = 0, ST_ESC = 1 };
+enum ChunkStatus : int32_t { ST_OK = 0, ST_ESC = 1, ST_CONV = 3, ST_DONE = 4, ST_TRUNC = 5 };
+// A fix-up whose predecessor is re-walked in the same round starts from a stale entry: its result
+// counts only if it converges, so it gives up after this many target positions without converging
+// (a stale entry is often garbage, whose walk is a chunk-long stuck literal scan).
+constexpr int32_t STALE_BUDGET_DEFAULT = 0;   // 0: off (SCCG_STALE_BUDGET sets it for tuning runs)
+// A speculative walk that has gone RESEED_GAP target positions without a match re-seeds P from a
+// fresh anchor vote at its position: a bad start guess otherwise leaves it stuck in a chunk-long
+// literal scan.  The trajectory is then a walk from a different state after the re-seed, so a
+// later fix-up may converge only onto its matches from the re-seed on (seedq).
+constexpr int32_t RESEED_GAP = 1024;
 
 struct WalkPtrs {
     const uint8_t* R;
@@ -71,6 +80,9 @@ struct WalkPtrs {
     int32_t* conv;
     int32_t* changed;
     int32_t* walked;      // round in which the chunk was last re-walked
+    int32_t* lround;      // round for which the chunk was last put on the walk list
+    int32_t* seedq;       // first match of the committed trajectory after its last re-seed
+    int32_t stale_budget; // positions a stale-entry fix-up may walk without converging (0: no limit)
     int32_t* frozen;      // fix-up ended in a long literal run at the chunk end
     int32_t* flist;       // committed frozen chunks of the round
     int32_t* fy;          // per listed frozen chunk: first window hit after its exit (k_frozen_scan)
@@ -141,26 +153,27 @@ __device__ __forceinline__ void load16u(const uint8_t* p, uint32_t (&o)[4]) {
     for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
 }
 
-// longest common extension of R[a..] and T[b..], at most maxlen bytes; whole wave, 1 KiB / step
+// longest common extension of R[a..] and T[b..], at most maxlen bytes; whole wave, 2 KiB / step
+// (32 bytes per lane: most matches end inside the first step, one dependent round trip)
 __device__ int32_t wave_lce(const uint8_t* __restrict__ R, int32_t a, const uint8_t* __restrict__ T, int32_t b,
                             int32_t maxlen) {
     const int lane = lane_id();
-    for (int32_t off = 0; off < maxlen; off += 1024) {
-        const int32_t my = off + 16 * lane;
+    for (int32_t off = 0; off < maxlen; off += 2048) {
+        const int32_t my = off + 32 * lane;
         int32_t valid = maxlen - my;
         int32_t e = INT32_MAX;
         if (valid > 0) {
-            uint32_t r[4], t[4];
-            load16u(R + a + my, r);
-            load16u(T + b + my, t);
-            int pos = 16;
+            uint32_t r[8], t[8];
+            loadw<8>(R + a + my, r);
+            loadw<8>(T + b + my, t);
+            int pos = 32;
 #pragma unroll
-            for (int i = 3; i >= 0; i--) {
+            for (int i = 7; i >= 0; i--) {
                 const uint32_t x = r[i] ^ t[i];
                 if (x) pos = 4 * i + (__builtin_ctz(x) >> 3);
             }
-            if (valid < 16 && pos > valid) pos = valid;
-            if (pos < 16) e = my + pos;
+            if (valid < 32 && pos > valid) pos = valid;
+            if (pos < 32) e = my + pos;
         }
         // lanes cover increasing offsets: the first lane that stops holds the extension
         const unsigned long long sm = __ballot(e != INT32_MAX);
@@ -207,6 +220,14 @@ __device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin&
     }
 }
 
+// key of the target k-mer at y from its 16 bytes w (loaded by the caller; k <= 15)
+__device__ __forceinline__ uint32_t target_key_w(const WalkPtrs& A, int32_t y, const uint32_t (&w)[4]) {
+    const int k = A.k;
+    uint64_t code;
+    uint32_t bad;
+    pack_codes<4>(w, code, bad);
+    return bad & ((1u << k) - 1u) ? exotic_key(A.T + y, k) : (uint32_t)code & ((1u << (2 * k)) - 1u);
+}
 // key of the target k-mer at y (one unaligned 16-byte load; k <= 15)
 __device__ __forceinline__ uint32_t target_key(const WalkPtrs& A, int32_t y) {
     const int k = A.k;
@@ -307,6 +328,8 @@ __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L
 // ---------------------------------------------------------------------------------------------
 // the chunk walk (one wave per chunk)
 // ---------------------------------------------------------------------------------------------
+__device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0);   // anchors, below
+
 constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail
 template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
@@ -346,7 +369,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
     if (lane == 0) A.status[j] = ST_OK;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.scal[5] = 0;   // frozen list of this round's commit
     const uint64_t dbg_t0 = DBG ? wall_clock64() : 0;
-    uint64_t dbg_c[10] = {};   // matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail
+    uint64_t dbg_c[13] = {};   // matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail,
+                               // t_hash, t_wide, wide positions
     uint64_t tq = dbg_t0;
     auto tick = [&](int slot) {
         if (DBG) { const uint64_t t = wall_clock64(); dbg_c[slot] += t - tq; tq = t; }
@@ -368,16 +392,26 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
     int32_t lme = x;   // target index after the last match of this walk (start of the open literal run)
     bool converged = false, escalated = false;
     const int32_t scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
+    // stale entry (predecessor re-walked in this round): converge within the budget or give up
+    const bool stale = A.stale_budget > 0 && kind == KIND_FIX && j > 0 && A.lround[j - 1] == A.round;
+    const int32_t budget_end = stale && x + A.stale_budget < scan_end ? x + A.stale_budget : scan_end;
+    const int32_t old_seedq = cb >= 0 ? uni(A.seedq[j]) : 0;
+    int32_t seed_x = x, seedq = 0;
+    bool truncated = false;
     while (x < scan_end) {
+        if (x >= budget_end) { truncated = true; break; }
         if (DBG) tick(9);
+        // the target probe's bytes are loaded before the window's, so both round trips overlap
+        const int32_t y_l = x + lane;
+        const bool valid = y_l < scan_end;
+        uint32_t tw[4];
+        loadw<4>(A.T + y_l, tw);   // 4 KiB readable slack after T: no bound needed for the load
         if (W.P != P) { reg_window(A, P, W); if (DBG) dbg_c[3]++; }
         if (DBG) tick(6);
         if (W.n <= 0) { x = scan_end; break; }
         if (DBG) dbg_c[1]++;
         // ---- literal steps: first y in [x, scan_end) whose k-mer has a candidate in the window
-        const int32_t y_l = x + lane;
-        const bool valid = y_l < scan_end;
-        const uint32_t key_l = valid ? target_key(A, y_l) : 0u;
+        const uint32_t key_l = valid ? target_key_w(A, y_l, tw) : 0u;
         int hl = -1;
         const int nb = scan_end - x < 64 ? scan_end - x : 64;
         for (int yy = 0; yy < nb; yy++) {
@@ -387,9 +421,26 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
         if (hl < 0) {
             x = (x + 64 < scan_end) ? x + 64 : scan_end;
             if (x < scan_end) {
+                int32_t wend = budget_end;
+                if (kind == KIND_SPEC) {   // re-seed a stuck speculative walk (see RESEED_GAP)
+                    if (x - (lme > seed_x ? lme : seed_x) >= RESEED_GAP) {
+                        seed_x = x;
+                        const int32_t d = anchor_diag(A, x);
+                        if (d != INVALID) {
+                            int64_t np = (int64_t)x - 1 + d;
+                            np = np < 0 ? 0 : (np > A.nR - 1 ? A.nR - 1 : np);
+                            if ((int32_t)np != P) { P = (int32_t)np; seedq = n; continue; }
+                        }
+                    }
+                    const int32_t cpt = (lme > seed_x ? lme : seed_x) + RESEED_GAP;
+                    if (cpt < wend) wend = cpt;
+                }
+                if (DBG) tick(9);
                 if (hashP != P) { hash_window(W, L); hashP = P; }
-                x = wide_scan(A, L, x, scan_end);
-                if (DBG) dbg_c[2]++;
+                if (DBG) tick(10);
+                const int32_t x0 = x;
+                x = wide_scan(A, L, x, wend);
+                if (DBG) { dbg_c[2]++; dbg_c[12] += x - x0; tick(11); }
             }
             continue;
         }
@@ -450,7 +501,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
                 if (gm) { q += first_lane(gm); break; }
                 q += 64;
             }
-            if (q < cc && ct[q] == y && cp[q] == p && cl[q] == bl) {
+            if (q < cc && q >= old_seedq && ct[q] == y && cp[q] == p && cl[q] == bl) {
                 const int32_t rest = cc - q - 1;
                 for (int i = lane; i < rest; i += 64) {
                     ot[n + i] = ct[q + 1 + i];
@@ -467,16 +518,26 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
         x = y + bl;       // compression.cpp:159
     }
     if (escalated) return;
-    if (DBG && lane == 0 && A.round == 1) {
+    if (DBG && lane == 0) {
         tick(9);
         uint64_t* d = A.dbg + (size_t)j * DBG_SLOTS;
         d[0] = wall_clock64() - dbg_t0;
-        for (int i = 0; i < 10; i++) d[1 + i] = dbg_c[i];
+        for (int i = 0; i < 13; i++) d[1 + i] = dbg_c[i];
+        d[14] = (uint64_t)A.round;
+    }
+    if (lane == 0 && truncated) {   // nothing to commit; the chunk stays pending
+        A.conv[j] = 0;
+        A.changed[j] = 0;
+        A.walked[j] = A.round;
+        A.frozen[j] = 0;
+        A.status[j] = ST_TRUNC;
+        return;
     }
     if (lane == 0) {
         A.cnt[ob][j] = n;
         if (cb < 0) {   // speculative: the trajectory is the chunk's first, take it as is
             A.exitX[j] = x; A.exitP[j] = P;
+            A.seedq[j] = seedq;
         } else {        // fix-up: staged; k_commit decides
             const int32_t nx = converged ? A.exitX[j] : x, np = converged ? A.exitP[j] : P;
             A.newX[j] = nx; A.newP[j] = np;
@@ -486,7 +547,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
             // ended in a long literal run with P frozen at the chunk end: k_frozen_scan territory
             A.frozen[j] = !converged && x == hi_j && x - lme >= FROZEN_MIN;
         }
-        A.status[j] = converged ? 3 : 4;   // diagnostics only (SCCG_DEBUG)
+        A.status[j] = converged ? ST_CONV : ST_DONE;
     }
 }
 
@@ -500,7 +561,7 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
     if (blockIdx.x == 0 && threadIdx.x < FROZEN_MAX) A.fy[threadIdx.x] = INT32_MAX;   // for k_frozen_scan
     for (int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); i < nlist; i += (int32_t)(gridDim.x * blockDim.x)) {
         const int32_t j = list[i];
-        if (A.kind[j] == KIND_SPEC || A.status[j] == ST_ESC) continue;
+        if (A.kind[j] == KIND_SPEC || A.status[j] == ST_ESC || A.status[j] == ST_TRUNC) continue;
         const int32_t round = A.round;
         const bool pred_changed = j > 0 && A.walked[j - 1] == round && A.changed[j - 1];
         if (!(A.conv[j] || !pred_changed)) continue;
@@ -509,6 +570,7 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
         A.exitP[j] = A.newP[j];
         A.usedX[j] = A.snapX[j];
         A.usedP[j] = A.snapP[j];
+        A.seedq[j] = 0;   // a fix-up (with a converged suffix) is a walk from its entry
         if (A.frozen[j]) A.flist[atomicAdd(&A.scal[5], 1)] = j;
     }
 }
@@ -581,6 +643,7 @@ __device__ void frozen_apply_wave(const WalkPtrs& A, int fbase, int fcap, int32_
                     A.exitX[q] = ex;
                     A.exitP[q] = P;
                     A.changed[q] = 0;
+                    A.seedq[q] = 0;
                 }
             }
             const unsigned long long fm = __ballot(fill);   // chunks are ordered: a prefix fills
@@ -607,6 +670,8 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
         A.exitP[j] = INVALID;
         A.kind[j] = j ? KIND_SPEC : KIND_FIX;
         A.plist[j] = j;
+        A.lround[j] = 1;
+        A.seedq[j] = 0;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.scal[0] = 0; A.scal[1] = 0; A.scal[2] = startX; A.scal[3] = startP;
@@ -630,6 +695,7 @@ __global__ __launch_bounds__(1024) void k_round_tail(WalkPtrs A, int fbase, int 
         A.snapX[j] = ex;
         A.snapP[j] = ep;
         A.kind[j] = KIND_FIX;
+        A.lround[j] = A.round + 1;
         A.plist[atomicAdd(&A.scal[0], 1)] = j;
     }
 }
@@ -685,16 +751,16 @@ __global__ void k_anchor_build(WalkPtrs A) {
     }
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
-    const int32_t j = (int32_t)blockIdx.x * WPB + wave_in_block();
-    if (j >= A.C) return;
+// Whole wave: probe the 256 target positions from y0; each hit on a sampled reference 32-mer
+// votes for its diagonal (reference - target position).  The diagonal with the most votes (>= 2;
+// a lone hit is often a repeat copy), ties to the earliest; else the earliest; INVALID if none.
+__device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0) {
     const int lane = lane_id();
-    // probe 256 target positions; each hit on a sampled reference 32-mer votes for a diagonal
     constexpr int NB = 4;
     int32_t dg[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        const int32_t y = j * A.S + b * 64 + lane;
+        const int32_t y = y0 + b * 64 + lane;
         dg[b] = INVALID;
         uint64_t code;
         if (y + ANCHOR_K <= A.nT && code32<false>(A.T + y, code)) {
@@ -703,8 +769,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
             if ((uint32_t)(v >> 32) == anchor_tag(key, A.agen) && (uint32_t)v != A_MULTI) dg[b] = (int32_t)(uint32_t)v - y;
         }
     }
-    // the diagonal with the most votes (>= 2; a lone hit is often a repeat copy), ties to the
-    // earliest; else the earliest
     int32_t g = INVALID, first = INVALID;
     int gv = 1;
     for (int tries = 0; tries < 8; tries++) {
@@ -724,14 +788,20 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
         }
         if (votes > gv) { g = d; gv = votes; }
     }
-    if (g == INVALID) g = first;
+    return g == INVALID ? first : g;
+}
+
+__global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
+    const int32_t j = (int32_t)blockIdx.x * WPB + wave_in_block();
+    if (j >= A.C) return;
+    int32_t g = anchor_diag(A, j * A.S);
     if (g != INVALID) {
         int64_t gp = (int64_t)j * A.S - 1 + g;
         if (gp < 0) gp = 0;
         if (gp > A.nR - 1) gp = A.nR - 1;
         g = (int32_t)gp;
     }
-    if (lane == 0) A.guess[j] = g;
+    if (lane_id() == 0) A.guess[j] = g;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1058,6 +1128,8 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.rlist = c.take<int32_t>(C);
     A.newX = c.take<int32_t>(C); A.newP = c.take<int32_t>(C);
     A.conv = c.take<int32_t>(C); A.changed = c.take<int32_t>(C); A.walked = c.take<int32_t>(C);
+    A.lround = c.take<int32_t>(C);
+    A.seedq = c.take<int32_t>(C);
     A.frozen = c.take<int32_t>(C); A.flist = c.take<int32_t>(C);
     A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);
@@ -1189,14 +1261,85 @@ int global_matches(void* /*ws*/, const int32_t** t, const int32_t** p, const int
         if (rc_) return rc_;          \
     } while (0)
 
+namespace {
+
+// The walk's input-only work -- the first step's key sweep (x0 = 0) and the anchor index with
+// every chunk's guess -- depends on R' and T' alone.  global_prepare queues it (no host sync), so
+// a caller can run it on a second stream while the local pass decides whether the walk is needed
+// at all; global_match_and_emit on the same workspace and inputs then skips it.
+struct Prepared {
+    const void* ws = nullptr;
+    const uint8_t* R = nullptr;
+    const uint8_t* T = nullptr;
+    int64_t nR = -1, nT = -1;
+    int k = 0, m = 0, chunk = 0;
+    uint32_t agen = 0;
+};
+thread_local Prepared g_prep;
+
+int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
+    const int32_t lastk = A.nT - A.k;
+    const bool walkable = A.nR >= A.k && lastk >= 0;
+    if (!walkable) return 0;
+    const unsigned gsweep = grid_for(A.nR - A.k + 1, 256 * FC_PER_T) > PRESENCE_GRID
+                                ? PRESENCE_GRID : grid_for(A.nR - A.k + 1, 256 * FC_PER_T);
+    // the usual first step first: x0 = 0's own k-mer (statistics land in fc[4..11])
+    hipLaunchKernelGGL(k_key0, dim3(gsweep), dim3(SCCG_BLOCK), 0, s, A, 0);
+    hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)gsweep, 0);
+    SCCG_HIP(hipGetLastError());
+    const int64_t slots = 1ll << A.abits;
+    // a fresh workspace is cleared once; afterwards every call's generation retires old slots
+    static thread_local const void* ws_seen = nullptr;
+    static thread_local uint32_t gen = 0;
+    if (ws != ws_seen) {
+        SCCG_HIP(hipMemsetAsync(A.atab, 0, (size_t)slots * sizeof(uint64_t), s));
+        ws_seen = ws;
+    }
+    A.agen = 0x9E3779B9u * ++gen;
+    const int64_t ns = (int64_t)A.nR / ANCHOR_STEP + 1;
+    const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
+    PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
+                   size_t ws_bytes, size_t* used) {
+    WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, used);
+    if (!getenv("SCCG_DEBUG")) A.dbg = nullptr;   // per-chunk counters only in diagnostic runs
+    static const int32_t sb = [] {
+        const char* e = getenv("SCCG_STALE_BUDGET");
+        return e ? atoi(e) : STALE_BUDGET_DEFAULT;
+    }();
+    A.stale_budget = sb;
+    return A;
+}
+
+}  // namespace
+
+void global_prepare_reset() { g_prep = Prepared{}; }
+
+int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
+                   size_t ws_bytes, hipStream_t s) {
+    g_prep = Prepared{};
+    if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
+    size_t used = 0;
+    WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
+    if (used > ws_bytes) return SCCG_E_INTERNAL;
+    RC(queue_prepare(A, ws, s));
+    g_prep = Prepared{ws, Rp, Tp, nRp, nTp, k, m, chunk, A.agen};
+    return 0;
+}
+
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
                           void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
                           bool abs_p) {
     if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
     size_t used = 0;
-    WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, &used);
+    WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
     if (used > ws_bytes) return SCCG_E_INTERNAL;
-    if (!getenv("SCCG_DEBUG")) A.dbg = nullptr;   // per-chunk counters only in diagnostic runs
     res->rounds = 0;
     res->chunks = A.C;
     res->n_matches = 0;
@@ -1216,26 +1359,13 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     const bool walkable = nRp >= k && lastk >= 0;
     const unsigned gsweep = grid_for(nRp - k + 1 > 0 ? nRp - k + 1 : 1, 256 * FC_PER_T) > PRESENCE_GRID
                                 ? PRESENCE_GRID : grid_for(nRp - k + 1 > 0 ? nRp - k + 1 : 1, 256 * FC_PER_T);
-    if (walkable) {
-        // the usual first step first: x0 = 0's own k-mer (statistics land in fc[4..11])
-        hipLaunchKernelGGL(k_key0, dim3(gsweep), dim3(SCCG_BLOCK), 0, s, A, 0);
-        hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)gsweep, 0);
-        SCCG_HIP(hipGetLastError());
-        const int64_t slots = 1ll << A.abits;
-        // a fresh workspace is cleared once; afterwards every call's generation retires old slots
-        static thread_local const void* ws_seen = nullptr;
-        static thread_local uint32_t gen = 0;
-        if (ws != ws_seen) {
-            SCCG_HIP(hipMemsetAsync(A.atab, 0, (size_t)slots * sizeof(uint64_t), s));
-            ws_seen = ws;
-        }
-        A.agen = 0x9E3779B9u * ++gen;
-        const int64_t ns = nRp / ANCHOR_STEP + 1;
-        const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
-        PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
-        hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
-        hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
-        SCCG_HIP(hipGetLastError());
+    {
+        const Prepared& g = g_prep;
+        const bool prepared = g.ws == ws && g.R == Rp && g.T == Tp && g.nR == nRp && g.nT == nTp && g.k == k &&
+                              g.m == m && g.chunk == chunk;
+        if (prepared) A.agen = g.agen;   // queued by global_prepare (the caller ordered s after it)
+        else RC(queue_prepare(A, ws, s));
+        g_prep = Prepared{};
     }
 
     // ---- the exact first (ungated) step: first target position with any candidate
@@ -1359,16 +1489,17 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                         std::chrono::duration<double, std::milli>(tnow - tprev).count());
                 tprev = tnow;
             }
-            if (dbg && round == 1) {   // per-chunk cost profile of the speculative round
+            if (dbg && round <= 2) {   // per-chunk cost profile of the rounds' walked chunks
                 constexpr size_t DS = DBG_SLOTS;
                 std::vector<uint64_t> d(C * DS);
                 SCCG_HIP(hipMemcpyAsync(d.data(), A.dbg, C * DS * 8, hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipStreamSynchronize(s));
                 std::vector<uint64_t> tk(C);
-                uint64_t sum[11] = {};
+                uint64_t sum[14] = {};
                 for (size_t j = 0; j < C; j++) {
-                    tk[j] = d[j * DS];
-                    for (int i = 0; i < 11; i++) sum[i] += d[j * DS + i];
+                    const bool mine = d[j * DS + 14] == (uint64_t)round;
+                    tk[j] = mine ? d[j * DS] : 0;
+                    if (mine) for (int i = 0; i < 14; i++) sum[i] += d[j * DS + i];
                 }
                 std::vector<uint64_t> sorted = tk;
                 std::sort(sorted.begin(), sorted.end());
@@ -1378,24 +1509,27 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
                     fprintf(stderr, "[walk] wall clock rate %d kHz\n", khz);
                 }
-                fprintf(stderr, "[walk] r1 chunk ticks(10ns): mean %.0f p50 %llu p90 %llu p99 %llu max %llu | totals: matches %llu "
+                fprintf(stderr, "[walk] r%lld chunk ticks(10ns): mean %.0f p50 %llu p90 %llu p99 %llu max %llu | totals: matches %llu "
                         "batches %llu wides %llu windows %llu cands %llu extbases %llu\n",
-                        (double)sum[0] / C, (unsigned long long)sorted[C / 2], (unsigned long long)sorted[C * 9 / 10],
+                        (long long)round, (double)sum[0] / C, (unsigned long long)sorted[C / 2], (unsigned long long)sorted[C * 9 / 10],
                         (unsigned long long)sorted[C * 99 / 100], (unsigned long long)sorted[C - 1],
                         (unsigned long long)sum[1], (unsigned long long)sum[2], (unsigned long long)sum[3],
                         (unsigned long long)sum[4], (unsigned long long)sum[5], (unsigned long long)sum[6]);
-                fprintf(stderr, "[walk] r1 step phases (10ns, summed over chunks): window %llu find %llu cand+lce %llu tail %llu\n",
-                        (unsigned long long)sum[7], (unsigned long long)sum[8], (unsigned long long)sum[9], (unsigned long long)sum[10]);
+                fprintf(stderr, "[walk] r1 step phases (10ns, summed over chunks): window %llu find %llu cand+lce %llu tail %llu "
+                        "hash %llu wide %llu (wide positions %llu)\n",
+                        (unsigned long long)sum[7], (unsigned long long)sum[8], (unsigned long long)sum[9], (unsigned long long)sum[10],
+                        (unsigned long long)sum[11], (unsigned long long)sum[12], (unsigned long long)sum[13]);
                 std::vector<size_t> idx(C);
                 for (size_t j = 0; j < C; j++) idx[j] = j;
                 std::partial_sort(idx.begin(), idx.begin() + 5, idx.end(), [&](size_t a, size_t b) { return tk[a] > tk[b]; });
                 for (int q = 0; q < 5; q++) {
                     const uint64_t* e = &d[idx[q] * DS];
                     fprintf(stderr, "   slow chunk %zu: ticks %llu matches %llu batches %llu wides %llu windows %llu cands %llu ext %llu "
-                            "| win %llu find %llu cand %llu tail %llu\n",
+                            "| win %llu find %llu cand %llu tail %llu hash %llu wide %llu widepos %llu\n",
                             idx[q], (unsigned long long)e[0], (unsigned long long)e[1], (unsigned long long)e[2],
                             (unsigned long long)e[3], (unsigned long long)e[4], (unsigned long long)e[5], (unsigned long long)e[6],
-                            (unsigned long long)e[7], (unsigned long long)e[8], (unsigned long long)e[9], (unsigned long long)e[10]);
+                            (unsigned long long)e[7], (unsigned long long)e[8], (unsigned long long)e[9], (unsigned long long)e[10],
+                            (unsigned long long)e[11], (unsigned long long)e[12], (unsigned long long)e[13]);
                 }
             }
             if (dbg && (round <= 3 || round % 1000 == 0)) {
