@@ -140,10 +140,17 @@ size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk);
 int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
                    size_t ws_bytes, hipStream_t s);
 void global_prepare_reset();   // forget a preparation that will not be used
-// (abs_p: absolute p on the record line, the text before delta_encode)
+// Where the record text goes, when the caller learns it only during the walk: resolve() is called
+// once, after the rounds and before the text is written, and returns the output pointer.
+struct EmitTarget {
+    int (*resolve)(void* user, uint8_t** out);
+    void* user;
+};
+// (abs_p: absolute p on the record line, the text before delta_encode; late_out: out is ignored
+// and resolved through it)
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m,
                           int chunk, void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len,
-                          WalkResult* res, hipStream_t s, bool abs_p = false);
+                          WalkResult* res, hipStream_t s, bool abs_p = false, const EmitTarget* late_out = nullptr);
 // the raw match list of the last global_match_and_emit (device pointers inside ws)
 int global_matches(void* ws, const int32_t** t, const int32_t** p, const int32_t** l, int64_t* n);
 

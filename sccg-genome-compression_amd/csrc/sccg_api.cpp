@@ -14,11 +14,15 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "decomp.h"
@@ -58,11 +62,64 @@ constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide com
 
 }  // namespace
 
+// One persistent host thread per context: it runs side work whose launches need host syncs (the
+// run lines read their run counts back) while the calling thread drives the main stream.
+struct HostWorker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<int()> task;
+    bool has_task = false, done = true, quit = false;
+    int rc = 0;
+
+    void start(int device) {
+        th = std::thread([this, device] {
+            (void)hipSetDevice(device);
+            std::unique_lock<std::mutex> lk(mu);
+            for (;;) {
+                cv.wait(lk, [this] { return has_task || quit; });
+                if (quit) return;
+                std::function<int()> f = std::move(task);
+                has_task = false;
+                lk.unlock();
+                const int r = f();
+                lk.lock();
+                rc = r;
+                done = true;
+                cv.notify_all();
+            }
+        });
+    }
+    void submit(std::function<int()> f) {
+        std::lock_guard<std::mutex> lk(mu);
+        task = std::move(f);
+        has_task = true;
+        done = false;
+        cv.notify_all();
+    }
+    int wait() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [this] { return done; });
+        return rc;
+    }
+    void stop() {
+        if (!th.joinable()) return;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+            cv.notify_all();
+        }
+        th.join();
+    }
+};
+
 struct sccg_ctx {
     int device = 0;
+    HostWorker worker;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;       // second stream: work that overlaps the local pass
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t side = nullptr;       // walk preparation, overlapping the local pass
+    hipStream_t side2 = nullptr;      // header + run lines, overlapping the local pass
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr;
     std::string err;
     sccg_stats stats{};
     void* buf[B_COUNT] = {};
@@ -126,25 +183,32 @@ int sccg_ctx_create(int device, sccg_ctx** out) {
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_lines, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SCCG_E_HIP;
     }
+    c->worker.start(device);
     *out = c;
     return SCCG_OK;
 }
 
 void sccg_ctx_destroy(sccg_ctx* ctx) {
     if (!ctx) return;
+    ctx->worker.stop();
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamSynchronize(ctx->side);
+    (void)hipStreamSynchronize(ctx->side2);
     for (int i = 0; i < B_COUNT; i++)
         if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
     (void)hipEventDestroy(ctx->ev_fork);
     (void)hipEventDestroy(ctx->ev_join);
+    (void)hipEventDestroy(ctx->ev_lines);
     (void)hipStreamDestroy(ctx->side);
+    (void)hipStreamDestroy(ctx->side2);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -291,11 +355,12 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     if (out_cap < hlen + 1 + 11 * nT + 64) return ctx->fail(SCCG_E_INVALID, "output capacity too small");
 
     // ---- fork.  The local pass (compression.cpp:372-474, main stream) is latency-bound; the
-    //      header + run lines and the global walk's input-only preparation (first-step sweep,
-    //      anchor index) only read T/R/T'/R', so they run beside it on the side stream.
-    hipStream_t s2 = ctx->side;
+    //      global walk's input-only preparation (first-step sweep, anchor index; side stream)
+    //      and the header + run lines (side2) only read T/R/T'/R', so they run beside it.
+    hipStream_t s2 = ctx->side, s3 = ctx->side2;
     HIPTRY(hipEventRecord(ctx->ev_fork, s));
     HIPTRY(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
+    HIPTRY(hipStreamWaitEvent(s3, ctx->ev_fork, 0));
 
     // ---- local segments (main stream; the switch point is read after the side work is queued)
     const int64_t nRs = (nR + SEG_L - 1) / SEG_L, nTs = (nT + SEG_L - 1) / SEG_L;
@@ -319,21 +384,6 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         TRY(launch_local_all(R, nR, T, nT, iters, recs, stat, cls, gen, ctl, s));
     }
 
-    // ---- header + lowercase line (compression.cpp:337-368), side stream
-    int64_t pos = 0;
-    if (has_hdr) {
-        HIPTRY(hipMemcpyAsync(out, tfa + hdr[0], (size_t)hlen, hipMemcpyDeviceToDevice, s2));
-        TRY(dev_put_bytes(out + hlen, "\n", 1, s2));
-        pos = hlen + 1;
-    }
-    // both run lines now (the N line is kept aside until the mode is known)
-    uint8_t* nline = nullptr;
-    int64_t rl_len[2];
-    TRY(run_lines(ctx, T, nT, out + pos, &nline, sc + 10, rl_len, s2));
-    const int64_t llen = rl_len[0];
-    pos += llen;
-    const int64_t lower_end = pos;
-
     // ---- the global walk's preparation, side stream (wasted only if the pass stays local)
     const int64_t np[2] = {lt[1], lr[1]};
     const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, walk_chunk());
@@ -341,6 +391,38 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
     TRY(global_prepare(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(), ws, wsb, s2));
     HIPTRY(hipEventRecord(ctx->ev_join, s2));
+
+    // ---- header + lowercase line (compression.cpp:337-368): side2, driven by the context's host
+    //      worker (its launches wait on run counts), so this thread goes on with the walk
+    int64_t pos = 0;
+    uint8_t* nline = nullptr;
+    int64_t rl_len[2] = {0, 0};
+    ctx->worker.submit([&]() -> int {
+        if (has_hdr) {
+            HIPTRY(hipMemcpyAsync(out, tfa + hdr[0], (size_t)hlen, hipMemcpyDeviceToDevice, s3));
+            TRY(dev_put_bytes(out + hlen, "\n", 1, s3));
+        }
+        // both run lines now (the N line is kept aside until the mode is known)
+        TRY(run_lines(ctx, T, nT, out + (has_hdr ? hlen + 1 : 0), &nline, sc + 10, rl_len, s3));
+        HIPTRY(hipEventRecord(ctx->ev_lines, s3));
+        return 0;
+    });
+    struct WorkerJoin {   // every exit path waits for the side work (it captures this frame)
+        HostWorker* w;
+        bool joined = false;
+        int join() {
+            if (joined) return 0;
+            joined = true;
+            return w->wait();
+        }
+        ~WorkerJoin() { join(); }
+    } lines{&ctx->worker};
+    auto join_lines = [&]() -> int {   // the lowercase line's end, main stream ordered after it
+        TRY(lines.join());
+        HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
+        pos = (has_hdr ? hlen + 1 : 0) + rl_len[0];
+        return 0;
+    };
 
     // ---- join: the switch point, then everything after it runs behind the side work
     if (iters > 0) {
@@ -353,6 +435,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     mark("local");
     if (sw < 0) {
         global_prepare_reset();
+        TRY(join_lines());
         // ---- local: "\n,\n" + records + leftover segments
         TRY(dev_put_bytes(out + pos, "\n,\n", 3, s));
         pos += 3;
@@ -383,23 +466,35 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     } else {
         // ---- global (compression.cpp:484-574)
         st.mode_global = 1;
-        pos = lower_end;
-        TRY(dev_put_bytes(out + pos, "\n", 1, s));
-        pos += 1;
-        const int64_t nlen = rl_len[1];
-        if (nlen) HIPTRY(hipMemcpyAsync(out + pos, nline, (size_t)nlen, hipMemcpyDeviceToDevice, s));
-        pos += nlen;
-        TRY(dev_put_bytes(out + pos, "\n", 1, s));
-        pos += 1;
-        mark("n_line");
+        // N line + record text go after the lowercase line: resolved once the walk's rounds are
+        // done (the run lines finish on the side meanwhile)
+        uint8_t* X = nullptr;
+        struct Late {
+            std::function<int(uint8_t**)> f;
+            static int call(void* u, uint8_t** o) { return static_cast<Late*>(u)->f(o); }
+        } late{[&](uint8_t** o) -> int {
+            TRY(join_lines());
+            TRY(dev_put_bytes(out + pos, "\n", 1, s));
+            pos += 1;
+            const int64_t nlen = rl_len[1];
+            if (nlen) HIPTRY(hipMemcpyAsync(out + pos, nline, (size_t)nlen, hipMemcpyDeviceToDevice, s));
+            pos += nlen;
+            TRY(dev_put_bytes(out + pos, "\n", 1, s));
+            pos += 1;
+            X = out + pos;
+            if (paren) {
+                GET(uint8_t, xb, B_DX, out_cap - pos);
+                X = xb;
+            }
+            *o = X;
+            return 0;
+        }};
+        const EmitTarget target{&Late::call, &late};
         WalkResult wr{};
         int64_t rlen = 0;
-        uint8_t* X = out + pos;
-        if (paren) {
-            GET(uint8_t, xb, B_DX, out_cap - pos);
-            X = xb;
-        }
-        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(), ws, wsb, X, &rlen, &wr, s, paren));
+        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(), ws, wsb, nullptr, &rlen, &wr, s, paren,
+                                  &target));
+        if (!X) return ctx->fail(SCCG_E_INTERNAL, "record text position never resolved");
         if (paren) TRY(paren_delta(ctx, X, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
         st.n_matches = wr.n_matches;
         st.walk_rounds = wr.rounds;

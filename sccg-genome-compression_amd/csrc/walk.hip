@@ -1335,7 +1335,7 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
                           void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
-                          bool abs_p) {
+                          bool abs_p, const EmitTarget* late_out) {
     if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
     size_t used = 0;
     WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
@@ -1599,6 +1599,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     g_last_n = nm;
 
     // ---- record text: literal gap + "(dp,l)" per match, then the tail literal
+    if (late_out) RC(late_out->resolve(late_out->user, &out));   // the caller's text position is known now
     int64_t text = 0;
     int32_t tail_from = 0;
     if (nm > 0) {
