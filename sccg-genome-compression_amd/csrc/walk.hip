@@ -33,7 +33,8 @@ constexpr int WTBITS = 9;              // window hash slots
 constexpr int WTSLOTS = 1 << WTBITS;
 constexpr int32_t INVALID = INT32_MIN;
 constexpr int ANCHOR_K = 32;
-constexpr int ANCHOR_STEP = 32;
+constexpr int ANCHOR_STEP_DEFAULT = 32;   // reference sample stride (SCCG_ANCHOR_STEP for tuning runs)
+constexpr int ANCHOR_LOAD_DEFAULT = 4;    // table slots per sample (SCCG_ANCHOR_LOAD)
 constexpr uint32_t A_MULTI = 0xFFFFFFFFu;    // anchor position of a 32-mer seen more than once
 constexpr int32_t FROZEN_MIN = 4096;   // literal bases at a chunk end that trigger a frozen-P scan
 constexpr int FROZEN_MAX = 256;        // frozen chunks handled per batch (grid.y of k_frozen_scan)
@@ -92,6 +93,8 @@ struct WalkPtrs {
     uint32_t agen;            // anchor tag generation (one per call)
     int32_t round;            // walk round of the launch (kernel argument copy)
     int32_t abits;
+    int32_t astep;            // anchor sample stride
+    int32_t amulti;           // 1: second build pass marks repeated 32-mers
     unsigned long long* fc;   // full-candidate scan scalars: [0] lmax [1] cnt [2] has0 [3] minkey [4] firsthit [5] firstexo
                               // [8..11] the same four for the batch's first position (k_presence + k_cand_reduce)
     unsigned long long* fcb;  // per presence block: 4 candidate statistics
@@ -734,9 +737,9 @@ __device__ __forceinline__ uint32_t anchor_tag(uint64_t key, uint32_t gen) { ret
 // pass 1 (mark = false): store every sample; pass 2 (mark = true): flag repeated 32-mers
 template <bool MARK>
 __global__ void k_anchor_build(WalkPtrs A) {
-    const int64_t ns = A.nR >= ANCHOR_K ? ((int64_t)A.nR - ANCHOR_K) / ANCHOR_STEP + 1 : 0;
+    const int64_t ns = A.nR >= ANCHOR_K ? ((int64_t)A.nR - ANCHOR_K) / A.astep + 1 : 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t p = (int32_t)(i * ANCHOR_STEP);
+        const int32_t p = (int32_t)(i * A.astep);
         uint64_t code;
         if (!code32<true>(A.R + p, code)) continue;
         const uint64_t key = mix64(code);
@@ -820,12 +823,22 @@ __device__ __forceinline__ int32_t serial_ext(const uint8_t* R, int32_t nR, cons
 // their 64 + 16 bytes as five aligned 16-byte loads, tests each position's walk key (and whether
 // the k-mer holds a non-ACGT byte) with `pred`, then calls `hit` for every position that passed
 // (out of the unrolled part).  HBM-bound: R' is read once per sweep.
+template <typename Pred, typename Hit, typename Words>
+__device__ __forceinline__ void sweep_kmers_w(const uint8_t* __restrict__ R, int64_t npos, int k, Pred&& pred, Hit&& hit,
+                                              Words&& words);
 template <typename Pred, typename Hit>
 __device__ __forceinline__ void sweep_kmers(const uint8_t* __restrict__ R, int64_t npos, int k, Pred&& pred, Hit&& hit) {
+    sweep_kmers_w(R, npos, k, pred, hit, [](int64_t, const uint32_t (&)[20], const uint32_t (&)[20], uint32_t) {});
+}
+// the same, handing every thread's 64-position block (codes cw, non-ACGT masks dw of its 20 words)
+// to `words` as well
+template <typename Pred, typename Hit, typename Words>
+__device__ __forceinline__ void sweep_kmers_w(const uint8_t* __restrict__ R, int64_t npos, int k, Pred&& pred, Hit&& hit,
+                                              Words&& words) {
     const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * FC_PER_T;
     for (int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * FC_PER_T; p0 < npos; p0 += stride) {
-        uint32_t cw[20], acc = 0;
+        uint32_t cw[20], dw[20], acc = 0;
         {
             const uint4* src = reinterpret_cast<const uint4*>(R + p0);
             uint32_t w[20];
@@ -835,8 +848,9 @@ __device__ __forceinline__ void sweep_kmers(const uint8_t* __restrict__ R, int64
                 w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
             }
 #pragma unroll
-            for (int i = 0; i < 20; i++) { uint32_t d; cw[i] = swar_codes(w[i], d); acc |= d; }
+            for (int i = 0; i < 20; i++) { cw[i] = swar_codes(w[i], dw[i]); acc |= dw[i]; }
         }
+        words(p0, cw, dw, acc);
         uint64_t hits = 0;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
@@ -982,17 +996,39 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
 // The usual first step: does the target's first k-mer (x0) occur in R' at all, and the candidate
 // statistics if so.  One key, no tables: a plain compare per reference position, so this sweep
 // runs at streaming speed; k_presence (the general batch search) runs only when it finds nothing.
+// ANCH: the same pass also stores the anchor samples (every 32nd position, astep == 32) -- their
+// 2-bit codes are the words the sweep already packed, so the anchor index costs no extra read of R'.
+template <bool ANCH>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
     __shared__ CandBest wbest[SCCG_BLOCK / 64];
     const int k = A.k;
     const uint32_t key0 = walk_key(A.T + x0, k);
     CandBest best{0, 0, 0, ~0ull};
-    if (key0 < KEY_EXOTIC) {   // exotic: no statistics, the caller falls back to k_presence
-        sweep_kmers(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) { return pure && code == key0; },
-                    [&](int64_t c) {
-                        const uint32_t l = (uint32_t)serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, x0, k);
-                        best = cb_merge(best, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key((int32_t)c, -1) : ~0ull});
-                    });
+    if (key0 < KEY_EXOTIC || ANCH) {   // exotic: no statistics, the caller falls back to k_presence
+        const bool want = key0 < KEY_EXOTIC;
+        sweep_kmers_w(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) { return want && pure && code == key0; },
+                      [&](int64_t c) {
+                          const uint32_t l = (uint32_t)serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, x0, k);
+                          best = cb_merge(best, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key((int32_t)c, -1) : ~0ull});
+                      },
+                      [&](int64_t p0, const uint32_t (&cw)[20], const uint32_t (&dw)[20], uint32_t acc) {
+                          if (!ANCH) return;
+#pragma unroll
+                          for (int h = 0; h < 2; h++) {
+                              const int64_t p = p0 + 32 * h;
+                              if (p + ANCHOR_K > A.nR) break;
+                              uint64_t code = 0;
+                              uint32_t bad = 0;
+#pragma unroll
+                              for (int i = 0; i < 8; i++) {
+                                  code |= (uint64_t)cw[8 * h + i] << (8 * i);
+                                  bad |= dw[8 * h + i];
+                              }
+                              if (acc && bad) continue;
+                              const uint64_t key = mix64(code);
+                              A.atab[key >> (64 - A.abits)] = ((uint64_t)anchor_tag(key, A.agen) << 32) | (uint32_t)p;
+                          }
+                      });
     }
     best = cb_wave(best);
     if (lane_id() == 0) wbest[wave_in_block()] = best;
@@ -1094,8 +1130,17 @@ struct Carve {
     }
 };
 
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+int anchor_step() {
+    static const int v = [] { const int x = env_int("SCCG_ANCHOR_STEP", ANCHOR_STEP_DEFAULT); return x >= 8 && x <= 1024 ? x : ANCHOR_STEP_DEFAULT; }();
+    return v;
+}
 int anchor_bits(int64_t nR) {
-    int64_t want = 4 * (nR / ANCHOR_STEP + 1);   // load <= 1/4: few samples lose their slot
+    static const int load = [] { const int x = env_int("SCCG_ANCHOR_LOAD", ANCHOR_LOAD_DEFAULT); return x >= 1 && x <= 16 ? x : ANCHOR_LOAD_DEFAULT; }();
+    int64_t want = load * (nR / anchor_step() + 1);   // load <= 1/4: few samples lose their slot
     int b = 10;
     while ((1ll << b) < want && b < 34) b++;
     return b;
@@ -1134,6 +1179,11 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);
     A.abits = anchor_bits(nR);
+    A.astep = anchor_step();
+    {
+        static const int multi = env_int("SCCG_ANCHOR_MULTI", 0);
+        A.amulti = multi;
+    }
     A.atab = c.take<uint64_t>((size_t)1 << A.abits);
     A.fc = c.take<unsigned long long>(16);
     A.fcb = c.take<unsigned long long>(4 * PRESENCE_GRID);
@@ -1283,10 +1333,6 @@ int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
     if (!walkable) return 0;
     const unsigned gsweep = grid_for(A.nR - A.k + 1, 256 * FC_PER_T) > PRESENCE_GRID
                                 ? PRESENCE_GRID : grid_for(A.nR - A.k + 1, 256 * FC_PER_T);
-    // the usual first step first: x0 = 0's own k-mer (statistics land in fc[4..11])
-    hipLaunchKernelGGL(k_key0, dim3(gsweep), dim3(SCCG_BLOCK), 0, s, A, 0);
-    hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)gsweep, 0);
-    SCCG_HIP(hipGetLastError());
     const int64_t slots = 1ll << A.abits;
     // a fresh workspace is cleared once; afterwards every call's generation retires old slots
     static thread_local const void* ws_seen = nullptr;
@@ -1296,10 +1342,17 @@ int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
         ws_seen = ws;
     }
     A.agen = 0x9E3779B9u * ++gen;
-    const int64_t ns = (int64_t)A.nR / ANCHOR_STEP + 1;
+    // the usual first step: x0 = 0's own k-mer (statistics land in fc[4..11]); with the default
+    // sample stride the same sweep stores the anchor samples
+    const bool fused = A.astep == 32;
+    if (fused) PROF_LAUNCH(PROF_ANCHOR, s, k_key0<true>, dim3(gsweep), dim3(SCCG_BLOCK), 0, s, A, 0);
+    else hipLaunchKernelGGL(k_key0<false>, dim3(gsweep), dim3(SCCG_BLOCK), 0, s, A, 0);
+    hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)gsweep, 0);
+    SCCG_HIP(hipGetLastError());
+    const int64_t ns = (int64_t)A.nR / A.astep + 1;
     const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
-    PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
-    hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
+    if (!fused) PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
+    if (A.amulti) hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
     hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
     SCCG_HIP(hipGetLastError());
     return 0;
