@@ -77,6 +77,31 @@ __device__ __forceinline__ void keys16(const uint8_t* s, uint64_t& code, uint32_
     pack_codes<8>(w, code, bad);
 }
 
+// extend_alignment (compression.cpp:27-34) of r[qc..] against t[y..] in LDS, whole wave, 4 bytes
+// per lane per step; returns the extension clamped to [K, maxl]
+template <int K>
+__device__ __forceinline__ int wave_ext(const uint32_t* r4, const uint32_t* t4, int qc, int y, int maxl) {
+    const int lane = lane_id();
+    int l = maxl;
+    for (int off = K; off < maxl; off += 256) {
+        const int i = off + 4 * lane;
+        int e = INT32_MAX;
+        if (i < maxl) {
+            const int ra = qc + i, ta = y + i;
+            const uint32_t rv = __builtin_amdgcn_alignbyte(r4[(ra >> 2) + 1], r4[ra >> 2], (uint32_t)(ra & 3));
+            const uint32_t tv = __builtin_amdgcn_alignbyte(t4[(ta >> 2) + 1], t4[ta >> 2], (uint32_t)(ta & 3));
+            const uint32_t x = rv ^ tv;
+            if (x) e = i + (__builtin_ctz(x) >> 3);
+            else if (maxl - i <= 4) e = maxl;
+        }
+        const unsigned long long sm = __ballot(e != INT32_MAX);
+        if (sm) { l = lane_val(e, first_lane(sm)); break; }
+    }
+    if (l > maxl) l = maxl;
+    if (l < K) l = K;
+    return l;
+}
+
 // SCCG_DEBUG: phase ticks (10 ns) summed over segments: load, keys, insert, hits, walk, count
 __device__ unsigned long long g_local_dbg[16];
 
@@ -225,6 +250,24 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
         int bl = 0, bcnt = 0;
         bool bhas0 = false;
         uint64_t bkey = ~0ull;
+        // A candidate's extension is bounded by min(nr - q, nt - nxt); one whose bound is below the
+        // best extension found cannot change the pick.  With more than one batch of entries, the
+        // candidate with the largest bound (the least q) is extended first, so the bound prunes the
+        // rest (all-N / homopolymer segments: ~1000 candidates, one of which reaches the end).
+        int lb = 0;
+        if (e1 - e0 > 64) {
+            int qmin = INT32_MAX;
+            for (int eb = e0; eb < e1; eb += 64) {
+                const int e = eb + lane;
+                if (e < e1 && L.skey[e] == key) {
+                    const int q = L.spos[e];
+                    if (q < qmin && (key < KEY_EXOTIC || bytes_eq(&L.r[q], &L.t[nxt], K))) qmin = q;
+                }
+            }
+            qmin = wave_min(qmin);
+            if (qmin != INT32_MAX)
+                lb = wave_ext<K>(r4, t4, qmin, nxt, (nr - qmin) < (nt - nxt) ? (nr - qmin) : (nt - nxt));
+        }
         for (int eb = e0; eb < e1; eb += 64) {
             const int e = eb + lane;
             int q = -1;
@@ -232,6 +275,8 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
                 q = L.spos[e];
                 if (key >= KEY_EXOTIC && !bytes_eq(&L.r[q], &L.t[nxt], K)) q = -1;
             }
+            const int thr = bl > lb ? bl : lb;
+            if (q >= 0 && ((nr - q) < (nt - nxt) ? (nr - q) : (nt - nxt)) < thr) q = -1;   // pruned (see above)
             unsigned long long cm = __ballot(q >= 0);
             if (__popcll(cm) <= MANY) {
                 while (cm) {   // few candidates: the whole wave extends each
@@ -239,23 +284,8 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
                     cm &= cm - 1;
                     const int qc = lane_val(q, cl);
                     const int maxl = (nr - qc) < (nt - nxt) ? (nr - qc) : (nt - nxt);
-                    int l = maxl;   // extend_alignment (compression.cpp:27-34): 4 bytes per lane per step
-                    for (int off = K; off < maxl; off += 256) {
-                        const int i = off + 4 * lane;
-                        int e = INT32_MAX;
-                        if (i < maxl) {
-                            const int ra = qc + i, ta = nxt + i;
-                            const uint32_t rv = __builtin_amdgcn_alignbyte(r4[(ra >> 2) + 1], r4[ra >> 2], (uint32_t)(ra & 3));
-                            const uint32_t tv = __builtin_amdgcn_alignbyte(t4[(ta >> 2) + 1], t4[ta >> 2], (uint32_t)(ta & 3));
-                            const uint32_t x = rv ^ tv;
-                            if (x) e = i + (__builtin_ctz(x) >> 3);
-                            else if (maxl - i <= 4) e = maxl;
-                        }
-                        const unsigned long long sm = __ballot(e != INT32_MAX);
-                        if (sm) { l = lane_val(e, first_lane(sm)); break; }
-                    }
-                    if (l > maxl) l = maxl;
-                    if (l < K) l = K;
+                    if (maxl < bl) continue;   // cannot reach the best extension: no effect on the pick
+                    const int l = wave_ext<K>(r4, t4, qc, nxt, maxl);
                     if (l > bl) { bl = l; bcnt = 1; bhas0 = (qc == 0); bkey = qc ? pick_key(qc, pme) : ~0ull; }
                     else if (l == bl) {
                         bcnt++;
@@ -610,8 +640,9 @@ int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT,
         SCCG_HIP(hipStreamSynchronize(s));
         const double n = d[5] ? (double)d[5] : 1.0;
         fprintf(stderr, "[local all] %llu segment passes, per pass (us): load %.2f keys %.2f insert %.2f hits %.2f walk %.2f"
-                " | max %.2f\n", d[5], d[0] / n / 100, d[1] / n / 100, d[2] / n / 100, d[3] / n / 100, d[4] / n / 100,
-                d[6] / 100.0);
+                " | max %.2f (seg %llu, %llu matches: load %.2f keys %.2f insert %.2f hits %.2f walk %.2f)\n", d[5],
+                d[0] / n / 100, d[1] / n / 100, d[2] / n / 100, d[3] / n / 100, d[4] / n / 100, d[6] / 100.0, d[13], d[14],
+                d[8] / 100.0, d[9] / 100.0, d[10] / 100.0, d[11] / 100.0, d[12] / 100.0);
     } else {
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, nR, T, nT, (int32_t)nseg, recs,
                     stat, cls, gen, ctl);
