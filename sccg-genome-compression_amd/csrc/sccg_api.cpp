@@ -397,6 +397,13 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     int64_t pos = 0;
     uint8_t* nline = nullptr;
     int64_t rl_len[2] = {0, 0};
+    // the run lines are needed only for the final text; SCCG_LINES_AFTER_PREP=1 holds them back
+    // until the walk preparation is done (measured: no gain, the walk then slows instead)
+    static const bool lines_after_prep = [] {
+        const char* e = getenv("SCCG_LINES_AFTER_PREP");
+        return e ? atoi(e) != 0 : false;
+    }();
+    if (lines_after_prep) HIPTRY(hipStreamWaitEvent(s3, ctx->ev_join, 0));
     ctx->worker.submit([&]() -> int {
         if (has_hdr) {
             HIPTRY(hipMemcpyAsync(out, tfa + hdr[0], (size_t)hlen, hipMemcpyDeviceToDevice, s3));

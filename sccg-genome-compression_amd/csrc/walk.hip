@@ -906,6 +906,7 @@ __global__ void k_fullc(WalkPtrs A, int32_t y, int32_t P, int pass) {
 constexpr int PB = 1024;
 constexpr int PBBITS = 11;
 constexpr int PRESENCE_GRID = 1024;   // blocks of a presence sweep (each first builds the batch's LDS tables)
+constexpr int KEY0_GRID_MAX = 16384;  // blocks of the first-step sweep (no LDS tables: as many as pay)
 constexpr int PFBITS = 17;   // presence pre-filter: 2^17-bit LDS bitmap of the batch's keys
 
 // candidate statistics of one target position (compression.cpp:114-130 over ALL candidates):
@@ -1090,17 +1091,30 @@ __global__ void k_match_textlen(WalkPtrs A, int64_t nm, int abs_p) {
     }
 }
 
+// One thread per match: its literal gap (short ones by the thread, long ones by the whole wave)
+// and its "(dp,l)" token.
 __global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int64_t nm, uint8_t* __restrict__ out,
                                                                 int abs_p) {
-    const int64_t i = (int64_t)blockIdx.x * WPB + wave_in_block();
-    if (i >= nm) return;
-    const int lane = lane_id();
-    const int32_t pend = i ? A.ft[i - 1] + A.fl[i - 1] : 0;
-    const int32_t t = A.ft[i];
-    uint8_t* o = out + A.tlen[i];
-    for (int32_t q = lane; q < t - pend; q += 64) o[q] = A.T[pend + q];
-    if (lane == 0) {
-        uint8_t* d = o + (t - pend);
+    constexpr int32_t SHORT_GAP = 32;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = i < nm;
+    int32_t pend = 0, gap = 0;
+    int64_t o = 0;
+    if (valid) {
+        pend = i ? A.ft[i - 1] + A.fl[i - 1] : 0;
+        gap = A.ft[i] - pend;
+        o = A.tlen[i];
+        if (gap <= SHORT_GAP)
+            for (int32_t q = 0; q < gap; q++) out[o + q] = A.T[pend + q];
+    }
+    for (unsigned long long lm = __ballot(valid && gap > SHORT_GAP); lm; lm &= lm - 1) {
+        const int l = __ffsll((long long)lm) - 1;
+        const int32_t gp = __shfl(pend, l, 64), gg = __shfl(gap, l, 64);
+        const int64_t go = __shfl(o, l, 64);
+        for (int32_t q = lane_id(); q < gg; q += 64) out[go + q] = A.T[gp + q];
+    }
+    if (valid) {
+        uint8_t* d = out + o + gap;
         const int32_t pprev = i && !abs_p ? A.fp[i - 1] : 0;
         *d++ = '(';
         d += write_i32(d, (int32_t)((uint32_t)A.fp[i] - (uint32_t)pprev));
@@ -1186,7 +1200,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     }
     A.atab = c.take<uint64_t>((size_t)1 << A.abits);
     A.fc = c.take<unsigned long long>(16);
-    A.fcb = c.take<unsigned long long>(4 * PRESENCE_GRID);
+    A.fcb = c.take<unsigned long long>(4 * KEY0_GRID_MAX);
     A.flat_off = c.take<int64_t>(C + 1);
     const size_t maxm = (size_t)(nT / k + 2);
     A.ft = c.take<int32_t>(maxm); A.fp = c.take<int32_t>(maxm); A.fl = c.take<int32_t>(maxm);
@@ -1331,8 +1345,13 @@ int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
     const int32_t lastk = A.nT - A.k;
     const bool walkable = A.nR >= A.k && lastk >= 0;
     if (!walkable) return 0;
-    const unsigned gsweep = grid_for(A.nR - A.k + 1, 256 * FC_PER_T) > PRESENCE_GRID
-                                ? PRESENCE_GRID : grid_for(A.nR - A.k + 1, 256 * FC_PER_T);
+    static const unsigned key0_grid = [] {
+        const char* e = getenv("SCCG_KEY0_GRID");
+        const int v = e ? atoi(e) : 1024;
+        return (unsigned)(v >= 64 && v <= KEY0_GRID_MAX ? v : 1024);
+    }();
+    const unsigned gsweep = grid_for(A.nR - A.k + 1, 256 * FC_PER_T) > key0_grid
+                                ? key0_grid : grid_for(A.nR - A.k + 1, 256 * FC_PER_T);
     const int64_t slots = 1ll << A.abits;
     // a fresh workspace is cleared once; afterwards every call's generation retires old slots
     static thread_local const void* ws_seen = nullptr;
@@ -1659,7 +1678,8 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         const unsigned g = grid_for(nm, 256) > 4096 ? 4096 : grid_for(nm, 256);
         hipLaunchKernelGGL(k_match_textlen, dim3(g), dim3(256), 0, s, A, nm, (int)abs_p);
         RC(dev_excl_sum(A.tlen, A.tlen, nm, A.scal64 + 1, A.partial, s));
-        PROF_LAUNCH(PROF_MATCH_EMIT, s, k_match_textwrite, dim3(grid_for(nm, WPB)), dim3(SCCG_BLOCK), 0, s, A, nm, out, (int)abs_p);
+        PROF_LAUNCH(PROF_MATCH_EMIT, s, k_match_textwrite, dim3(grid_for(nm, SCCG_BLOCK)), dim3(SCCG_BLOCK), 0, s, A, nm, out,
+                    (int)abs_p);
         SCCG_HIP(hipGetLastError());
         int32_t lt[2];
         const RbItem it[3] = {{A.scal64 + 1, &text, (int)sizeof text}, {A.ft + nm - 1, &lt[0], 4}, {A.fl + nm - 1, &lt[1], 4}};
