@@ -1604,7 +1604,8 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                             (unsigned long long)e[11], (unsigned long long)e[12], (unsigned long long)e[13]);
                 }
             }
-            if (dbg && (round <= 3 || round % 1000 == 0)) {
+            static const int dbg_rounds = getenv("SCCG_DEBUG_ROUNDS") ? atoi(getenv("SCCG_DEBUG_ROUNDS")) : 3;
+            if (dbg && (round <= dbg_rounds || round % 1000 == 0)) {
                 std::vector<int32_t> g(C), ex(C), ep(C), ux(C), up(C), cur(C), c0(C), c1(C);
                 SCCG_HIP(hipMemcpyAsync(g.data(), A.guess, C * 4, hipMemcpyDeviceToHost, s));
                 SCCG_HIP(hipMemcpyAsync(ex.data(), A.exitX, C * 4, hipMemcpyDeviceToHost, s));

@@ -14,6 +14,16 @@ import torch
 import torch.distributed as dist
 
 
+# UCSC chromInfo lengths: chr1..22, X, Y.  hg18 = reference, hg19 = target.
+CHROMS = [f"chr{i}" for i in range(1, 23)] + ["chrX", "chrY"]
+HG18 = [247249719, 242951149, 199501827, 191273063, 180857866, 170899992, 158821424, 146274826, 140273252,
+        135374737, 134452384, 132349534, 114142980, 106368585, 100338915, 88827254, 78774742, 76117153,
+        63811651, 62435964, 46944323, 49691432, 154913754, 57772954]
+HG19 = [249250621, 243199373, 198022430, 191154276, 180915260, 171115067, 159138663, 146364022, 141213431,
+        135534747, 135006516, 133851895, 115169878, 107349540, 102531392, 90354753, 81195210, 78077248,
+        59128983, 63025520, 48129895, 51304566, 155270560, 59373566]
+
+
 def lpt_shard(sizes: list[int], world: int) -> list[list[int]]:
     """Longest-processing-time-first: item indices per rank, each rank's list in input order."""
     if world < 1:

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
 """Secondary measurements (not the bench.py line): device-resident throughput of
+  * the whole hg19-vs-hg18 genome on ONE GPU (BASELINE configs[2]: 24 chromosome pairs at their
+    UCSC lengths, synthetic, compressed one after another; the 8-GPU job LPT-shards them),
   * decompression of a chr1-sized record stream (BASELINE configs[3]),
   * compression of a T2T-like divergent pair (configs[4] shape, literal-heavy),
   * compression of a pair that stays in local mode (no switch).
@@ -48,6 +50,8 @@ def main() -> None:
     work = [("chr1_decompress", "hg", 247_249_719, 249_250_621, 1),
             ("t2t_like_compress", "t2t", 100_000_000, 100_000_000, 7),
             ("local_mode_compress", "local", 247_249_719, 247_249_719, 8)]
+    if not args.only or args.only in "genome":
+        genome(ctx, dev, stream, args, to_dev)
     for name, prof, rl, tl, seed in work:
         if args.only and args.only not in name:
             continue
@@ -76,6 +80,55 @@ def main() -> None:
         print(json.dumps(out), flush=True)
         del d_ref, d_tgt, d_rec
         torch.cuda.empty_cache()
+
+
+def genome(ctx, dev, stream, args, to_dev) -> None:
+    """BASELINE configs[2] on one GPU: every chromosome pair resident in HBM, compressed in turn."""
+    import torch
+    import multigpu
+    import synth
+    t0 = time.perf_counter()
+    pairs = []
+    for i, (rl, tl) in enumerate(zip(multigpu.HG18, multigpu.HG19)):
+        rfa, tfa = synth.synth_pair("hg", int(rl * args.scale), int(tl * args.scale), i + 1)
+        pairs.append((to_dev(rfa), len(rfa), to_dev(tfa), len(tfa)))
+        del rfa, tfa
+    gen_s = time.perf_counter() - t0
+    cap = max(ctx.compress_bound(r, t) for _, r, _, t in pairs)
+    d_rec = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ctx.compress_device(pairs[20][0].data_ptr(), pairs[20][1], pairs[20][2].data_ptr(), pairs[20][3],
+                        d_rec.data_ptr(), cap, stream)   # warm-up (chr21)
+    best = None
+    for _ in range(args.steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        bases = rec_bytes = 0
+        per = []
+        for dr, rn, dt_, tn in pairs:
+            n = ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, d_rec.data_ptr(), cap, stream)
+            st = ctx.stats()
+            bases += st["target_bases"]
+            rec_bytes += n
+            per.append(st["target_bases"])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None or dt < best else best
+    # per chromosome (synchronised individually; diagnostics)
+    per_s = []
+    for dr, rn, dt_, tn in pairs:
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, d_rec.data_ptr(), cap, stream)
+        st = ctx.stats()
+        per_s.append({"ms": round((time.perf_counter() - t1) * 1e3, 2), "rounds": st["walk_rounds"],
+                      "switch": st["switch_segment"], "matches": st["n_matches"]})
+    print(json.dumps({"workload": "hg19_vs_hg18_genome_1gpu", "chromosomes": len(pairs), "target_bases": bases,
+                      "record_bytes": rec_bytes, "seconds": best, "bases_per_s": bases / best,
+                      "lpt_max_over_mean_8gpu": multigpu.max_over_mean(per, 8), "generate_seconds": gen_s,
+                      "per_chromosome": dict(zip(multigpu.CHROMS, per_s))}),
+          flush=True)
+    del pairs, d_rec
+    torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

@@ -9,9 +9,7 @@ from pkg import PKG_DIR  # noqa: F401
 import multigpu
 
 # UCSC chromInfo lengths: hg19 chr1..22, X, Y (targets)
-HG19 = [249250621, 243199373, 198022430, 191154276, 180915260, 171115067, 159138663, 146364022, 141213431,
-        135534747, 135006516, 133851895, 115169878, 107349540, 102531392, 90354753, 81195210, 78077248,
-        59128983, 63025520, 48129895, 51304566, 155270560, 59373566]
+HG19 = multigpu.HG19
 
 
 def test_lpt_partitions_everything_once():
