@@ -51,6 +51,14 @@ constexpr int32_t STALE_BUDGET_DEFAULT = 0;   // 0: off (SCCG_STALE_BUDGET sets 
 // literal scan.  The trajectory is then a walk from a different state after the re-seed, so a
 // later fix-up may converge only onto its matches from the re-seed on (seedq).
 constexpr int32_t RESEED_GAP = 1024;
+// A fix-up that crossed at least half its chunk while P moved less than TRAP_P is "trapped": the
+// sequential walk is stuck near one reference window (a frozen P, or chance hits inside a
+// low-complexity window that keep nudging P).  Its successors are then usually trapped near the
+// same P, so up to RESPEC_AHEAD chunks after the next pending one are walked again speculatively
+// from that P in the same round, instead of resolving one chunk per round.
+constexpr int32_t TRAP_P = 4096;
+constexpr int RESPEC_AHEAD = 256;
+constexpr int RESPEC_MAX_TRIGGERS = 64;
 
 struct WalkPtrs {
     const uint8_t* R;
@@ -83,6 +91,7 @@ struct WalkPtrs {
     int32_t* walked;      // round in which the chunk was last re-walked
     int32_t* lround;      // round for which the chunk was last put on the walk list
     int32_t* seedq;       // first match of the committed trajectory after its last re-seed
+    int32_t* trapped;     // last fix-up walk (or frozen fill) of the chunk was trapped (TRAP_P)
     int32_t stale_budget; // positions a stale-entry fix-up may walk without converging (0: no limit)
     int32_t* frozen;      // fix-up ended in a long literal run at the chunk end
     int32_t* flist;       // committed frozen chunks of the round
@@ -371,6 +380,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
     }
     if (lane == 0) A.status[j] = ST_OK;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.scal[5] = 0;   // frozen list of this round's commit
+    const int32_t x_entry = x, P_entry = P;
     const uint64_t dbg_t0 = DBG ? wall_clock64() : 0;
     uint64_t dbg_c[13] = {};   // matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail,
                                // t_hash, t_wide, wide positions
@@ -425,7 +435,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
             x = (x + 64 < scan_end) ? x + 64 : scan_end;
             if (x < scan_end) {
                 int32_t wend = budget_end;
-                if (kind == KIND_SPEC) {   // re-seed a stuck speculative walk (see RESEED_GAP)
+                if (kind == KIND_SPEC && A.round == 1) {   // re-seed a stuck first guess (see RESEED_GAP)
                     if (x - (lme > seed_x ? lme : seed_x) >= RESEED_GAP) {
                         seed_x = x;
                         const int32_t d = anchor_diag(A, x);
@@ -549,6 +559,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* 
             A.walked[j] = A.round;
             // ended in a long literal run with P frozen at the chunk end: k_frozen_scan territory
             A.frozen[j] = !converged && x == hi_j && x - lme >= FROZEN_MIN;
+            A.trapped[j] = !converged && x - x_entry >= A.S / 2 && (P - P_entry < TRAP_P && P_entry - P < TRAP_P);
         }
         A.status[j] = converged ? ST_CONV : ST_DONE;
     }
@@ -647,6 +658,7 @@ __device__ void frozen_apply_wave(const WalkPtrs& A, int fbase, int fcap, int32_
                     A.exitP[q] = P;
                     A.changed[q] = 0;
                     A.seedq[q] = 0;
+                    A.trapped[q] = 0;
                 }
             }
             const unsigned long long fm = __ballot(fill);   // chunks are ordered: a prefix fills
@@ -675,6 +687,7 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
         A.plist[j] = j;
         A.lround[j] = 1;
         A.seedq[j] = 0;
+        A.trapped[j] = 0;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.scal[0] = 0; A.scal[1] = 0; A.scal[2] = startX; A.scal[3] = startP;
@@ -687,19 +700,51 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
 // entry state (predecessor's exit) differs from the one their trajectory used -> plist, scal[0].
 __global__ __launch_bounds__(1024) void k_round_tail(WalkPtrs A, int fbase, int fcap) {
     __shared__ int32_t sj[FROZEN_MAX], sy[FROZEN_MAX];
+    __shared__ int32_t trig[RESPEC_MAX_TRIGGERS];
+    __shared__ int32_t ntrig;
     if (threadIdx.x < 64 && fcap > 0) frozen_apply_wave(A, fbase, fcap, sj, sy);
-    if (threadIdx.x == 0) A.scal[0] = 0;
+    if (threadIdx.x == 0) { A.scal[0] = 0; ntrig = 0; }
     __syncthreads();
+    const int32_t next = A.round + 1;
     for (int32_t j = (int32_t)threadIdx.x; j < A.C; j += (int32_t)blockDim.x) {
         const int32_t ex = j ? A.exitX[j - 1] : A.scal[2];
         const int32_t ep = j ? A.exitP[j - 1] : A.scal[3];
-        if (ex == INVALID) continue;
-        if (ex == A.usedX[j] && ep == A.usedP[j]) continue;
+        const bool pend = ex != INVALID && !(ex == A.usedX[j] && ep == A.usedP[j]);
+        if (!pend) {
+            if (A.lround[j] == next) A.lround[j] = A.round;   // listed by an earlier batch of this round
+            continue;
+        }
         A.snapX[j] = ex;
         A.snapP[j] = ep;
         A.kind[j] = KIND_FIX;
-        A.lround[j] = A.round + 1;
+        A.lround[j] = next;
         A.plist[atomicAdd(&A.scal[0], 1)] = j;
+        if (j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round) {
+            const int t = atomicAdd(&ntrig, 1);
+            if (t < RESPEC_MAX_TRIGGERS) trig[t] = j;
+        }
+    }
+    __syncthreads();
+    // re-speculate the still-speculative chunks after each trapped trigger (see TRAP_P)
+    const int nt = ntrig < RESPEC_MAX_TRIGGERS ? ntrig : RESPEC_MAX_TRIGGERS;
+    const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6), lane = lane_id();
+    for (int t = w; t < nt; t += nw) {
+        const int32_t j = trig[t], P = A.snapP[j];
+        for (int32_t q0 = j + 1; q0 <= j + RESPEC_AHEAD && q0 < A.C; q0 += 64) {
+            const int32_t q = q0 + lane;
+            // every chunk after a pending one is unconfirmed, so replacing its trajectory by another
+            // guess never discards settled work; the run stops at the next pending chunk
+            const bool ok = q < A.C && q <= j + RESPEC_AHEAD && A.lround[q] != next;
+            const unsigned long long okm = __ballot(ok);
+            const unsigned long long run = ~okm ? okm & ((1ull << first_lane(~okm)) - 1) : okm;   // up to the first stop
+            if ((run >> lane) & 1ull) {
+                A.kind[q] = KIND_SPEC;
+                A.guess[q] = P;
+                A.lround[q] = next;
+                A.plist[atomicAdd(&A.scal[0], 1)] = q;
+            }
+            if (run != ~0ull) break;
+        }
     }
 }
 
@@ -1189,6 +1234,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.conv = c.take<int32_t>(C); A.changed = c.take<int32_t>(C); A.walked = c.take<int32_t>(C);
     A.lround = c.take<int32_t>(C);
     A.seedq = c.take<int32_t>(C);
+    A.trapped = c.take<int32_t>(C);
     A.frozen = c.take<int32_t>(C); A.flist = c.take<int32_t>(C);
     A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);

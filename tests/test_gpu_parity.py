@@ -240,3 +240,12 @@ def test_paren_large_vs_oracle(ctx, pieces):
     got, rc = _gpu_compress(ctx, rfa, tfa)
     assert rc == wrc
     assert got == want
+
+
+def test_trapped_chain_vs_oracle(ctx):
+    """chr22-shaped pair (hg18/hg19 lengths, seed 22): from ~45.8 Mb on the reference walk is trapped
+    on a poly-A window (chance hits keep nudging P), the case the walk re-speculates chunks for."""
+    rfa, tfa = synthlib.synth_pair("hg", 49_691_432, 51_304_566, 22)
+    got = ctx.compress(rfa, tfa)
+    assert ctx.stats()["walk_rounds"] < 40
+    assert got == oraclelib.compress(rfa, tfa)
