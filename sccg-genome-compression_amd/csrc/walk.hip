@@ -59,6 +59,7 @@ constexpr int32_t RESEED_GAP = 1024;
 constexpr int32_t TRAP_P = 4096;
 constexpr int RESPEC_AHEAD = 256;
 constexpr int RESPEC_MAX_TRIGGERS = 64;
+constexpr int32_t LONG_GAP = 4096;   // literal gaps of the record text copied grid-wide
 
 struct WalkPtrs {
     const uint8_t* R;
@@ -113,7 +114,9 @@ struct WalkPtrs {
     int32_t* fl;
     int64_t* tlen;            // per flat match: text length -> offsets
     int64_t* partial;
-    int64_t* scal64;          // [0] total matches [1] text bytes
+    int64_t* scal64;          // [0] total matches [1] text bytes [2] long literal gaps
+    int64_t* lgap;            // long literal gaps of the record text: (source, destination, length) triples
+    int64_t lgap_cap;
     uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
 };
 
@@ -1136,8 +1139,8 @@ __global__ void k_match_textlen(WalkPtrs A, int64_t nm, int abs_p) {
     }
 }
 
-// One thread per match: its literal gap (short ones by the thread, long ones by the whole wave)
-// and its "(dp,l)" token.
+// One thread per match: its literal gap (short ones by the thread, longer ones by the whole wave,
+// LONG_GAP and more queued for k_long_copy's grid) and its "(dp,l)" token.
 __global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int64_t nm, uint8_t* __restrict__ out,
                                                                 int abs_p) {
     constexpr int32_t SHORT_GAP = 32;
@@ -1152,7 +1155,11 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int6
         if (gap <= SHORT_GAP)
             for (int32_t q = 0; q < gap; q++) out[o + q] = A.T[pend + q];
     }
-    for (unsigned long long lm = __ballot(valid && gap > SHORT_GAP); lm; lm &= lm - 1) {
+    if (valid && gap >= LONG_GAP) {   // literal-heavy stretches: the whole grid copies them
+        const int64_t e = (int64_t)atomicAdd((unsigned long long*)&A.scal64[2], 1ull);
+        if (e < A.lgap_cap) { A.lgap[3 * e] = pend; A.lgap[3 * e + 1] = o; A.lgap[3 * e + 2] = gap; }
+    }
+    for (unsigned long long lm = __ballot(valid && gap > SHORT_GAP && gap < LONG_GAP); lm; lm &= lm - 1) {
         const int l = __ffsll((long long)lm) - 1;
         const int32_t gp = __shfl(pend, l, 64), gg = __shfl(gap, l, 64);
         const int64_t go = __shfl(o, l, 64);
@@ -1166,6 +1173,21 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int6
         *d++ = ',';
         d += write_i32(d, A.fl[i]);
         *d = ')';
+    }
+}
+
+// the queued long gaps, one after another, each spread over the whole grid (16 bytes per thread)
+__global__ void k_long_copy(WalkPtrs A, uint8_t* __restrict__ out) {
+    const int64_t ne = A.scal64[2] < A.lgap_cap ? A.scal64[2] : A.lgap_cap;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, G = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = 0; e < ne; e++) {
+        const uint8_t* src = A.T + A.lgap[3 * e];
+        uint8_t* dst = out + A.lgap[3 * e + 1];
+        const int64_t len = A.lgap[3 * e + 2];
+        for (int64_t b = tid * 16; b < len; b += G * 16) {
+            const int64_t nb = len - b < 16 ? len - b : 16;
+            for (int i = 0; i < nb; i++) dst[b + i] = src[b + i];
+        }
     }
 }
 
@@ -1253,6 +1275,8 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.tlen = c.take<int64_t>(maxm + 1);
     A.partial = c.take<int64_t>((size_t)scan_partials_needed((int64_t)(maxm > C ? maxm : C) + 1) + 16);
     A.scal64 = c.take<int64_t>(8);
+    A.lgap_cap = nT / LONG_GAP + 2;
+    A.lgap = c.take<int64_t>(3 * (size_t)A.lgap_cap);
     A.dbg = c.take<uint64_t>(C * DBG_SLOTS);
     *used = c.off;
     return A;
@@ -1724,9 +1748,11 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     if (nm > 0) {
         const unsigned g = grid_for(nm, 256) > 4096 ? 4096 : grid_for(nm, 256);
         hipLaunchKernelGGL(k_match_textlen, dim3(g), dim3(256), 0, s, A, nm, (int)abs_p);
+        RC(set_u64(reinterpret_cast<unsigned long long*>(A.scal64 + 2), {0}, s));
         RC(dev_excl_sum(A.tlen, A.tlen, nm, A.scal64 + 1, A.partial, s));
         PROF_LAUNCH(PROF_MATCH_EMIT, s, k_match_textwrite, dim3(grid_for(nm, SCCG_BLOCK)), dim3(SCCG_BLOCK), 0, s, A, nm, out,
                     (int)abs_p);
+        hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
         SCCG_HIP(hipGetLastError());
         int32_t lt[2];
         const RbItem it[3] = {{A.scal64 + 1, &text, (int)sizeof text}, {A.ft + nm - 1, &lt[0], 4}, {A.fl + nm - 1, &lt[1], 4}};
