@@ -45,6 +45,8 @@ enum Slot {
     B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC,
     // delta_encode's own token scan (targets holding '(')
     B_DX, B_DELTA,
+    // a second FASTA-strip scratch set (the reference strips beside the target, on the side stream)
+    B_TILE2_A, B_TILE2_B, B_TILE2_FA, B_TILE2_FB, B_TILE2_LAST, B_TILE2_OFF, B_TILE2_OFF2, B_TILE2_CARRY, B_TILE2_BSUM,
     B_COUNT
 };
 
@@ -251,24 +253,28 @@ int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n, hipStream_t s = 
 
 // strips one FASTA into `out` (and its filtered copy into out2, when given); returns the kept
 // length(s): h_len[0] strip, h_len[1] filter (d_len[0..1] on the device)
+// (set 1: the second scratch set, so two strips can run at once; s: stream, default the context's)
 int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const int64_t* d_hdr, uint8_t* out,
-          int64_t* d_len, int32_t* d_flags, int64_t* h_len, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr) {
+          int64_t* d_len, int32_t* d_flags, int64_t* h_len, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
+          int set = 0, hipStream_t s = nullptr) {
     const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE + 1;
+    const int o = set ? B_TILE2_A - B_TILE_A : 0;
+    static_assert(B_TILE_BSUM - B_TILE_A == B_TILE2_BSUM - B_TILE2_A, "scratch sets line up");
     IngestScratch sc;
-    GET(int64_t, ta, B_TILE_A, ntiles);
-    GET(int64_t, tb, B_TILE_B, ntiles);
-    GET(int64_t, tfa, B_TILE_FA, ntiles);
-    GET(int64_t, tfb, B_TILE_FB, ntiles);
-    GET(int32_t, tl, B_TILE_LAST, ntiles);
-    GET(int64_t, to, B_TILE_OFF, ntiles);
-    GET(int64_t, to2, B_TILE_OFF2, ntiles);
-    GET(int32_t, tc, B_TILE_CARRY, ntiles);
-    GET(int64_t, bs, B_TILE_BSUM, 1025 * 5);
+    GET(int64_t, ta, B_TILE_A + o, ntiles);
+    GET(int64_t, tb, B_TILE_B + o, ntiles);
+    GET(int64_t, tfa, B_TILE_FA + o, ntiles);
+    GET(int64_t, tfb, B_TILE_FB + o, ntiles);
+    GET(int32_t, tl, B_TILE_LAST + o, ntiles);
+    GET(int64_t, to, B_TILE_OFF + o, ntiles);
+    GET(int64_t, to2, B_TILE_OFF2 + o, ntiles);
+    GET(int32_t, tc, B_TILE_CARRY + o, ntiles);
+    GET(int64_t, bs, B_TILE_BSUM + o, 1025 * 5);
     sc.tile_a = ta; sc.tile_b = tb; sc.tile_fa = tfa; sc.tile_fb = tfb; sc.tile_last = tl; sc.tile_off = to;
     sc.tile_off2 = to2; sc.tile_carry = tc; sc.block_sums = bs; sc.scalars = nullptr;
-    TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, ctx->stream, fmode, out2,
+    TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, s ? s : ctx->stream, fmode, out2,
                            out2 ? d_len + 1 : nullptr));
-    return h_len ? d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1) : 0;   // h_len null: the caller reads d_len later
+    return h_len ? d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1, s) : 0;   // h_len null: the caller reads d_len later
 }
 
 // Both run lines of the stripped target (compression.cpp:341-368 lowercase, :495-522 N) in two
@@ -331,9 +337,14 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
 
     // ---- ingest (compression.cpp:181-220)
     // header search and both strips run back to back; one sync reads every length (sc[0..9])
+    // the reference strips on the side stream beside the target's header search + strip
+    HIPTRY(hipEventRecord(ctx->ev_fork, s));
+    HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side));
+    HIPTRY(hipEventRecord(ctx->ev_join, ctx->side));
     TRY(launch_find_header(tfa, tn, sc, s));
     TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp));
+    HIPTRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
     int64_t hsc[10];
     int32_t flags = 0;
     {
