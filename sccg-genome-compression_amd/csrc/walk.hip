@@ -346,8 +346,12 @@ __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L
 __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0);   // anchors, below
 
 constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail
+#ifndef WALK_WAVES_PER_EU
+#define WALK_WAVES_PER_EU 6
+#endif
 template <bool DBG>
-__global__ __launch_bounds__(SCCG_BLOCK) void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
+__global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
+void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
     __shared__ WalkLds lds_all[WPB];
     const int w = wave_in_block(), lane = lane_id();
     const int32_t li = (int32_t)blockIdx.x * WPB + w;

@@ -12,7 +12,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsccg.so")
+# SCCG_LIB_PATH: an alternative build of the same library (tuning runs compare variants)
+LIB_PATH = os.environ.get("SCCG_LIB_PATH") or os.path.join(HERE, "lib", "libsccg.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "sccg.h")
 
 SCCG_OK = 0
