@@ -35,6 +35,9 @@ constexpr int32_t INVALID = INT32_MIN;
 constexpr int ANCHOR_K = 32;
 constexpr int ANCHOR_STEP_DEFAULT = 32;   // reference sample stride (SCCG_ANCHOR_STEP for tuning runs)
 constexpr int ANCHOR_LOAD_DEFAULT = 4;    // table slots per sample (SCCG_ANCHOR_LOAD)
+#ifndef ANCHOR_PROBE_BATCHES
+#define ANCHOR_PROBE_BATCHES 2            // 64 target probes per batch per anchor vote (measured: 2 beats 4)
+#endif
 constexpr uint32_t A_MULTI = 0xFFFFFFFFu;    // anchor position of a 32-mer seen more than once
 constexpr int32_t FROZEN_MIN = 4096;   // literal bases at a chunk end that trigger a frozen-P scan
 constexpr int FROZEN_MAX = 256;        // frozen chunks handled per batch (grid.y of k_frozen_scan)
@@ -811,7 +814,7 @@ __global__ void k_anchor_build(WalkPtrs A) {
 // a lone hit is often a repeat copy), ties to the earliest; else the earliest; INVALID if none.
 __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0) {
     const int lane = lane_id();
-    constexpr int NB = 4;
+    constexpr int NB = ANCHOR_PROBE_BATCHES;
     int32_t dg[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
