@@ -45,6 +45,8 @@ int dev_set_i64(int64_t* p, int n, std::initializer_list<int64_t> vals, hipStrea
 int dev_set_i32(int32_t* p, int n, std::initializer_list<int32_t> vals, hipStream_t s);
 // stream-ordered write of up to 16 bytes (copied into the kernel arguments)
 int dev_put_bytes(uint8_t* p, const char* bytes, int n, hipStream_t s);
+// stream-ordered dst = pre, src[0, n), post (one launch)
+int dev_put_framed(uint8_t* dst, const uint8_t* src, int64_t n, char pre, char post, hipStream_t s);
 int64_t scan_partials_needed(int64_t n);
 int dev_excl_sum(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
                  hipStream_t s);
@@ -147,10 +149,12 @@ struct EmitTarget {
     void* user;
 };
 // (abs_p: absolute p on the record line, the text before delta_encode; late_out: out is ignored
-// and resolved through it)
+// and resolved through it; keep_flat: also keep the flat match list for global_matches, else the
+// text is written straight from the chunks' trajectories)
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m,
                           int chunk, void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len,
-                          WalkResult* res, hipStream_t s, bool abs_p = false, const EmitTarget* late_out = nullptr);
+                          WalkResult* res, hipStream_t s, bool abs_p = false, const EmitTarget* late_out = nullptr,
+                          bool keep_flat = true);
 // the raw match list of the last global_match_and_emit (device pointers inside ws)
 int global_matches(void* ws, const int32_t** t, const int32_t** p, const int32_t** l, int64_t* n);
 

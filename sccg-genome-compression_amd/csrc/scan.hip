@@ -108,9 +108,9 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(const int64_t* __restr
     }
 }
 
-// small inputs (<= 8 Ki elements): one 1024-thread block, one launch; a thread's (<= 8) loads are
+// small inputs (<= 16 Ki elements): one 1024-thread block, one launch; a thread's (<= 16) loads are
 // issued together
-constexpr int SMALL_PER = 8;
+constexpr int SMALL_PER = 16;
 template <class Op>
 __global__ __launch_bounds__(1024) void k_small_scan(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ out,
                                                      int64_t* __restrict__ total) {
@@ -174,6 +174,22 @@ __global__ void k_set_u8(uint8_t* p, int n, Bytes16 v) {
 }
 
 }  // namespace
+
+namespace {
+// dst = pre, src[0, n), post
+__global__ void k_put_framed(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t n, uint8_t pre,
+                             uint8_t post) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + 2; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = i == 0 ? pre : (i == n + 1 ? post : src[i - 1]);
+}
+}  // namespace
+
+int dev_put_framed(uint8_t* dst, const uint8_t* src, int64_t n, char pre, char post, hipStream_t s) {
+    const unsigned g = grid_for(n + 2, 256) > 1024 ? 1024 : grid_for(n + 2, 256);
+    hipLaunchKernelGGL(k_put_framed, dim3(g), dim3(256), 0, s, dst, src, n, (uint8_t)pre, (uint8_t)post);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
 
 int dev_put_bytes(uint8_t* p, const char* bytes, int n, hipStream_t s) {
     Bytes16 v{};

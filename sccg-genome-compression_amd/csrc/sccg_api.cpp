@@ -492,13 +492,9 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
             static int call(void* u, uint8_t** o) { return static_cast<Late*>(u)->f(o); }
         } late{[&](uint8_t** o) -> int {
             TRY(join_lines());
-            TRY(dev_put_bytes(out + pos, "\n", 1, s));
-            pos += 1;
             const int64_t nlen = rl_len[1];
-            if (nlen) HIPTRY(hipMemcpyAsync(out + pos, nline, (size_t)nlen, hipMemcpyDeviceToDevice, s));
-            pos += nlen;
-            TRY(dev_put_bytes(out + pos, "\n", 1, s));
-            pos += 1;
+            TRY(dev_put_framed(out + pos, nline, nlen, '\n', '\n', s));   // "\n" + N line + "\n"
+            pos += nlen + 2;
             X = out + pos;
             if (paren) {
                 GET(uint8_t, xb, B_DX, out_cap - pos);
@@ -511,7 +507,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         WalkResult wr{};
         int64_t rlen = 0;
         TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(), ws, wsb, nullptr, &rlen, &wr, s, paren,
-                                  &target));
+                                  &target, /*keep_flat=*/false));
         if (!X) return ctx->fail(SCCG_E_INTERNAL, "record text position never resolved");
         if (paren) TRY(paren_delta(ctx, X, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
         st.n_matches = wr.n_matches;

@@ -119,6 +119,8 @@ struct WalkPtrs {
     int64_t* partial;
     int64_t* scal64;          // [0] total matches [1] text bytes [2] long literal gaps
     int64_t* lgap;            // long literal gaps of the record text: (source, destination, length) triples
+    int64_t* cprev;           // per chunk: last earlier chunk holding a match (max-scan), then text offsets
+    int64_t* ctext;           // per chunk: record text bytes of its target range -> offsets
     int64_t lgap_cap;
     uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
 };
@@ -1183,17 +1185,138 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int6
     }
 }
 
-// the queued long gaps, one after another, each spread over the whole grid (16 bytes per thread)
-__global__ void k_long_copy(WalkPtrs A, uint8_t* __restrict__ out) {
+// ---------------------------------------------------------------------------------------------
+// Record text straight from the chunks' final trajectories (no flattened match list): the chunks'
+// target ranges [usedX, exitX) tile the target (the last one runs to |T'|), so chunk j's text is
+// its literal gaps and "(dp,l)" tokens, dp taken against the last match of an earlier chunk (or
+// the first step's).  Chunk 0 also carries the first step: T'[0, first_y) and its token.
+// ---------------------------------------------------------------------------------------------
+struct FirstMatch {
+    int32_t y, p, l, valid;
+};
+
+__global__ void k_chunk_meta(WalkPtrs A) {
+    for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
+        const int32_t n = A.cnt[A.cur[j]][j];
+        A.cprev[j] = n > 0 ? j : -1;   // -> exclusive max-scan: the last earlier chunk with a match
+        A.flat_off[j] = n;             // -> exclusive sum: match count
+    }
+}
+
+__device__ __forceinline__ int64_t token_len(int32_t d, int32_t l) { return 3 + ndigits_i32(d) + ndigits_i32(l); }
+__device__ __forceinline__ int write_token(uint8_t* o, int32_t d, int32_t l) {
+    uint8_t* q = o;
+    *q++ = '(';
+    q += write_i32(q, d);
+    *q++ = ',';
+    q += write_i32(q, l);
+    *q++ = ')';
+    return (int)(q - o);
+}
+
+// wave per chunk: WRITE = false -> ctext[j] = its text bytes; WRITE = true -> the text at ctext[j]
+template <bool WRITE>
+__global__ __launch_bounds__(SCCG_BLOCK) void k_chunk_text(WalkPtrs A, FirstMatch F, int abs_p, uint8_t* __restrict__ out) {
+    constexpr int32_t SHORT_GAP = 32;
+    const int32_t j = (int32_t)blockIdx.x * WPB + wave_in_block();
+    if (j >= A.C) return;
+    const int lane = lane_id();
+    const int32_t b = A.cur[j], n = A.cnt[b][j];
+    const int32_t* tt = A.bt[b] + (size_t)j * A.cap;
+    const int32_t* pp = A.bp[b] + (size_t)j * A.cap;
+    const int32_t* ll = A.bl[b] + (size_t)j * A.cap;
+    const int64_t x0 = A.usedX[j], end = j == A.C - 1 ? (int64_t)A.nT : (int64_t)A.exitX[j];
+    int32_t pprev = F.valid ? F.p : 0;
+    if (j > 0) {
+        const int64_t q = A.cprev[j];
+        if (q >= 0) pprev = A.bp[A.cur[q]][(size_t)q * A.cap + A.cnt[A.cur[q]][q] - 1];
+    }
+    if (abs_p) pprev = 0;
+    int64_t o = WRITE ? A.ctext[j] : 0;   // running output offset (wave-uniform)
+    // a literal stretch [src, src + len) at o: the lane / the wave / the whole grid (queued)
+    auto literal = [&](int64_t src, int64_t len, int64_t at, bool mine) {
+        if (!WRITE) return;
+        const bool lng = mine && len >= LONG_GAP, med = mine && len > SHORT_GAP && len < LONG_GAP;
+        if (mine && len <= SHORT_GAP)
+            for (int64_t q = 0; q < len; q++) out[at + q] = A.T[src + q];
+        if (lng) {
+            const int64_t e = (int64_t)atomicAdd((unsigned long long*)&A.scal64[2], 1ull);
+            if (e < A.lgap_cap) { A.lgap[3 * e] = src; A.lgap[3 * e + 1] = at; A.lgap[3 * e + 2] = len; }
+        }
+        for (unsigned long long lm = __ballot(med); lm; lm &= lm - 1) {
+            const int l = __ffsll((long long)lm) - 1;
+            const int64_t gs = __shfl(src, l, 64), gl = __shfl(len, l, 64), go = __shfl(at, l, 64);
+            for (int64_t q = lane; q < gl; q += 64) out[go + q] = A.T[gs + q];
+        }
+    };
+    if (j == 0 && F.valid) {   // the first step: T'[0, y) + its token (dp against 0)
+        literal(0, F.y, o, lane == 0);
+        o += F.y;
+        if (WRITE && lane == 0) write_token(out + o, F.p, F.l);
+        o += token_len(F.p, F.l);
+    }
+    int64_t last_end = x0;
+    for (int32_t b0 = 0; b0 < n; b0 += 64) {
+        const int32_t i = b0 + lane;
+        const bool valid = i < n;
+        int32_t t = 0, p = 0, l = 0, pe = 0, pv = 0;
+        if (valid) {
+            t = tt[i]; p = pp[i]; l = ll[i];
+            pe = i ? tt[i - 1] + ll[i - 1] : (int32_t)x0;
+            pv = abs_p ? 0 : (i ? pp[i - 1] : pprev);
+        }
+        const int32_t d = (int32_t)((uint32_t)p - (uint32_t)pv);
+        const int64_t gap = valid ? (int64_t)(t - pe) : 0;
+        const int64_t len = valid ? gap + token_len(d, l) : 0;
+        const int64_t incl = wave_incl_add(len);
+        const int64_t at = o + incl - len;
+        literal(pe, gap, at, valid);
+        if (WRITE && valid) write_token(out + at + gap, d, l);
+        o += __shfl(incl, 63, 64);
+        const int32_t lastl = (n - b0 < 64 ? n - b0 : 64) - 1;
+        last_end = (int64_t)__shfl(t + l, lastl, 64);
+    }
+    // the chunk's trailing literal [last_end, end)
+    if (end > last_end) {
+        literal(last_end, end - last_end, o, lane == 0);
+        o += end - last_end;
+    }
+    if (!WRITE && lane == 0) A.ctext[j] = o;
+}
+
+// the queued long gaps: every gap is cut into 4 KiB pieces, numbered across the gaps in queue
+// order and dealt round-robin to the blocks; the queue is read through LDS 256 entries at a time
+__global__ __launch_bounds__(256) void k_long_copy(WalkPtrs A, uint8_t* __restrict__ out) {
+    constexpr int64_t PIECE = 4096;   // one 16-byte stretch per thread
+    __shared__ int64_t es[3 * 256];
     const int64_t ne = A.scal64[2] < A.lgap_cap ? A.scal64[2] : A.lgap_cap;
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, G = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = 0; e < ne; e++) {
-        const uint8_t* src = A.T + A.lgap[3 * e];
-        uint8_t* dst = out + A.lgap[3 * e + 1];
-        const int64_t len = A.lgap[3 * e + 2];
-        for (int64_t b = tid * 16; b < len; b += G * 16) {
-            const int64_t nb = len - b < 16 ? len - b : 16;
-            for (int i = 0; i < nb; i++) dst[b + i] = src[b + i];
+    int64_t pc = 0;   // pieces of the gaps before the current one (identical in every block)
+    for (int64_t e0 = 0; e0 < ne; e0 += 256) {
+        const int m = ne - e0 < 256 ? (int)(ne - e0) : 256;
+        __syncthreads();
+        if ((int)threadIdx.x < m)
+            for (int c = 0; c < 3; c++) es[3 * threadIdx.x + c] = A.lgap[3 * (e0 + threadIdx.x) + c];
+        __syncthreads();
+        for (int i = 0; i < m; i++) {
+            const int64_t len = es[3 * i + 2], np = (len + PIECE - 1) / PIECE;
+            // this block's first piece of the gap: the least g >= pc with g % gridDim.x == blockIdx.x
+            int64_t q = ((int64_t)blockIdx.x - pc % gridDim.x + gridDim.x) % gridDim.x;
+            for (; q < np; q += gridDim.x) {
+                const uint8_t* src = A.T + es[3 * i] + q * PIECE;
+                uint8_t* dst = out + es[3 * i + 1] + q * PIECE;
+                const int64_t plen = len - q * PIECE < PIECE ? len - q * PIECE : PIECE;
+                const int64_t b = (int64_t)threadIdx.x * 16;
+                if (b + 16 <= plen) {
+                    uint8_t v[16];
+#pragma unroll
+                    for (int k2 = 0; k2 < 16; k2++) v[k2] = src[b + k2];
+#pragma unroll
+                    for (int k2 = 0; k2 < 16; k2++) dst[b + k2] = v[k2];
+                } else {
+                    for (int64_t k2 = b; k2 < plen; k2++) dst[k2] = src[k2];
+                }
+            }
+            pc += np;
         }
     }
 }
@@ -1284,6 +1407,8 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.scal64 = c.take<int64_t>(8);
     A.lgap_cap = nT / LONG_GAP + 2;
     A.lgap = c.take<int64_t>(3 * (size_t)A.lgap_cap);
+    A.cprev = c.take<int64_t>(C + 1);
+    A.ctext = c.take<int64_t>(C + 1);
     A.dbg = c.take<uint64_t>(C * DBG_SLOTS);
     *used = c.off;
     return A;
@@ -1484,7 +1609,7 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
                           void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
-                          bool abs_p, const EmitTarget* late_out) {
+                          bool abs_p, const EmitTarget* late_out, bool keep_flat) {
     if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
     size_t used = 0;
     WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
@@ -1727,8 +1852,42 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     }
 
     mark("rounds");
-    // ---- flatten: first match, then every chunk's trajectory
     const int32_t nfirst = first_y != INVALID ? 1 : 0;
+    if (!keep_flat) {
+        // ---- record text straight from the chunks (k_chunk_text): no flattened match list
+        if (late_out) RC(late_out->resolve(late_out->user, &out));   // the caller's text position is known now
+        int64_t text = 0, nmc = 0;
+        if (startP != INVALID && lastk >= 0) {
+            const unsigned gc = grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256);
+            hipLaunchKernelGGL(k_chunk_meta, dim3(gc), dim3(256), 0, s, A);
+            RC(dev_excl_max(A.cprev, A.cprev, A.C, nullptr, A.partial, s));
+            RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
+            RC(set_u64(reinterpret_cast<unsigned long long*>(A.scal64 + 2), {0}, s));
+            const FirstMatch F{first_y, first_p, first_l, nfirst};
+            hipLaunchKernelGGL(k_chunk_text<false>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F, (int)abs_p, out);
+            RC(dev_excl_sum(A.ctext, A.ctext, A.C, A.scal64 + 1, A.partial, s));
+            PROF_LAUNCH(PROF_MATCH_EMIT, s, k_chunk_text<true>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F,
+                        (int)abs_p, out);
+            hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
+            SCCG_HIP(hipGetLastError());
+            int64_t r[2];
+            const RbItem it{A.scal64, r, (int)sizeof r};
+            RC(dev_readback(&it, 1, s));
+            nmc = r[0];
+            text = r[1];
+        } else if (nTp > 0) {   // no first match: the whole target is one literal
+            const unsigned g = grid_for(nTp, 256) > 8192 ? 8192 : grid_for(nTp, 256);
+            hipLaunchKernelGGL(k_copy, dim3(g), dim3(256), 0, s, Tp, nTp, out);
+            SCCG_HIP(hipGetLastError());
+            text = nTp;
+        }
+        res->n_matches = nmc + nfirst;
+        g_last_n = 0;
+        *out_len = text;
+        mark("emit");
+        return 0;
+    }
+    // ---- flatten: first match, then every chunk's trajectory
     hipLaunchKernelGGL(k_chunk_counts, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
     RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
     if (nfirst) {
