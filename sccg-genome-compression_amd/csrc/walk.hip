@@ -373,7 +373,18 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
     if (kind == KIND_SPEC) {
         ob = uni(A.cur[j]);
         x = lo_j;
-        P = uni(A.guess[j]);
+        if (A.round == 1) {   // first guess: the anchor vote at the chunk start (anchor_diag)
+            const int32_t d = anchor_diag(A, lo_j);
+            P = INVALID;
+            if (d != INVALID) {
+                int64_t gp = (int64_t)lo_j - 1 + d;
+                P = (int32_t)(gp < 0 ? 0 : (gp > A.nR - 1 ? A.nR - 1 : gp));
+            }
+            P = uni(P);
+            if (lane == 0) A.guess[j] = P;
+        } else {
+            P = uni(A.guess[j]);   // re-speculation (k_round_tail)
+        }
         if (lane == 0) { A.usedX[j] = lo_j; A.usedP[j] = P; }
     } else if (kind == KIND_FIX) {   // result is committed (or discarded) by k_commit
         cb = uni(A.cur[j]);
@@ -851,18 +862,6 @@ __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0) {
     return g == INVALID ? first : g;
 }
 
-__global__ __launch_bounds__(SCCG_BLOCK) void k_anchor_lookup(WalkPtrs A) {
-    const int32_t j = (int32_t)blockIdx.x * WPB + wave_in_block();
-    if (j >= A.C) return;
-    int32_t g = anchor_diag(A, j * A.S);
-    if (g != INVALID) {
-        int64_t gp = (int64_t)j * A.S - 1 + g;
-        if (gp < 0) gp = 0;
-        if (gp > A.nR - 1) gp = A.nR - 1;
-        g = (int32_t)gp;
-    }
-    if (lane_id() == 0) A.guess[j] = g;
-}
 
 // ---------------------------------------------------------------------------------------------
 // exact full-reference candidate scans (the ungated first step and the p2 == 0 escalation)
@@ -1574,7 +1573,7 @@ int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
     const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
     if (!fused) PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
     if (A.amulti) hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
-    hipLaunchKernelGGL(k_anchor_lookup, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
+    // (the chunks' first guesses are voted by the round-1 walk itself: anchor_diag at each chunk start)
     SCCG_HIP(hipGetLastError());
     return 0;
 }
