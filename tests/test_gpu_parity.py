@@ -249,3 +249,17 @@ def test_trapped_chain_vs_oracle(ctx):
     got = ctx.compress(rfa, tfa)
     assert ctx.stats()["walk_rounds"] < 40
     assert got == oraclelib.compress(rfa, tfa)
+
+
+def test_chr21_vs_oracle(ctx):
+    """BASELINE configs[0] size: hg18/hg19 chr21 lengths (46.9 / 48.1 Mb), seed 21."""
+    rfa, tfa = synthlib.synth_pair("hg", 46_944_323, 48_129_895, 21)
+    assert ctx.compress(rfa, tfa) == oraclelib.compress(rfa, tfa)
+    assert ctx.stats()["mode_global"] == 1
+
+
+@pytest.mark.parametrize("seed", [81, 82, 83])
+def test_t2t_seeds_vs_oracle(ctx, seed):
+    """Literal-heavy walks (frozen and trapped chains, long literal gaps) at 4 Mb."""
+    rfa, tfa = synthlib.synth_pair("t2t", 4_000_000, 4_000_000, seed)
+    assert ctx.compress(rfa, tfa) == oraclelib.compress(rfa, tfa)
