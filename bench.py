@@ -55,6 +55,8 @@ def algorithmic_bytes(kernel: str, shape: dict) -> float | None:
         return None                   # per-launch bytes vary by round; see walk_bytes below
     if kernel in ("run_extract", "n_filter"):
         return float(nT + nT)
+    if kernel == "first_sweep_anchors":   # R' once + one 8-byte anchor slot per 32 reference bases
+        return float(nR + nR / 32 * 8)
     return None
 
 
