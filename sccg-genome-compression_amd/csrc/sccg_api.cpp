@@ -121,7 +121,7 @@ struct sccg_ctx {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;       // walk preparation, overlapping the local pass
     hipStream_t side2 = nullptr;      // header + run lines, overlapping the local pass
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr;
     std::string err;
     sccg_stats stats{};
     void* buf[B_COUNT] = {};
@@ -188,7 +188,9 @@ int sccg_ctx_create(int device, sccg_ctx** out) {
         hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_lines, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_lines, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_rstrip, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_hdr, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SCCG_E_HIP;
     }
@@ -209,6 +211,8 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_fork);
     (void)hipEventDestroy(ctx->ev_join);
     (void)hipEventDestroy(ctx->ev_lines);
+    (void)hipEventDestroy(ctx->ev_rstrip);
+    (void)hipEventDestroy(ctx->ev_hdr);
     (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->side2);
     (void)hipStreamDestroy(ctx->stream);
@@ -338,13 +342,28 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     // ---- ingest (compression.cpp:181-220)
     // header search and both strips run back to back; one sync reads every length (sc[0..9])
     // the reference strips on the side stream beside the target's header search + strip
+    global_prepare_reset();
     HIPTRY(hipEventRecord(ctx->ev_fork, s));
     HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side));
-    HIPTRY(hipEventRecord(ctx->ev_join, ctx->side));
+    HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
     TRY(launch_find_header(tfa, tn, sc, s));
+    HIPTRY(hipEventRecord(ctx->ev_hdr, s));
     TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
-    HIPTRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    // The walk's R'-only preparation (anchor samples, positions of the target's first k-mer read off
+    // its FASTA) starts on the side stream as soon as R' exists, beside the target's strip.
+    {
+        int64_t hr[2];
+        TRY(d2h_i64(ctx, sc + 7, hr, 2, ctx->side));   // |R|, |R'|
+        if (hr[1] < INT32_MAX - 8 && tn < INT32_MAX - 8) {
+            HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
+            const size_t wsb_early = walk_workspace_bytes(hr[1], tn, 14, walk_chunk());   // |T'| <= tn
+            void* ws_early = ctx->get(B_WALK, wsb_early);
+            if (!ws_early) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb_early);
+            TRY(global_sweep_early(Rp, hr[1], tfa, tn, sc, 14, 100, walk_chunk(), ws_early, wsb_early, ctx->side));
+        }
+    }
+    HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
     int64_t hsc[10];
     int32_t flags = 0;
     {

@@ -63,6 +63,7 @@ constexpr int32_t TRAP_P = 4096;
 constexpr int RESPEC_AHEAD = 256;
 constexpr int RESPEC_MAX_TRIGGERS = 64;
 constexpr int32_t LONG_GAP = 4096;   // literal gaps of the record text copied grid-wide
+constexpr int32_t CAND_CAP = 65536;  // early sweep: first-k-mer occurrences kept (more: full sweep later)
 
 struct WalkPtrs {
     const uint8_t* R;
@@ -111,6 +112,8 @@ struct WalkPtrs {
     unsigned long long* fc;   // full-candidate scan scalars: [0] lmax [1] cnt [2] has0 [3] minkey [4] firsthit [5] firstexo
                               // [8..11] the same four for the batch's first position (k_presence + k_cand_reduce)
     unsigned long long* fcb;  // per presence block: 4 candidate statistics
+    int32_t* cand;            // early sweep: reference positions of the target's first k-mer (fc[13] of them)
+    uint8_t* kb;              // early sweep: the target's first k bytes of T', read from its FASTA
     int64_t* flat_off;        // per chunk
     int32_t* ft;
     int32_t* fp;
@@ -1097,6 +1100,111 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Early sweep: the anchor samples need only R', and the first step's k-mer is the first k bytes of
+// T', which can be read straight off the target FASTA.  So the R' sweep runs as soon as R' exists,
+// beside the target's strip: it stores the anchors and the positions of that k-mer (k_sweep_early);
+// once T' exists, k_cand_stats extends those positions -- what k_key0 + k_cand_reduce would give.
+// fc[12]: 1 = early statistics valid, 2 = not usable (too many positions, exotic key, or the FASTA
+// reading disagreed with T') -> the caller runs the full k_key0 sweep.  fc[13]: positions found.
+// ---------------------------------------------------------------------------------------------
+// one wave: the first k bytes of T' (strip + toupper + N erase of the target FASTA, the header line
+// [hdr[0], hdr[1]) excluded) within the first `limit` FASTA bytes -> kb[0, k), their count -> kb[16..19]
+__global__ void k_first_kmer(const uint8_t* __restrict__ fa, int64_t n, const int64_t* __restrict__ hdr, int k,
+                             int64_t limit, uint8_t* __restrict__ kb) {
+    const int lane = lane_id();
+    const int64_t h = hdr[0], he = hdr[1];
+    const int64_t end = n < limit ? n : limit;
+    int found = 0;
+    for (int64_t base = 0; base < end && found < k; base += 64 * 16) {
+        uint32_t keep = 0;
+        uint8_t b[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int64_t p = base + 16 * lane + i;
+            b[i] = p < end ? fa[p] : (uint8_t)' ';
+            const bool kp = p < end && !(p >= h && p < he) && !c_isspace(b[i]) && c_toupper(b[i]) != 'N';
+            keep |= (uint32_t)kp << i;
+        }
+        const int cnt = __popc(keep);
+        const int incl = wave_incl_add(cnt);
+        int idx = found + incl - cnt;
+        for (int i = 0; i < 16; i++)
+            if ((keep >> i) & 1u) { if (idx < k) kb[idx] = c_toupper(b[i]); idx++; }
+        found += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) *reinterpret_cast<int32_t*>(kb + 16) = found < k ? found : k;
+}
+
+template <bool ANCH>
+__global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
+    const int k = A.k;
+    const bool have = *reinterpret_cast<const int32_t*>(A.kb + 16) == k;
+    const uint32_t key0 = have ? walk_key(A.kb, k) : KEY_EXOTIC;
+    const bool want = key0 < KEY_EXOTIC;
+    sweep_kmers_w(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) { return want && pure && code == key0; },
+                  [&](int64_t c) {
+                      const unsigned long long i = atomicAdd(&A.fc[13], 1ull);
+                      if (i < (unsigned long long)CAND_CAP) A.cand[i] = (int32_t)c;
+                  },
+                  [&](int64_t p0, const uint32_t (&cw)[20], const uint32_t (&dw)[20], uint32_t acc) {
+                      if (!ANCH) return;
+#pragma unroll
+                      for (int h = 0; h < 2; h++) {
+                          const int64_t p = p0 + 32 * h;
+                          if (p + ANCHOR_K > A.nR) break;
+                          uint64_t code = 0;
+                          uint32_t bad = 0;
+#pragma unroll
+                          for (int i = 0; i < 8; i++) {
+                              code |= (uint64_t)cw[8 * h + i] << (8 * i);
+                              bad |= dw[8 * h + i];
+                          }
+                          if (acc && bad) continue;
+                          const uint64_t key = mix64(code);
+                          A.atab[key >> (64 - A.abits)] = ((uint64_t)anchor_tag(key, A.agen) << 32) | (uint32_t)p;
+                      }
+                  });
+}
+
+// one block, after T' exists: statistics of x0 = 0 over the early sweep's positions (as k_key0 +
+// k_cand_reduce would leave them in fc[4..11])
+__global__ __launch_bounds__(1024) void k_cand_stats(WalkPtrs A) {
+    __shared__ CandBest wbest[16];
+    __shared__ int ok;
+    const int k = A.k;
+    const unsigned long long cnt = A.fc[13];
+    if (threadIdx.x == 0) {
+        bool good = *reinterpret_cast<const int32_t*>(A.kb + 16) == k && cnt <= (unsigned long long)CAND_CAP &&
+                    walk_key(A.kb, k) < KEY_EXOTIC && A.nT >= k;
+        for (int i = 0; good && i < k; i++) good = A.kb[i] == A.T[i];
+        ok = good;
+        A.fc[12] = good ? 1 : 2;
+    }
+    __syncthreads();
+    if (!ok) return;
+    // one position per wave at a time, extended by the whole wave (wave_lce: 2 KiB per round trip)
+    CandBest v{0, 0, 0, ~0ull};
+    const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
+    for (unsigned long long i = w; i < cnt; i += nw) {
+        const int32_t c = A.cand[i];
+        int32_t maxlen = A.nR - (c + k);
+        if (A.nT - k < maxlen) maxlen = A.nT - k;
+        const uint32_t l = (uint32_t)(k + wave_lce(A.R, c + k, A.T, k, maxlen));
+        v = cb_merge(v, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key(c, -1) : ~0ull});
+    }
+    if (lane_id() != 0) v = CandBest{0, 0, 0, ~0ull};   // the wave's lanes hold the same value: keep one
+    v = cb_wave(v);
+    if (lane_id() == 0) wbest[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); i++) v = cb_merge(v, wbest[i]);
+        A.fc[8] = v.l; A.fc[9] = v.cnt; A.fc[10] = v.has0; A.fc[11] = v.minkey;
+        A.fc[4] = v.cnt ? 0ull : ~0ull;
+        A.fc[5] = ~0ull;
+    }
+}
+
 // fc[8..11] = statistics merged over the sweep's blocks; with x0 >= 0 (after k_key0) also
 // fc[4] = x0 when x0's k-mer has a candidate, fc[5] = none
 __global__ __launch_bounds__(1024) void k_cand_reduce(WalkPtrs A, int nblk, int32_t x0) {
@@ -1112,7 +1220,7 @@ __global__ __launch_bounds__(1024) void k_cand_reduce(WalkPtrs A, int nblk, int3
     if (threadIdx.x == 0) {
         for (int i = 1; i < (int)(blockDim.x >> 6); i++) v = cb_merge(v, wbest[i]);
         A.fc[8] = v.l; A.fc[9] = v.cnt; A.fc[10] = v.has0; A.fc[11] = v.minkey;
-        if (x0 >= 0) { A.fc[4] = v.cnt ? (unsigned long long)x0 : ~0ull; A.fc[5] = ~0ull; }
+        if (x0 >= 0) { A.fc[4] = v.cnt ? (unsigned long long)x0 : ~0ull; A.fc[5] = ~0ull; A.fc[12] = 0; }
     }
 }
 
@@ -1366,6 +1474,18 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     if (A.C < 1) A.C = 1;
     A.cap = S / k + 4;
     const size_t C = (size_t)A.C, cap = (size_t)A.cap;
+    // front: what depends on R' alone (the early sweep fills it before |T'| is known)
+    A.abits = anchor_bits(nR);
+    A.astep = anchor_step();
+    {
+        static const int multi = env_int("SCCG_ANCHOR_MULTI", 0);
+        A.amulti = multi;
+    }
+    A.atab = c.take<uint64_t>((size_t)1 << A.abits);
+    A.fc = c.take<unsigned long long>(16);
+    A.fcb = c.take<unsigned long long>(4 * KEY0_GRID_MAX);
+    A.cand = c.take<int32_t>(CAND_CAP);
+    A.kb = c.take<uint8_t>(64);
     for (int b = 0; b < 2; b++) {
         A.bt[b] = c.take<int32_t>(C * cap);
         A.bp[b] = c.take<int32_t>(C * cap);
@@ -1389,15 +1509,6 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.frozen = c.take<int32_t>(C); A.flist = c.take<int32_t>(C);
     A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);
-    A.abits = anchor_bits(nR);
-    A.astep = anchor_step();
-    {
-        static const int multi = env_int("SCCG_ANCHOR_MULTI", 0);
-        A.amulti = multi;
-    }
-    A.atab = c.take<uint64_t>((size_t)1 << A.abits);
-    A.fc = c.take<unsigned long long>(16);
-    A.fcb = c.take<unsigned long long>(4 * KEY0_GRID_MAX);
     A.flat_off = c.take<int64_t>(C + 1);
     const size_t maxm = (size_t)(nT / k + 2);
     A.ft = c.take<int32_t>(maxm); A.fp = c.take<int32_t>(maxm); A.fl = c.take<int32_t>(maxm);
@@ -1542,26 +1653,43 @@ struct Prepared {
 };
 thread_local Prepared g_prep;
 
-int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
-    const int32_t lastk = A.nT - A.k;
-    const bool walkable = A.nR >= A.k && lastk >= 0;
-    if (!walkable) return 0;
+struct Early {   // an early sweep queued by global_sweep_early
+    const void* ws = nullptr;
+    const uint8_t* R = nullptr;
+    int64_t nR = -1;
+    int k = 0;
+    uint32_t agen = 0;
+};
+thread_local Early g_early;
+
+unsigned first_sweep_grid(const WalkPtrs& A) {
     static const unsigned key0_grid = [] {
         const char* e = getenv("SCCG_KEY0_GRID");
         const int v = e ? atoi(e) : 1024;
         return (unsigned)(v >= 64 && v <= KEY0_GRID_MAX ? v : 1024);
     }();
-    const unsigned gsweep = grid_for(A.nR - A.k + 1, 256 * FC_PER_T) > key0_grid
-                                ? key0_grid : grid_for(A.nR - A.k + 1, 256 * FC_PER_T);
-    const int64_t slots = 1ll << A.abits;
-    // a fresh workspace is cleared once; afterwards every call's generation retires old slots
+    return grid_for(A.nR - A.k + 1, 256 * FC_PER_T) > key0_grid ? key0_grid : grid_for(A.nR - A.k + 1, 256 * FC_PER_T);
+}
+
+// the anchor table's generation for this call (a fresh workspace is cleared once; afterwards every
+// call's generation retires old slots)
+int anchor_generation(WalkPtrs& A, const void* ws, hipStream_t s) {
     static thread_local const void* ws_seen = nullptr;
     static thread_local uint32_t gen = 0;
     if (ws != ws_seen) {
-        SCCG_HIP(hipMemsetAsync(A.atab, 0, (size_t)slots * sizeof(uint64_t), s));
+        SCCG_HIP(hipMemsetAsync(A.atab, 0, ((size_t)1 << A.abits) * sizeof(uint64_t), s));
         ws_seen = ws;
     }
     A.agen = 0x9E3779B9u * ++gen;
+    return 0;
+}
+
+int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
+    const int32_t lastk = A.nT - A.k;
+    const bool walkable = A.nR >= A.k && lastk >= 0;
+    if (!walkable) return 0;
+    const unsigned gsweep = first_sweep_grid(A);
+    RC(anchor_generation(A, ws, s));
     // the usual first step: x0 = 0's own k-mer (statistics land in fc[4..11]); with the default
     // sample stride the same sweep stores the anchor samples
     const bool fused = A.astep == 32;
@@ -1592,7 +1720,33 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 
 }  // namespace
 
-void global_prepare_reset() { g_prep = Prepared{}; }
+void global_prepare_reset() { g_prep = Prepared{}; g_early = Early{}; }
+
+int global_sweep_early(const uint8_t* Rp, int64_t nRp, const uint8_t* tgt_fa, int64_t tn, const int64_t* d_hdr, int k,
+                       int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s) {
+    g_early = Early{};
+    if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
+    if (nRp < k || tn <= 0) return 0;   // no walk can use it
+    size_t used = 0;
+    // |T'| <= tn: the carve's R'-only front (anchor table, fc, positions, kb) does not depend on it
+    WalkPtrs A = make_ptrs(Rp, nRp, nullptr, tn, k, m, chunk, ws, ws_bytes, &used);
+    if (used > ws_bytes) return SCCG_E_INTERNAL;
+    RC(anchor_generation(A, ws, s));
+    RC(set_u64(A.fc + 12, {0, 0}, s));
+    hipLaunchKernelGGL(k_first_kmer, dim3(1), dim3(64), 0, s, tgt_fa, tn, d_hdr, k, (int64_t)1 << 20, A.kb);
+    const unsigned g = first_sweep_grid(A);
+    if (A.astep == 32) {
+        PROF_LAUNCH(PROF_ANCHOR, s, k_sweep_early<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
+    } else {
+        hipLaunchKernelGGL(k_sweep_early<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
+        const int64_t ns = (int64_t)A.nR / A.astep + 1;
+        const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
+        PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
+    }
+    SCCG_HIP(hipGetLastError());
+    g_early = Early{ws, Rp, nRp, k, A.agen};
+    return 0;
+}
 
 int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
                    size_t ws_bytes, hipStream_t s) {
@@ -1601,7 +1755,23 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
     size_t used = 0;
     WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
     if (used > ws_bytes) return SCCG_E_INTERNAL;
-    RC(queue_prepare(A, ws, s));
+    const Early e = g_early;
+    g_early = Early{};
+    if (e.ws == ws && e.R == Rp && e.nR == nRp && e.k == k) {
+        // the early sweep already stored the anchors and the first k-mer's positions
+        A.agen = e.agen;
+        if (A.nR >= A.k && A.nT >= A.k) {
+            hipLaunchKernelGGL(k_cand_stats, dim3(1), dim3(1024), 0, s, A);
+            if (A.amulti) {
+                const int64_t ns = (int64_t)A.nR / A.astep + 1;
+                const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
+                hipLaunchKernelGGL(k_anchor_build<true>, dim3(ga), dim3(256), 0, s, A);
+            }
+            SCCG_HIP(hipGetLastError());
+        }
+    } else {
+        RC(queue_prepare(A, ws, s));
+    }
     g_prep = Prepared{ws, Rp, Tp, nRp, nTp, k, m, chunk, A.agen};
     return 0;
 }
@@ -1645,8 +1815,16 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     int32_t first_y = INVALID, first_p = 0, first_l = 0;
     if (walkable) {
         int32_t x0 = 0;
-        unsigned long long r[8];   // fc[4..11]: first hit, first exotic, statistics of the batch's x0
+        unsigned long long r[9];   // fc[4..11]: first hit, first exotic, statistics of the batch's x0; fc[12]
         {
+            const RbItem it{A.fc + 4, r, (int)sizeof r};
+            RC(dev_readback(&it, 1, s));
+        }
+        if (r[8] == 2) {   // the early sweep's statistics are not usable: the full first-step sweep
+            const unsigned g = first_sweep_grid(A);
+            hipLaunchKernelGGL(k_key0<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, A, 0);
+            hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)g, 0);
+            SCCG_HIP(hipGetLastError());
             const RbItem it{A.fc + 4, r, (int)sizeof r};
             RC(dev_readback(&it, 1, s));
         }
