@@ -115,11 +115,12 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
                       int64_t seg_end, uint32_t* recs, SegStat* stat, hipStream_t s);
 // switch FSM (compression.cpp:395-473) over segments [seg0, seg_end) from counter state *state
 // (min(mismatch, 5); 6 = switched): *switch_seg = first segment where mismatch > T2, or -1
-// every local segment of a compress (k = 14, then k2 = 10 without a match) and the switch point:
+// every local segment of a compress (k = 14, then k2 = 10 without a match) and the switch point
+// (|R|, |T| read from device memory, so no host sync precedes it; nseg_max bounds the grid):
 // ctl = {unused 0, early-exit bound INT32_MAX, switch segment INT32_MAX (= none), 0} on
 // entry; cls: per-segment classes tagged with gen (never cleared: zero-filled once, gen >= 1)
-int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t nseg, uint32_t* recs,
-                     SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s);
+int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
+                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s);
 // record text for local mode (delta-encoded, compression.cpp:406-415 + :222-304) + leftover
 // (abs_p: "(p," with absolute p instead, the text before delta_encode)
 int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_t* recs,

@@ -406,12 +406,21 @@ __device__ __forceinline__ int seg_class(const SegStat& s) {
 }
 __device__ __forceinline__ bool mism(int c) { return c == 1 || c == 2; }
 
+// The lengths come from device memory (the FASTA strips' counts), so the launch needs no host sync.
+__device__ __forceinline__ int32_t seg_count(int64_t nR, int64_t nT) {
+    const int64_t a = (nR + SEG_L - 1) / SEG_L, b = (nT + SEG_L - 1) / SEG_L;
+    const int64_t n = a < b ? a : b;
+    return n >= INT32_MAX / 2 ? 0 : (int32_t)n;   // beyond int positions: the host reports it
+}
+
 template <bool DBG>
-__global__ __launch_bounds__(SCCG_BLOCK) void k_local_all(const uint8_t* __restrict__ R, int64_t nR,
-                                                          const uint8_t* __restrict__ T, int64_t nT, int32_t nseg,
+__global__ __launch_bounds__(SCCG_BLOCK) void k_local_all(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
+                                                          const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
                                                           uint32_t* __restrict__ recs, SegStat* __restrict__ stat,
                                                           int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl) {
     __shared__ SegLds lds_all[WPB];
+    const int64_t nR = *dnR, nT = *dnT;
+    const int32_t nseg = seg_count(nR, nT);
     const int w = wave_in_block(), lane = lane_id();
     SegLds& L = lds_all[w];
     const int32_t G = (int32_t)gridDim.x * WPB;
@@ -447,16 +456,18 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_all(const uint8_t* __restr
     }
 }
 
-__global__ void k_switch_final(const int32_t* __restrict__ cls, int32_t gen, int32_t nseg, int32_t* __restrict__ ctl) {
-    const int32_t e = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x) + 4;
-    if (e >= nseg) return;
-    int k[5];
+__global__ void k_switch_final(const int32_t* __restrict__ cls, int32_t gen, const int64_t* __restrict__ dnR,
+                               const int64_t* __restrict__ dnT, int32_t* __restrict__ ctl) {
+    const int32_t nseg = seg_count(*dnR, *dnT);
+    for (int32_t e = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x) + 4; e < nseg; e += (int32_t)(gridDim.x * blockDim.x)) {
+        int k[5];
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-        const int32_t t = cls[e - 4 + i];
-        k[i] = (t >> 2) == gen ? (t & 3) : -1;
+        for (int i = 0; i < 5; i++) {
+            const int32_t t = cls[e - 4 + i];
+            k[i] = (t >> 2) == gen ? (t & 3) : -1;
+        }
+        if (k[4] == 2 && mism(k[0]) && mism(k[1]) && mism(k[2]) && mism(k[3])) atomicMin(&ctl[2], e);
     }
-    if (k[4] == 2 && mism(k[0]) && mism(k[1]) && mism(k[2]) && mism(k[3])) atomicMin(&ctl[2], e);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -615,10 +626,9 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
     return 0;
 }
 
-int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t nseg, uint32_t* recs,
-                     SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s) {
-    if (nseg <= 0) return 0;
-    if (nseg >= INT32_MAX / 2) return SCCG_E_UNSUPPORTED;
+int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
+                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s) {
+    if (nseg_max <= 0) return 0;
     // resident capacity: the grid drains the counter, extra blocks would only find it exhausted
     static const unsigned cap = [] {
         int dev = 0, cus = 256, per = 4;
@@ -627,14 +637,14 @@ int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT,
             per = 4;
         return (unsigned)(cus * per);
     }();
-    unsigned g = grid_for(nseg, WPB);
+    unsigned g = grid_for(nseg_max, WPB);
     if (g > cap) g = cap;
     static const bool dbg = getenv("SCCG_DEBUG") != nullptr;
     if (dbg) {
         const unsigned long long z[16] = {};
         SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
-        PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, nR, T, nT, (int32_t)nseg, recs,
-                    stat, cls, gen, ctl);
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
+                    gen, ctl);
         unsigned long long d[16];
         SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
         SCCG_HIP(hipStreamSynchronize(s));
@@ -644,12 +654,13 @@ int launch_local_all(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT,
                 d[0] / n / 100, d[1] / n / 100, d[2] / n / 100, d[3] / n / 100, d[4] / n / 100, d[6] / 100.0, d[13], d[14],
                 d[8] / 100.0, d[9] / 100.0, d[10] / 100.0, d[11] / 100.0, d[12] / 100.0);
     } else {
-        PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, nR, T, nT, (int32_t)nseg, recs,
-                    stat, cls, gen, ctl);
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
+                    gen, ctl);
     }
-    if (nseg > 4)
-        hipLaunchKernelGGL(k_switch_final, dim3(grid_for(nseg - 4, 256)), dim3(256), 0, s, (const int32_t*)cls, gen,
-                           (int32_t)nseg, ctl);
+    if (nseg_max > 4) {
+        const unsigned gs = grid_for(nseg_max - 4, 256) > 2048 ? 2048 : grid_for(nseg_max - 4, 256);
+        hipLaunchKernelGGL(k_switch_final, dim3(gs), dim3(256), 0, s, (const int32_t*)cls, gen, d_nR, d_nT, ctl);
+    }
     SCCG_HIP(hipGetLastError());
     return 0;
 }

@@ -338,6 +338,8 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     GET(uint8_t, Rp, B_RP, rn + 64);
     int32_t* d_flags = reinterpret_cast<int32_t*>(sc + 32);
     HIPTRY(hipMemsetAsync(d_flags, 0, sizeof(int32_t), s));
+    // local pass control {0, early-exit bound, switch segment, 0}: INT32_MAX = none yet
+    TRY(dev_set_i64(sc + 20, 2, {(int64_t)INT32_MAX << 32, (int64_t)INT32_MAX}, s));
 
     // ---- ingest (compression.cpp:181-220)
     // header search and both strips run back to back; one sync reads every length (sc[0..9])
@@ -364,11 +366,36 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         }
     }
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
+    // ---- fork.  The local pass (compression.cpp:372-474, main stream) is latency-bound; the
+    //      global walk's input-only preparation (side stream) and the header + run lines (side2)
+    //      only read T/R/T'/R', so they run beside it.  The local pass reads |R|, |T| from device
+    //      memory and is queued before the host reads the lengths back (on side2).
+    hipStream_t s2 = ctx->side, s3 = ctx->side2;
+    HIPTRY(hipEventRecord(ctx->ev_fork, s));
+    HIPTRY(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
+    HIPTRY(hipStreamWaitEvent(s3, ctx->ev_fork, 0));
+    const int64_t iters_max = ((rn < tn ? rn : tn) + SEG_L - 1) / SEG_L;   // FASTA lengths bound the sequences'
+    GET(uint32_t, recs, B_RECS, (iters_max > 0 ? iters_max : 1) * SEG_REC_CAP);
+    GET(SegStat, stat, B_STAT, iters_max > 0 ? iters_max : 1);
+    GET(int32_t, cls, B_SEGCLS, iters_max > 0 ? iters_max : 1);
+    int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
+    if (iters_max > 0) {
+        if (cls != ctx->cls_buf || ctx->cap[B_SEGCLS] != ctx->cls_cap || ctx->cls_gen >= (1 << 28)) {
+            // new buffer (or tags about to wrap): zero it once, so no stale tag can match
+            HIPTRY(hipMemsetAsync(cls, 0, ctx->cap[B_SEGCLS], s));
+            ctx->cls_buf = cls;
+            ctx->cls_cap = ctx->cap[B_SEGCLS];
+            ctx->cls_gen = 0;
+        }
+        const int32_t gen = ++ctx->cls_gen;
+        // one launch over every segment; segments past a detected switch are never started
+        TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, s));
+    }
     int64_t hsc[10];
     int32_t flags = 0;
     {
         const RbItem it[2] = {{sc, hsc, (int)sizeof hsc}, {d_flags, &flags, (int)sizeof flags}};
-        TRY(dev_readback(it, 2, s));
+        TRY(dev_readback(it, 2, s3));
     }
     const int64_t hdr[2] = {hsc[0], hsc[1]}, lt[2] = {hsc[2], hsc[3]}, lr[2] = {hsc[7], hsc[8]};
     const int64_t nT = lt[0], nR = lr[0];
@@ -384,35 +411,9 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     const int64_t hlen = has_hdr ? hdr[1] - hdr[0] : 0;
     if (out_cap < hlen + 1 + 11 * nT + 64) return ctx->fail(SCCG_E_INVALID, "output capacity too small");
 
-    // ---- fork.  The local pass (compression.cpp:372-474, main stream) is latency-bound; the
-    //      global walk's input-only preparation (first-step sweep, anchor index; side stream)
-    //      and the header + run lines (side2) only read T/R/T'/R', so they run beside it.
-    hipStream_t s2 = ctx->side, s3 = ctx->side2;
-    HIPTRY(hipEventRecord(ctx->ev_fork, s));
-    HIPTRY(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
-    HIPTRY(hipStreamWaitEvent(s3, ctx->ev_fork, 0));
-
-    // ---- local segments (main stream; the switch point is read after the side work is queued)
     const int64_t nRs = (nR + SEG_L - 1) / SEG_L, nTs = (nT + SEG_L - 1) / SEG_L;
-    const int64_t iters = nRs < nTs ? nRs : nTs;
+    const int64_t iters = nRs < nTs ? nRs : nTs;   // segments the local pass took (its device count)
     int64_t sw = -1;
-    GET(uint32_t, recs, B_RECS, (iters > 0 ? iters : 1) * SEG_REC_CAP);
-    GET(SegStat, stat, B_STAT, iters > 0 ? iters : 1);
-    if (iters > 0) {
-        // one launch over every segment; segments past a detected switch are never started
-        GET(int32_t, cls, B_SEGCLS, iters);
-        if (cls != ctx->cls_buf || ctx->cap[B_SEGCLS] != ctx->cls_cap || ctx->cls_gen >= (1 << 28)) {
-            // new buffer (or tags about to wrap): zero it once, so no stale tag can match
-            HIPTRY(hipMemsetAsync(cls, 0, ctx->cap[B_SEGCLS], s));
-            ctx->cls_buf = cls;
-            ctx->cls_cap = ctx->cap[B_SEGCLS];
-            ctx->cls_gen = 0;
-        }
-        const int32_t gen = ++ctx->cls_gen;
-        int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
-        TRY(dev_set_i64(sc + 20, 2, {(int64_t)INT32_MAX << 32, (int64_t)INT32_MAX}, s));
-        TRY(launch_local_all(R, nR, T, nT, iters, recs, stat, cls, gen, ctl, s));
-    }
 
     // ---- the global walk's preparation, side stream (wasted only if the pass stays local)
     const int64_t np[2] = {lt[1], lr[1]};
