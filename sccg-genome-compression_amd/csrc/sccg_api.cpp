@@ -50,15 +50,21 @@ enum Slot {
     B_COUNT
 };
 
-constexpr int WALK_CHUNK_DEFAULT = 16384;
-// target bases per speculative walk chunk (SCCG_WALK_CHUNK overrides it for tuning runs)
-int walk_chunk() {
-    static const int v = [] {
+// Target bases per speculative walk chunk.  Larger chunks mean fewer convergence checks per base,
+// smaller ones more chunks in flight: chr1-sized targets (~7.7k chunks of 32 Ki) measured fastest at
+// 32 Ki, chromosomes under ~130 Mb and literal-heavy targets at 16 Ki, so the chunk follows the
+// target's size in 4 Ki steps between the two (SCCG_WALK_CHUNK overrides it for tuning runs).
+constexpr int WALK_CHUNK_MIN = 16384, WALK_CHUNK_MAX = 32768;
+constexpr int64_t WALK_CHUNKS_TARGET = 7800;
+int walk_chunk(int64_t target_bytes) {
+    static const int env = [] {
         const char* e = getenv("SCCG_WALK_CHUNK");
         const int c = e ? atoi(e) : 0;
-        return c >= 1024 && c <= (1 << 20) ? c : WALK_CHUNK_DEFAULT;
+        return c >= 1024 && c <= (1 << 20) ? c : 0;
     }();
-    return v;
+    if (env) return env;
+    const int64_t c = (target_bytes / WALK_CHUNKS_TARGET) & ~int64_t(4095);
+    return (int)(c < WALK_CHUNK_MIN ? WALK_CHUNK_MIN : c > WALK_CHUNK_MAX ? WALK_CHUNK_MAX : c);
 }
 constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide compares, tails)
 
@@ -359,10 +365,10 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         TRY(d2h_i64(ctx, sc + 7, hr, 2, ctx->side));   // |R|, |R'|
         if (hr[1] < INT32_MAX - 8 && tn < INT32_MAX - 8) {
             HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
-            const size_t wsb_early = walk_workspace_bytes(hr[1], tn, 14, walk_chunk());   // |T'| <= tn
+            const size_t wsb_early = walk_workspace_bytes(hr[1], tn, 14, walk_chunk(tn));   // |T'| <= tn
             void* ws_early = ctx->get(B_WALK, wsb_early);
             if (!ws_early) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb_early);
-            TRY(global_sweep_early(Rp, hr[1], tfa, tn, sc, 14, 100, walk_chunk(), ws_early, wsb_early, ctx->side));
+            TRY(global_sweep_early(Rp, hr[1], tfa, tn, sc, 14, 100, walk_chunk(tn), ws_early, wsb_early, ctx->side));
         }
     }
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
@@ -417,10 +423,10 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
 
     // ---- the global walk's preparation, side stream (wasted only if the pass stays local)
     const int64_t np[2] = {lt[1], lr[1]};
-    const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, walk_chunk());
+    const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, walk_chunk(tn));
     void* ws = ctx->get(B_WALK, wsb);
     if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
-    TRY(global_prepare(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(), ws, wsb, s2));
+    TRY(global_prepare(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(tn), ws, wsb, s2));
     HIPTRY(hipEventRecord(ctx->ev_join, s2));
 
     // ---- header + lowercase line (compression.cpp:337-368): side2, driven by the context's host
@@ -526,7 +532,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         const EmitTarget target{&Late::call, &late};
         WalkResult wr{};
         int64_t rlen = 0;
-        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(), ws, wsb, nullptr, &rlen, &wr, s, paren,
+        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(tn), ws, wsb, nullptr, &rlen, &wr, s, paren,
                                   &target, /*keep_flat=*/false));
         if (!X) return ctx->fail(SCCG_E_INTERNAL, "record text position never resolved");
         if (paren) TRY(paren_delta(ctx, X, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
@@ -779,13 +785,13 @@ int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, s
         GET(uint8_t, T, B_TP, nt + 64);
         if (nr) HIPTRY(hipMemcpyAsync(R, sr, nr, hipMemcpyHostToDevice, s));
         if (nt) HIPTRY(hipMemcpyAsync(T, st, nt, hipMemcpyHostToDevice, s));
-        const size_t wsb = walk_workspace_bytes((int64_t)nr, (int64_t)nt, k, walk_chunk());
+        const size_t wsb = walk_workspace_bytes((int64_t)nr, (int64_t)nt, k, walk_chunk((int64_t)nt));
         void* ws = ctx->get(B_WALK, wsb);
         GET(uint8_t, txt, B_OUT, 4 * nt + 64);
         if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace");
         WalkResult wr{};
         int64_t tl = 0;
-        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, k, m, walk_chunk(), ws, wsb, txt, &tl, &wr, s));
+        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, k, m, walk_chunk((int64_t)nt), ws, wsb, txt, &tl, &wr, s));
         const int32_t *dt, *dp, *dl;
         int64_t nm;
         global_matches(ws, &dt, &dp, &dl, &nm);
