@@ -107,10 +107,32 @@ __device__ unsigned long long g_local_dbg[16];
 
 // One segment with one k (pass 1: k = 14, pass 2: k2 = 10 on a segment pass 1 left without a match,
 // keeping pass 1's non-N flag); returns its statistics (wave-uniform), the records are in recs.
+// The words of a segment pair one lane loads (dword i = lane + 64 j, j < 4): the persistent local
+// pass loads its next segment's words before working on the current one, so the HBM round trip of
+// the load overlaps a whole segment's LDS work instead of starting each segment.
+struct SegWords {
+    uint32_t r[SEGB / 256], t[SEGB / 256];
+};
+__device__ __forceinline__ void seg_words_load(SegWords& W, int64_t seg, const uint8_t* __restrict__ R, int64_t nR,
+                                               const uint8_t* __restrict__ T, int64_t nT) {
+    const int lane = lane_id();
+    const int64_t base = seg * SEG_L;
+    const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
+    const int nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
+    const uint32_t* R4 = reinterpret_cast<const uint32_t*>(R + base);
+    const uint32_t* T4 = reinterpret_cast<const uint32_t*>(T + base);
+#pragma unroll
+    for (int j = 0; j < SEGB / 256; j++) {
+        const int i = lane + 64 * j, b0 = 4 * i;
+        W.r[j] = b0 < nr ? R4[i] : 0u;
+        W.t[j] = b0 < nt ? T4[i] : 0u;
+    }
+}
+
 template <int K, bool DBG>
 __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pass, int non_n_prev, int upper,
                                                  const uint8_t* __restrict__ R, int64_t nR, const uint8_t* __restrict__ T,
-                                                 int64_t nT, uint32_t* __restrict__ recs) {
+                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr) {
     const int lane = lane_id();
     const int64_t base = seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
@@ -129,9 +151,12 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
         const uint32_t* T4 = reinterpret_cast<const uint32_t*>(T + base);
         uint32_t* r4 = reinterpret_cast<uint32_t*>(L.r);
         uint32_t* t4 = reinterpret_cast<uint32_t*>(L.t);
-        for (int i = lane; i < SEGB / 4; i += 64) {
-            const int b0 = 4 * i;
-            uint32_t rw = b0 < nr ? R4[i] : 0u, tw = b0 < nt ? T4[i] : 0u;
+#pragma unroll
+        for (int j = 0; j < SEGB / 256; j++) {
+            const int i = lane + 64 * j, b0 = 4 * i;
+            uint32_t rw, tw;
+            if (pre) { rw = pre->r[j]; tw = pre->t[j]; }
+            else { rw = b0 < nr ? R4[i] : 0u; tw = b0 < nt ? T4[i] : 0u; }
             if (nr - b0 < 4) rw &= nr - b0 <= 0 ? 0u : (1u << (8 * (nr - b0))) - 1u;
             if (nt - b0 < 4) tw &= nt - b0 <= 0 ? 0u : (1u << (8 * (nt - b0))) - 1u;
             if (upper) { rw = upper4(rw); tw = upper4(tw); }
@@ -424,9 +449,13 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_all(const uint8_t* __restr
     const int w = wave_in_block(), lane = lane_id();
     SegLds& L = lds_all[w];
     const int32_t G = (int32_t)gridDim.x * WPB;
-    for (int32_t seg = (int32_t)blockIdx.x * WPB + w; seg < nseg; seg += G) {
+    SegWords cur, nxt;
+    int32_t seg = (int32_t)blockIdx.x * WPB + w;
+    if (seg < nseg) seg_words_load(cur, seg, R, nR, T, nT);
+    for (; seg < nseg; seg += G) {
         if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
-        SegStat st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs);
+        if (seg + G < nseg) seg_words_load(nxt, seg + G, R, nR, T, nT);   // in flight during this segment
+        SegStat st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, &cur);
         if (!st.pass) {
             wave_sync();
             st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs);
@@ -453,6 +482,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_all(const uint8_t* __restr
         if (hit != INT32_MAX && lane == 0)
             __hip_atomic_fetch_min(&ctl[1], hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         wave_sync();   // the next segment reuses this wave's LDS
+        cur = nxt;
     }
 }
 

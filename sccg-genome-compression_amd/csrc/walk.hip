@@ -1167,33 +1167,61 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
                   });
 }
 
-// one block, after T' exists: statistics of x0 = 0 over the early sweep's positions (as k_key0 +
-// k_cand_reduce would leave them in fc[4..11])
-__global__ __launch_bounds__(1024) void k_cand_stats(WalkPtrs A) {
-    __shared__ CandBest wbest[16];
+// after T' exists: statistics of x0 = 0 over the early sweep's positions (as k_key0 +
+// k_cand_reduce would leave them in fc[4..11]).  Grid-wide: every wave extends one position at a
+// time (wave_lce: 2 KiB per round trip), per-block results go to fcb and k_cand_stats_fin merges
+// them -- a repeat-rich first k-mer (hundreds of positions) no longer serialises on one block.
+constexpr int CAND_STATS_GRID = 256;
+__device__ __forceinline__ bool cand_stats_usable(const WalkPtrs& A) {
+    const int k = A.k;
+    bool good = *reinterpret_cast<const int32_t*>(A.kb + 16) == k && A.fc[13] <= (unsigned long long)CAND_CAP &&
+                walk_key(A.kb, k) < KEY_EXOTIC && A.nT >= k;
+    for (int i = 0; good && i < k; i++) good = A.kb[i] == A.T[i];
+    return good;
+}
+__global__ __launch_bounds__(SCCG_BLOCK) void k_cand_stats(WalkPtrs A) {
+    __shared__ CandBest wbest[SCCG_BLOCK / 64];
     __shared__ int ok;
     const int k = A.k;
     const unsigned long long cnt = A.fc[13];
+    if (threadIdx.x == 0) ok = cand_stats_usable(A);
+    __syncthreads();
+    CandBest v{0, 0, 0, ~0ull};
+    if (ok) {
+        const unsigned long long nw = (unsigned long long)gridDim.x * (SCCG_BLOCK / 64);
+        for (unsigned long long i = blockIdx.x * (SCCG_BLOCK / 64) + (threadIdx.x >> 6); i < cnt; i += nw) {
+            const int32_t c = A.cand[i];
+            int32_t maxlen = A.nR - (c + k);
+            if (A.nT - k < maxlen) maxlen = A.nT - k;
+            const uint32_t l = (uint32_t)(k + wave_lce(A.R, c + k, A.T, k, maxlen));
+            v = cb_merge(v, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key(c, -1) : ~0ull});
+        }
+    }
+    if (lane_id() != 0) v = CandBest{0, 0, 0, ~0ull};   // the wave's lanes hold the same value: keep one
+    v = cb_wave(v);
+    if (lane_id() == 0) wbest[threadIdx.x >> 6] = v;
+    __syncthreads();
     if (threadIdx.x == 0) {
-        bool good = *reinterpret_cast<const int32_t*>(A.kb + 16) == k && cnt <= (unsigned long long)CAND_CAP &&
-                    walk_key(A.kb, k) < KEY_EXOTIC && A.nT >= k;
-        for (int i = 0; good && i < k; i++) good = A.kb[i] == A.T[i];
-        ok = good;
-        A.fc[12] = good ? 1 : 2;
+        for (int i = 1; i < SCCG_BLOCK / 64; i++) v = cb_merge(v, wbest[i]);
+        unsigned long long* o = A.fcb + 4 * blockIdx.x;
+        o[0] = v.l; o[1] = v.cnt; o[2] = v.has0; o[3] = v.minkey;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_cand_stats_fin(WalkPtrs A, int nblk) {
+    __shared__ CandBest wbest[16];
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        ok = cand_stats_usable(A);
+        A.fc[12] = ok ? 1 : 2;
     }
     __syncthreads();
     if (!ok) return;
-    // one position per wave at a time, extended by the whole wave (wave_lce: 2 KiB per round trip)
     CandBest v{0, 0, 0, ~0ull};
-    const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
-    for (unsigned long long i = w; i < cnt; i += nw) {
-        const int32_t c = A.cand[i];
-        int32_t maxlen = A.nR - (c + k);
-        if (A.nT - k < maxlen) maxlen = A.nT - k;
-        const uint32_t l = (uint32_t)(k + wave_lce(A.R, c + k, A.T, k, maxlen));
-        v = cb_merge(v, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key(c, -1) : ~0ull});
+    for (int b = (int)threadIdx.x; b < nblk; b += (int)blockDim.x) {
+        const unsigned long long* o = A.fcb + 4 * b;
+        v = cb_merge(v, CandBest{(uint32_t)o[0], (uint32_t)o[1], (uint32_t)o[2], o[3]});
     }
-    if (lane_id() != 0) v = CandBest{0, 0, 0, ~0ull};   // the wave's lanes hold the same value: keep one
     v = cb_wave(v);
     if (lane_id() == 0) wbest[threadIdx.x >> 6] = v;
     __syncthreads();
@@ -1761,7 +1789,8 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
         // the early sweep already stored the anchors and the first k-mer's positions
         A.agen = e.agen;
         if (A.nR >= A.k && A.nT >= A.k) {
-            hipLaunchKernelGGL(k_cand_stats, dim3(1), dim3(1024), 0, s, A);
+            hipLaunchKernelGGL(k_cand_stats, dim3(CAND_STATS_GRID), dim3(SCCG_BLOCK), 0, s, A);
+            hipLaunchKernelGGL(k_cand_stats_fin, dim3(1), dim3(1024), 0, s, A, CAND_STATS_GRID);
             if (A.amulti) {
                 const int64_t ns = (int64_t)A.nR / A.astep + 1;
                 const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
