@@ -39,6 +39,8 @@ constexpr int ANCHOR_LOAD_DEFAULT = 4;    // table slots per sample (SCCG_ANCHOR
 #define ANCHOR_PROBE_BATCHES 2            // 64 target probes per batch per anchor vote (measured: 2 beats 4)
 #endif
 constexpr uint32_t A_MULTI = 0xFFFFFFFFu;    // anchor position of a 32-mer seen more than once
+constexpr int ANCHOR_RETRIES = 8;             // later votes for a chunk whose start has none
+constexpr int32_t ANCHOR_RETRY_STEP = 512;    // target bases between them
 constexpr int32_t FROZEN_MIN = 4096;   // literal bases at a chunk end that trigger a frozen-P scan
 constexpr int FROZEN_MAX = 256;        // frozen chunks handled per batch (grid.y of k_frozen_scan)
 constexpr int FROZEN_FIRST = 16;       // the batch launched blind, before the round's sync
@@ -377,7 +379,12 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
         ob = uni(A.cur[j]);
         x = lo_j;
         if (A.round == 1) {   // first guess: the anchor vote at the chunk start (anchor_diag)
-            const int32_t d = anchor_diag(A, lo_j);
+            int32_t d = anchor_diag(A, lo_j);
+            // no vote there (an indel, N run or diverged copy under the 128 probes): vote further
+            // into the chunk.  A chunk left without a guess costs a whole serial re-walk next round
+            // and delays its successor's settlement by one more round.
+            for (int i = 1; d == INVALID && i <= ANCHOR_RETRIES && lo_j + i * ANCHOR_RETRY_STEP < hi_j; i++)
+                d = uni(anchor_diag(A, lo_j + i * ANCHOR_RETRY_STEP));
             P = INVALID;
             if (d != INVALID) {
                 int64_t gp = (int64_t)lo_j - 1 + d;
@@ -2010,6 +2017,33 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                             (unsigned long long)e[3], (unsigned long long)e[4], (unsigned long long)e[5], (unsigned long long)e[6],
                             (unsigned long long)e[7], (unsigned long long)e[8], (unsigned long long)e[9], (unsigned long long)e[10],
                             (unsigned long long)e[11], (unsigned long long)e[12], (unsigned long long)e[13]);
+                }
+            }
+            static const int dbg_chunk = getenv("SCCG_DEBUG_CHUNK") ? atoi(getenv("SCCG_DEBUG_CHUNK")) : -1;
+            if (dbg && dbg_chunk >= 0 && dbg_chunk < A.C) {   // both trajectory buffers of one chunk
+                const size_t j = (size_t)dbg_chunk;
+                int32_t cur = 0, cn[2] = {0, 0}, ux = 0, up = 0, ex = 0, ep = 0, sq = 0;
+                SCCG_HIP(hipMemcpy(&cur, A.cur + j, 4, hipMemcpyDeviceToHost));
+                SCCG_HIP(hipMemcpy(&cn[0], A.cnt[0] + j, 4, hipMemcpyDeviceToHost));
+                SCCG_HIP(hipMemcpy(&cn[1], A.cnt[1] + j, 4, hipMemcpyDeviceToHost));
+                SCCG_HIP(hipMemcpy(&ux, A.usedX + j, 4, hipMemcpyDeviceToHost));
+                SCCG_HIP(hipMemcpy(&up, A.usedP + j, 4, hipMemcpyDeviceToHost));
+                SCCG_HIP(hipMemcpy(&ex, A.exitX + j, 4, hipMemcpyDeviceToHost));
+                SCCG_HIP(hipMemcpy(&ep, A.exitP + j, 4, hipMemcpyDeviceToHost));
+                SCCG_HIP(hipMemcpy(&sq, A.seedq + j, 4, hipMemcpyDeviceToHost));
+                fprintf(stderr, "[chunk %zu] round %lld cur=%d used=(%d,%d) exit=(%d,%d) seedq=%d\n", j, (long long)round, cur, ux,
+                        up, ex, ep, sq);
+                for (int b = 0; b < 2; b++) {
+                    const int n = cn[b] < 80 ? cn[b] : 80;
+                    std::vector<int32_t> tt(n > 0 ? n : 1), pp(tt.size()), ll(tt.size());
+                    if (n > 0) {
+                        SCCG_HIP(hipMemcpy(tt.data(), A.bt[b] + j * A.cap, n * 4, hipMemcpyDeviceToHost));
+                        SCCG_HIP(hipMemcpy(pp.data(), A.bp[b] + j * A.cap, n * 4, hipMemcpyDeviceToHost));
+                        SCCG_HIP(hipMemcpy(ll.data(), A.bl[b] + j * A.cap, n * 4, hipMemcpyDeviceToHost));
+                    }
+                    fprintf(stderr, "  buf%d (%d):", b, cn[b]);
+                    for (int q = 0; q < n; q++) fprintf(stderr, " (%d,%d,%d)", tt[q], pp[q], ll[q]);
+                    fprintf(stderr, "\n");
                 }
             }
             static const int dbg_rounds = getenv("SCCG_DEBUG_ROUNDS") ? atoi(getenv("SCCG_DEBUG_ROUNDS")) : 3;
