@@ -153,7 +153,12 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const uint8_t* tgt_fa, in
 struct EmitTarget {
     int (*resolve)(void* user, uint8_t** out);
     void* user;
+    // optional, polled after every walk round: nonzero = the walk's result is not wanted (the
+    // caller's local pass found no switch), so global_match_and_emit stops with WALK_ABANDONED
+    int (*abandon)(void* user) = nullptr;
 };
+// global_match_and_emit's return when EmitTarget::resolve/abandon gave up on the walk (not an error)
+constexpr int WALK_ABANDONED = -1;
 // (abs_p: absolute p on the record line, the text before delta_encode; late_out: out is ignored
 // and resolved through it; keep_flat: also keep the flat match list for global_matches, else the
 // text is written straight from the chunks' trajectories)

@@ -127,7 +127,8 @@ struct sccg_ctx {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;       // walk preparation, overlapping the local pass
     hipStream_t side2 = nullptr;      // header + run lines, overlapping the local pass
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr,
+               ev_local = nullptr;
     std::string err;
     sccg_stats stats{};
     void* buf[B_COUNT] = {};
@@ -196,7 +197,8 @@ int sccg_ctx_create(int device, sccg_ctx** out) {
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_lines, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rstrip, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_hdr, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_hdr, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_local, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SCCG_E_HIP;
     }
@@ -219,6 +221,7 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_lines);
     (void)hipEventDestroy(ctx->ev_rstrip);
     (void)hipEventDestroy(ctx->ev_hdr);
+    (void)hipEventDestroy(ctx->ev_local);
     (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->side2);
     (void)hipStreamDestroy(ctx->stream);
@@ -461,41 +464,92 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         }
         ~WorkerJoin() { join(); }
     } lines{&ctx->worker};
-    auto join_lines = [&]() -> int {   // the lowercase line's end, main stream ordered after it
+    auto join_lines = [&](hipStream_t on) -> int {   // the lowercase line's end, `on` ordered after it
         TRY(lines.join());
-        HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
+        HIPTRY(hipStreamWaitEvent(on, ctx->ev_lines, 0));
         pos = (has_hdr ? hlen + 1 : 0) + rl_len[0];
         return 0;
     };
 
-    // ---- join: the switch point, then everything after it runs behind the side work
-    if (iters > 0) {
+    // ---- the switch point (compression.cpp:417-481), read once the local pass is done
+    bool sw_known = iters <= 0;
+    auto read_switch = [&]() -> int {
+        if (sw_known) return 0;
         int64_t h_sw = 0;
         TRY(d2h_i64(ctx, sc + 21, &h_sw, 1));   // ctl[2] | ctl[3] << 32
         sw = h_sw >= INT32_MAX ? -1 : h_sw;
+        sw_known = true;
+        return 0;
+    };
+    HIPTRY(hipEventRecord(ctx->ev_local, s));
+
+    // ---- global (compression.cpp:484-574), speculatively: the walk runs on the side stream right
+    //      behind its preparation, beside the local pass, and is abandoned if the pass finds no
+    //      switch (checked after every walk round, and before any record text is written).
+    bool global_done = false;
+    int64_t g_rlen = 0;
+    uint8_t* X = nullptr;
+    WalkResult wr{};
+    if (iters > 0) {
+        struct Late {
+            std::function<int(uint8_t**)> f;
+            std::function<int()> poll;
+            static int call(void* u, uint8_t** o) { return static_cast<Late*>(u)->f(o); }
+            static int abandon(void* u) { return static_cast<Late*>(u)->poll(); }
+        } late{[&](uint8_t** o) -> int {
+                   TRY(read_switch());
+                   if (sw < 0) return WALK_ABANDONED;
+                   TRY(join_lines(s2));
+                   const int64_t nlen = rl_len[1];
+                   TRY(dev_put_framed(out + pos, nline, nlen, '\n', '\n', s2));   // "\n" + N line + "\n"
+                   pos += nlen + 2;
+                   X = out + pos;
+                   if (paren) {
+                       GET(uint8_t, xb, B_DX, out_cap - pos);
+                       X = xb;
+                   }
+                   *o = X;
+                   return 0;
+               },
+               [&]() -> int {
+                   if (!sw_known && hipEventQuery(ctx->ev_local) != hipSuccess) return 0;   // pass still running
+                   if (read_switch()) return 0;   // the resolve step reports the error
+                   return sw < 0;
+               }};
+        const EmitTarget target{&Late::call, &late, &Late::abandon};
+        const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
+                                             s2, paren, &target, /*keep_flat=*/false);
+        if (rc != WALK_ABANDONED) {
+            TRY(rc);
+            if (!X) return ctx->fail(SCCG_E_INTERNAL, "record text position never resolved");
+            global_done = true;
+        }
     }
+    HIPTRY(hipEventRecord(ctx->ev_join, s2));   // all side work (preparation, walk) before anything reuses it
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    TRY(read_switch());
     st.switch_segment = sw;
     mark("local");
-    if (sw < 0) {
+    if (!global_done) {
+        if (sw >= 0) return ctx->fail(SCCG_E_INTERNAL, "switch found but the global walk was abandoned");
         global_prepare_reset();
-        TRY(join_lines());
+        TRY(join_lines(s));
         // ---- local: "\n,\n" + records + leftover segments
         TRY(dev_put_bytes(out + pos, "\n,\n", 3, s));
         pos += 3;
         GET(int64_t, sa, B_SEG_A, iters + 1);
         GET(int64_t, sb, B_SEG_B, iters + 1);
         GET(int64_t, part, B_PARTIAL, scan_partials_needed(iters + 1) + 16);
-        uint8_t* X = out + pos;
+        uint8_t* XL = out + pos;
         if (paren) {
             GET(uint8_t, xb, B_DX, out_cap - pos);
-            X = xb;
+            XL = xb;
         }
-        TRY(launch_local_emit(T, nT, iters, recs, stat, X, sc + 5, sa, sb, part, s, paren));
+        TRY(launch_local_emit(T, nT, iters, recs, stat, XL, sc + 5, sa, sb, part, s, paren));
         int64_t rlen = 0;
         TRY(d2h_i64(ctx, sc + 5, &rlen, 1));
-        if (paren) TRY(paren_delta(ctx, X, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
-        // statistics: match tokens / literal bytes of the record line
+        if (paren) TRY(paren_delta(ctx, XL, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
+        // statistics: match tokens / literal bases of the record line
         std::vector<SegStat> hs((size_t)(iters > 0 ? iters : 0));
         if (iters > 0) {
             HIPTRY(hipMemcpyAsync(hs.data(), stat, (size_t)iters * sizeof(SegStat), hipMemcpyDeviceToHost, s));
@@ -508,33 +562,8 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         st.literal_bases = lit + (nT - lead);
         pos += rlen;
     } else {
-        // ---- global (compression.cpp:484-574)
         st.mode_global = 1;
-        // N line + record text go after the lowercase line: resolved once the walk's rounds are
-        // done (the run lines finish on the side meanwhile)
-        uint8_t* X = nullptr;
-        struct Late {
-            std::function<int(uint8_t**)> f;
-            static int call(void* u, uint8_t** o) { return static_cast<Late*>(u)->f(o); }
-        } late{[&](uint8_t** o) -> int {
-            TRY(join_lines());
-            const int64_t nlen = rl_len[1];
-            TRY(dev_put_framed(out + pos, nline, nlen, '\n', '\n', s));   // "\n" + N line + "\n"
-            pos += nlen + 2;
-            X = out + pos;
-            if (paren) {
-                GET(uint8_t, xb, B_DX, out_cap - pos);
-                X = xb;
-            }
-            *o = X;
-            return 0;
-        }};
-        const EmitTarget target{&Late::call, &late};
-        WalkResult wr{};
-        int64_t rlen = 0;
-        TRY(global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(tn), ws, wsb, nullptr, &rlen, &wr, s, paren,
-                                  &target, /*keep_flat=*/false));
-        if (!X) return ctx->fail(SCCG_E_INTERNAL, "record text position never resolved");
+        int64_t rlen = g_rlen;
         if (paren) TRY(paren_delta(ctx, X, rlen, out + pos, out_cap - pos, &rlen, &stoi_fail));
         st.n_matches = wr.n_matches;
         st.walk_rounds = wr.rounds;

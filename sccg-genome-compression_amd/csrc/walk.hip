@@ -2088,6 +2088,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             }
             if (!nlist) break;
             if (round > 4 * (int64_t)A.C + 16) return SCCG_E_INTERNAL;
+            if (late_out && late_out->abandon && late_out->abandon(late_out->user)) return WALK_ABANDONED;
         }
     }
 
