@@ -129,6 +129,7 @@ struct sccg_ctx {
     hipStream_t side2 = nullptr;      // header + run lines, overlapping the local pass
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr,
                ev_local = nullptr;
+    int64_t* h_switch = nullptr;      // pinned: the local pass's switch word, copied behind the pass
     std::string err;
     sccg_stats stats{};
     void* buf[B_COUNT] = {};
@@ -198,7 +199,8 @@ int sccg_ctx_create(int device, sccg_ctx** out) {
         hipEventCreateWithFlags(&c->ev_lines, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rstrip, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_hdr, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_local, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_local, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c->h_switch), 64, hipHostMallocDefault) != hipSuccess) {
         delete c;
         return SCCG_E_HIP;
     }
@@ -222,6 +224,7 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_rstrip);
     (void)hipEventDestroy(ctx->ev_hdr);
     (void)hipEventDestroy(ctx->ev_local);
+    if (ctx->h_switch) (void)hipHostFree(ctx->h_switch);
     (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->side2);
     (void)hipStreamDestroy(ctx->stream);
@@ -475,12 +478,13 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     bool sw_known = iters <= 0;
     auto read_switch = [&]() -> int {
         if (sw_known) return 0;
-        int64_t h_sw = 0;
-        TRY(d2h_i64(ctx, sc + 21, &h_sw, 1));   // ctl[2] | ctl[3] << 32
+        HIPTRY(hipEventSynchronize(ctx->ev_local));
+        const int64_t h_sw = *ctx->h_switch;   // ctl[2] | ctl[3] << 32
         sw = h_sw >= INT32_MAX ? -1 : h_sw;
         sw_known = true;
         return 0;
     };
+    if (iters > 0) HIPTRY(hipMemcpyAsync(ctx->h_switch, sc + 21, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIPTRY(hipEventRecord(ctx->ev_local, s));
 
     // ---- global (compression.cpp:484-574), speculatively: the walk runs on the side stream right

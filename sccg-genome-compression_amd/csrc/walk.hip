@@ -1179,19 +1179,23 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
 // time (wave_lce: 2 KiB per round trip), per-block results go to fcb and k_cand_stats_fin merges
 // them -- a repeat-rich first k-mer (hundreds of positions) no longer serialises on one block.
 constexpr int CAND_STATS_GRID = 256;
+// whole wave (one round trip: lane i compares byte i of the FASTA-read k-mer with T')
 __device__ __forceinline__ bool cand_stats_usable(const WalkPtrs& A) {
-    const int k = A.k;
-    bool good = *reinterpret_cast<const int32_t*>(A.kb + 16) == k && A.fc[13] <= (unsigned long long)CAND_CAP &&
-                walk_key(A.kb, k) < KEY_EXOTIC && A.nT >= k;
-    for (int i = 0; good && i < k; i++) good = A.kb[i] == A.T[i];
-    return good;
+    const int k = A.k, lane = lane_id();
+    const bool head = *reinterpret_cast<const int32_t*>(A.kb + 16) == k && A.fc[13] <= (unsigned long long)CAND_CAP &&
+                      A.nT >= k;
+    const bool same = lane >= k || A.kb[lane] == A.T[lane];   // T' has readable slack past nT
+    return head && __ballot(!same) == 0 && walk_key(A.kb, k) < KEY_EXOTIC;
 }
 __global__ __launch_bounds__(SCCG_BLOCK) void k_cand_stats(WalkPtrs A) {
     __shared__ CandBest wbest[SCCG_BLOCK / 64];
     __shared__ int ok;
     const int k = A.k;
     const unsigned long long cnt = A.fc[13];
-    if (threadIdx.x == 0) ok = cand_stats_usable(A);
+    if (threadIdx.x < 64) {
+        const bool u = cand_stats_usable(A);
+        if (threadIdx.x == 0) ok = u;
+    }
     __syncthreads();
     CandBest v{0, 0, 0, ~0ull};
     if (ok) {
@@ -1218,9 +1222,9 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_cand_stats(WalkPtrs A) {
 __global__ __launch_bounds__(1024) void k_cand_stats_fin(WalkPtrs A, int nblk) {
     __shared__ CandBest wbest[16];
     __shared__ int ok;
-    if (threadIdx.x == 0) {
-        ok = cand_stats_usable(A);
-        A.fc[12] = ok ? 1 : 2;
+    if (threadIdx.x < 64) {
+        const bool u = cand_stats_usable(A);
+        if (threadIdx.x == 0) { ok = u; A.fc[12] = u ? 1 : 2; }
     }
     __syncthreads();
     if (!ok) return;
