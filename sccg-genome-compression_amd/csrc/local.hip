@@ -665,6 +665,10 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_local_all<false>, SCCG_BLOCK, 0) != hipSuccess || per < 1)
             per = 4;
+        // SCCG_LOCAL_BPC: fewer resident blocks per CU (leaves LDS for the walk that runs beside it)
+        const char* e = getenv("SCCG_LOCAL_BPC");
+        const int bpc = e ? atoi(e) : 0;
+        if (bpc >= 1 && bpc < per) per = bpc;
         return (unsigned)(cus * per);
     }();
     unsigned g = grid_for(nseg_max, WPB);

@@ -707,7 +707,23 @@ __device__ void frozen_apply_wave(const WalkPtrs& A, int fbase, int fcap, int32_
 // chunk 0 exact (a fix-up from the first match's end, with an empty trajectory), the others
 // speculative.
 constexpr int32_t NEVER = INT32_MIN + 1;   // "no entry used yet": differs from every state
+// DEV: the start state comes from the first-step statistics in fc (the usual case: the target's
+// first k-mer has candidates, compression.cpp:64-161 with pme == -1); when they say otherwise,
+// chunk 0 gets no entry (its walk is a no-op) and the host redoes the first step and the init.
+template <bool DEV>
 __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
+    if (DEV && blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long* r = A.fc + 4;
+        if (r[8] != 2 && r[0] == 0 && r[4] > 0) {
+            const uint64_t k0 = 1ull << 32;   // pick_key(0, -1)
+            const uint64_t pk = (r[5] >= 2 && r[6]) ? r[7] : ((r[6] && k0 < r[7]) ? k0 : r[7]);
+            startX = (int32_t)r[4];
+            startP = (int32_t)(uint32_t)pk + (int32_t)r[4] - 1;
+        } else {
+            startX = A.nT - A.k + 1;
+            startP = INVALID;
+        }
+    }
     for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
         A.cur[j] = 0;
         A.cnt[0][j] = 0;
@@ -1851,12 +1867,41 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         g_prep = Prepared{};
     }
 
+    // ---- round 1 is queued before the host knows the first step: k_walk_init<true> resolves the
+    //      usual start on the device, and the round's status comes back with the first-step
+    //      statistics in one readback (a host round trip less).  If the first step is not the
+    //      usual one, that round is dropped and everything below runs as before.
+    auto queue_round = [&](int fbase_cap) -> int {
+        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist,
+                    A.C);
+        hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
+                           (const int32_t*)A.plist, A.C);
+        if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fbase_cap), dim3(SCCG_BLOCK), 0, s, A, 0);
+        hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(1024), 0, s, A, 0, fbase_cap);
+        SCCG_HIP(hipGetLastError());
+        return 0;
+    };
+    static const bool dev_first = getenv("SCCG_HOST_FIRST_STEP") == nullptr;
+    bool pre_round = false;
+    int32_t rs_pre[6] = {};
+    if (walkable && dev_first && A.C > 0) {
+        hipLaunchKernelGGL(k_walk_init<true>, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s,
+                           A, 0, 0);
+        A.round = 1;
+        RC(queue_round(FROZEN_FIRST));
+        pre_round = true;
+    }
+
     // ---- the exact first (ungated) step: first target position with any candidate
     int32_t first_y = INVALID, first_p = 0, first_l = 0;
     if (walkable) {
         int32_t x0 = 0;
         unsigned long long r[9];   // fc[4..11]: first hit, first exotic, statistics of the batch's x0; fc[12]
-        {
+        if (pre_round) {
+            const RbItem it[2] = {{A.fc + 4, r, (int)sizeof r}, {A.scal, rs_pre, (int)sizeof rs_pre}};
+            RC(dev_readback(it, 2, s));
+            if (!(r[8] != 2 && r[0] == 0 && r[4] > 0)) pre_round = false;   // not the usual first step: redo
+        } else {
             const RbItem it{A.fc + 4, r, (int)sizeof r};
             RC(dev_readback(&it, 1, s));
         }
@@ -1919,8 +1964,9 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
 
     // ---- init chunk state
     const size_t C = (size_t)A.C;
-    hipLaunchKernelGGL(k_walk_init, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
-                       startX, startP);
+    if (!pre_round)
+        hipLaunchKernelGGL(k_walk_init<false>, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s,
+                           A, startX, startP);
     SCCG_HIP(hipGetLastError());
 
     if (startP != INVALID && lastk >= 0) {
@@ -1929,14 +1975,19 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
         for (int64_t round = 1;; round++) {
             A.round = (int32_t)round;   // every kernel of the round gets it by value
-            PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist, nlist);
-            SCCG_HIP(hipGetLastError());
+            const bool queued = round == 1 && pre_round;   // round 1 went out before the first step's readback
+            if (!queued) {
+                PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A,
+                            (const int32_t*)A.plist, nlist);
+                SCCG_HIP(hipGetLastError());
+            }
             res->rounds = round;
             // Commit, fill the first frozen runs and find the next round's pending chunks without
             // waiting for the host; more frozen chunks and the rare escalated (pn2 == 0) ones are
             // handled after the round's one sync.
-            hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
-                               (const int32_t*)A.plist, nlist);
+            if (!queued)
+                hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
+                                   (const int32_t*)A.plist, nlist);
             auto frozen_batch = [&](int fbase, int fcap, bool init_fy) -> int {   // no-op past the list
                 if (init_fy) SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.fy, INT32_MAX, fcap, s));
                 if (fcap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fcap), dim3(SCCG_BLOCK), 0, s, A, fbase);
@@ -1944,10 +1995,14 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 SCCG_HIP(hipGetLastError());
                 return 0;
             };
-            RC(frozen_batch(0, FROZEN_FIRST, false));   // fy was set by k_commit
             int32_t rs[6];
             const RbItem rs_item{A.scal, rs, (int)sizeof rs};
-            RC(dev_readback(&rs_item, 1, s));
+            if (queued) {
+                for (int i = 0; i < 6; i++) rs[i] = rs_pre[i];
+            } else {
+                RC(frozen_batch(0, FROZEN_FIRST, false));   // fy was set by k_commit
+                RC(dev_readback(&rs_item, 1, s));
+            }
             if (rs[5] > FROZEN_FIRST) {   // more frozen chunks than the blind batch covered
                 for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, true));
                 RC(dev_readback(&rs_item, 1, s));
