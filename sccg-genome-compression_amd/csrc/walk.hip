@@ -1962,6 +1962,31 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     if (first_y != INVALID) { startX = first_y + first_l; startP = first_p + first_l - 1; }
     else { startX = lastk + 1 > 0 ? lastk + 1 : 0; startP = INVALID; }
 
+    // ---- record text emission (k_chunk_text), queued after the rounds or speculatively (below)
+    bool resolved = false, spec_text = false, text_done = false;
+    int64_t spec_r[2] = {0, 0};   // total chunk matches, text bytes
+    auto resolve_out = [&]() -> int {
+        if (!resolved && late_out) RC(late_out->resolve(late_out->user, &out));
+        resolved = true;
+        return 0;
+    };
+    auto queue_text = [&]() -> int {
+        const int32_t nf = first_y != INVALID ? 1 : 0;
+        const unsigned gc = grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256);
+        hipLaunchKernelGGL(k_chunk_meta, dim3(gc), dim3(256), 0, s, A);
+        RC(dev_excl_max(A.cprev, A.cprev, A.C, nullptr, A.partial, s));
+        RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
+        RC(set_u64(reinterpret_cast<unsigned long long*>(A.scal64 + 2), {0}, s));
+        const FirstMatch F{first_y, first_p, first_l, nf};
+        hipLaunchKernelGGL(k_chunk_text<false>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F, (int)abs_p, out);
+        RC(dev_excl_sum(A.ctext, A.ctext, A.C, A.scal64 + 1, A.partial, s));
+        PROF_LAUNCH(PROF_MATCH_EMIT, s, k_chunk_text<true>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F,
+                    (int)abs_p, out);
+        hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
+        SCCG_HIP(hipGetLastError());
+        return 0;
+    };
+
     // ---- init chunk state
     const size_t C = (size_t)A.C;
     if (!pre_round)
@@ -1973,6 +1998,11 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         mark("anchors");
         int32_t nlist = A.C;
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
+        // Round 2 usually settles every chunk (round 1 speculates, round 2 confirms): its record text
+        // is queued right behind it, before the host knows, and comes back with the round's status.
+        // If the round left work (pending chunks, more frozen chunks, escalations) that text is
+        // simply written again after the last round.
+        static const bool spec_text_on = getenv("SCCG_NO_SPEC_TEXT") == nullptr;
         for (int64_t round = 1;; round++) {
             A.round = (int32_t)round;   // every kernel of the round gets it by value
             const bool queued = round == 1 && pre_round;   // round 1 went out before the first step's readback
@@ -2001,7 +2031,15 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 for (int i = 0; i < 6; i++) rs[i] = rs_pre[i];
             } else {
                 RC(frozen_batch(0, FROZEN_FIRST, false));   // fy was set by k_commit
-                RC(dev_readback(&rs_item, 1, s));
+                if (round == 2 && !keep_flat && !dbg && spec_text_on) {
+                    RC(resolve_out());
+                    RC(queue_text());
+                    const RbItem it2[2] = {rs_item, {A.scal64, spec_r, (int)sizeof spec_r}};
+                    RC(dev_readback(it2, 2, s));
+                    spec_text = rs[5] <= FROZEN_FIRST && rs[1] == 0;   // nothing changes after this readback
+                } else {
+                    RC(dev_readback(&rs_item, 1, s));
+                }
             }
             if (rs[5] > FROZEN_FIRST) {   // more frozen chunks than the blind batch covered
                 for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, true));
@@ -2145,6 +2183,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                     for (int q = 0; q < nshow; q++) fprintf(stderr, "      m%d (%d,%d,%d)\n", q, tt[q], pp[q], ll[q]);
                 }
             }
+            if (round == 2 && spec_text && nlist == 0) text_done = true;
             if (!nlist) break;
             if (round > 4 * (int64_t)A.C + 16) return SCCG_E_INTERNAL;
             if (late_out && late_out->abandon && late_out->abandon(late_out->user)) return WALK_ABANDONED;
@@ -2155,26 +2194,16 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     const int32_t nfirst = first_y != INVALID ? 1 : 0;
     if (!keep_flat) {
         // ---- record text straight from the chunks (k_chunk_text): no flattened match list
-        if (late_out) RC(late_out->resolve(late_out->user, &out));   // the caller's text position is known now
+        RC(resolve_out());   // the caller's text position is known now
         int64_t text = 0, nmc = 0;
         if (startP != INVALID && lastk >= 0) {
-            const unsigned gc = grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256);
-            hipLaunchKernelGGL(k_chunk_meta, dim3(gc), dim3(256), 0, s, A);
-            RC(dev_excl_max(A.cprev, A.cprev, A.C, nullptr, A.partial, s));
-            RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
-            RC(set_u64(reinterpret_cast<unsigned long long*>(A.scal64 + 2), {0}, s));
-            const FirstMatch F{first_y, first_p, first_l, nfirst};
-            hipLaunchKernelGGL(k_chunk_text<false>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F, (int)abs_p, out);
-            RC(dev_excl_sum(A.ctext, A.ctext, A.C, A.scal64 + 1, A.partial, s));
-            PROF_LAUNCH(PROF_MATCH_EMIT, s, k_chunk_text<true>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F,
-                        (int)abs_p, out);
-            hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
-            SCCG_HIP(hipGetLastError());
-            int64_t r[2];
-            const RbItem it{A.scal64, r, (int)sizeof r};
-            RC(dev_readback(&it, 1, s));
-            nmc = r[0];
-            text = r[1];
+            if (!text_done) {   // (else round 2's speculative text stands)
+                RC(queue_text());
+                const RbItem it{A.scal64, spec_r, (int)sizeof spec_r};
+                RC(dev_readback(&it, 1, s));
+            }
+            nmc = spec_r[0];
+            text = spec_r[1];
         } else if (nTp > 0) {   // no first match: the whole target is one literal
             const unsigned g = grid_for(nTp, 256) > 8192 ? 8192 : grid_for(nTp, 256);
             hipLaunchKernelGGL(k_copy, dim3(g), dim3(256), 0, s, Tp, nTp, out);
