@@ -365,7 +365,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
     __shared__ WalkLds lds_all[WPB];
     const int w = wave_in_block(), lane = lane_id();
     const int32_t li = (int32_t)blockIdx.x * WPB + w;
-    if (li >= nlist) return;
+    if (li >= nlist || A.scal[9]) return;
     WalkLds& L = lds_all[w];
     const int32_t j = uni(list[li]);
     const int32_t kind = uni(A.kind[j]);
@@ -605,6 +605,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
 // never depends on this choice -- the loop only ends when every chunk's trajectory was walked from
 // its predecessor's final exit.
 __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
+    if (A.scal[9]) return;   // void pre-queued round
     if (blockIdx.x == 0 && threadIdx.x < FROZEN_MAX) A.fy[threadIdx.x] = INT32_MAX;   // for k_frozen_scan
     for (int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); i < nlist; i += (int32_t)(gridDim.x * blockDim.x)) {
         const int32_t j = list[i];
@@ -628,6 +629,7 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
 // the frozen chunk; every wave builds its own copy of the window and scans a strided share).
 __global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int fbase) {
     __shared__ WalkLds lds_all[WPB];
+    if (A.scal[9]) return;   // void pre-queued round
     const int fi = (int)blockIdx.y, f = fbase + fi;
     if (f >= A.scal[5]) return;
     const int32_t j = A.flist[f];
@@ -724,6 +726,8 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
             startP = INVALID;
         }
     }
+    // scal[9]: the pre-queued round 1 is void (its kernels return at once; the host redoes it)
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.scal[9] = DEV && startP == INVALID ? 1 : 0;
     for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
         A.cur[j] = 0;
         A.cnt[0][j] = 0;
@@ -748,6 +752,7 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
 // The end of a round in one block: the frozen fills of a batch (wave 0), then the chunks whose
 // entry state (predecessor's exit) differs from the one their trajectory used -> plist, scal[0].
 __global__ __launch_bounds__(1024) void k_round_tail(WalkPtrs A, int fbase, int fcap) {
+    if (A.scal[9]) return;   // void pre-queued round
     __shared__ int32_t sj[FROZEN_MAX], sy[FROZEN_MAX];
     __shared__ int32_t trig[RESPEC_MAX_TRIGGERS];
     __shared__ int32_t ntrig;
@@ -1970,7 +1975,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         resolved = true;
         return 0;
     };
-    auto queue_text = [&]() -> int {
+    auto queue_text = [&](bool long_copy) -> int {
         const int32_t nf = first_y != INVALID ? 1 : 0;
         const unsigned gc = grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256);
         hipLaunchKernelGGL(k_chunk_meta, dim3(gc), dim3(256), 0, s, A);
@@ -1982,7 +1987,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         RC(dev_excl_sum(A.ctext, A.ctext, A.C, A.scal64 + 1, A.partial, s));
         PROF_LAUNCH(PROF_MATCH_EMIT, s, k_chunk_text<true>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F,
                     (int)abs_p, out);
-        hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
+        if (long_copy) hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
         SCCG_HIP(hipGetLastError());
         return 0;
     };
@@ -2003,6 +2008,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         // If the round left work (pending chunks, more frozen chunks, escalations) that text is
         // simply written again after the last round.
         static const bool spec_text_on = getenv("SCCG_NO_SPEC_TEXT") == nullptr;
+        int32_t frozen_r1 = 0;
         for (int64_t round = 1;; round++) {
             A.round = (int32_t)round;   // every kernel of the round gets it by value
             const bool queued = round == 1 && pre_round;   // round 1 went out before the first step's readback
@@ -2031,9 +2037,10 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 for (int i = 0; i < 6; i++) rs[i] = rs_pre[i];
             } else {
                 RC(frozen_batch(0, FROZEN_FIRST, false));   // fy was set by k_commit
-                if (round == 2 && !keep_flat && !dbg && spec_text_on) {
+                // (not after a round that left frozen chunks: a frozen chain means more rounds)
+                if (round == 2 && !keep_flat && !dbg && spec_text_on && frozen_r1 == 0) {
                     RC(resolve_out());
-                    RC(queue_text());
+                    RC(queue_text(false));   // the long literal copies only once the text is confirmed
                     const RbItem it2[2] = {rs_item, {A.scal64, spec_r, (int)sizeof spec_r}};
                     RC(dev_readback(it2, 2, s));
                     spec_text = rs[5] <= FROZEN_FIRST && rs[1] == 0;   // nothing changes after this readback
@@ -2183,6 +2190,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                     for (int q = 0; q < nshow; q++) fprintf(stderr, "      m%d (%d,%d,%d)\n", q, tt[q], pp[q], ll[q]);
                 }
             }
+            if (round == 1) frozen_r1 = rs[5];
             if (round == 2 && spec_text && nlist == 0) text_done = true;
             if (!nlist) break;
             if (round > 4 * (int64_t)A.C + 16) return SCCG_E_INTERNAL;
@@ -2197,10 +2205,13 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         RC(resolve_out());   // the caller's text position is known now
         int64_t text = 0, nmc = 0;
         if (startP != INVALID && lastk >= 0) {
-            if (!text_done) {   // (else round 2's speculative text stands)
-                RC(queue_text());
+            if (!text_done) {   // (else round 2's speculative text stands, but for its long copies)
+                RC(queue_text(true));
                 const RbItem it{A.scal64, spec_r, (int)sizeof spec_r};
                 RC(dev_readback(&it, 1, s));
+            } else {
+                hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
+                SCCG_HIP(hipGetLastError());
             }
             nmc = spec_r[0];
             text = spec_r[1];
