@@ -144,15 +144,15 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def gather(n: int) -> None:
-        # per-chromosome record streams -> rank 0 (sizes, then a padded all-gather over RCCL)
+        # per-chromosome record streams -> rank 0 over RCCL: the sizes (one all-gather, one host
+        # read), then a gather of each rank's first max-size bytes of its output buffer (no
+        # staging copy; rank 0 alone receives, so no rank pulls the other streams it has no use for)
         sz = torch.tensor([n], dtype=torch.int64, device=dev)
-        sizes = [torch.zeros_like(sz) for _ in range(world)]
-        dist.all_gather(sizes, sz)
-        mx = int(max(s.item() for s in sizes))
-        buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
-        buf[:n] = d_out[:n]
-        parts = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(parts, buf)
+        sizes = torch.empty(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(sizes, sz)
+        mx = int(sizes.max().item())
+        parts = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+        dist.gather(d_out[:mx], parts, dst=0)
 
     def step() -> int:
         n = ctx.compress_device(d_ref.data_ptr(), len(rfa), d_tgt.data_ptr(), len(tfa), d_out.data_ptr(), cap, stream)
