@@ -240,12 +240,15 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
                                                      int64_t nlr, uint8_t* __restrict__ out) {
     __shared__ uint8_t sdec[FSPAN];
     __shared__ uint8_t sout[FSPAN + FSPAN / 50 + 2];
-    __shared__ int64_t sd[2];
+    __shared__ int64_t sd[4];
     const int64_t J0 = (int64_t)blockIdx.x * FSPAN;
     if (J0 >= nres) return;
     const int64_t J1 = J0 + FSPAN < nres ? J0 + FSPAN : nres;
+    // one search per block for each run list (threads walk forward from there: a span holds few runs)
     if (threadIdx.x == 0) sd[0] = J0 - n_before(ns, nl, ncum, nn, J0);
     if (threadIdx.x == 64) sd[1] = J1 - n_before(ns, nl, ncum, nn, J1);
+    if (threadIdx.x == 128) sd[2] = first_run_ending_after(ns, nl, nn, J0);
+    if (threadIdx.x == 192) sd[3] = first_run_ending_after(ls, ll, nlr, J0);
     __syncthreads();
     const int64_t d0 = sd[0], dn = sd[1] - d0;
     for (int64_t i = threadIdx.x; i < dn; i += 256) sdec[i] = dec[d0 + i];
@@ -255,18 +258,23 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
     __syncthreads();
     const int64_t j0 = J0 + (int64_t)threadIdx.x * FPER;
     if (j0 < J1) {
-        int64_t rn = first_run_ending_after(ns, nl, nn, j0);
-        int64_t rl = first_run_ending_after(ls, ll, nlr, j0);
+        // the current N run [n_s, n_e) with the N count before it, the current lowercase run [l_s, l_e)
+        int64_t rn = sd[2], rl = sd[3], n_s, n_e, n_b, l_s, l_e;
+        auto load_n = [&]() {
+            if (rn < nn) { n_s = ns[rn]; n_e = n_s + nl[rn]; n_b = ncum[rn]; }
+            else { n_s = n_e = INT64_MAX; n_b = nn ? ncum[nn - 1] + nl[nn - 1] : 0; }
+        };
+        auto load_l = [&]() {
+            if (rl < nlr) { l_s = ls[rl]; l_e = l_s + ll[rl]; }
+            else l_s = l_e = INT64_MAX;
+        };
+        load_n();
+        load_l();
         for (int64_t j = j0; j < j0 + FPER && j < J1; j++) {
-            while (rn < nn && (int64_t)ns[rn] + nl[rn] <= j) rn++;
-            while (rl < nlr && (int64_t)ls[rl] + ll[rl] <= j) rl++;
-            uint8_t c;
-            if (rn < nn && ns[rn] <= j) c = 'N';
-            else {
-                const int64_t nbefore = rn < nn ? ncum[rn] : (nn ? ncum[nn - 1] + nl[nn - 1] : 0);
-                c = sdec[j - nbefore - d0];
-            }
-            if (rl < nlr && ls[rl] <= j) c = c_tolower(c);
+            while (j >= n_e) { rn++; load_n(); }
+            while (j >= l_e) { rl++; load_l(); }
+            uint8_t c = j >= n_s ? (uint8_t)'N' : sdec[j - n_b - d0];
+            if (j >= l_s) c = c_tolower(c);
             const int64_t o = j + j / 50 - O0;
             sout[o] = c;
             if (j % 50 == 49 && j != nres - 1) sout[o + 1] = '\n';
