@@ -143,21 +143,16 @@ def main() -> None:
     d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def gather(n: int) -> None:
-        # per-chromosome record streams -> rank 0 over RCCL: the sizes (one all-gather, one host
-        # read), then a gather of each rank's first max-size bytes of its output buffer (no
-        # staging copy; rank 0 alone receives, so no rank pulls the other streams it has no use for)
-        sz = torch.tensor([n], dtype=torch.int64, device=dev)
-        sizes = torch.empty(world, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(sizes, sz)
-        mx = int(sizes.max().item())
-        parts = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
-        dist.gather(d_out[:mx], parts, dst=0)
+    import multigpu
+    gathered: list = [None]
 
     def step() -> int:
         n = ctx.compress_device(d_ref.data_ptr(), len(rfa), d_tgt.data_ptr(), len(tfa), d_out.data_ptr(), cap, stream)
         if world > 1:
-            gather(n)
+            # per-chromosome record streams -> rank 0 over RCCL (multigpu.gather_to_root, the
+            # genome driver's exchange): one size all-gather, then a gather of each rank's output
+            # prefix straight out of d_out; only rank 0 receives
+            gathered[0] = multigpu.gather_to_root(d_out, n)
         return n
 
     for _ in range(args.warmup):
@@ -181,6 +176,12 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    gather_ok = None
+    if world > 1 and rank == 0:
+        parts = gathered[0]
+        gather_ok = all(p.numel() > 0 for p in parts) and torch.equal(parts[0], d_out[:n_out])
+        if not gather_ok:
+            raise SystemExit("bench: gathered record streams are wrong (empty part or rank 0 mismatch)")
     parity = None
     if not args.no_check:
         rec = d_out[:n_out].cpu().numpy().tobytes()

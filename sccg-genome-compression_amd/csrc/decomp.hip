@@ -129,8 +129,7 @@ __global__ void k_tok_parse(const uint8_t* __restrict__ s, int64_t n, const int6
                 atomicOr(err, 1);
             cb = l;
         } else if (c == ')') {
-            if (!inside) atomicOr(err, 1);   // a stray ')' outside a token
-            cb = 0;
+            cb = inside ? 0 : 1;             // a ')' outside a token is a literal (decompression.cpp:231-234)
         } else if (!inside) {
             cb = 1;
         }
@@ -171,7 +170,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill(const uint8_t* __restri
         const uint8_t c = s[i];
         const bool inside = lp[i] >= 0 && s[lp[i]] == '(';
         if (c == '(') tok = true;
-        else if (c != ')' && !inside) dec[off[i]] = c;
+        else if (!inside) dec[off[i]] = c;   // literals, a stray ')' included
     }
     unsigned long long tm = __ballot(tok);
     while (tm) {
@@ -186,8 +185,9 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill(const uint8_t* __restri
 // ---------------------------------------------------------------------------------------------
 // output: header '\n' then result wrapped at 50 columns + final '\n'
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t first_run_ending_after(const int32_t* st, const int32_t* ln, int64_t nr, int64_t j) {
-    int64_t a = 0, b = nr;   // first r with st[r] + ln[r] > j
+__device__ __forceinline__ int64_t first_run_ending_after(const int32_t* st, const int32_t* ln, int64_t nr, int64_t j,
+                                                          int64_t a = 0) {
+    int64_t b = nr;   // first r >= a with st[r] + ln[r] > j (runs sorted and disjoint)
     while (a < b) {
         const int64_t m = (a + b) >> 1;
         if ((int64_t)st[m] + ln[m] > j) b = m; else a = m + 1;
@@ -195,37 +195,12 @@ __device__ __forceinline__ int64_t first_run_ending_after(const int32_t* st, con
     return a;
 }
 
-constexpr int OUT_PER_T = 64;
-__global__ void k_format(const uint8_t* __restrict__ dec, int64_t nres, const int32_t* __restrict__ ns,
-                         const int32_t* __restrict__ nl, const int64_t* __restrict__ ncum, int64_t nn,
-                         const int32_t* __restrict__ ls, const int32_t* __restrict__ ll, int64_t nlr,
-                         uint8_t* __restrict__ out) {
-    const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * OUT_PER_T;
-    if (j0 >= nres) return;
-    int64_t rn = first_run_ending_after(ns, nl, nn, j0);
-    int64_t rl = first_run_ending_after(ls, ll, nlr, j0);
-    for (int64_t j = j0; j < j0 + OUT_PER_T && j < nres; j++) {
-        while (rn < nn && (int64_t)ns[rn] + nl[rn] <= j) rn++;
-        while (rl < nlr && (int64_t)ls[rl] + ll[rl] <= j) rl++;
-        uint8_t c;
-        if (rn < nn && ns[rn] <= j) c = 'N';
-        else {
-            const int64_t nbefore = rn < nn ? ncum[rn] : (nn ? ncum[nn - 1] + nl[nn - 1] : 0);
-            c = dec[j - nbefore];
-        }
-        if (rl < nlr && ls[rl] <= j) c = c_tolower(c);
-        const int64_t o = j + j / 50;
-        out[o] = c;
-        if (j % 50 == 49 && j != nres - 1) out[o + 1] = '\n';
-    }
-}
-
-// Coalesced form of k_format: a block owns FSPAN consecutive sequence positions.  Their decoded
-// bytes (one contiguous range of dec, N positions excluded) are loaded into LDS with stride-1
-// reads, every thread formats FPER positions into the block's LDS copy of its output range
-// (N runs, lowercase runs, a '\n' after every 50th base but the last), and the block stores that
-// range with stride-1 writes.  (k_format: each thread's 64 positions went straight to HBM, lanes
-// 64 bytes apart: 4.6 ms for a chr1-sized FASTA.)
+// A block owns FSPAN consecutive sequence positions.  Their decoded bytes (one contiguous range
+// of dec, N positions excluded) are loaded into LDS with stride-1 reads, every thread formats FPER
+// positions into the block's LDS copy of its output range (N runs, lowercase runs, a '\n' after
+// every 50th base but the last), and the block stores that range with stride-1 writes.  (A
+// thread-per-64-positions writer straight to HBM, lanes 64 bytes apart, took 4.6 ms for a
+// chr1-sized FASTA.)
 constexpr int FPER = 16, FSPAN = 256 * FPER;
 // N positions before j (j inside an N run: those of the run before j included)
 __device__ __forceinline__ int64_t n_before(const int32_t* ns, const int32_t* nl, const int64_t* ncum, int64_t nn, int64_t j) {
@@ -240,15 +215,17 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
                                                      int64_t nlr, uint8_t* __restrict__ out) {
     __shared__ uint8_t sdec[FSPAN];
     __shared__ uint8_t sout[FSPAN + FSPAN / 50 + 2];
-    __shared__ int64_t sd[4];
+    __shared__ int64_t sd[6];
     const int64_t J0 = (int64_t)blockIdx.x * FSPAN;
     if (J0 >= nres) return;
     const int64_t J1 = J0 + FSPAN < nres ? J0 + FSPAN : nres;
-    // one search per block for each run list (threads walk forward from there: a span holds few runs)
+    // one search per block for each run list bounds the runs the span touches: [sd[2], sd[4]] for
+    // N, [sd[3], sd[5]] for lowercase; each thread then searches only that range (a span with dense
+    // case or N alternation holds up to FSPAN/2 runs, too many to walk forward through)
     if (threadIdx.x == 0) sd[0] = J0 - n_before(ns, nl, ncum, nn, J0);
     if (threadIdx.x == 64) sd[1] = J1 - n_before(ns, nl, ncum, nn, J1);
-    if (threadIdx.x == 128) sd[2] = first_run_ending_after(ns, nl, nn, J0);
-    if (threadIdx.x == 192) sd[3] = first_run_ending_after(ls, ll, nlr, J0);
+    if (threadIdx.x == 128) { sd[2] = first_run_ending_after(ns, nl, nn, J0); sd[4] = first_run_ending_after(ns, nl, nn, J1 - 1); }
+    if (threadIdx.x == 192) { sd[3] = first_run_ending_after(ls, ll, nlr, J0); sd[5] = first_run_ending_after(ls, ll, nlr, J1 - 1); }
     __syncthreads();
     const int64_t d0 = sd[0], dn = sd[1] - d0;
     for (int64_t i = threadIdx.x; i < dn; i += 256) sdec[i] = dec[d0 + i];
@@ -259,7 +236,9 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
     const int64_t j0 = J0 + (int64_t)threadIdx.x * FPER;
     if (j0 < J1) {
         // the current N run [n_s, n_e) with the N count before it, the current lowercase run [l_s, l_e)
-        int64_t rn = sd[2], rl = sd[3], n_s, n_e, n_b, l_s, l_e;
+        int64_t rn = first_run_ending_after(ns, nl, sd[4] < nn ? sd[4] + 1 : nn, j0, sd[2]);
+        int64_t rl = first_run_ending_after(ls, ll, sd[5] < nlr ? sd[5] + 1 : nlr, j0, sd[3]);
+        int64_t n_s, n_e, n_b, l_s, l_e;
         auto load_n = [&]() {
             if (rn < nn) { n_s = ns[rn]; n_e = n_s + nl[rn]; n_b = ncum[rn]; }
             else { n_s = n_e = INT64_MAX; n_b = nn ? ncum[nn - 1] + nl[nn - 1] : 0; }

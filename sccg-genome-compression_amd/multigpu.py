@@ -42,54 +42,82 @@ def max_over_mean(sizes: list[int], world: int) -> float:
     return max(loads) / (sum(loads) / world) if sum(loads) else 1.0
 
 
+def gather_to_root(buf: torch.Tensor, n: int, group=None) -> list[torch.Tensor] | None:
+    """Gather the first `n` bytes of every rank's uint8 buffer `buf` to rank 0 (a gatherv).
+
+    One all-gather of the int64 sizes (one host read of their max), then one gather of each rank's
+    first max-size bytes straight out of `buf` (no staging copy unless `buf` is shorter than the
+    largest part).  Only rank 0 receives.  Returns [part of rank r] (views, trimmed to the sizes)
+    on rank 0 and None elsewhere.  `buf` lives on the device for RCCL, on the CPU for gloo."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    dev = buf.device
+    sz = torch.tensor([n], dtype=torch.int64, device=dev)
+    sizes = [torch.empty(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, sz, group=group)
+    sizes_h = torch.cat(sizes).cpu().tolist()
+    mx = max(sizes_h) if sizes_h else 0
+    if mx == 0:
+        return [buf[:0] for _ in range(world)] if rank == 0 else None
+    if buf.numel() >= mx:
+        send = buf[:mx]
+    else:
+        send = torch.zeros(mx, dtype=torch.uint8, device=dev)
+        send[:n] = buf[:n]
+    parts = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+    dist.gather(send, parts, dst=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    if rank != 0:
+        return None
+    return [parts[r][: sizes_h[r]] for r in range(world)]
+
+
+def pack_records(parts: dict[str, bytes | torch.Tensor], device: torch.device) -> torch.Tensor:
+    """One uint8 buffer: int64 header [n_names, len(names blob), len(blob_i)...], the NUL-joined
+    names, then the blobs in name order."""
+    names = sorted(parts)
+    blobs = []
+    for nme in names:
+        v = parts[nme]
+        if isinstance(v, torch.Tensor):
+            blobs.append(v.to(device).reshape(-1))
+        else:
+            blobs.append(torch.frombuffer(bytearray(v), dtype=torch.uint8).to(device) if len(v)
+                         else torch.zeros(0, dtype=torch.uint8, device=device))
+    name_bytes = "\0".join(names).encode()
+    head = torch.tensor([len(names), len(name_bytes)] + [int(b.numel()) for b in blobs], dtype=torch.int64)
+    pieces = [head.view(torch.uint8).to(device)]
+    if name_bytes:
+        pieces.append(torch.frombuffer(bytearray(name_bytes), dtype=torch.uint8).to(device))
+    return torch.cat(pieces + blobs)
+
+
+def unpack_records(raw: bytes) -> dict[str, bytes]:
+    """Inverse of pack_records."""
+    import struct
+    n_names, nb = struct.unpack_from("<qq", raw, 0)
+    lens = struct.unpack_from(f"<{n_names}q", raw, 16)
+    off = 16 + 8 * n_names
+    names = raw[off: off + nb].decode().split("\0") if n_names else []
+    off += nb
+    out = {}
+    for nme, ln in zip(names, lens):
+        out[nme] = raw[off: off + ln]
+        off += ln
+    return out
+
+
 def gather_records(parts: dict[str, bytes | torch.Tensor], device: torch.device | None = None,
                    group=None) -> dict[str, bytes] | None:
-    """Gather {chromosome: record text} from every rank to rank 0.
+    """Gather {chromosome: record text} from every rank to rank 0 (pack_records + gather_to_root).
 
     `parts` values may be bytes or uint8 tensors (device tensors stay on the device for RCCL).
     Returns the merged dict on rank 0, None elsewhere."""
-    rank = dist.get_rank(group)
-    world = dist.get_world_size(group)
     dev = device or torch.device("cpu")
-    names = sorted(parts)
-    blobs = []
-    for n in names:
-        v = parts[n]
-        blobs.append(v.to(dev) if isinstance(v, torch.Tensor) else torch.frombuffer(bytearray(v), dtype=torch.uint8).to(dev)
-                     if len(v) else torch.zeros(0, dtype=torch.uint8, device=dev))
-    # header: one length per chromosome name and one per blob, both variable -> gather sizes first
-    name_bytes = "\0".join(names).encode()
-    lens = torch.tensor([len(name_bytes)] + [int(b.numel()) for b in blobs] + [len(blobs)], dtype=torch.int64,
-                        device=dev)
-    n_lens = torch.tensor([lens.numel()], dtype=torch.int64, device=dev)
-    all_n = [torch.zeros_like(n_lens) for _ in range(world)]
-    dist.all_gather(all_n, n_lens, group=group)
-    maxn = int(max(int(x.item()) for x in all_n))
-    padded_lens = torch.zeros(maxn, dtype=torch.int64, device=dev)
-    padded_lens[: lens.numel()] = lens
-    all_lens = [torch.zeros_like(padded_lens) for _ in range(world)]
-    dist.all_gather(all_lens, padded_lens, group=group)
-    payload = torch.cat([torch.frombuffer(bytearray(name_bytes), dtype=torch.uint8).to(dev)
-                         if name_bytes else torch.zeros(0, dtype=torch.uint8, device=dev)] + blobs)
-    sizes = []
-    for r in range(world):
-        ln = all_lens[r][: int(all_n[r].item())].tolist()
-        sizes.append(sum(ln[:-1]))
-    mx = max(sizes) if sizes else 0
-    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    buf[: payload.numel()] = payload
-    bufs = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(bufs, buf, group=group)
-    if rank != 0:
+    buf = pack_records(parts, dev)
+    got = gather_to_root(buf, int(buf.numel()), group=group)
+    if got is None:
         return None
     merged: dict[str, bytes] = {}
-    for r in range(world):
-        ln = all_lens[r][: int(all_n[r].item())].tolist()
-        nb, blob_lens = ln[0], ln[1:-1]
-        raw = bufs[r].cpu().numpy().tobytes()
-        rnames = raw[:nb].decode().split("\0") if nb else []
-        off = nb
-        for name, L in zip(rnames, blob_lens):
-            merged[name] = raw[off: off + L]
-            off += L
+    for part in got:
+        merged.update(unpack_records(part.cpu().numpy().tobytes()))
     return merged

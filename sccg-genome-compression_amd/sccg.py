@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("SCCG_LIB_PATH") or os.path.join(HERE, "lib", "libsccg
 HEADER = os.path.join(os.path.dirname(HERE), "include", "sccg.h")
 
 SCCG_OK = 0
+SCCG_E_DELTA_STOI = 4
 ERRORS = {1: "SCCG_E_INVALID", 2: "SCCG_E_HIP", 3: "SCCG_E_NOMEM", 4: "SCCG_E_DELTA_STOI",
           5: "SCCG_E_FORMAT", 6: "SCCG_E_RANGE", 7: "SCCG_E_PARSE", 8: "SCCG_E_UNSUPPORTED",
           9: "SCCG_E_INTERNAL"}

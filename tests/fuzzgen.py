@@ -187,6 +187,26 @@ SAFE_PIECES = [")", ",", "(12,", "(-5,", "(+7,", "(0000000000007,", "(2147483647
 BAD_PIECES = ["(", "(99999999999,", "(2147483648,", "(,", "(A5,", "(("]
 
 
+def close_paren_case(seed: int) -> tuple[bytes, bytes]:
+    """Targets whose only punctuation is ')': delta_encode leaves every such byte alone, so the record
+    line holds ')' outside any token, which decompression.cpp:231-234 copies as a literal."""
+    rng = random.Random(60_000 + seed)
+    rfa, tfa = global_case(seed) if seed % 2 else local_case(seed % 24)
+    rate = rng.choice([0.001, 0.005, 0.02])
+    out = []
+    for ln in tfa.split(b"\n"):
+        if ln.startswith(b">") or not ln:
+            out.append(ln)
+            continue
+        b = bytearray()
+        for c in ln:
+            if rng.random() < rate:
+                b += b")" * rng.randint(1, 3)
+            b.append(c)
+        out.append(bytes(b))
+    return rfa, b"\n".join(out)
+
+
 def paren_case(seed: int) -> tuple[bytes, bytes]:
     """Targets holding '(' ')' ',' digits and signs among the bases: literal bytes that
     delta_encode's own token scan (compression.cpp:262-293) pairs with the real "(p,l)" tokens.

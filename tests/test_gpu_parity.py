@@ -219,6 +219,37 @@ def test_paren_vs_oracle(ctx, seed):
         assert _gpu_reconstruct(ctx, got, rfa) == _oracle_reconstruct(want, rfa)
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_close_paren_literals_vs_oracle(ctx, seed):
+    """Targets whose only punctuation is ')': the record line holds ')' outside every token, which
+    decompression.cpp:231-234 copies as a literal byte (round trip exact where the oracle's is)."""
+    rfa, tfa = fuzzgen.close_paren_case(seed)
+    want = oraclelib.compress(rfa, tfa)
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert (rc, got) == (0, want)
+    assert _gpu_reconstruct(ctx, got, rfa) == _oracle_reconstruct(want, rfa)
+
+
+@pytest.mark.parametrize("period", [1, 2, 3, 7])
+def test_dense_case_and_n_alternation(ctx, period):
+    """Soft-masking and N that flip every `period` bases over long stretches: up to one run per two
+    bases in a formatter span (decompression.cpp:241-262 run lists), round trip exact."""
+    rng = random.Random(900 + period)
+    ref = _rand(rng, 300_000).decode()
+    tgt = list(ref[:150_000] + _rand(rng, 3000).decode() + ref[150_000:])
+    for i in range(20_000, 120_000):
+        if (i // period) % 2:
+            tgt[i] = tgt[i].lower()
+    for i in range(200_000, 260_000, 2 * period):
+        tgt[i] = "N" if (i // 7) % 2 else "n"
+    rfa, tfa = fuzzgen.to_fasta(ref), fuzzgen.to_fasta("".join(tgt), ">alt")
+    want = oraclelib.compress(rfa, tfa)
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert (rc, got) == (0, want)
+    fa = ctx.reconstruct(got, rfa)
+    assert fa == oraclelib.decompress(want, rfa)
+
+
 @pytest.mark.parametrize("pieces", ["safe", "mixed"])
 def test_paren_large_vs_oracle(ctx, pieces):
     """Multi-tile scans of the paren path: a 3 Mb global-mode pair with punctuation literals."""

@@ -68,3 +68,72 @@ def test_gather_records_gloo_world2():
             want[f"chr{i}"] = (f"rec-{i}-" * (i + r + 1)).encode()
     want["empty"] = b""
     assert res[0] == want
+
+
+def _root_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = [5, 0, 17][rank]
+        buf = torch.arange(64, dtype=torch.uint8) + 10 * rank   # capacity > n, like bench's d_out
+        got = multigpu.gather_to_root(buf, n)
+        short = torch.full((2,), rank + 1, dtype=torch.uint8)    # shorter than the largest part
+        got2 = multigpu.gather_to_root(short, 2)
+        q.put((rank, None if got is None else [g.tolist() for g in got],
+               None if got2 is None else [g.tolist() for g in got2]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_to_root_gloo_world3():
+    """The bench's and the genome driver's exchange: sizes all-gather + gather to rank 0 only."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_root_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = {r: (a, b) for r, a, b in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] == (None, None) and res[2] == (None, None)
+    parts, parts2 = res[0]
+    assert parts == [[(i + 10 * r) % 256 for i in range(n)] for r, n in enumerate([5, 0, 17])]
+    assert parts2 == [[r + 1] * 2 for r in range(3)]
+
+
+def test_pack_unpack_records():
+    import torch
+    d = {"chr2": b"abc", "chrX": b"", "chr1": bytes(range(256)) * 3}
+    buf = multigpu.pack_records(d, torch.device("cpu"))
+    assert multigpu.unpack_records(buf.numpy().tobytes()) == d
+    assert multigpu.unpack_records(multigpu.pack_records({}, torch.device("cpu")).numpy().tobytes()) == {}
+
+
+def test_emitter_status_and_7z(tmp_path):
+    """genome.py's rank-0 output side: file layout, the reference's 7z argv, per-chromosome rc."""
+    import genome
+    import sccg
+    fake = tmp_path / "fake7z"
+    log = tmp_path / "argv.log"
+    fake.write_text(f"#!/bin/bash\necho \"$@\" >> {log}\ncp \"$4\" \"$3\"\n")
+    fake.chmod(0o755)
+    out = tmp_path / "out"
+    em = genome.Emitter(str(out), True, str(fake))
+    em.emit('chr1"$(touch pwned)', b"rec1", 0)
+    em.emit("chr2", b"abs-text", sccg.SCCG_E_DELTA_STOI)
+    em.emit("chr3", b"", 2)
+    assert em.wait() == 1
+    p1 = out / 'chr1"$(touch pwned)' / "compressed_genome.txt"
+    assert p1.read_bytes() == b"rec1" and (p1.parent / "compressed_genome.txt.7z").read_bytes() == b"rec1"
+    assert not (tmp_path / "pwned").exists() and not os.path.exists("pwned")
+    assert (out / "chr2" / "compressed_genome.txt").read_bytes() == b"abs-text"
+    assert not (out / "chr2" / "compressed_genome.txt.7z").exists()
+    assert not (out / "chr3").exists()
+    assert log.read_text().count("a -mx=9") == 1
+    em2 = genome.Emitter(str(out), True, str(fake))
+    em2.emit("chr4", b"x", 0)
+    assert em2.wait() == 0

@@ -90,3 +90,31 @@ def _run_ref(rfa, tfa):
 def test_differential_vs_reference(kind, seed):
     rfa, tfa = (fuzzgen.local_case if kind == "local" else fuzzgen.global_case)(seed)
     assert oraclelib.compress(rfa, tfa) == _run_ref(rfa, tfa)
+
+
+def _run_ref_decompress(rec, rfa):
+    """decompression <arc> <ref> <out> with the stub 7z (which copies the archive to out/<stem>)."""
+    env = dict(os.environ, PATH=os.path.join(REPO, "oracle", "stub7z") + os.pathsep + os.environ["PATH"])
+    with tempfile.TemporaryDirectory() as d:
+        ap, rp = os.path.join(d, "compressed_genome.txt.7z"), os.path.join(d, "r.fa")
+        open(ap, "wb").write(rec)
+        open(rp, "wb").write(rfa)
+        p = subprocess.run([os.path.join(REF_BIN, "decompression"), ap, rp, os.path.join(d, "o")], env=env,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        if p.returncode:
+            return p.returncode, None
+        return 0, open(os.path.join(d, "o", "reconstructed_genome.fa"), "rb").read()
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref not built (reference sources absent)")
+@pytest.mark.parametrize("seed", range(16))
+def test_close_paren_literals_vs_reference(seed):
+    """')' bytes in the target survive delta_encode and decode as literals (decompression.cpp:231-234)."""
+    rfa, tfa = fuzzgen.close_paren_case(seed)
+    rec = oraclelib.compress(rfa, tfa)
+    assert rec == _run_ref(rfa, tfa)
+    rc, fa = _run_ref_decompress(rec, rfa)
+    try:
+        assert (rc, fa) == (0, oraclelib.decompress(rec, rfa))
+    except oraclelib.OracleError as e:
+        assert rc != 0 and e.rc != 0
