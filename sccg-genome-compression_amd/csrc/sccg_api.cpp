@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <future>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -127,7 +128,7 @@ struct sccg_ctx {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;       // walk preparation, overlapping the local pass
     hipStream_t side2 = nullptr;      // header + run lines, overlapping the local pass
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr,
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr, ev_tstrip = nullptr,
                ev_local = nullptr;
     int64_t* h_switch = nullptr;      // pinned: the local pass's switch word, copied behind the pass
     std::string err;
@@ -197,6 +198,7 @@ int sccg_ctx_create(int device, sccg_ctx** out) {
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_lines, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_tstrip, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rstrip, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_hdr, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_local, hipEventDisableTiming) != hipSuccess ||
@@ -221,6 +223,7 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_fork);
     (void)hipEventDestroy(ctx->ev_join);
     (void)hipEventDestroy(ctx->ev_lines);
+    (void)hipEventDestroy(ctx->ev_tstrip);
     (void)hipEventDestroy(ctx->ev_rstrip);
     (void)hipEventDestroy(ctx->ev_hdr);
     (void)hipEventDestroy(ctx->ev_local);
@@ -364,11 +367,55 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     TRY(launch_find_header(tfa, tn, sc, s));
     HIPTRY(hipEventRecord(ctx->ev_hdr, s));
     TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
+    // ---- header + lowercase line (compression.cpp:337-368) and the N line: side2, driven by the
+    //      context's host worker (its launches wait on run counts).  They need only T, so they are
+    //      queued right behind the target's strip -- ahead of the local pass and the walk, which
+    //      would otherwise share the GPU with these bandwidth-heavy passes.
+    HIPTRY(hipEventRecord(ctx->ev_tstrip, s));
+    hipStream_t s3 = ctx->side2;
+    HIPTRY(hipStreamWaitEvent(s3, ctx->ev_tstrip, 0));
+    uint8_t* nline = nullptr;
+    int64_t rl_len[2] = {0, 0};
+    // the worker's first readback (header range, |T|, |T'|, the '(' flag) is this thread's too
+    int64_t h4[4] = {0, 0, 0, 0};
+    int32_t flags = 0;
+    std::promise<int> lens_read;
+    std::future<int> lens = lens_read.get_future();
+    ctx->worker.submit([&, s3]() -> int {
+        {
+            const RbItem it[2] = {{sc, h4, (int)sizeof h4}, {d_flags, &flags, (int)sizeof flags}};
+            const int rc = dev_readback(it, 2, s3);
+            lens_read.set_value(rc);
+            if (rc) return ctx->hipfail(rc);
+        }
+        const bool hh = h4[0] < tn;
+        const int64_t hl = hh ? h4[1] - h4[0] : 0;
+        // (this thread reports both conditions; the worker only must not write)
+        if (h4[2] >= INT32_MAX - 8 || out_cap < hl + 1 + 11 * h4[2] + 64) return 0;
+        if (hh) {
+            HIPTRY(hipMemcpyAsync(out, tfa + h4[0], (size_t)hl, hipMemcpyDeviceToDevice, s3));
+            TRY(dev_put_bytes(out + hl, "\n", 1, s3));
+        }
+        // both run lines now (the N line is kept aside until the mode is known)
+        TRY(run_lines(ctx, T, h4[2], out + (hh ? hl + 1 : 0), &nline, sc + 10, rl_len, s3));
+        HIPTRY(hipEventRecord(ctx->ev_lines, s3));
+        return 0;
+    });
+    struct WorkerJoin {   // every exit path waits for the side work (it captures this frame)
+        HostWorker* w;
+        bool joined = false;
+        int join() {
+            if (joined) return 0;
+            joined = true;
+            return w->wait();
+        }
+        ~WorkerJoin() { join(); }
+    } lines{&ctx->worker};
     // The walk's R'-only preparation (anchor samples, positions of the target's first k-mer read off
     // its FASTA) starts on the side stream as soon as R' exists, beside the target's strip.
+    int64_t hr[2];   // |R|, |R'|
     {
-        int64_t hr[2];
-        TRY(d2h_i64(ctx, sc + 7, hr, 2, ctx->side));   // |R|, |R'|
+        TRY(d2h_i64(ctx, sc + 7, hr, 2, ctx->side));
         if (hr[1] < INT32_MAX - 8 && tn < INT32_MAX - 8) {
             HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
             const size_t wsb_early = walk_workspace_bytes(hr[1], tn, 14, walk_chunk(tn));   // |T'| <= tn
@@ -382,10 +429,9 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     //      global walk's input-only preparation (side stream) and the header + run lines (side2)
     //      only read T/R/T'/R', so they run beside it.  The local pass reads |R|, |T| from device
     //      memory and is queued before the host reads the lengths back (on side2).
-    hipStream_t s2 = ctx->side, s3 = ctx->side2;
+    hipStream_t s2 = ctx->side;
     HIPTRY(hipEventRecord(ctx->ev_fork, s));
     HIPTRY(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
-    HIPTRY(hipStreamWaitEvent(s3, ctx->ev_fork, 0));
     const int64_t iters_max = ((rn < tn ? rn : tn) + SEG_L - 1) / SEG_L;   // FASTA lengths bound the sequences'
     GET(uint32_t, recs, B_RECS, (iters_max > 0 ? iters_max : 1) * SEG_REC_CAP);
     GET(SegStat, stat, B_STAT, iters_max > 0 ? iters_max : 1);
@@ -403,13 +449,8 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         // one launch over every segment; segments past a detected switch are never started
         TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, s));
     }
-    int64_t hsc[10];
-    int32_t flags = 0;
-    {
-        const RbItem it[2] = {{sc, hsc, (int)sizeof hsc}, {d_flags, &flags, (int)sizeof flags}};
-        TRY(dev_readback(it, 2, s3));
-    }
-    const int64_t hdr[2] = {hsc[0], hsc[1]}, lt[2] = {hsc[2], hsc[3]}, lr[2] = {hsc[7], hsc[8]};
+    TRY(lens.get());
+    const int64_t hdr[2] = {h4[0], h4[1]}, lt[2] = {h4[2], h4[3]}, lr[2] = {hr[0], hr[1]};
     const int64_t nT = lt[0], nR = lr[0];
     if (nT >= INT32_MAX - 8 || nR >= INT32_MAX - 8)
         return ctx->fail(SCCG_E_UNSUPPORTED, "sequence longer than the reference's int positions allow");
@@ -435,38 +476,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     TRY(global_prepare(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(tn), ws, wsb, s2));
     HIPTRY(hipEventRecord(ctx->ev_join, s2));
 
-    // ---- header + lowercase line (compression.cpp:337-368): side2, driven by the context's host
-    //      worker (its launches wait on run counts), so this thread goes on with the walk
     int64_t pos = 0;
-    uint8_t* nline = nullptr;
-    int64_t rl_len[2] = {0, 0};
-    // the run lines are needed only for the final text; SCCG_LINES_AFTER_PREP=1 holds them back
-    // until the walk preparation is done (measured: no gain, the walk then slows instead)
-    static const bool lines_after_prep = [] {
-        const char* e = getenv("SCCG_LINES_AFTER_PREP");
-        return e ? atoi(e) != 0 : false;
-    }();
-    if (lines_after_prep) HIPTRY(hipStreamWaitEvent(s3, ctx->ev_join, 0));
-    ctx->worker.submit([&]() -> int {
-        if (has_hdr) {
-            HIPTRY(hipMemcpyAsync(out, tfa + hdr[0], (size_t)hlen, hipMemcpyDeviceToDevice, s3));
-            TRY(dev_put_bytes(out + hlen, "\n", 1, s3));
-        }
-        // both run lines now (the N line is kept aside until the mode is known)
-        TRY(run_lines(ctx, T, nT, out + (has_hdr ? hlen + 1 : 0), &nline, sc + 10, rl_len, s3));
-        HIPTRY(hipEventRecord(ctx->ev_lines, s3));
-        return 0;
-    });
-    struct WorkerJoin {   // every exit path waits for the side work (it captures this frame)
-        HostWorker* w;
-        bool joined = false;
-        int join() {
-            if (joined) return 0;
-            joined = true;
-            return w->wait();
-        }
-        ~WorkerJoin() { join(); }
-    } lines{&ctx->worker};
     auto join_lines = [&](hipStream_t on) -> int {   // the lowercase line's end, `on` ordered after it
         TRY(lines.join());
         HIPTRY(hipStreamWaitEvent(on, ctx->ev_lines, 0));

@@ -29,8 +29,6 @@ namespace {
 
 constexpr int WPB = 4;                 // chunks (waves) per block
 constexpr int WCAP = 256;              // window positions held in LDS (2m+1 <= WCAP)
-constexpr int WTBITS = 9;              // window hash slots
-constexpr int WTSLOTS = 1 << WTBITS;
 constexpr int32_t INVALID = INT32_MIN;
 constexpr int ANCHOR_K = 32;
 constexpr int ANCHOR_STEP_DEFAULT = 32;   // reference sample stride (SCCG_ANCHOR_STEP for tuning runs)
@@ -128,14 +126,32 @@ struct WalkPtrs {
     int64_t* ctext;           // per chunk: record text bytes of its target range -> offsets
     int64_t lgap_cap;
     uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
+    int32_t dbg_phases;       // SCCG_DEBUG_PHASES: also per-phase clocks
 };
 
-constexpr int WFBITS = 14;             // window pre-filter: 16384-bit Bloom filter, 2 hashes
+// Per-wave LDS: the window's Bloom filter (wide literal scans) and a copy of the last 2 KiB the
+// extension loaded from R' and from T'.  A match step reads its next window (R' around the new P),
+// its next probe (T' right after the match) and usually the start of its next extension from that
+// copy: after a match the walk continues on the same diagonal, inside the bytes it just compared.
+// So most steps make no dependent HBM round trip at all; only an extension that runs past the copy
+// loads (and refreshes it).
+constexpr int WFBITS = 14;             // window pre-filter: 16384-bit Bloom filter, 3 hashes
+constexpr int LBV = 2048;              // bytes of R' and of T' kept per wave
+constexpr int LEAD = 128;              // of which before the extension's start (the next window reaches back m)
+__device__ __forceinline__ uint32_t wf_h1(uint32_t key) { return slot_hash(key, WFBITS); }
 __device__ __forceinline__ uint32_t wf_h2(uint32_t key) { return (key * 0x85EBCA77u) >> (32 - WFBITS); }
-struct WalkLds {   // per wave: LDS hash of the window keys (wide literal scans)
-    uint32_t wkeys[WCAP];
-    uint32_t wtab[WTSLOTS / 2];
+__device__ __forceinline__ uint32_t wf_h3(uint32_t key) { return (key * 0xC2B2AE3Du + 0x27D4EB2Fu) >> (32 - WFBITS); }
+struct WalkLds {
     uint32_t wbits[1 << (WFBITS - 5)];
+    uint8_t rbuf[LBV + 64];   // R'[rb0, rb0 + LBV)  (+ slack read by the unaligned word loads)
+    uint8_t tbuf[LBV + 64];   // T'[tb0, tb0 + LBV)
+};
+// the copy's bases (wave-uniform); NO_BUF: nothing copied yet
+constexpr int32_t NO_BUF = INT32_MIN / 2;
+struct BufPos {
+    int32_t rb0 = NO_BUF, tb0 = NO_BUF;
+    __device__ __forceinline__ bool has_r(int32_t a, int32_t n) const { return a >= rb0 && a + n <= rb0 + LBV; }
+    __device__ __forceinline__ bool has_t(int32_t a, int32_t n) const { return a >= tb0 && a + n <= tb0 + LBV; }
 };
 
 __device__ __forceinline__ uint64_t pick_key(int32_t p, int32_t pme) {
@@ -143,64 +159,112 @@ __device__ __forceinline__ uint64_t pick_key(int32_t p, int32_t pme) {
     return ((uint64_t)(uint32_t)(d < 0 ? -d : d) << 32) | (uint32_t)p;
 }
 
-__device__ __forceinline__ uint32_t wt_get(const uint32_t* tab, int slot) {
-    return (tab[slot >> 1] >> ((slot & 1) * 16)) & 0xffffu;
-}
-__device__ __forceinline__ void wt_insert(uint32_t* tab, uint32_t key, uint32_t val) {
-    int slot = (int)slot_hash(key, WTBITS);
-    for (;;) {
-        uint32_t* w = &tab[slot >> 1];
-        const int sh = (slot & 1) * 16;
-        uint32_t old = *w;
-        while (((old >> sh) & 0xffffu) == 0) {
-            const uint32_t prev = atomicCAS(w, old, old | (val << sh));
-            if (prev == old) return;
-            old = prev;
-        }
-        slot = (slot + 1) & (WTSLOTS - 1);
-    }
-}
-
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int k) {
     for (int i = 0; i < k; i++) if (a[i] != b[i]) return false;
     return true;
 }
 
-// 16 bytes at an arbitrary address as 4 little-endian words (5 aligned dword loads)
-__device__ __forceinline__ void load16u(const uint8_t* p, uint32_t (&o)[4]) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    uint32_t v[5];
+// ND words at byte offset off of an LDS byte array (ND + 1 aligned ds_read_b32)
+template <int ND>
+__device__ __forceinline__ void loadw_lds(const uint8_t* lds, int32_t off, uint32_t (&o)[ND]) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (off >> 2);
+    const uint32_t sh = (uint32_t)(off & 3);
+    uint32_t v[ND + 1];
 #pragma unroll
-    for (int i = 0; i < 5; i++) v[i] = w[i];
+    for (int i = 0; i <= ND; i++) v[i] = w[i];
 #pragma unroll
-    for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+    for (int i = 0; i < ND; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
 }
 
-// longest common extension of R[a..] and T[b..], at most maxlen bytes; whole wave, 2 KiB / step
-// (32 bytes per lane: most matches end inside the first step, one dependent round trip)
-__device__ int32_t wave_lce(const uint8_t* __restrict__ R, int32_t a, const uint8_t* __restrict__ T, int32_t b,
-                            int32_t maxlen) {
+// first differing byte of two 32-byte stretches (32: none)
+__device__ __forceinline__ int first_diff32(const uint32_t (&r)[8], const uint32_t (&t)[8]) {
+    int pos = 32;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) {
+        const uint32_t x = r[i] ^ t[i];
+        if (x) pos = 4 * i + (__builtin_ctz(x) >> 3);
+    }
+    return pos;
+}
+
+// longest common extension of R[a..] and T[b..], at most maxlen bytes (extend_alignment,
+// compression.cpp:27-34); whole wave.  First from the LDS copy when both starts lie in it; then
+// from HBM, 2 KiB per round trip (lanes 0-3 load the LEAD bytes before the stretch compared), every
+// HBM step leaving its bytes in the copy.
+__device__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a, int32_t b, int32_t maxlen) {
+    const int lane = lane_id();
+    if (maxlen <= 0) return 0;
+    int32_t off = 0;
+    if (a >= B.rb0 && b >= B.tb0 && a < B.rb0 + LBV && b < B.tb0 + LBV) {
+        int32_t avail = B.rb0 + LBV - a < B.tb0 + LBV - b ? B.rb0 + LBV - a : B.tb0 + LBV - b;
+        if (avail > maxlen) avail = maxlen;
+        const int32_t my = 32 * lane;
+        int32_t e = INT32_MAX;
+        if (my < avail) {
+            uint32_t r[8], t[8];
+            loadw_lds<8>(L.rbuf, a - B.rb0 + my, r);
+            loadw_lds<8>(L.tbuf, b - B.tb0 + my, t);
+            int pos = first_diff32(r, t);
+            if (avail - my < 32 && pos >= avail - my) pos = avail - my == maxlen - my ? avail - my : 32;
+            if (pos < 32) e = my + pos;
+        }
+        const unsigned long long sm = __ballot(e != INT32_MAX);
+        if (sm) {
+            const int32_t m = lane_val(e, first_lane(sm));
+            return m < maxlen ? m : maxlen;
+        }
+        if (avail >= maxlen) return maxlen;
+        off = avail;
+    }
+    while (off < maxlen) {
+        const int32_t lead = (a + off >= LEAD && b + off >= LEAD) ? LEAD : 0;
+        const int32_t sa = a + off - lead, sb = b + off - lead;
+        uint32_t r[8], t[8];
+        loadw<8>(A.R + sa + 32 * lane, r);
+        loadw<8>(A.T + sb + 32 * lane, t);
+        wave_sync();   // the copy's previous readers are done
+        {
+            uint4* dr = reinterpret_cast<uint4*>(L.rbuf) + 2 * lane;
+            uint4* dt = reinterpret_cast<uint4*>(L.tbuf) + 2 * lane;
+            dr[0] = make_uint4(r[0], r[1], r[2], r[3]); dr[1] = make_uint4(r[4], r[5], r[6], r[7]);
+            dt[0] = make_uint4(t[0], t[1], t[2], t[3]); dt[1] = make_uint4(t[4], t[5], t[6], t[7]);
+        }
+        wave_sync();
+        B.rb0 = sa;
+        B.tb0 = sb;
+        const int32_t rel = 32 * lane - lead;   // this lane's bytes, from a + off
+        int32_t e = INT32_MAX;
+        if (rel >= 0 && rel < maxlen - off) {
+            int pos = first_diff32(r, t);
+            const int32_t lim = maxlen - off - rel;
+            if (lim < 32 && pos > lim) pos = lim;
+            if (pos < 32) e = off + rel + pos;
+        }
+        const unsigned long long sm = __ballot(e != INT32_MAX);
+        if (sm) {
+            const int32_t m = lane_val(e, first_lane(sm));
+            return m < maxlen ? m : maxlen;
+        }
+        off += LBV - lead;
+    }
+    return maxlen;
+}
+
+// the same from HBM only (no copy kept; 2 KiB per round trip)
+__device__ int32_t wave_lce_hbm(const uint8_t* __restrict__ R, int32_t a, const uint8_t* __restrict__ T, int32_t b,
+                                int32_t maxlen) {
     const int lane = lane_id();
     for (int32_t off = 0; off < maxlen; off += 2048) {
         const int32_t my = off + 32 * lane;
-        int32_t valid = maxlen - my;
         int32_t e = INT32_MAX;
-        if (valid > 0) {
+        if (maxlen - my > 0) {
             uint32_t r[8], t[8];
             loadw<8>(R + a + my, r);
             loadw<8>(T + b + my, t);
-            int pos = 32;
-#pragma unroll
-            for (int i = 7; i >= 0; i--) {
-                const uint32_t x = r[i] ^ t[i];
-                if (x) pos = 4 * i + (__builtin_ctz(x) >> 3);
-            }
-            if (valid < 32 && pos > valid) pos = valid;
+            int pos = first_diff32(r, t);
+            if (maxlen - my < 32 && pos > maxlen - my) pos = maxlen - my;
             if (pos < 32) e = my + pos;
         }
-        // lanes cover increasing offsets: the first lane that stops holds the extension
         const unsigned long long sm = __ballot(e != INT32_MAX);
         if (sm) {
             const int32_t m = lane_val(e, first_lane(sm));
@@ -213,7 +277,8 @@ __device__ int32_t wave_lce(const uint8_t* __restrict__ R, int32_t a, const uint
 // ---------------------------------------------------------------------------------------------
 // window of P in registers: lane l holds the keys of window indices 4l+q (q < 4), i.e. of the
 // reference k-mers starting at lo+4l+q, lo = max(0, P-m), up to hi = min(nR-k, P+m).
-// 2m+1 <= 4*64 window positions (m = 100: 201).
+// 2m+1 <= 4*64 window positions (m = 100: 201).  Its bytes come from the LDS copy when they lie
+// in it.
 // ---------------------------------------------------------------------------------------------
 struct RegWin {
     int32_t P, lo, n;
@@ -221,7 +286,8 @@ struct RegWin {
     uint32_t vmask;   // bit q: index 4*lane+q is inside the window
 };
 
-__device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin& W) {
+__device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin& W, const WalkLds* L = nullptr,
+                                           const BufPos* B = nullptr) {
     const int lane = lane_id(), k = A.k;
     W.P = P;
     W.lo = P - A.m < 0 ? 0 : P - A.m;
@@ -230,10 +296,12 @@ __device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin&
     if (W.n < 0) W.n = 0;
     W.vmask = 0;
     W.key[0] = W.key[1] = W.key[2] = W.key[3] = 0;
+    const bool lds = L && B->has_r(W.lo, W.n + 20);
     const int i0 = 4 * lane;
     if (i0 >= W.n) return;
     uint32_t w[5];   // 20 bytes >= 3 + k
-    loadw<5>(A.R + W.lo + i0, w);
+    if (lds) loadw_lds<5>(L->rbuf, W.lo - B->rb0 + i0, w);
+    else loadw<5>(A.R + W.lo + i0, w);
     uint64_t code;
     uint32_t bad;
     pack_codes<5>(w, code, bad);
@@ -248,16 +316,6 @@ __device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin&
 // key of the target k-mer at y from its 16 bytes w (loaded by the caller; k <= 15)
 __device__ __forceinline__ uint32_t target_key_w(const WalkPtrs& A, int32_t y, const uint32_t (&w)[4]) {
     const int k = A.k;
-    uint64_t code;
-    uint32_t bad;
-    pack_codes<4>(w, code, bad);
-    return bad & ((1u << k) - 1u) ? exotic_key(A.T + y, k) : (uint32_t)code & ((1u << (2 * k)) - 1u);
-}
-// key of the target k-mer at y (one unaligned 16-byte load; k <= 15)
-__device__ __forceinline__ uint32_t target_key(const WalkPtrs& A, int32_t y) {
-    const int k = A.k;
-    uint32_t w[4];
-    loadw<4>(A.T + y, w);
     uint64_t code;
     uint32_t bad;
     pack_codes<4>(w, code, bad);
@@ -278,43 +336,29 @@ __device__ __forceinline__ uint32_t win_match(const WalkPtrs& A, const RegWin& W
     return m;
 }
 
-// LDS hash of the register window's keys (only needed for wide literal scans)
-__device__ void hash_window(const RegWin& W, WalkLds& L) {
+// LDS Bloom filter of the register window's keys (only needed for wide literal scans)
+__device__ void bloom_window(const RegWin& W, WalkLds& L) {
     const int lane = lane_id();
-    for (int i = lane; i < WTSLOTS / 2; i += 64) L.wtab[i] = 0;
-    for (int i = lane; i < (1 << (WFBITS - 5)); i += 64) L.wbits[i] = 0;
+    uint4* b4 = reinterpret_cast<uint4*>(L.wbits);
+    for (int i = lane; i < (1 << (WFBITS - 5)) / 4; i += 64) b4[i] = make_uint4(0, 0, 0, 0);
     wave_sync();
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         if ((W.vmask >> q) & 1u) {
-            const int i = 4 * lane + q;
-            L.wkeys[i] = W.key[q];
-            wt_insert(L.wtab, W.key[q], (uint32_t)i + 1);
-            const uint32_t fb = slot_hash(W.key[q], WFBITS), fb2 = wf_h2(W.key[q]);
-            atomicOr(&L.wbits[fb >> 5], 1u << (fb & 31));
-            atomicOr(&L.wbits[fb2 >> 5], 1u << (fb2 & 31));
+            const uint32_t f1 = wf_h1(W.key[q]), f2 = wf_h2(W.key[q]), f3 = wf_h3(W.key[q]);
+            atomicOr(&L.wbits[f1 >> 5], 1u << (f1 & 31));
+            atomicOr(&L.wbits[f2 >> 5], 1u << (f2 & 31));
+            atomicOr(&L.wbits[f3 >> 5], 1u << (f3 & 31));
         }
     }
     wave_sync();
 }
 
-__device__ __forceinline__ bool window_has_key(const WalkLds& L, uint32_t key) {
-    int slot = (int)slot_hash(key, WTBITS);
-    for (int probes = 0; probes < WTSLOTS; probes++) {
-        const uint32_t v = wt_get(L.wtab, slot);
-        if (!v) return false;
-        if (L.wkeys[v - 1] == key) return true;
-        slot = (slot + 1) & (WTSLOTS - 1);
-    }
-    return false;
-}
-
-// Wide literal scan: first position in [x, end) whose k-mer key occurs in the window (1024
-// positions per wave step: 16 consecutive per lane, keys by shifting one packed code word).  Key
-// equality is a superset of byte equality, so every position skipped is certainly a literal step;
-// a returned position is re-checked exactly by the caller.  Returns `end` when there is none.
+// Wide literal scan: first position in [x, end) whose k-mer occurs in the window W, or `end` (1024
+// positions per wave step: 16 consecutive per lane, keys by shifting one packed code word; the
+// Bloom filter passes a superset, confirmed exactly against the register window in position order).
 constexpr int WIDE = 16;   // positions per lane per step (1024 per wave step)
-__device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, int32_t x, int32_t end) {
+__device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, const RegWin& W, int32_t x, int32_t end) {
     const int lane = lane_id(), k = A.k;
     const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
     uint32_t w[8];   // 32 bytes >= WIDE + k - 1; the next step's words are loaded one step ahead
@@ -325,27 +369,34 @@ __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L
         uint32_t bad;
         pack_codes<8>(w, code, bad);
         if (base + 64 * WIDE < end) loadw<8>(A.T + p0 + 64 * WIDE, w);
-        // bitmap pre-filter for all 16 positions (independent LDS reads), exact probes in order
+        // Bloom test for all 16 positions (independent LDS reads)
         uint32_t cand = 0;
 #pragma unroll
         for (int st = 0; st < WIDE; st++) {
             const uint32_t key = (bad >> st) & KM ? KEY_EXOTIC : (uint32_t)(code >> (2 * st)) & MASK;
-            const uint32_t fb = slot_hash(key, WFBITS), fb2 = wf_h2(key);
+            const uint32_t f1 = wf_h1(key), f2 = wf_h2(key), f3 = wf_h3(key);
             // exotic k-mers always go to the exact check (their key needs the bytes)
-            if (key == KEY_EXOTIC || ((L.wbits[fb >> 5] >> (fb & 31)) & (L.wbits[fb2 >> 5] >> (fb2 & 31)) & 1u))
+            if (key == KEY_EXOTIC ||
+                ((L.wbits[f1 >> 5] >> (f1 & 31)) & (L.wbits[f2 >> 5] >> (f2 & 31)) & (L.wbits[f3 >> 5] >> (f3 & 31)) & 1u))
                 cand |= 1u << st;
         }
         const int32_t lim = end - p0;
         if (lim < WIDE) cand &= lim > 0 ? (1u << lim) - 1u : 0u;
-        int32_t first = INT32_MAX;
-        while (cand) {
-            const int st = __ffs((int)cand) - 1;
-            cand &= cand - 1;
-            const uint32_t key = (bad >> st) & KM ? exotic_key(A.T + p0 + st, k) : (uint32_t)(code >> (2 * st)) & MASK;
-            if (window_has_key(L, key)) { first = p0 + st; break; }
+        // exact check of the candidates, lanes in position order
+        for (unsigned long long hm = __ballot(cand != 0); hm; hm &= hm - 1) {
+            const int l = __ffsll((long long)hm) - 1;
+            uint32_t c = lane_val(cand, l);
+            const uint32_t clo = lane_val((uint32_t)code, l), chi = lane_val((uint32_t)(code >> 32), l);
+            const uint32_t cbad = lane_val(bad, l);
+            const uint64_t lc = ((uint64_t)chi << 32) | clo;
+            while (c) {
+                const int st = __ffs((int)c) - 1;
+                c &= c - 1;
+                const int32_t y = base + WIDE * l + st;
+                const uint32_t key = (cbad >> st) & KM ? exotic_key(A.T + y, k) : (uint32_t)(lc >> (2 * st)) & MASK;
+                if (__ballot(win_match(A, W, key, y) != 0)) return y;
+            }
         }
-        const unsigned long long hm = __ballot(first != INT32_MAX);   // lanes in position order
-        if (hm) return lane_val(first, first_lane(hm));
     }
     return end;
 }
@@ -357,7 +408,7 @@ __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0);   // anchors, bel
 
 constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail
 #ifndef WALK_WAVES_PER_EU
-#define WALK_WAVES_PER_EU 6
+#define WALK_WAVES_PER_EU 5
 #endif
 template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
@@ -418,8 +469,10 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
     uint64_t dbg_c[13] = {};   // matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail,
                                // t_hash, t_wide, wide positions
     uint64_t tq = dbg_t0;
+    // per-phase clocks only with SCCG_DEBUG_PHASES (each clock read costs a scalar-memory round trip)
+    const bool phases = DBG && A.dbg_phases;
     auto tick = [&](int slot) {
-        if (DBG) { const uint64_t t = wall_clock64(); dbg_c[slot] += t - tq; tq = t; }
+        if (DBG && phases) { const uint64_t t = wall_clock64(); dbg_c[slot] += t - tq; tq = t; }
     };
     if (P == INVALID) {   // speculative chunk without an anchor: nothing to offer
         if (lane == 0) { A.cnt[ob][j] = 0; A.exitX[j] = INVALID; A.exitP[j] = INVALID; }
@@ -434,7 +487,8 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
 
     RegWin W;
     W.P = INVALID;
-    int32_t hashP = INVALID;   // P whose window keys are in the LDS hash (built only for wide scans)
+    int32_t bloomP = INVALID;   // P whose window keys are in the LDS Bloom filter (built only for wide scans)
+    BufPos B;                   // the LDS copy of R'/T' (see WalkLds)
     int32_t lme = x;   // target index after the last match of this walk (start of the open literal run)
     bool converged = false, escalated = false;
     const int32_t scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
@@ -444,15 +498,33 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
     const int32_t old_seedq = cb >= 0 ? uni(A.seedq[j]) : 0;
     int32_t seed_x = x, seedq = 0;
     bool truncated = false;
+    // the previous trajectory (fix-ups), 64 entries at a time in registers: lane i holds entry cq0 + i
+    int32_t cq0 = -1, ctv = INT32_MAX, cpv = 0, clv = 0;
+    auto load_prev = [&](int32_t from) {
+        cq0 = from;
+        const int32_t qi = from + lane;
+        ctv = qi < cc ? ct[qi] : INT32_MAX;
+        cpv = qi < cc ? cp[qi] : 0;
+        clv = qi < cc ? cl[qi] : 0;
+    };
+    if (cb >= 0) load_prev(q);   // issued now, waited for at the first match
+    // records of the trajectory not stored yet: entries [rb_n0, n), entry rb_n0 + i in lane i (a store
+    // per step would make every later load wait for it: vmcnt counts stores and loads in issue order)
+    int32_t rb_n0 = n, rbt = 0, rbp = 0, rbl = 0;
+    auto flush_recs = [&]() {
+        if (lane < n - rb_n0) { ot[rb_n0 + lane] = rbt; op[rb_n0 + lane] = rbp; ol[rb_n0 + lane] = rbl; }
+        rb_n0 = n;
+    };
     while (x < scan_end) {
         if (x >= budget_end) { truncated = true; break; }
         if (DBG) tick(9);
-        // the target probe's bytes are loaded before the window's, so both round trips overlap
+        // the probe: keys of the 64 target positions from x (from the LDS copy when it holds them)
         const int32_t y_l = x + lane;
         const bool valid = y_l < scan_end;
         uint32_t tw[4];
-        loadw<4>(A.T + y_l, tw);   // 4 KiB readable slack after T: no bound needed for the load
-        if (W.P != P) { reg_window(A, P, W); if (DBG) dbg_c[3]++; }
+        if (B.has_t(x, 64 + 16)) loadw_lds<4>(L.tbuf, y_l - B.tb0, tw);
+        else loadw<4>(A.T + y_l, tw);   // 4 KiB readable slack after T: no bound needed for the load
+        if (W.P != P) { reg_window(A, P, W, &L, &B); if (DBG) dbg_c[3]++; }
         if (DBG) tick(6);
         if (W.n <= 0) { x = scan_end; break; }
         if (DBG) dbg_c[1]++;
@@ -482,10 +554,10 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
                     if (cpt < wend) wend = cpt;
                 }
                 if (DBG) tick(9);
-                if (hashP != P) { hash_window(W, L); hashP = P; }
+                if (bloomP != P) { bloom_window(W, L); bloomP = P; }
                 if (DBG) tick(10);
                 const int32_t x0 = x;
-                x = wide_scan(A, L, x, wend);
+                x = wide_scan(A, L, W, x, wend);   // exact: x is a hit (or wend)
                 if (DBG) { dbg_c[2]++; dbg_c[12] += x - x0; tick(11); }
             }
             continue;
@@ -509,7 +581,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
                 int32_t maxlen = A.nR - (c + k);
                 const int32_t mt = A.nT - (y + k);
                 if (mt < maxlen) maxlen = mt;
-                const int32_t l = k + wave_lce(A.R, c + k, A.T, y + k, maxlen);   // extend_alignment
+                const int32_t l = k + wave_lce(A, L, B, c + k, y + k, maxlen);   // extend_alignment
                 ncand++;
                 if (l > bl) { bl = l; bcnt = 1; bhas0 = (c == 0); bkey = c ? pick_key(c, P) : ~0ull; }
                 else if (l == bl) {
@@ -535,19 +607,27 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
             }
             break;
         }
-        if (lane == 0) { ot[n] = y; op[n] = p; ol[n] = bl; }
-        n++;
+        {   // the record goes to lane n - rb_n0's registers; 64 at a time are stored together
+            const int slot = n - rb_n0;
+            if (lane == slot) { rbt = y; rbp = p; rbl = bl; }
+            n++;
+            if (slot == 63) flush_recs();
+        }
         if (DBG) { dbg_c[0]++; dbg_c[4] += ncand; dbg_c[5] += bl; tick(8); }
-        // ---- convergence with the previous trajectory of this chunk
+        // ---- convergence with the previous trajectory of this chunk: q = its first entry with
+        //      t >= y (entries are in t order)
         if (cb >= 0) {
             for (;;) {
-                const int32_t qi = q + lane;
-                const bool ge = qi >= cc || ct[qi] >= y;
+                if (q >= cq0 + 64) load_prev(q);
+                const int32_t qi = cq0 + lane;
+                const bool ge = qi >= q && (qi >= cc || ctv >= y);
                 const unsigned long long gm = __ballot(ge);
-                if (gm) { q += first_lane(gm); break; }
-                q += 64;
+                if (gm) { q = cq0 + first_lane(gm); break; }
+                q = cq0 + 64;
             }
-            if (q < cc && q >= old_seedq && ct[q] == y && cp[q] == p && cl[q] == bl) {
+            const int ql = q - cq0;
+            if (q < cc && q >= old_seedq && lane_val(ctv, ql) == y && lane_val(cpv, ql) == p && lane_val(clv, ql) == bl) {
+                flush_recs();
                 const int32_t rest = cc - q - 1;
                 for (int i = lane; i < rest; i += 64) {
                     ot[n + i] = ct[q + 1 + i];
@@ -555,6 +635,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
                     ol[n + i] = cl[q + 1 + i];
                 }
                 n += rest;
+                rb_n0 = n;   // the copied suffix is stored already
                 converged = true;
                 break;
             }
@@ -563,6 +644,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
         P = p + bl - 1;   // compression.cpp:149
         x = y + bl;       // compression.cpp:159
     }
+    flush_recs();
     if (escalated) return;
     if (DBG && lane == 0) {
         tick(9);
@@ -570,6 +652,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
         d[0] = wall_clock64() - dbg_t0;
         for (int i = 0; i < 13; i++) d[1 + i] = dbg_c[i];
         d[14] = (uint64_t)A.round;
+        d[15] = dbg_t0;   // start (wall clock), for the launch's start spread
     }
     if (lane == 0 && truncated) {   // nothing to commit; the chunk stays pending
         A.conv[j] = 0;
@@ -638,13 +721,13 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int fbas
     RegWin W;
     reg_window(A, P, W);
     if (W.n <= 0) return;
-    hash_window(W, L);
+    bloom_window(W, L);
     const int32_t end = A.nT - A.k + 1;
     const int64_t gw = (int64_t)blockIdx.x * WPB + wave_in_block(), G = (int64_t)gridDim.x * WPB;
     for (int64_t base = x0 + gw * 64 * WIDE; base < end; base += G * 64 * WIDE) {
         if (base >= (int64_t)__hip_atomic_load(&A.fy[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
         const int32_t seg_end = base + 64 * WIDE < end ? (int32_t)(base + 64 * WIDE) : end;
-        const int32_t y = wide_scan(A, L, (int32_t)base, seg_end);
+        const int32_t y = wide_scan(A, L, W, (int32_t)base, seg_end);
         if (y < seg_end) {
             if (lane_id() == 0) atomicMin(&A.fy[fi], y);
             return;
@@ -744,6 +827,7 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.scal[0] = 0; A.scal[1] = 0; A.scal[2] = startX; A.scal[3] = startP;
+        A.scal[5] = 0;   // frozen count (k_walk resets it too, but a void round's k_walk returns first)
         A.snapX[0] = startX;
         A.snapP[0] = startP;
     }
@@ -1225,7 +1309,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_cand_stats(WalkPtrs A) {
             const int32_t c = A.cand[i];
             int32_t maxlen = A.nR - (c + k);
             if (A.nT - k < maxlen) maxlen = A.nT - k;
-            const uint32_t l = (uint32_t)(k + wave_lce(A.R, c + k, A.T, k, maxlen));
+            const uint32_t l = (uint32_t)(k + wave_lce_hbm(A.R, c + k, A.T, k, maxlen));
             v = cb_merge(v, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key(c, -1) : ~0ull});
         }
     }
@@ -1305,6 +1389,48 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_flatten(WalkPtrs A, int32_t firs
     for (int i = lane; i < n; i += 64) { A.ft[o + i] = t[i]; A.fp[o + i] = p[i]; A.fl[o + i] = l[i]; }
 }
 
+// A long literal stretch of the record text, queued for k_long_copy in pieces of at most
+// LONG_PIECE bytes (one wave copies one piece).  Every piece but a stretch's last is LONG_PIECE
+// long and every stretch is >= LONG_GAP, so nT / LONG_GAP + nT / LONG_PIECE + 2 entries suffice.
+constexpr int64_t LONG_PIECE = 64 * 1024;
+__device__ __forceinline__ void queue_long(const WalkPtrs& A, int64_t src, int64_t dst, int64_t len) {
+    const int64_t np = (len + LONG_PIECE - 1) / LONG_PIECE;
+    const int64_t e = (int64_t)atomicAdd((unsigned long long*)&A.scal64[2], (unsigned long long)np);
+    for (int64_t i = 0; i < np && e + i < A.lgap_cap; i++) {
+        int64_t* q = A.lgap + 3 * (e + i);
+        q[0] = src + i * LONG_PIECE;
+        q[1] = dst + i * LONG_PIECE;
+        q[2] = len - i * LONG_PIECE < LONG_PIECE ? len - i * LONG_PIECE : LONG_PIECE;
+    }
+}
+
+// One wave copies n bytes s -> d: byte head up to 16-byte alignment of d, then 16-byte stores fed by
+// unaligned dword loads (s needs 4 readable bytes of slack), eight per lane in flight, byte tail.
+__device__ __forceinline__ void wave_copy(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, int64_t n) {
+    const int lane = lane_id();
+    int64_t head = (int64_t)((16 - ((uintptr_t)d & 15)) & 15);
+    if (head > n) head = n;
+    if (lane < head) d[lane] = s[lane];
+    s += head; d += head; n -= head;
+    const int64_t nb = n >> 4;
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    for (int64_t c0 = 0; c0 < nb; c0 += 8 * 64) {
+        uint32_t w[8][4];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int64_t c = c0 + u * 64 + lane;
+            if (c < nb) loadw<4>(s + 16 * c, w[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int64_t c = c0 + u * 64 + lane;
+            if (c < nb) d4[c] = make_uint4(w[u][0], w[u][1], w[u][2], w[u][3]);
+        }
+    }
+    const int64_t t = nb << 4;
+    if (t + lane < n) d[t + lane] = s[t + lane];
+}
+
 // abs_p: absolute p (the text compress_genome writes before delta_encode, compression.cpp:567)
 __global__ void k_match_textlen(WalkPtrs A, int64_t nm, int abs_p) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1331,10 +1457,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_match_textwrite(WalkPtrs A, int6
         if (gap <= SHORT_GAP)
             for (int32_t q = 0; q < gap; q++) out[o + q] = A.T[pend + q];
     }
-    if (valid && gap >= LONG_GAP) {   // literal-heavy stretches: the whole grid copies them
-        const int64_t e = (int64_t)atomicAdd((unsigned long long*)&A.scal64[2], 1ull);
-        if (e < A.lgap_cap) { A.lgap[3 * e] = pend; A.lgap[3 * e + 1] = o; A.lgap[3 * e + 2] = gap; }
-    }
+    if (valid && gap >= LONG_GAP) queue_long(A, pend, o, gap);   // literal-heavy stretches: k_long_copy
     for (unsigned long long lm = __ballot(valid && gap > SHORT_GAP && gap < LONG_GAP); lm; lm &= lm - 1) {
         const int l = __ffsll((long long)lm) - 1;
         const int32_t gp = __shfl(pend, l, 64), gg = __shfl(gap, l, 64);
@@ -1406,10 +1529,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_chunk_text(WalkPtrs A, FirstMatc
         const bool lng = mine && len >= LONG_GAP, med = mine && len > SHORT_GAP && len < LONG_GAP;
         if (mine && len <= SHORT_GAP)
             for (int64_t q = 0; q < len; q++) out[at + q] = A.T[src + q];
-        if (lng) {
-            const int64_t e = (int64_t)atomicAdd((unsigned long long*)&A.scal64[2], 1ull);
-            if (e < A.lgap_cap) { A.lgap[3 * e] = src; A.lgap[3 * e + 1] = at; A.lgap[3 * e + 2] = len; }
-        }
+        if (lng) queue_long(A, src, at, len);
         for (unsigned long long lm = __ballot(med); lm; lm &= lm - 1) {
             const int l = __ffsll((long long)lm) - 1;
             const int64_t gs = __shfl(src, l, 64), gl = __shfl(len, l, 64), go = __shfl(at, l, 64);
@@ -1451,46 +1571,21 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_chunk_text(WalkPtrs A, FirstMatc
     if (!WRITE && lane == 0) A.ctext[j] = o;
 }
 
-// the queued long gaps: every gap is cut into 4 KiB pieces, numbered across the gaps in queue
-// order and dealt round-robin to the blocks; the queue is read through LDS 256 entries at a time
-__global__ __launch_bounds__(256) void k_long_copy(WalkPtrs A, uint8_t* __restrict__ out) {
-    constexpr int64_t PIECE = 4096;   // one 16-byte stretch per thread
-    __shared__ int64_t es[3 * 256];
+// the queued long literal pieces: one wave per piece
+__global__ __launch_bounds__(SCCG_BLOCK) void k_long_copy(WalkPtrs A, uint8_t* __restrict__ out) {
     const int64_t ne = A.scal64[2] < A.lgap_cap ? A.scal64[2] : A.lgap_cap;
-    int64_t pc = 0;   // pieces of the gaps before the current one (identical in every block)
-    for (int64_t e0 = 0; e0 < ne; e0 += 256) {
-        const int m = ne - e0 < 256 ? (int)(ne - e0) : 256;
-        __syncthreads();
-        if ((int)threadIdx.x < m)
-            for (int c = 0; c < 3; c++) es[3 * threadIdx.x + c] = A.lgap[3 * (e0 + threadIdx.x) + c];
-        __syncthreads();
-        for (int i = 0; i < m; i++) {
-            const int64_t len = es[3 * i + 2], np = (len + PIECE - 1) / PIECE;
-            // this block's first piece of the gap: the least g >= pc with g % gridDim.x == blockIdx.x
-            int64_t q = ((int64_t)blockIdx.x - pc % gridDim.x + gridDim.x) % gridDim.x;
-            for (; q < np; q += gridDim.x) {
-                const uint8_t* src = A.T + es[3 * i] + q * PIECE;
-                uint8_t* dst = out + es[3 * i + 1] + q * PIECE;
-                const int64_t plen = len - q * PIECE < PIECE ? len - q * PIECE : PIECE;
-                const int64_t b = (int64_t)threadIdx.x * 16;
-                if (b + 16 <= plen) {
-                    uint8_t v[16];
-#pragma unroll
-                    for (int k2 = 0; k2 < 16; k2++) v[k2] = src[b + k2];
-#pragma unroll
-                    for (int k2 = 0; k2 < 16; k2++) dst[b + k2] = v[k2];
-                } else {
-                    for (int64_t k2 = b; k2 < plen; k2++) dst[k2] = src[k2];
-                }
-            }
-            pc += np;
-        }
+    const int64_t G = (int64_t)gridDim.x * WPB;
+    for (int64_t e = (int64_t)blockIdx.x * WPB + wave_in_block(); e < ne; e += G) {
+        const int64_t src = A.lgap[3 * e], dst = A.lgap[3 * e + 1], len = A.lgap[3 * e + 2];
+        wave_copy(A.T + src, out + dst, len);
     }
 }
 
-__global__ void k_copy(const uint8_t* __restrict__ in, int64_t n, uint8_t* __restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = in[i];
+// out[0, n) = in[0, n): every wave takes LONG_PIECE-byte pieces
+__global__ __launch_bounds__(SCCG_BLOCK) void k_copy(const uint8_t* __restrict__ in, int64_t n, uint8_t* __restrict__ out) {
+    const int64_t G = (int64_t)gridDim.x * WPB;
+    for (int64_t o = ((int64_t)blockIdx.x * WPB + wave_in_block()) * LONG_PIECE; o < n; o += G * LONG_PIECE)
+        wave_copy(in + o, out + o, n - o < LONG_PIECE ? n - o : LONG_PIECE);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1575,7 +1670,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.tlen = c.take<int64_t>(maxm + 1);
     A.partial = c.take<int64_t>((size_t)scan_partials_needed((int64_t)(maxm > C ? maxm : C) + 1) + 16);
     A.scal64 = c.take<int64_t>(8);
-    A.lgap_cap = nT / LONG_GAP + 2;
+    A.lgap_cap = nT / LONG_GAP + nT / LONG_PIECE + 2;
     A.lgap = c.take<int64_t>(3 * (size_t)A.lgap_cap);
     A.cprev = c.take<int64_t>(C + 1);
     A.ctext = c.take<int64_t>(C + 1);
@@ -1770,6 +1865,7 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
                    size_t ws_bytes, size_t* used) {
     WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, used);
     if (!getenv("SCCG_DEBUG")) A.dbg = nullptr;   // per-chunk counters only in diagnostic runs
+    A.dbg_phases = getenv("SCCG_DEBUG_PHASES") != nullptr;
     static const int32_t sb = [] {
         const char* e = getenv("SCCG_STALE_BUDGET");
         return e ? atoi(e) : STALE_BUDGET_DEFAULT;
@@ -2106,14 +2202,31 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                         (unsigned long long)sorted[C * 99 / 100], (unsigned long long)sorted[C - 1],
                         (unsigned long long)sum[1], (unsigned long long)sum[2], (unsigned long long)sum[3],
                         (unsigned long long)sum[4], (unsigned long long)sum[5], (unsigned long long)sum[6]);
+                {   // launch spread: when the chunks' waves started and ended, from the first start
+                    uint64_t s0 = ~0ull;
+                    for (size_t j = 0; j < C; j++) if (d[j * DS + 14] == (uint64_t)round && d[j * DS + 15] < s0) s0 = d[j * DS + 15];
+                    std::vector<uint64_t> st, en;
+                    for (size_t j = 0; j < C; j++)
+                        if (d[j * DS + 14] == (uint64_t)round) { st.push_back(d[j * DS + 15] - s0); en.push_back(d[j * DS + 15] - s0 + d[j * DS]); }
+                    if (!st.empty()) {
+                        std::sort(st.begin(), st.end());
+                        std::sort(en.begin(), en.end());
+                        const size_t m = st.size();
+                        fprintf(stderr, "[walk] r%lld %zu waves: start p50 %llu p90 %llu max %llu | end p50 %llu p90 %llu p99 %llu max %llu (10ns)\n",
+                                (long long)round, m, (unsigned long long)st[m / 2], (unsigned long long)st[m * 9 / 10],
+                                (unsigned long long)st[m - 1], (unsigned long long)en[m / 2], (unsigned long long)en[m * 9 / 10],
+                                (unsigned long long)en[m * 99 / 100], (unsigned long long)en[m - 1]);
+                    }
+                }
                 fprintf(stderr, "[walk] r1 step phases (10ns, summed over chunks): window %llu find %llu cand+lce %llu tail %llu "
                         "hash %llu wide %llu (wide positions %llu)\n",
                         (unsigned long long)sum[7], (unsigned long long)sum[8], (unsigned long long)sum[9], (unsigned long long)sum[10],
                         (unsigned long long)sum[11], (unsigned long long)sum[12], (unsigned long long)sum[13]);
                 std::vector<size_t> idx(C);
                 for (size_t j = 0; j < C; j++) idx[j] = j;
-                std::partial_sort(idx.begin(), idx.begin() + 5, idx.end(), [&](size_t a, size_t b) { return tk[a] > tk[b]; });
-                for (int q = 0; q < 5; q++) {
+                const size_t nshow = C < 5 ? C : 5;
+                std::partial_sort(idx.begin(), idx.begin() + nshow, idx.end(), [&](size_t a, size_t b) { return tk[a] > tk[b]; });
+                for (size_t q = 0; q < nshow; q++) {
                     const uint64_t* e = &d[idx[q] * DS];
                     fprintf(stderr, "   slow chunk %zu: ticks %llu matches %llu batches %llu wides %llu windows %llu cands %llu ext %llu "
                             "| win %llu find %llu cand %llu tail %llu hash %llu wide %llu widepos %llu\n",
@@ -2216,8 +2329,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             nmc = spec_r[0];
             text = spec_r[1];
         } else if (nTp > 0) {   // no first match: the whole target is one literal
-            const unsigned g = grid_for(nTp, 256) > 8192 ? 8192 : grid_for(nTp, 256);
-            hipLaunchKernelGGL(k_copy, dim3(g), dim3(256), 0, s, Tp, nTp, out);
+            hipLaunchKernelGGL(k_copy, dim3(grid_for(nTp, WPB * LONG_PIECE)), dim3(SCCG_BLOCK), 0, s, Tp, nTp, out);
             SCCG_HIP(hipGetLastError());
             text = nTp;
         }
@@ -2267,8 +2379,8 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     }
     const int64_t tail = nTp - tail_from;
     if (tail > 0) {
-        const unsigned g = grid_for(tail, 256) > 8192 ? 8192 : grid_for(tail, 256);
-        hipLaunchKernelGGL(k_copy, dim3(g), dim3(256), 0, s, Tp + tail_from, tail, out + text);
+        hipLaunchKernelGGL(k_copy, dim3(grid_for(tail, WPB * LONG_PIECE)), dim3(SCCG_BLOCK), 0, s, Tp + tail_from, tail,
+                           out + text);
         SCCG_HIP(hipGetLastError());
     }
     *out_len = text + (tail > 0 ? tail : 0);
