@@ -71,6 +71,7 @@ typedef struct {
     int64_t walk_rounds;      /* global walk: speculative + fix-up rounds */
     int64_t walk_chunks;      /* global walk: chunks */
     int64_t record_bytes;     /* length of the whole compressed_genome.txt */
+    int64_t walk_chains;      /* global walk: frozen chains resolved by the chain kernels */
 } sccg_stats;
 
 int sccg_ctx_create(int device, sccg_ctx** out);

@@ -18,6 +18,7 @@ enum ProfId {
     PROF_PRESENCE,       // k_presence
     PROF_FULLC,          // k_fullc
     PROF_MATCH_EMIT,     // k_match_textwrite
+    PROF_WALK_CHAIN,     // k_chain_fill (end of a frozen chain)
     PROF_DC_DECODE,      // k_tok_fill
     PROF_DC_FORMAT,      // k_format
     PROF_COUNT
@@ -133,6 +134,7 @@ struct WalkResult {
     int64_t n_matches;
     int64_t rounds;
     int64_t chunks;
+    int64_t chains;   // frozen chains walked by k_chain_* (rounds that had a frozen chunk)
 };
 size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk);
 // Global pass match_sequences(R', T', 14, 100, true) (compression.cpp:561) and its record text

@@ -582,6 +582,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         st.n_matches = wr.n_matches;
         st.walk_rounds = wr.rounds;
         st.walk_chunks = wr.chunks;
+        st.walk_chains = wr.chains;
         pos += rlen;
         mark("global_walk");
     }

@@ -64,6 +64,19 @@ constexpr int RESPEC_AHEAD = 256;
 constexpr int RESPEC_MAX_TRIGGERS = 64;
 constexpr int32_t LONG_GAP = 4096;   // literal gaps of the record text copied grid-wide
 constexpr int32_t CAND_CAP = 65536;  // early sweep: first-k-mer occurrences kept (more: full sweep later)
+// Frozen chains (k_chain_*): a committed frozen chunk's exit state is walked on over the rest of the
+// target by one wave that visits only "band hits" -- target positions whose k-mer occurs among the
+// reference k-mers within CH_BAND of the generation's P -- found by a grid scan.
+constexpr int CH_BAND = 512;           // band half-width (reference positions around P)
+constexpr int CH_TBITS = 13;           // band key table: 8192 LDS slots (load <= 1/2)
+constexpr int CH_GRID = 512;           // scan blocks (1024 threads, 16 positions each per step)
+constexpr int CH_HCAP = 4096;          // band hits kept per block and generation
+constexpr int32_t CHAIN_MCAP = 1 << 22;   // matches a chain may take
+constexpr int CH_GENS_PER_SYNC = 4;    // generations queued per host check
+constexpr int CH_MAX_GENS = 4096;      // generations per chain
+constexpr int64_t CH_DENSE_HITS = 32768;  // band hits of one generation that switch the chain to find-first generations
+constexpr int CH_DENSE_N = 32;         // hand back to the chunk rounds when CH_DENSE_N matches
+constexpr int32_t CH_DENSE_SPAN = 8192;   // fall within this many target bases (the walk is aligned again)
 
 struct WalkPtrs {
     const uint8_t* R;
@@ -125,6 +138,19 @@ struct WalkPtrs {
     int64_t* cprev;           // per chunk: last earlier chunk holding a match (max-scan), then text offsets
     int64_t* ctext;           // per chunk: record text bytes of its target range -> offsets
     int64_t lgap_cap;
+    // frozen chains (k_chain_*): state, the chain's matches, per-block band hits of a generation
+    int32_t* chs;             // [0] active [1] x [2] P [3] matches [4] start chunk [5] end reason
+                              // [6] band lo [7] band hi [8] generations [9] start x [10] start P
+                              // [11] consecutive generations whose first block overflowed
+                              // [12] mode (0 band hits, 1 find-first on the window) [13] first hit (mode 1)
+    int32_t* chm_t;
+    int32_t* chm_p;
+    int32_t* chm_l;
+    int32_t chm_cap;
+    int32_t* chh_y;           // CH_GRID x CH_HCAP band hits (position, key), in position order per block
+    uint32_t* chh_k;
+    int32_t* chh_n;           // per block: hits recorded, first position not covered (INT32_MAX: none)
+    int32_t* chh_tr;
     uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
     int32_t dbg_phases;       // SCCG_DEBUG_PHASES: also per-phase clocks
 };
@@ -883,6 +909,357 @@ __global__ __launch_bounds__(1024) void k_round_tail(WalkPtrs A, int fbase, int 
             }
             if (run != ~0ull) break;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Frozen chains.  After a deletion longer than m the reference walk's P stays near one reference
+// window (compression.cpp:83-101 admits only candidates within m of it): every later target
+// position is a literal step except rare chance hits, each of which moves P a little.  Resolving
+// that one chunk per round costs a round per hit.  Instead, from the exit state of the earliest
+// committed frozen chunk:
+//   k_chain_scan  (grid)   every target position from x whose k-mer occurs among the reference
+//                          k-mers within CH_BAND of P ("band hits"; exact keys, in position order);
+//   k_chain_step  (1 wave) the exact walk over those hits: a hit is a step only if its k-mer is in
+//                          the window of the current P (the same candidate / extension / selection
+//                          code as k_walk); every other position is a literal step, which is exact
+//                          as long as the window stays inside the band.  When it leaves the band,
+//                          or a block's hits overflowed, the next generation rescans from x.
+//   k_chain_fill           the chunks the chain covered get their trajectories and entry / exit
+//                          states, so the round tail finds them settled.
+// The chain hands back to the chunk rounds (reason 2) when its matches get dense (the walk is
+// aligned again), on a pn2 == 0 step, or when its match list is full.
+// ---------------------------------------------------------------------------------------------
+__global__ void k_chain_init(WalkPtrs A) {
+    if (A.scal[9]) return;
+    const int lane = lane_id();
+    const int nf = A.scal[5];
+    int32_t jm = INT32_MAX;
+    for (int f = lane; f < nf; f += 64) { const int32_t j = A.flist[f]; jm = j < jm ? j : jm; }
+    jm = wave_min(jm);
+    if (lane) return;
+    if (jm == INT32_MAX) { A.chs[0] = 0; A.chs[5] = 0; return; }
+    const int32_t x0 = A.exitX[jm], P0 = A.exitP[jm];
+    A.chs[0] = 1; A.chs[1] = x0; A.chs[2] = P0; A.chs[3] = 0; A.chs[4] = jm; A.chs[5] = 0;
+    A.chs[8] = 0; A.chs[9] = x0; A.chs[10] = P0; A.chs[11] = 0; A.chs[12] = 0; A.chs[13] = INT32_MAX;
+}
+
+__device__ __forceinline__ uint32_t ch_slot(uint32_t key) { return slot_hash(key, CH_TBITS); }
+constexpr uint32_t CH_EMPTY = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
+    __shared__ uint32_t tab[1 << CH_TBITS];
+    __shared__ int32_t wsum[17];
+    __shared__ int32_t trunc_s;
+    if (!A.chs[0]) return;
+    const int tid = (int)threadIdx.x, lane = lane_id(), w = wave_in_block(), k = A.k;
+    const int32_t x = A.chs[1], P = A.chs[2];
+    // mode 1 (band hits were dense): the band is the window itself and each block keeps only its
+    // first hit -- a find-first over the rest of the target (blocks past a found hit stop)
+    const bool first_only = A.chs[12] != 0;
+    const int32_t half = first_only ? A.m : CH_BAND;
+    const int32_t blo = P - half < 0 ? 0 : P - half;
+    const int32_t bhi = P + half < A.nR - k ? P + half : A.nR - k;
+    if (blockIdx.x == 0 && tid == 0) { A.chs[6] = blo; A.chs[7] = bhi; }
+    for (int i = tid; i < (1 << CH_TBITS); i += 1024) tab[i] = CH_EMPTY;
+    if (tid == 0) trunc_s = INT32_MAX;
+    __syncthreads();
+    const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
+    for (int32_t q = blo + tid; q <= bhi; q += 1024) {   // the band's keys
+        uint32_t wv[4], bad;
+        uint64_t code;
+        loadw<4>(A.R + q, wv);
+        pack_codes<4>(wv, code, bad);
+        uint32_t key = bad & KM ? exotic_key(A.R + q, k) : (uint32_t)code & MASK;
+        if (key == CH_EMPTY) key = CH_EMPTY - 1;   // (exotic hash collision: a superset is fine)
+        uint32_t sl = ch_slot(key);
+        for (;;) {
+            const uint32_t prev = atomicCAS(&tab[sl], CH_EMPTY, key);
+            if (prev == CH_EMPTY || prev == key) break;
+            sl = (sl + 1) & ((1u << CH_TBITS) - 1);
+        }
+    }
+    __syncthreads();
+    auto in_band = [&](uint32_t key) -> bool {
+        if (key == CH_EMPTY) key = CH_EMPTY - 1;
+        uint32_t sl = ch_slot(key);
+        for (;;) {
+            const uint32_t v = tab[sl];
+            if (v == key) return true;
+            if (v == CH_EMPTY) return false;
+            sl = (sl + 1) & ((1u << CH_TBITS) - 1);
+        }
+    };
+    const int32_t lastk1 = A.nT - k + 1;
+    const int64_t total = (int64_t)lastk1 - x;
+    int64_t span = total > 0 ? (total + CH_GRID - 1) / CH_GRID : 0;
+    span = (span + 15) & ~(int64_t)15;
+    const int64_t b0 = (int64_t)x + (int64_t)blockIdx.x * span;
+    const int64_t b1 = b0 + span < lastk1 ? b0 + span : lastk1;
+    int32_t* oy = A.chh_y + (size_t)blockIdx.x * CH_HCAP;
+    uint32_t* ok = A.chh_k + (size_t)blockIdx.x * CH_HCAP;
+    int32_t cnt = 0;
+    int64_t covered = b1;   // first position of the span not covered (b1: all of it)
+    for (int64_t base = b0; base < b1; base += 16 * 1024) {
+        if (first_only && base > (int64_t)__hip_atomic_load(&A.chs[13], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            covered = base;   // a hit lies before this block's rest: the step never gets here
+            break;
+        }
+        const int64_t p0 = base + 16 * tid;
+        uint32_t mask = 0;
+        uint64_t code = 0;
+        uint32_t bad = 0;
+        if (p0 < b1) {
+            uint32_t wv[8];
+            loadw<8>(A.T + p0, wv);   // 4 KiB readable slack after T'
+            pack_codes<8>(wv, code, bad);
+            const int lim = b1 - p0 < 16 ? (int)(b1 - p0) : 16;
+            for (int st = 0; st < lim; st++) {
+                const uint32_t key = (bad >> st) & KM ? exotic_key(A.T + p0 + st, k) : (uint32_t)(code >> (2 * st)) & MASK;
+                if (in_band(key)) mask |= 1u << st;
+            }
+        }
+        // block-wide exclusive count of the hits before this thread's (threads in position order)
+        const int c = __popc(mask);
+        const int incl = wave_incl_add(c);
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int i = 0; i < 16; i++) { const int t = wsum[i]; wsum[i] = acc; acc += t; }
+            wsum[16] = acc;
+        }
+        __syncthreads();
+        int idx = cnt + wsum[w] + incl - c;
+        const int tot = wsum[16];
+        for (uint32_t m = mask; m; m &= m - 1) {
+            const int st = __ffs((int)m) - 1;
+            const int32_t y = (int32_t)(p0 + st);
+            if (idx < CH_HCAP) {
+                oy[idx] = y;
+                ok[idx] = (bad >> st) & KM ? exotic_key(A.T + y, k) : (uint32_t)(code >> (2 * st)) & MASK;
+            } else if (idx == CH_HCAP) {
+                trunc_s = y;   // the first hit not kept: positions from here on are not covered
+            }
+            idx++;
+        }
+        cnt += tot;
+        __syncthreads();   // wsum reuse; trunc_s visible
+        if (cnt > CH_HCAP) { covered = trunc_s; break; }
+        if (first_only && cnt > 0) {   // this block's first hit is kept (the step needs no more)
+            const int32_t y0 = oy[0];
+            if (tid == 0) atomicMin(&A.chs[13], y0);
+            cnt = 1;
+            covered = (int64_t)y0 + 1;
+            break;
+        }
+    }
+    if (tid == 0) {
+        A.chh_n[blockIdx.x] = cnt < CH_HCAP ? cnt : CH_HCAP;
+        A.chh_tr[blockIdx.x] = covered < b1 ? (int32_t)covered : INT32_MAX;
+    }
+}
+
+// LDS table of the register window's keys (512 slots, <= 256 keys): 64 band hits are tested at once
+constexpr int CH_WBITS = 9;
+__device__ void chain_wtab_build(const RegWin& W, uint32_t* tab) {
+    const int lane = lane_id();
+    for (int i = lane; i < (1 << CH_WBITS); i += 64) tab[i] = CH_EMPTY;
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if ((W.vmask >> q) & 1u) {
+            uint32_t key = W.key[q] == CH_EMPTY ? CH_EMPTY - 1 : W.key[q];
+            uint32_t sl = slot_hash(key, CH_WBITS);
+            for (;;) {
+                const uint32_t prev = atomicCAS(&tab[sl], CH_EMPTY, key);
+                if (prev == CH_EMPTY || prev == key) break;
+                sl = (sl + 1) & ((1u << CH_WBITS) - 1);
+            }
+        }
+    }
+    wave_sync();
+}
+__device__ __forceinline__ bool chain_wtab_has(const uint32_t* tab, uint32_t key) {
+    if (key == CH_EMPTY) key = CH_EMPTY - 1;
+    uint32_t sl = slot_hash(key, CH_WBITS);
+    for (;;) {
+        const uint32_t v = tab[sl];
+        if (v == key) return true;
+        if (v == CH_EMPTY) return false;
+        sl = (sl + 1) & ((1u << CH_WBITS) - 1);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_chain_step(WalkPtrs A) {
+    __shared__ WalkLds L;
+    __shared__ uint32_t wtab[1 << CH_WBITS];
+    if (!A.chs[0]) return;
+    const int lane = lane_id(), k = A.k;
+    int32_t x = A.chs[1], P = A.chs[2], nm = A.chs[3];
+    const int32_t blo = A.chs[6], bhi = A.chs[7];
+    RegWin W;
+    W.P = INVALID;
+    BufPos B;
+    int32_t rt = INT32_MIN;   // lane i: target position of the last chain match with index = i (mod CH_DENSE_N)
+    int reason = 0;           // 0: next generation, 1: end of the target reached, 2: hand back
+    bool gen_end = false;
+    int64_t hits = 0;         // band hits of this generation
+    int64_t visited = 0;      // of which the step visited
+    for (int b = 0; b < CH_GRID && !gen_end && !reason; b++) {
+        const int32_t nh = A.chh_n[b], tr = A.chh_tr[b];
+        hits += nh;
+        const int32_t* hy = A.chh_y + (size_t)b * CH_HCAP;
+        const uint32_t* hk = A.chh_k + (size_t)b * CH_HCAP;
+        int32_t yv = lane < nh ? hy[lane] : INT32_MAX;
+        uint32_t kv = lane < nh ? hk[lane] : 0u;
+        for (int32_t i0 = 0; i0 < nh && !gen_end && !reason; i0 += 64) {
+            if (visited >= CH_DENSE_HITS) {
+                // band hits this dense cost the step more than one find-first generation per match:
+                // stop here (every position before this batch's first hit is settled) and switch
+                const int32_t y0 = lane_val(yv, 0);
+                if (x < y0) x = y0;
+                if (lane == 0) A.chs[12] = 1;
+                gen_end = true;
+                break;
+            }
+            visited += nh - i0 < 64 ? nh - i0 : 64;
+            // the next 64 hits are loaded while these are visited
+            const int32_t in = i0 + 64 + lane;
+            const int32_t yn = in < nh ? hy[in] : INT32_MAX;
+            const uint32_t kn = in < nh ? hk[in] : 0u;
+            const int cntl = nh - i0 < 64 ? nh - i0 : 64;
+            for (int li = 0; li < cntl;) {
+                if (W.P != P) {
+                    reg_window(A, P, W, &L, &B);
+                    chain_wtab_build(W, wtab);
+                }
+                if (W.n <= 0) break;
+                // the next of these 64 hits (from lane li) whose key is in the window (a superset
+                // for hash keys; win_match below is exact)
+                const bool cand = lane >= li && lane < cntl && yv >= x && chain_wtab_has(wtab, kv);
+                const unsigned long long cmk = __ballot(cand);
+                if (!cmk) break;
+                const int hl_ = first_lane(cmk);
+                li = hl_ + 1;
+                const int32_t y = lane_val(yv, hl_);
+                const uint32_t key = lane_val(kv, hl_);
+                const uint32_t mine = win_match(A, W, key, y);
+                if (!__ballot(mine != 0)) continue;
+                // ---- the step (as in k_walk: compression.cpp:110-159)
+                int32_t bl = 0, bcnt = 0;
+                bool bhas0 = false;
+                uint64_t bkey = ~0ull;
+                for (int qq = 0; qq < 4; qq++) {
+                    unsigned long long cm = __ballot((mine >> qq) & 1u);
+                    while (cm) {
+                        const int cl_ = __ffsll((long long)cm) - 1;
+                        cm &= cm - 1;
+                        const int32_t c = W.lo + 4 * cl_ + qq;
+                        int32_t maxlen = A.nR - (c + k);
+                        const int32_t mt = A.nT - (y + k);
+                        if (mt < maxlen) maxlen = mt;
+                        const int32_t l = k + wave_lce(A, L, B, c + k, y + k, maxlen);
+                        if (l > bl) { bl = l; bcnt = 1; bhas0 = (c == 0); bkey = c ? pick_key(c, P) : ~0ull; }
+                        else if (l == bl) {
+                            bcnt++;
+                            if (c == 0) bhas0 = true;
+                            else { const uint64_t pk = pick_key(c, P); bkey = pk < bkey ? pk : bkey; }
+                        }
+                    }
+                }
+                uint64_t pk;
+                if (bcnt >= 2 && bhas0) pk = bkey;
+                else { const uint64_t k0 = bhas0 ? pick_key(0, P) : ~0ull; pk = k0 < bkey ? k0 : bkey; }
+                const int32_t p = (int32_t)(uint32_t)pk;
+                if (p == 0 || nm >= A.chm_cap) { reason = 2; break; }   // pn2 == 0 or list full: the rounds take over at (x, P)
+                if (lane == 0) { A.chm_t[nm] = y; A.chm_p[nm] = p; A.chm_l[nm] = bl; }
+                const int slot = nm % CH_DENSE_N;
+                const int32_t old = lane_val(rt, slot);
+                if (lane == slot) rt = y;
+                nm++;
+                x = y + bl;
+                P = p + bl - 1;
+                if (nm > CH_DENSE_N && y - old < CH_DENSE_SPAN) { reason = 2; break; }   // aligned again
+                const int32_t wlo = P - A.m < 0 ? 0 : P - A.m;
+                const int32_t whi = P + A.m < A.nR - k ? P + A.m : A.nR - k;
+                if (wlo < blo || whi > bhi) { gen_end = true; break; }   // window left the band
+            }
+            yv = yn;
+            kv = kn;
+        }
+        if (!gen_end && !reason && tr != INT32_MAX) {   // hits past tr were not kept
+            gen_end = true;
+            if (x < tr) x = tr;   // every position before tr is settled (a literal step or a visited hit)
+            // band hits this dense twice running: the chunk rounds are the better engine here
+            // (find-first generations stop at their first hit by design)
+            if (A.chs[11] >= 1 && !A.chs[12]) reason = 2;
+            if (lane == 0) A.chs[11] += 1;
+        } else if (lane == 0 && b == 0) {
+            A.chs[11] = 0;
+        }
+    }
+    if (!gen_end && !reason) reason = 1;
+    if (!reason && A.chs[8] + 1 >= CH_MAX_GENS) reason = 2;   // a wandering chain: back to the rounds
+    if (lane == 0) {
+        // band hits this dense cost the step more than one find-first generation per match
+        if (hits > CH_DENSE_HITS) A.chs[12] = 1;
+        A.chs[13] = INT32_MAX;
+        A.chs[1] = x;
+        A.chs[2] = P;
+        A.chs[3] = nm;
+        A.chs[5] = reason;
+        A.chs[0] = reason == 0;
+        A.chs[8] += 1;
+    }
+}
+
+// first chain match with t >= v (chain matches are in t order)
+__device__ __forceinline__ int32_t ch_lower(const int32_t* t, int32_t n, int32_t v) {
+    int32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (t[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// one wave per chunk after the chain's start chunk that the chain determined
+__global__ __launch_bounds__(SCCG_BLOCK) void k_chain_fill(WalkPtrs A) {
+    const int32_t reason = A.chs[5];
+    if (A.scal[9] || reason == 0) return;
+    const int32_t q = (int32_t)blockIdx.x * WPB + wave_in_block();
+    const int32_t j0 = A.chs[4];
+    if (q <= j0 || q >= A.C) return;
+    const int lane = lane_id(), k = A.k;
+    const int32_t lastk1 = A.nT - k + 1;
+    const int32_t xe = A.chs[1], nm = A.chs[3], x0 = A.chs[9], P0 = A.chs[10];
+    const int32_t lo = q * A.S, hi = lo + A.S < A.nT ? lo + A.S : A.nT;
+    const int32_t lo_c = lo < lastk1 ? lo : lastk1, hi_c = hi < lastk1 ? hi : lastk1;
+    if (reason == 2 && hi_c > xe) return;   // the chain handed back before this chunk's end
+    // walk state at a boundary v: after the last chain match starting before v (or the start)
+    auto state_at = [&](int32_t v, int32_t vc, int32_t& sx, int32_t& sp, int32_t& i) {
+        i = ch_lower(A.chm_t, nm, v);
+        int32_t e = x0, pe = P0;
+        if (i > 0) { e = A.chm_t[i - 1] + A.chm_l[i - 1]; pe = A.chm_p[i - 1] + A.chm_l[i - 1] - 1; }
+        sx = e > vc ? e : vc;
+        sp = pe;
+    };
+    int32_t ux, up, i1, ex, ep, i2;
+    state_at(lo, lo_c, ux, up, i1);
+    state_at(hi, hi_c, ex, ep, i2);
+    const int32_t n = i2 - i1;
+    const int32_t b = A.cur[q];
+    int32_t* ot = A.bt[b] + (size_t)q * A.cap;
+    int32_t* op = A.bp[b] + (size_t)q * A.cap;
+    int32_t* ol = A.bl[b] + (size_t)q * A.cap;
+    for (int32_t i = lane; i < n; i += 64) { ot[i] = A.chm_t[i1 + i]; op[i] = A.chm_p[i1 + i]; ol[i] = A.chm_l[i1 + i]; }
+    if (lane == 0) {
+        A.cnt[b][q] = n;
+        A.usedX[q] = ux; A.usedP[q] = up;
+        A.exitX[q] = ex; A.exitP[q] = ep;
+        A.changed[q] = 0; A.seedq[q] = 0; A.trapped[q] = 0; A.frozen[q] = 0;
     }
 }
 
@@ -1674,6 +2051,18 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.lgap = c.take<int64_t>(3 * (size_t)A.lgap_cap);
     A.cprev = c.take<int64_t>(C + 1);
     A.ctext = c.take<int64_t>(C + 1);
+    A.chs = c.take<int32_t>(16);
+    {
+        const int64_t mc = nT / k + 2;
+        A.chm_cap = (int32_t)(mc < CHAIN_MCAP ? mc : CHAIN_MCAP);
+    }
+    A.chm_t = c.take<int32_t>((size_t)A.chm_cap);
+    A.chm_p = c.take<int32_t>((size_t)A.chm_cap);
+    A.chm_l = c.take<int32_t>((size_t)A.chm_cap);
+    A.chh_y = c.take<int32_t>((size_t)CH_GRID * CH_HCAP);
+    A.chh_k = c.take<uint32_t>((size_t)CH_GRID * CH_HCAP);
+    A.chh_n = c.take<int32_t>(CH_GRID);
+    A.chh_tr = c.take<int32_t>(CH_GRID);
     A.dbg = c.take<uint64_t>(C * DBG_SLOTS);
     *used = c.off;
     return A;
@@ -1722,6 +2111,40 @@ int h2d_sync(void* dst, const void* src, size_t bytes, hipStream_t s) {
     if (!bytes) return 0;
     SCCG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     SCCG_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+// The frozen chain from the earliest frozen chunk committed in this round (k_chain_*): generations
+// are queued CH_GENS_PER_SYNC at a time (a finished chain turns the rest into no-ops), then the
+// covered chunks are filled.  *gens: generations run.
+int run_chain(WalkPtrs& A, hipStream_t s, int* gens) {
+    hipLaunchKernelGGL(k_chain_init, dim3(1), dim3(64), 0, s, A);
+    SCCG_HIP(hipGetLastError());
+    int32_t st[2] = {0, 0};
+    for (int it = 0;; it++) {
+        for (int g = 0; g < CH_GENS_PER_SYNC; g++) {
+            hipLaunchKernelGGL(k_chain_scan, dim3(CH_GRID), dim3(1024), 0, s, A);
+            hipLaunchKernelGGL(k_chain_step, dim3(1), dim3(64), 0, s, A);
+        }
+        SCCG_HIP(hipGetLastError());
+        const RbItem it0{A.chs, st, (int)sizeof st};
+        const int rc = dev_readback(&it0, 1, s);
+        if (rc) return rc;
+        if (!st[0]) break;
+        if (it > CH_MAX_GENS / CH_GENS_PER_SYNC + 1) return SCCG_E_INTERNAL;   // k_chain_step caps the generations
+    }
+    PROF_LAUNCH(PROF_WALK_CHAIN, s, k_chain_fill, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A);
+    SCCG_HIP(hipGetLastError());
+    int32_t cs[12];
+    {
+        const RbItem it1{A.chs, cs, (int)sizeof cs};
+        const int rc = dev_readback(&it1, 1, s);
+        if (rc) return rc;
+    }
+    *gens = cs[8];
+    if (getenv("SCCG_DEBUG"))
+        fprintf(stderr, "[chain] from chunk %d (x %d, P %d): %d generations, %d matches, end x %d P %d, reason %d\n", cs[4], cs[9],
+                cs[10], cs[8], cs[3], cs[1], cs[2], cs[5]);
     return 0;
 }
 
@@ -1941,6 +2364,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
     if (used > ws_bytes) return SCCG_E_INTERNAL;
     res->rounds = 0;
+    res->chains = 0;
     res->chunks = A.C;
     res->n_matches = 0;
     const int32_t lastk = (int32_t)nTp - k;
@@ -2104,6 +2528,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         // If the round left work (pending chunks, more frozen chunks, escalations) that text is
         // simply written again after the last round.
         static const bool spec_text_on = getenv("SCCG_NO_SPEC_TEXT") == nullptr;
+        static const bool chains_on = getenv("SCCG_NO_CHAINS") == nullptr;   // (A/B and tests)
         int32_t frozen_r1 = 0;
         for (int64_t round = 1;; round++) {
             A.round = (int32_t)round;   // every kernel of the round gets it by value
@@ -2144,7 +2569,20 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                     RC(dev_readback(&rs_item, 1, s));
                 }
             }
-            if (rs[5] > FROZEN_FIRST) {   // more frozen chunks than the blind batch covered
+            // A chain pays where rounds would resolve a frozen stretch hit by hit: a frozen chunk in
+            // round 1 (only chunk 0 is exact there, so the true walk froze at once), more frozen chunks
+            // than the blind batch covers, or frozen chunks still turning up from round 3 on.  A few
+            // frozen chunks in round 2 (N gaps of aligned pairs) stay with the blind batch.
+            const bool chain_now = chains_on && rs[5] > 0 && (round == 1 || round >= 3 || rs[5] > FROZEN_FIRST);
+            if (chain_now) {
+                // a frozen chain: walk it on over the rest of the target, then the pending list again
+                int gens = 0;
+                RC(run_chain(A, s, &gens));
+                RC(frozen_batch(0, 0, false));
+                RC(dev_readback(&rs_item, 1, s));
+                spec_text = false;   // the chain rewrote chunks after the round's text was queued
+                res->chains++;
+            } else if (rs[5] > FROZEN_FIRST) {   // more frozen chunks than the blind batch covered
                 for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, true));
                 RC(dev_readback(&rs_item, 1, s));
             }

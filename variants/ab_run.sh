@@ -1,16 +1,20 @@
 #!/bin/bash
 # GPU box: interleaved A/B of library variants on the chr1 bench and (optionally) one bench_configs
-# workload.  VARIANTS="name:lib ..." (lib "-" = in-tree), REPS, STEPS, CONFIG (bench_configs --only).
+# workload.  VARIANTS="name:lib[:VAR=v,VAR=v] ..." (lib "-" = in-tree), REPS, STEPS, CONFIG
+# (bench_configs --only).
 set -eo pipefail
 mkdir -p gpurun_out/ab
 for r in $(seq 1 ${REPS:-3}); do
   for v in $VARIANTS; do
-    name=${v%%:*}; lib=${v#*:}
+    name=${v%%:*}; rest=${v#*:}; lib=${rest%%:*}; envs=""
+    if [ "$rest" != "$lib" ]; then envs=${rest#*:}; fi
     if [ "$lib" = "-" ]; then lib=""; fi
-    SCCG_LIB_PATH=$lib timeout -k 10 120 python -u bench.py --no-cpu-baseline --no-check --steps ${STEPS:-20} \
+    args=("SCCG_LIB_PATH=$lib")
+    if [ -n "$envs" ]; then IFS=',' read -ra kv <<< "$envs"; args+=("${kv[@]}"); fi
+    env "${args[@]}" timeout -k 10 120 python -u bench.py --no-cpu-baseline --no-check --steps ${STEPS:-20} \
         > gpurun_out/ab/${name}_$r.json 2>/dev/null
     if [ -n "$CONFIG" ]; then
-      SCCG_LIB_PATH=$lib timeout -k 10 120 python -u sccg-genome-compression_amd/tools/bench_configs.py --only $CONFIG --steps 2 \
+      env "${args[@]}" timeout -k 10 120 python -u sccg-genome-compression_amd/tools/bench_configs.py --only $CONFIG --steps 2 \
           > gpurun_out/ab/${name}_${CONFIG}_$r.json 2>/dev/null
     fi
   done
