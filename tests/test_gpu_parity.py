@@ -294,3 +294,15 @@ def test_t2t_seeds_vs_oracle(ctx, seed):
     """Literal-heavy walks (frozen and trapped chains, long literal gaps) at 4 Mb."""
     rfa, tfa = synthlib.synth_pair("t2t", 4_000_000, 4_000_000, seed)
     assert ctx.compress(rfa, tfa) == oraclelib.compress(rfa, tfa)
+
+
+@pytest.mark.parametrize("seed", [7, 90])
+def test_frozen_chains_vs_oracle(ctx, seed):
+    """T2T-shaped pairs whose reference walk freezes right after its first step: the frozen-chain
+    kernels (k_chain_scan / k_chain_step / k_chain_fill) walk most of the target; the record stream
+    must still equal the oracle's."""
+    rfa, tfa = synthlib.synth_pair("t2t", 8_000_000, 8_000_000, seed)
+    got = ctx.compress(rfa, tfa)
+    st = ctx.stats()
+    assert st["walk_chains"] >= 1
+    assert got == oraclelib.compress(rfa, tfa)
