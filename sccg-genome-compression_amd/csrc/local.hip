@@ -33,7 +33,6 @@ struct SegLds {
     uint32_t skey[1024];          // reference k-mer keys, grouped by bucket (first: the bucket counters)
     uint16_t spos[1024];          // their positions
     uint16_t bstart[NB + 1];      // bucket b holds entries [bstart[b], bstart[b+1])
-    uint64_t hits[16];            // bit p: target k-mer at p has >= 1 candidate
 };
 
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int k) {
@@ -166,7 +165,6 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
             for (int q = 0; q < 4; q++) non_n |= (b0 + q < nt && (uint8_t)(tw >> (8 * q)) != 'N');
         }
     }
-    if (lane < 16) L.hits[lane] = 0;
     non_n = __ballot(non_n) != 0;
     wave_sync();
     tick(0);
@@ -217,48 +215,40 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     wave_sync();
     tick(1);
     tick(2);
-
-    // ---- hit bits for every target k-mer start (compression.cpp:77 "H.find")
-    const int lastk = nt - K;
-    {
-        const int p0 = lane * 16;
-        uint32_t mask16 = 0;
-        if (lastr >= 0) {
-            uint64_t code = 0;
-            uint32_t bad = 0;
-            if (p0 <= lastk) keys16<K>(&L.t[p0], code, bad);
-            for (int st = 0; st < 16; st++) {
-                const int p = p0 + st;
-                if (p > lastk) break;
-                const uint32_t key = (bad >> st) & KM ? exotic_key(&L.t[p], K) : (uint32_t)(code >> (2 * st)) & MASK;
-                const uint32_t b = slot_hash(key, NBB);
-                const int e1 = (int)L.bstart[b + 1];
-                for (int e = (int)L.bstart[b]; e < e1; e++) {
-                    if (L.skey[e] == key && (key < KEY_EXOTIC || bytes_eq(&L.r[L.spos[e]], &L.t[p], K))) {
-                        mask16 |= 1u << st;
-                        break;
-                    }
-                }
-            }
-        }
-        reinterpret_cast<uint16_t*>(L.hits)[lane] = (uint16_t)mask16;
-    }
-    wave_sync();
     tick(3);
 
-    // ---- the greedy walk (compression.cpp:64-161), wave-uniform
+    // ---- the greedy walk (compression.cpp:64-161), wave-uniform.  The next target position with
+    //      a candidate (compression.cpp:77 "H.find") is found 64 positions at a time from idx: an
+    //      aligned segment takes a step or two, so probing only where the walk goes is far cheaper
+    //      than a hit bit for every target k-mer.
+    const int lastk = nt - K;
     uint32_t* out = recs + seg * SEG_REC_CAP;
     int idx = 0, pme = -1, nrec = 0, nmatch = 0, lit = 0, firstp = -1, lastp = -1;
     for (;;) {
         // next target position >= idx with a candidate
         int nxt = -1;
-        if (idx <= lastk) {
-            for (int wd = idx >> 6; wd < 16; wd++) {
-                uint64_t m = L.hits[wd];
-                if (wd == (idx >> 6)) m &= ~0ull << (idx & 63);
-                if (m) { nxt = wd * 64 + __ffsll((long long)m) - 1; break; }
+        if (lastr >= 0) {
+            for (int p0 = idx; p0 <= lastk; p0 += 64) {
+                const int p = p0 + lane;
+                bool hit = false;
+                if (p <= lastk) {
+                    uint32_t w[4], bad;
+                    uint64_t code;
+                    loadw<4>(&L.t[p], w);
+                    pack_codes<4>(w, code, bad);
+                    const uint32_t key = bad & KM ? exotic_key(&L.t[p], K) : (uint32_t)code & MASK;
+                    const uint32_t b = slot_hash(key, NBB);
+                    const int e1 = (int)L.bstart[b + 1];
+                    for (int e = (int)L.bstart[b]; e < e1; e++) {
+                        if (L.skey[e] == key && (key < KEY_EXOTIC || bytes_eq(&L.r[L.spos[e]], &L.t[p], K))) {
+                            hit = true;
+                            break;
+                        }
+                    }
+                }
+                const unsigned long long hm = __ballot(hit);
+                if (hm) { nxt = p0 + first_lane(hm); break; }
             }
-            if (nxt > lastk) nxt = -1;
         }
         if (nxt < 0) break;
         if (nxt > idx) {
