@@ -428,8 +428,11 @@ __device__ __forceinline__ int32_t seg_count(int64_t nR, int64_t nT) {
     return n >= INT32_MAX / 2 ? 0 : (int32_t)n;   // beyond int positions: the host reports it
 }
 
+#ifndef LOCAL_WAVES_PER_EU
+#define LOCAL_WAVES_PER_EU 4   // the LDS allows 4 waves/SIMD (4 blocks of SegLds x 4); VGPRs must fit 128
+#endif
 template <bool DBG>
-__global__ __launch_bounds__(SCCG_BLOCK) void k_local_all(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
+__global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_all(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
                                                           const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
                                                           uint32_t* __restrict__ recs, SegStat* __restrict__ stat,
                                                           int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl) {

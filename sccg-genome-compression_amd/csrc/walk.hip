@@ -436,12 +436,14 @@ constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cand
 #ifndef WALK_WAVES_PER_EU
 #define WALK_WAVES_PER_EU 5
 #endif
+// nlist_dev (optional): the list length from device memory (a round queued before the host knows it)
 template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
-void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
+void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const int32_t* __restrict__ nlist_dev) {
     __shared__ WalkLds lds_all[WPB];
     const int w = wave_in_block(), lane = lane_id();
     const int32_t li = (int32_t)blockIdx.x * WPB + w;
+    if (nlist_dev) nlist = *nlist_dev;
     if (li >= nlist || A.scal[9]) return;
     WalkLds& L = lds_all[w];
     const int32_t j = uni(list[li]);
@@ -713,8 +715,9 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
 // round.  Discarded chunks stay pending and are re-walked from the corrected entry.  Exactness
 // never depends on this choice -- the loop only ends when every chunk's trajectory was walked from
 // its predecessor's final exit.
-__global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist) {
+__global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const int32_t* __restrict__ nlist_dev) {
     if (A.scal[9]) return;   // void pre-queued round
+    if (nlist_dev) nlist = *nlist_dev;
     if (blockIdx.x == 0 && threadIdx.x < FROZEN_MAX) A.fy[threadIdx.x] = INT32_MAX;   // for k_frozen_scan
     for (int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); i < nlist; i += (int32_t)(gridDim.x * blockDim.x)) {
         const int32_t j = list[i];
@@ -1862,7 +1865,9 @@ struct FirstMatch {
     int32_t y, p, l, valid;
 };
 
+// (the text kernels return at once after a void pre-queued round: its chunk state is not a walk's)
 __global__ void k_chunk_meta(WalkPtrs A) {
+    if (A.scal[9]) return;
     for (int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); j < A.C; j += (int32_t)(gridDim.x * blockDim.x)) {
         const int32_t n = A.cnt[A.cur[j]][j];
         A.cprev[j] = n > 0 ? j : -1;   // -> exclusive max-scan: the last earlier chunk with a match
@@ -1881,18 +1886,28 @@ __device__ __forceinline__ int write_token(uint8_t* o, int32_t d, int32_t l) {
     return (int)(q - o);
 }
 
+// the usual first step (x0 = 0 has candidates), as k_walk_init<true> resolves it from fc[8..11]
+__device__ __forceinline__ FirstMatch first_match_dev(const WalkPtrs& A) {
+    const unsigned long long* r = A.fc + 4;
+    const uint64_t k0 = 1ull << 32;   // pick_key(0, -1)
+    const uint64_t pk = (r[5] >= 2 && r[6]) ? r[7] : ((r[6] && k0 < r[7]) ? k0 : r[7]);
+    return FirstMatch{0, (int32_t)(uint32_t)pk, (int32_t)r[4], 1};
+}
+
 // wave per chunk: WRITE = false -> ctext[j] = its text bytes; WRITE = true -> the text at ctext[j]
+// (F.valid == 2: the first match comes from first_match_dev)
 template <bool WRITE>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_chunk_text(WalkPtrs A, FirstMatch F, int abs_p, uint8_t* __restrict__ out) {
     constexpr int32_t SHORT_GAP = 32;
     const int32_t j = (int32_t)blockIdx.x * WPB + wave_in_block();
-    if (j >= A.C) return;
+    if (j >= A.C || A.scal[9]) return;
     const int lane = lane_id();
     const int32_t b = A.cur[j], n = A.cnt[b][j];
     const int32_t* tt = A.bt[b] + (size_t)j * A.cap;
     const int32_t* pp = A.bp[b] + (size_t)j * A.cap;
     const int32_t* ll = A.bl[b] + (size_t)j * A.cap;
     const int64_t x0 = A.usedX[j], end = j == A.C - 1 ? (int64_t)A.nT : (int64_t)A.exitX[j];
+    if (F.valid == 2) F = first_match_dev(A);   // the device's resolution of the usual first step
     int32_t pprev = F.valid ? F.p : 0;
     if (j > 0) {
         const int64_t q = A.cprev[j];
@@ -1950,6 +1965,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_chunk_text(WalkPtrs A, FirstMatc
 
 // the queued long literal pieces: one wave per piece
 __global__ __launch_bounds__(SCCG_BLOCK) void k_long_copy(WalkPtrs A, uint8_t* __restrict__ out) {
+    if (A.scal[9]) return;
     const int64_t ne = A.scal64[2] < A.lgap_cap ? A.scal64[2] : A.lgap_cap;
     const int64_t G = (int64_t)gridDim.x * WPB;
     for (int64_t e = (int64_t)blockIdx.x * WPB + wave_in_block(); e < ne; e += G) {
@@ -2069,7 +2085,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
 }
 
 // SCCG_DEBUG runs take the instrumented walk
-using WalkKernel = void (*)(WalkPtrs, const int32_t*, int32_t);
+using WalkKernel = void (*)(WalkPtrs, const int32_t*, int32_t, const int32_t*);
 WalkKernel walk_kernel(const WalkPtrs& A) { return A.dbg ? k_walk<true> : k_walk<false>; }
 
 struct FullC {
@@ -2188,7 +2204,7 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s, std::vector<int32_t>* resume
         if (rc) return rc;
         if ((rc = h2d_sync(A.rlist, rl.data(), rl.size() * 4, s))) return rc;
         PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
-                    (const int32_t*)A.rlist, (int32_t)rl.size());
+                    (const int32_t*)A.rlist, (int32_t)rl.size(), (const int32_t*)nullptr);
         SCCG_HIP(hipGetLastError());
     }
 }
@@ -2396,36 +2412,82 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     //      usual start on the device, and the round's status comes back with the first-step
     //      statistics in one readback (a host round trip less).  If the first step is not the
     //      usual one, that round is dropped and everything below runs as before.
-    auto queue_round = [&](int fbase_cap) -> int {
+    // (dev_nlist: the list length is the previous round tail's pending count, scal[0])
+    auto queue_round = [&](int fbase_cap, bool dev_nlist) -> int {
+        const int32_t* nd = dev_nlist ? A.scal : nullptr;
         PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist,
-                    A.C);
+                    A.C, nd);
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
-                           (const int32_t*)A.plist, A.C);
+                           (const int32_t*)A.plist, A.C, nd);
         if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fbase_cap), dim3(SCCG_BLOCK), 0, s, A, 0);
         hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(1024), 0, s, A, 0, fbase_cap);
         SCCG_HIP(hipGetLastError());
         return 0;
     };
     static const bool dev_first = getenv("SCCG_HOST_FIRST_STEP") == nullptr;
-    bool pre_round = false;
+    // Round 2 usually settles every chunk (round 1 speculates, round 2 confirms): with the device
+    // first step it goes out right behind round 1 (its list length read on the device), followed by
+    // its record text when the caller resolves the text position (late_out) -- one host readback
+    // for the first step, both rounds and the text.  If round 2 left work (pending chunks, more
+    // frozen chunks, escalations) that text is simply written again after the last round.
+    static const bool spec_text_on = getenv("SCCG_NO_SPEC_TEXT") == nullptr;
+    const bool dbg_rounds = getenv("SCCG_DEBUG") != nullptr;
+    bool pre_round = false, spec_queued = false;
     int32_t rs_pre[6] = {};
     if (walkable && dev_first && A.C > 0) {
         hipLaunchKernelGGL(k_walk_init<true>, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s,
                            A, 0, 0);
         A.round = 1;
-        RC(queue_round(FROZEN_FIRST));
+        RC(queue_round(FROZEN_FIRST, false));
+        A.round = 2;
+        RC(queue_round(FROZEN_FIRST, true));
         pre_round = true;
     }
 
-    // ---- the exact first (ungated) step: first target position with any candidate
     int32_t first_y = INVALID, first_p = 0, first_l = 0;
+    // ---- record text emission (k_chunk_text), queued after the rounds or speculatively (below)
+    bool resolved = false, spec_text = false, text_done = false;
+    int64_t spec_r[2] = {0, 0};   // total chunk matches, text bytes
+    auto resolve_out = [&]() -> int {
+        if (!resolved && late_out) RC(late_out->resolve(late_out->user, &out));
+        resolved = true;
+        return 0;
+    };
+    // (dev_first: the first match is the device's resolution of the usual first step, see k_chunk_text)
+    auto queue_text = [&](bool long_copy, bool dev_first) -> int {
+        const int32_t nf = dev_first ? 2 : first_y != INVALID ? 1 : 0;
+        const unsigned gc = grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256);
+        hipLaunchKernelGGL(k_chunk_meta, dim3(gc), dim3(256), 0, s, A);
+        RC(dev_excl_max(A.cprev, A.cprev, A.C, nullptr, A.partial, s));
+        RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
+        RC(set_u64(reinterpret_cast<unsigned long long*>(A.scal64 + 2), {0}, s));
+        const FirstMatch F{first_y, first_p, first_l, nf};
+        hipLaunchKernelGGL(k_chunk_text<false>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F, (int)abs_p, out);
+        RC(dev_excl_sum(A.ctext, A.ctext, A.C, A.scal64 + 1, A.partial, s));
+        PROF_LAUNCH(PROF_MATCH_EMIT, s, k_chunk_text<true>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F,
+                    (int)abs_p, out);
+        if (long_copy) hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
+        SCCG_HIP(hipGetLastError());
+        return 0;
+    };
+
+    // ---- the exact first (ungated) step: first target position with any candidate
     if (walkable) {
         int32_t x0 = 0;
         unsigned long long r[9];   // fc[4..11]: first hit, first exotic, statistics of the batch's x0; fc[12]
         if (pre_round) {
-            const RbItem it[2] = {{A.fc + 4, r, (int)sizeof r}, {A.scal, rs_pre, (int)sizeof rs_pre}};
-            RC(dev_readback(it, 2, s));
-            if (!(r[8] != 2 && r[0] == 0 && r[4] > 0)) pre_round = false;   // not the usual first step: redo
+            // the text of the usual first step needs (first_y, first_p, first_l) = the device's start
+            // resolution: known only from this readback, so the pre-queued text uses the start that
+            // k_walk_init<true> derived on the device (k_chunk_text reads it from fc)
+            if (!keep_flat && !dbg_rounds && spec_text_on) {
+                RC(resolve_out());
+                RC(queue_text(true, true));
+                spec_queued = true;
+            }
+            const RbItem it[3] = {{A.fc + 4, r, (int)sizeof r}, {A.scal, rs_pre, (int)sizeof rs_pre},
+                                  {A.scal64, spec_r, (int)sizeof spec_r}};
+            RC(dev_readback(it, 3, s));
+            if (!(r[8] != 2 && r[0] == 0 && r[4] > 0)) { pre_round = false; spec_queued = false; }   // not the usual first step: redo
         } else {
             const RbItem it{A.fc + 4, r, (int)sizeof r};
             RC(dev_readback(&it, 1, s));
@@ -2487,31 +2549,6 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     if (first_y != INVALID) { startX = first_y + first_l; startP = first_p + first_l - 1; }
     else { startX = lastk + 1 > 0 ? lastk + 1 : 0; startP = INVALID; }
 
-    // ---- record text emission (k_chunk_text), queued after the rounds or speculatively (below)
-    bool resolved = false, spec_text = false, text_done = false;
-    int64_t spec_r[2] = {0, 0};   // total chunk matches, text bytes
-    auto resolve_out = [&]() -> int {
-        if (!resolved && late_out) RC(late_out->resolve(late_out->user, &out));
-        resolved = true;
-        return 0;
-    };
-    auto queue_text = [&](bool long_copy) -> int {
-        const int32_t nf = first_y != INVALID ? 1 : 0;
-        const unsigned gc = grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256);
-        hipLaunchKernelGGL(k_chunk_meta, dim3(gc), dim3(256), 0, s, A);
-        RC(dev_excl_max(A.cprev, A.cprev, A.C, nullptr, A.partial, s));
-        RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
-        RC(set_u64(reinterpret_cast<unsigned long long*>(A.scal64 + 2), {0}, s));
-        const FirstMatch F{first_y, first_p, first_l, nf};
-        hipLaunchKernelGGL(k_chunk_text<false>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F, (int)abs_p, out);
-        RC(dev_excl_sum(A.ctext, A.ctext, A.C, A.scal64 + 1, A.partial, s));
-        PROF_LAUNCH(PROF_MATCH_EMIT, s, k_chunk_text<true>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F,
-                    (int)abs_p, out);
-        if (long_copy) hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
-        SCCG_HIP(hipGetLastError());
-        return 0;
-    };
-
     // ---- init chunk state
     const size_t C = (size_t)A.C;
     if (!pre_round)
@@ -2523,19 +2560,15 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         mark("anchors");
         int32_t nlist = A.C;
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
-        // Round 2 usually settles every chunk (round 1 speculates, round 2 confirms): its record text
-        // is queued right behind it, before the host knows, and comes back with the round's status.
-        // If the round left work (pending chunks, more frozen chunks, escalations) that text is
-        // simply written again after the last round.
-        static const bool spec_text_on = getenv("SCCG_NO_SPEC_TEXT") == nullptr;
         static const bool chains_on = getenv("SCCG_NO_CHAINS") == nullptr;   // (A/B and tests)
-        int32_t frozen_r1 = 0;
-        for (int64_t round = 1;; round++) {
+        // with the device first step, rounds 1 and 2 went out before the first readback
+        const int64_t round0 = pre_round ? 2 : 1;
+        for (int64_t round = round0;; round++) {
             A.round = (int32_t)round;   // every kernel of the round gets it by value
-            const bool queued = round == 1 && pre_round;   // round 1 went out before the first step's readback
+            const bool queued = pre_round && round == round0;
             if (!queued) {
                 PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A,
-                            (const int32_t*)A.plist, nlist);
+                            (const int32_t*)A.plist, nlist, (const int32_t*)nullptr);
                 SCCG_HIP(hipGetLastError());
             }
             res->rounds = round;
@@ -2544,7 +2577,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             // handled after the round's one sync.
             if (!queued)
                 hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
-                                   (const int32_t*)A.plist, nlist);
+                                   (const int32_t*)A.plist, nlist, (const int32_t*)nullptr);
             auto frozen_batch = [&](int fbase, int fcap, bool init_fy) -> int {   // no-op past the list
                 if (init_fy) SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.fy, INT32_MAX, fcap, s));
                 if (fcap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fcap), dim3(SCCG_BLOCK), 0, s, A, fbase);
@@ -2556,18 +2589,10 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             const RbItem rs_item{A.scal, rs, (int)sizeof rs};
             if (queued) {
                 for (int i = 0; i < 6; i++) rs[i] = rs_pre[i];
+                spec_text = spec_queued && rs[5] <= FROZEN_FIRST && rs[1] == 0;   // nothing changes after that readback
             } else {
                 RC(frozen_batch(0, FROZEN_FIRST, false));   // fy was set by k_commit
-                // (not after a round that left frozen chunks: a frozen chain means more rounds)
-                if (round == 2 && !keep_flat && !dbg && spec_text_on && frozen_r1 == 0) {
-                    RC(resolve_out());
-                    RC(queue_text(false));   // the long literal copies only once the text is confirmed
-                    const RbItem it2[2] = {rs_item, {A.scal64, spec_r, (int)sizeof spec_r}};
-                    RC(dev_readback(it2, 2, s));
-                    spec_text = rs[5] <= FROZEN_FIRST && rs[1] == 0;   // nothing changes after this readback
-                } else {
-                    RC(dev_readback(&rs_item, 1, s));
-                }
+                RC(dev_readback(&rs_item, 1, s));
             }
             // A chain pays where rounds would resolve a frozen stretch hit by hit: a frozen chunk in
             // round 1 (only chunk 0 is exact there, so the true walk froze at once), more frozen chunks
@@ -2594,7 +2619,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                     const int32_t nr = (int32_t)resumed.size();
                     RC(dev_set_i32(A.scal + 5, 1, {0}, s));   // frozen list of the resumed chunks
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(nr, 256) > 4096 ? 4096 : grid_for(nr, 256)), dim3(256), 0, s, A,
-                                       (const int32_t*)A.rlist, nr);
+                                       (const int32_t*)A.rlist, nr, (const int32_t*)nullptr);
                     SCCG_HIP(hipGetLastError());
                 }
                 {
@@ -2741,7 +2766,6 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                     for (int q = 0; q < nshow; q++) fprintf(stderr, "      m%d (%d,%d,%d)\n", q, tt[q], pp[q], ll[q]);
                 }
             }
-            if (round == 1) frozen_r1 = rs[5];
             if (round == 2 && spec_text && nlist == 0) text_done = true;
             if (!nlist) break;
             if (round > 4 * (int64_t)A.C + 16) return SCCG_E_INTERNAL;
@@ -2756,13 +2780,10 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         RC(resolve_out());   // the caller's text position is known now
         int64_t text = 0, nmc = 0;
         if (startP != INVALID && lastk >= 0) {
-            if (!text_done) {   // (else round 2's speculative text stands, but for its long copies)
-                RC(queue_text(true));
+            if (!text_done) {   // (else round 2's speculative text, long copies included, stands)
+                RC(queue_text(true, false));
                 const RbItem it{A.scal64, spec_r, (int)sizeof spec_r};
                 RC(dev_readback(&it, 1, s));
-            } else {
-                hipLaunchKernelGGL(k_long_copy, dim3(1024), dim3(256), 0, s, A, out);
-                SCCG_HIP(hipGetLastError());
             }
             nmc = spec_r[0];
             text = spec_r[1];
