@@ -115,6 +115,7 @@ def main() -> None:
     ap.add_argument("--cpu-sample", type=int, default=10_000_000, help="reference CPU sample size (bases)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the round-trip parity check")
+    ap.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events in the timed region (A/B of their cost)")
     ap.add_argument("--ref-len", type=int, default=CHR1[0])
     ap.add_argument("--tgt-len", type=int, default=CHR1[1])
     args = ap.parse_args()
@@ -157,7 +158,7 @@ def main() -> None:
 
     for _ in range(args.warmup):
         n_out = step()
-    ctx.profile(True)
+    ctx.profile(not args.no_prof)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -58,12 +58,12 @@ __device__ __forceinline__ uint64_t pick_key(int p, int pme) {
     return ((uint64_t)(uint32_t)(d < 0 ? -d : d) << 32) | (uint32_t)p;
 }
 
-// uppercase 4 bytes (compression.cpp:369-370 toupper)
+// uppercase 4 bytes (compression.cpp:369-370 toupper, C locale: only 'a'..'z' change), SWAR: a
+// byte is lowercase iff its high bit is clear and (b & 0x7f) + 0x1f reaches 0x80 while + 0x05 does not
 __device__ __forceinline__ uint32_t upper4(uint32_t w) {
-    uint32_t o = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) o |= (uint32_t)c_toupper((uint8_t)(w >> (8 * i))) << (8 * i);
-    return o;
+    const uint32_t x = w & 0x7f7f7f7fu;
+    const uint32_t lower = (x + 0x1f1f1f1fu) & ~(x + 0x05050505u) & ~w & 0x80808080u;
+    return w ^ (lower >> 2);
 }
 
 // keys of the 16 K-mers starting at s[0..16) (s 16-byte aligned in LDS; 32 bytes readable)
@@ -225,18 +225,21 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     uint32_t* out = recs + seg * SEG_REC_CAP;
     int idx = 0, pme = -1, nrec = 0, nmatch = 0, lit = 0, firstp = -1, lastp = -1;
     for (;;) {
-        // next target position >= idx with a candidate
+        // next target position >= idx with a candidate (and its key)
         int nxt = -1;
+        uint32_t key = 0;
         if (lastr >= 0) {
             for (int p0 = idx; p0 <= lastk; p0 += 64) {
                 const int p = p0 + lane;
                 bool hit = false;
+                uint32_t pkey = 0;
                 if (p <= lastk) {
                     uint32_t w[4], bad;
                     uint64_t code;
                     loadw<4>(&L.t[p], w);
                     pack_codes<4>(w, code, bad);
-                    const uint32_t key = bad & KM ? exotic_key(&L.t[p], K) : (uint32_t)code & MASK;
+                    pkey = bad & KM ? exotic_key(&L.t[p], K) : (uint32_t)code & MASK;
+                    const uint32_t key = pkey;
                     const uint32_t b = slot_hash(key, NBB);
                     const int e1 = (int)L.bstart[b + 1];
                     for (int e = (int)L.bstart[b]; e < e1; e++) {
@@ -247,7 +250,7 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
                     }
                 }
                 const unsigned long long hm = __ballot(hit);
-                if (hm) { nxt = p0 + first_lane(hm); break; }
+                if (hm) { nxt = p0 + first_lane(hm); key = lane_val(pkey, first_lane(hm)); break; }
             }
         }
         if (nxt < 0) break;
@@ -256,7 +259,6 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
             nrec++;
             lit += nxt - idx;
         }
-        const uint32_t key = seg_key<K>(&L.t[nxt]);
         const uint32_t bk = slot_hash(key, NBB);
         const int e0 = (int)L.bstart[bk], e1 = (int)L.bstart[bk + 1];
         const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
