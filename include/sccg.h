@@ -9,6 +9,7 @@
  * Entry point                         replaces (reference file:line)
  * ----------------------------------  -------------------------------------------------------------
  * sccg_compress / _device             compress_genome up to the 7z call  compression.cpp:320-580
+ *   (_ex: with parameter overrides      of its constants                   compression.cpp:373-379)
  *                                     (read_genomes_from_files :181-220, lowercase/N run lines
  *                                     :341-368/:495-555, local loop :372-481, global pass
  *                                     :484-574, delta_encode :222-304)
@@ -91,9 +92,36 @@ int sccg_compress_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len, co
                          size_t tgt_len, void* d_out, size_t out_cap, size_t* out_len, void* stream);
 size_t sccg_compress_bound(size_t ref_len, size_t tgt_len);
 
+/* compress_genome's algorithm parameters (compression.cpp:373-379, hard-coded there).
+ * sccg_params_default() gives the reference's values, with which sccg_compress_ex is
+ * sccg_compress.  Other values are NON-PARITY overrides: the reference cannot
+ * run them, so their output is pinned against the parameterised CPU oracle only.  Accepted:
+ *   local = 1 (start with the local segment controller, :378): k, k2, L, T1, T2 at the reference's
+ *             values (the local kernels are built for them), 0 <= m <= 127;
+ *   local = 0 (straight to the global pass, as the reference with `local = false`): 1 <= k <= 32,
+ *             0 <= m <= 127 (k2, L, T1, T2 unused).
+ * Others: SCCG_E_UNSUPPORTED. */
+typedef struct {
+    int32_t k;       /* 14   primary k-mer length: local pass 1 and the global walk */
+    int32_t k2;      /* 10   local pass 2 */
+    int32_t L;       /* 1000 segment length */
+    int32_t m;       /* 100  global range gate |p - prev_match_end| <= m */
+    float T1;        /* 0.5  segment mismatch-ratio threshold */
+    int32_t T2;      /* 4    bad segments in a row before the switch to global */
+    int32_t local;   /* 1    start with the local controller */
+} sccg_params;
+
+void sccg_params_default(sccg_params* p);
+int sccg_compress_ex(sccg_ctx* ctx, const sccg_params* params, const char* ref_fa, size_t ref_len,
+                     const char* tgt_fa, size_t tgt_len, sccg_buf* out_text);
+int sccg_compress_device_ex(sccg_ctx* ctx, const sccg_params* params, const void* d_ref_fa,
+                            size_t ref_len, const void* d_tgt_fa, size_t tgt_len, void* d_out,
+                            size_t out_cap, size_t* out_len, void* stream);
+
 /* match_sequences(Sr, St, k, m, global, offset) on already-uppercased byte strings.  Accepted
  * shapes: global == 0 with |Sr| <= 1000 and |St| <= 1000 (the local-segment kernel), or
- * global == 1 with 0 <= m <= 1000 (the windowed global walk).  Others: SCCG_E_UNSUPPORTED. */
+ * global == 1 with 0 <= m <= 127 and 1 <= k <= 32 (the windowed global walk).  Others:
+ * SCCG_E_UNSUPPORTED. */
 int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, size_t nt, int k,
                int m, int global, int64_t offset, sccg_records* out);
 void sccg_records_free(sccg_records* r);

@@ -117,10 +117,16 @@ static inline int base2(unsigned char c) {
 }
 
 typedef struct {
+    uint64_t code;
+    int32_t pos;
+} kpos_t;
+
+typedef struct {
     int k;
     const char* s;
     int64_t n;            /* |Sr| */
-    uint64_t* pure;       /* (code << 32) | pos, sorted by code then pos */
+    uint64_t* pure;       /* k <= 16: (code << 32) | pos, sorted by code then pos */
+    kpos_t* pure2;        /* k > 16 (parameter overrides): (code, pos), sorted the same way */
     int64_t npure;
     int32_t* exo;         /* positions of k-mers holding a non-ACGT byte, sorted by bytes then pos */
     int64_t nexo;
@@ -137,6 +143,12 @@ static int cmp_exo(const void* a, const void* b) {
 static int cmp_u64(const void* a, const void* b) {
     uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
     return (x > y) - (x < y);
+}
+static int cmp_kpos(const void* a, const void* b) {
+    const kpos_t* x = (const kpos_t*)a;
+    const kpos_t* y = (const kpos_t*)b;
+    if (x->code != y->code) return (x->code > y->code) - (x->code < y->code);
+    return (x->pos > y->pos) - (x->pos < y->pos);
 }
 
 static void radix_sort_u64_hi(uint64_t* a, int64_t n, int bits) {
@@ -165,9 +177,11 @@ static int kindex_build(kindex_t* ix, const char* s, int64_t n, int k) {
     ix->k = k; ix->s = s; ix->n = n;
     if (n < k) return ORC_OK;   /* H stays empty (compression.cpp:44 loop never runs) */
     int64_t nk = n - k + 1;
-    ix->pure = (uint64_t*)malloc((size_t)nk * sizeof(uint64_t));
+    const int wide = k > 16;   /* 2k-bit codes no longer fit beside a 32-bit position */
+    if (wide) ix->pure2 = (kpos_t*)malloc((size_t)nk * sizeof(kpos_t));
+    else ix->pure = (uint64_t*)malloc((size_t)nk * sizeof(uint64_t));
     ix->exo = (int32_t*)malloc((size_t)nk * sizeof(int32_t));
-    if (!ix->pure || !ix->exo) return ORC_E_ALLOC;
+    if ((!ix->pure && !ix->pure2) || !ix->exo) return ORC_E_ALLOC;
     uint64_t mask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1);
     uint64_t code = 0;
     int64_t last_bad = -1;
@@ -178,9 +192,11 @@ static int kindex_build(kindex_t* ix, const char* s, int64_t n, int k) {
         int64_t st = i - k + 1;
         if (st < 0) continue;
         if (last_bad >= st) ix->exo[ix->nexo++] = (int32_t)st;
+        else if (wide) { ix->pure2[ix->npure].code = code; ix->pure2[ix->npure++].pos = (int32_t)st; }
         else ix->pure[ix->npure++] = (code << 32) | (uint64_t)st;
     }
-    if (ix->npure < 4096) qsort(ix->pure, (size_t)ix->npure, sizeof(uint64_t), cmp_u64);
+    if (wide) qsort(ix->pure2, (size_t)ix->npure, sizeof(kpos_t), cmp_kpos);
+    else if (ix->npure < 4096) qsort(ix->pure, (size_t)ix->npure, sizeof(uint64_t), cmp_u64);
     else radix_sort_u64_hi(ix->pure, ix->npure, 2 * k);
     g_cmp_s = s; g_cmp_k = k;
     qsort(ix->exo, (size_t)ix->nexo, sizeof(int32_t), cmp_exo);
@@ -189,6 +205,7 @@ static int kindex_build(kindex_t* ix, const char* s, int64_t n, int k) {
 
 static void kindex_free(kindex_t* ix) {
     free(ix->pure);
+    free(ix->pure2);
     free(ix->exo);
     memset(ix, 0, sizeof *ix);
 }
@@ -204,7 +221,15 @@ static void kindex_lookup(const kindex_t* ix, const char* q, int64_t* lo, int64_
         code = (code << 2) | (uint64_t)b;
     }
     *pure_mode = pure;
-    if (pure) {
+    if (pure && ix->pure2) {
+        *pure_mode = 2;
+        int64_t a = 0, z = ix->npure;
+        while (a < z) { int64_t mid = (a + z) / 2; if (ix->pure2[mid].code < code) a = mid + 1; else z = mid; }
+        *lo = a;
+        z = ix->npure;
+        while (a < z) { int64_t mid = (a + z) / 2; if (ix->pure2[mid].code <= code) a = mid + 1; else z = mid; }
+        *hi = a;
+    } else if (pure) {
         int64_t a = 0, z = ix->npure;
         while (a < z) { int64_t mid = (a + z) / 2; if ((ix->pure[mid] >> 32) < code) a = mid + 1; else z = mid; }
         *lo = a;
@@ -222,7 +247,7 @@ static void kindex_lookup(const kindex_t* ix, const char* q, int64_t* lo, int64_
 }
 
 static inline int32_t kindex_pos(const kindex_t* ix, int pure_mode, int64_t j) {
-    return pure_mode ? (int32_t)(ix->pure[j] & 0xffffffffu) : ix->exo[j];
+    return pure_mode == 2 ? ix->pure2[j].pos : pure_mode ? (int32_t)(ix->pure[j] & 0xffffffffu) : ix->exo[j];
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -466,8 +491,19 @@ static int any_match(const orc_rec* r, int64_t n) {
     return 0;
 }
 
+void orc_params_default(orc_params* p) {
+    p->k = 14; p->k2 = 10; p->L = 1000; p->m = 100; p->T1 = 0.5f; p->T2 = 4; p->local = 1;   /* :373-379 */
+}
+
 int orc_compress(const char* ref_fa, size_t ref_len, const char* tgt_fa, size_t tgt_len,
                  char** out, size_t* out_len) {
+    orc_params p;
+    orc_params_default(&p);
+    return orc_compress_params(&p, ref_fa, ref_len, tgt_fa, tgt_len, out, out_len);
+}
+
+int orc_compress_params(const orc_params* prm, const char* ref_fa, size_t ref_len, const char* tgt_fa,
+                        size_t tgt_len, char** out, size_t* out_len) {
     sb_t R = {0}, T = {0}, hdr = {0}, f = {0}, fin = {0};
     int has_header = 0, rc = ORC_OK;
     g_last_global = 0;
@@ -485,11 +521,12 @@ int orc_compress(const char* ref_fa, size_t ref_len, const char* tgt_fa, size_t 
     for (size_t i = 0; i < R.n; i++) Ru[i] = c_toupper(R.d[i]);          /* :369-370 */
     for (size_t i = 0; i < T.n; i++) Tu[i] = c_toupper(T.d[i]);
 
-    const int k = 14, k2 = 10, L = 1000, m = 100, T2 = 4;              /* :373-379 */
-    const float T1 = 0.5f;
+    const int k = prm->k, k2 = prm->k2, L = prm->L, m = prm->m, T2 = prm->T2;   /* :373-379 */
+    const float T1 = prm->T1;
     int64_t nRs = ((int64_t)R.n + L - 1) / L, nTs = ((int64_t)T.n + L - 1) / L;
     int64_t iters = nRs < nTs ? nRs : nTs;                              /* :392 */
-    int mism = 0, local = 1;
+    int mism = 0, local = prm->local != 0;
+    if (!local) iters = 0;   /* local = 0: the global pass alone (parameter override, see header) */
     for (int64_t i = 0; i < iters && rc == ORC_OK; i++) {               /* :395 */
         const char* ri = Ru + i * L;
         int64_t nri = (int64_t)R.n - i * L; if (nri > L) nri = L;

@@ -47,6 +47,19 @@ int orc_match(const char* sr, int64_t nr, const char* st, int64_t nt, int k, int
 int orc_compress(const char* ref_fa, size_t ref_len, const char* tgt_fa, size_t tgt_len,
                  char** out, size_t* out_len);
 
+/* compress_genome's constants (compression.cpp:373-379).  orc_params_default gives the
+ * reference's values (orc_compress); other values are the library's NON-PARITY overrides
+ * (sccg_params in include/sccg.h): the same algorithm with other constants, which the reference
+ * cannot run.  local = 0 runs the global pass (:484-574) alone. */
+typedef struct {
+    int k, k2, L, m;
+    float T1;
+    int T2, local;
+} orc_params;
+void orc_params_default(orc_params* p);
+int orc_compress_params(const orc_params* p, const char* ref_fa, size_t ref_len, const char* tgt_fa,
+                        size_t tgt_len, char** out, size_t* out_len);
+
 /* Diagnostics of the last orc_compress in this thread: 1 if it switched to global mode,
  * and the segment index at which it switched (-1 if it stayed local). */
 int orc_last_mode_global(void);

@@ -4,12 +4,41 @@
 // (compression.cpp:306-318).  Exit codes follow the reference: 1 on usage / open / 7z errors.
 #include "cli_common.h"
 
+#include <cstring>
+
+// Optional, non-parity parameter overrides before the three positional arguments (sccg_params,
+// include/sccg.h; the reference hard-codes them at compression.cpp:373-379):
+//   --k=<k> --m=<m> --global      (--global: the global pass alone, any 1 <= k <= 32)
+static bool parse_option(const std::string& a, sccg_params& p) {
+    auto num = [&](const char* pre, int32_t& v) {
+        const size_t n = strlen(pre);
+        if (a.compare(0, n, pre) != 0) return false;
+        char* end = nullptr;
+        const long x = strtol(a.c_str() + n, &end, 10);
+        if (end == a.c_str() + n || *end) return false;
+        v = (int32_t)x;
+        return true;
+    };
+    if (a == "--global") { p.local = 0; return true; }
+    return num("--k=", p.k) || num("--m=", p.m);
+}
+
 int main(int argc, char* argv[]) {
-    if (argc != 4) {
-        std::cerr << "Usage: " << argv[0] << " <reference_file> <target_file> <output_folder>\n";
+    sccg_params prm;
+    sccg_params_default(&prm);
+    int a0 = 1;
+    while (a0 < argc && std::string(argv[a0]).compare(0, 2, "--") == 0) {
+        if (!parse_option(argv[a0], prm)) {
+            std::cerr << "Unknown option: " << argv[a0] << "\n";
+            return 1;
+        }
+        a0++;
+    }
+    if (argc - a0 != 3) {
+        std::cerr << "Usage: " << argv[0] << " [--k=K --m=M --global] <reference_file> <target_file> <output_folder>\n";
         return 1;
     }
-    const std::string ref_path = argv[1], tgt_path = argv[2], out_dir = argv[3];
+    const std::string ref_path = argv[a0], tgt_path = argv[a0 + 1], out_dir = argv[a0 + 2];
     try {
         if (!std::filesystem::exists(out_dir)) std::filesystem::create_directory(out_dir);
     } catch (const std::exception& ex) {
@@ -34,7 +63,7 @@ int main(int argc, char* argv[]) {
         return 1;
     }
     sccg_buf text{};
-    rc = sccg_compress(ctx, ref.data(), ref.size(), tgt.data(), tgt.size(), &text);
+    rc = sccg_compress_ex(ctx, &prm, ref.data(), ref.size(), tgt.data(), tgt.size(), &text);
     if (rc && rc != SCCG_E_DELTA_STOI) {
         std::cerr << "Error: " << sccg_last_error(ctx) << " (rc=" << rc << ")\n";
         sccg_ctx_destroy(ctx);

@@ -329,9 +329,27 @@ int paren_delta(sccg_ctx* ctx, const uint8_t* X, int64_t n, uint8_t* out, int64_
     return 0;
 }
 
-int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_t* tfa, int64_t tn, uint8_t* out,
-                         int64_t out_cap, int64_t* out_len) {
+// the parameter sets the kernels are built for (sccg.h, sccg_params)
+int check_params(sccg_ctx* ctx, const sccg_params& P) {
+    if (P.m < 0 || 2 * P.m + 1 > 256)
+        return ctx->fail(SCCG_E_UNSUPPORTED, "m = %d: the global walk's window takes 0 <= m <= 127", P.m);
+    if (P.local) {
+        if (P.k != 14 || P.k2 != 10 || P.L != SEG_L || P.T1 != 0.5f || P.T2 != 4)
+            return ctx->fail(SCCG_E_UNSUPPORTED, "local = 1 takes the reference's k = 14, k2 = 10, L = 1000, T1 = 0.5, T2 = 4 "
+                                                 "(use local = 0 for other k)");
+    } else if (P.k < 1 || P.k > 32) {
+        return ctx->fail(SCCG_E_UNSUPPORTED, "k = %d: the global walk takes 1 <= k <= 32", P.k);
+    }
+    return 0;
+}
+
+int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa, int64_t rn, const uint8_t* tfa,
+                         int64_t tn, uint8_t* out, int64_t out_cap, int64_t* out_len) {
     hipStream_t s = ctx->stream;
+    if (const int rc = check_params(ctx, P)) return rc;
+    // local = 0: no local pass, the global pass from the start (compression.cpp:378, :484)
+    const bool force_global = !P.local;
+    const int kg = P.k, mg = P.m;   // the global call's k and m (compression.cpp:561)
     sccg_stats st{};
     st.switch_segment = -1;
     // SCCG_DEBUG: host-side phase clock (synchronises at every mark, diagnostics only)
@@ -418,10 +436,10 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         TRY(d2h_i64(ctx, sc + 7, hr, 2, ctx->side));
         if (hr[1] < INT32_MAX - 8 && tn < INT32_MAX - 8) {
             HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
-            const size_t wsb_early = walk_workspace_bytes(hr[1], tn, 14, walk_chunk(tn));   // |T'| <= tn
+            const size_t wsb_early = walk_workspace_bytes(hr[1], tn, kg, walk_chunk(tn));   // |T'| <= tn
             void* ws_early = ctx->get(B_WALK, wsb_early);
             if (!ws_early) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb_early);
-            TRY(global_sweep_early(Rp, hr[1], tfa, tn, sc, 14, 100, walk_chunk(tn), ws_early, wsb_early, ctx->side));
+            TRY(global_sweep_early(Rp, hr[1], tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb_early, ctx->side));
         }
     }
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
@@ -437,7 +455,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     GET(SegStat, stat, B_STAT, iters_max > 0 ? iters_max : 1);
     GET(int32_t, cls, B_SEGCLS, iters_max > 0 ? iters_max : 1);
     int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
-    if (iters_max > 0) {
+    if (iters_max > 0 && !force_global) {
         if (cls != ctx->cls_buf || ctx->cap[B_SEGCLS] != ctx->cls_cap || ctx->cls_gen >= (1 << 28)) {
             // new buffer (or tags about to wrap): zero it once, so no stale tag can match
             HIPTRY(hipMemsetAsync(cls, 0, ctx->cap[B_SEGCLS], s));
@@ -470,10 +488,10 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
 
     // ---- the global walk's preparation, side stream (wasted only if the pass stays local)
     const int64_t np[2] = {lt[1], lr[1]};
-    const size_t wsb = walk_workspace_bytes(np[1], np[0], 14, walk_chunk(tn));
+    const size_t wsb = walk_workspace_bytes(np[1], np[0], kg, walk_chunk(tn));
     void* ws = ctx->get(B_WALK, wsb);
     if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
-    TRY(global_prepare(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(tn), ws, wsb, s2));
+    TRY(global_prepare(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, s2));
     HIPTRY(hipEventRecord(ctx->ev_join, s2));
 
     int64_t pos = 0;
@@ -485,7 +503,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     };
 
     // ---- the switch point (compression.cpp:417-481), read once the local pass is done
-    bool sw_known = iters <= 0;
+    bool sw_known = iters <= 0 || force_global;
     auto read_switch = [&]() -> int {
         if (sw_known) return 0;
         HIPTRY(hipEventSynchronize(ctx->ev_local));
@@ -494,7 +512,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
         sw_known = true;
         return 0;
     };
-    if (iters > 0) HIPTRY(hipMemcpyAsync(ctx->h_switch, sc + 21, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    if (iters > 0 && !force_global) HIPTRY(hipMemcpyAsync(ctx->h_switch, sc + 21, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIPTRY(hipEventRecord(ctx->ev_local, s));
 
     // ---- global (compression.cpp:484-574), speculatively: the walk runs on the side stream right
@@ -504,7 +522,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     int64_t g_rlen = 0;
     uint8_t* X = nullptr;
     WalkResult wr{};
-    if (iters > 0) {
+    if (iters > 0 || force_global) {
         struct Late {
             std::function<int(uint8_t**)> f;
             std::function<int()> poll;
@@ -512,7 +530,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
             static int abandon(void* u) { return static_cast<Late*>(u)->poll(); }
         } late{[&](uint8_t** o) -> int {
                    TRY(read_switch());
-                   if (sw < 0) return WALK_ABANDONED;
+                   if (sw < 0 && !force_global) return WALK_ABANDONED;
                    TRY(join_lines(s2));
                    const int64_t nlen = rl_len[1];
                    TRY(dev_put_framed(out + pos, nline, nlen, '\n', '\n', s2));   // "\n" + N line + "\n"
@@ -526,12 +544,13 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
                    return 0;
                },
                [&]() -> int {
+                   if (force_global) return 0;
                    if (!sw_known && hipEventQuery(ctx->ev_local) != hipSuccess) return 0;   // pass still running
                    if (read_switch()) return 0;   // the resolve step reports the error
                    return sw < 0;
                }};
         const EmitTarget target{&Late::call, &late, &Late::abandon};
-        const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], 14, 100, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
+        const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
                                              s2, paren, &target, /*keep_flat=*/false);
         if (rc != WALK_ABANDONED) {
             TRY(rc);
@@ -545,7 +564,7 @@ int compress_device_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const ui
     st.switch_segment = sw;
     mark("local");
     if (!global_done) {
-        if (sw >= 0) return ctx->fail(SCCG_E_INTERNAL, "switch found but the global walk was abandoned");
+        if (sw >= 0 || force_global) return ctx->fail(SCCG_E_INTERNAL, "switch found but the global walk was abandoned");
         global_prepare_reset();
         TRY(join_lines(s));
         // ---- local: "\n,\n" + records + leftover segments
@@ -704,23 +723,42 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
 
 extern "C" {
 
-int sccg_compress_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len, const void* d_tgt_fa, size_t tgt_len,
-                         void* d_out, size_t out_cap, size_t* out_len, void* stream) {
-    if (!ctx || !d_out || !out_len || (!d_ref_fa && ref_len) || (!d_tgt_fa && tgt_len)) return SCCG_E_INVALID;
+void sccg_params_default(sccg_params* p) {
+    if (!p) return;
+    p->k = 14; p->k2 = 10; p->L = SEG_L; p->m = 100; p->T1 = 0.5f; p->T2 = 4; p->local = 1;   // compression.cpp:373-379
+}
+
+int sccg_compress_device_ex(sccg_ctx* ctx, const sccg_params* params, const void* d_ref_fa, size_t ref_len,
+                            const void* d_tgt_fa, size_t tgt_len, void* d_out, size_t out_cap, size_t* out_len, void* stream) {
+    if (!ctx || !params || !d_out || !out_len || (!d_ref_fa && ref_len) || (!d_tgt_fa && tgt_len)) return SCCG_E_INVALID;
     HIPTRY(hipSetDevice(ctx->device));
     hipStream_t saved = ctx->stream;
     if (stream) ctx->stream = (hipStream_t)stream;
     int64_t len = 0;
-    int rc = compress_device_impl(ctx, (const uint8_t*)d_ref_fa, (int64_t)ref_len, (const uint8_t*)d_tgt_fa,
+    int rc = compress_device_impl(ctx, *params, (const uint8_t*)d_ref_fa, (int64_t)ref_len, (const uint8_t*)d_tgt_fa,
                                   (int64_t)tgt_len, (uint8_t*)d_out, (int64_t)out_cap, &len);
     ctx->stream = saved;
     *out_len = (size_t)len;
     return rc;
 }
 
+int sccg_compress_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len, const void* d_tgt_fa, size_t tgt_len,
+                         void* d_out, size_t out_cap, size_t* out_len, void* stream) {
+    sccg_params p;
+    sccg_params_default(&p);
+    return sccg_compress_device_ex(ctx, &p, d_ref_fa, ref_len, d_tgt_fa, tgt_len, d_out, out_cap, out_len, stream);
+}
+
 int sccg_compress(sccg_ctx* ctx, const char* ref_fa, size_t ref_len, const char* tgt_fa, size_t tgt_len,
                   sccg_buf* out_text) {
-    if (!ctx || !out_text || (!ref_fa && ref_len) || (!tgt_fa && tgt_len)) return SCCG_E_INVALID;
+    sccg_params p;
+    sccg_params_default(&p);
+    return sccg_compress_ex(ctx, &p, ref_fa, ref_len, tgt_fa, tgt_len, out_text);
+}
+
+int sccg_compress_ex(sccg_ctx* ctx, const sccg_params* params, const char* ref_fa, size_t ref_len, const char* tgt_fa,
+                     size_t tgt_len, sccg_buf* out_text) {
+    if (!ctx || !params || !out_text || (!ref_fa && ref_len) || (!tgt_fa && tgt_len)) return SCCG_E_INVALID;
     out_text->data = nullptr;
     out_text->len = 0;
     HIPTRY(hipSetDevice(ctx->device));
@@ -732,7 +770,7 @@ int sccg_compress(sccg_ctx* ctx, const char* ref_fa, size_t ref_len, const char*
     if (ref_len) HIPTRY(hipMemcpyAsync(drf, ref_fa, ref_len, hipMemcpyHostToDevice, ctx->stream));
     if (tgt_len) HIPTRY(hipMemcpyAsync(dtf, tgt_fa, tgt_len, hipMemcpyHostToDevice, ctx->stream));
     int64_t len = 0;
-    int rc = compress_device_impl(ctx, drf, (int64_t)ref_len, dtf, (int64_t)tgt_len, dout, (int64_t)cap, &len);
+    int rc = compress_device_impl(ctx, *params, drf, (int64_t)ref_len, dtf, (int64_t)tgt_len, dout, (int64_t)cap, &len);
     if (rc && rc != SCCG_E_DELTA_STOI) return rc;   // DELTA_STOI still returns the file's text
     char* h = (char*)malloc((size_t)len + 1);
     if (!h) return ctx->fail(SCCG_E_NOMEM, "host allocation failed");
@@ -822,8 +860,8 @@ int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, s
         int64_t t = 0;
         for (size_t i = 0; i < kind.size(); i++) { if (kind[i]) tt[i] = t; t += len[i]; }
     } else {
-        if (m < 0 || 2 * m + 1 > 256 || k < 1 || k > 15 || nr >= (size_t)INT32_MAX - 8 || nt >= (size_t)INT32_MAX - 8)
-            return ctx->fail(SCCG_E_UNSUPPORTED, "global sccg_match takes 0 <= m <= 127, 1 <= k <= 15");
+        if (m < 0 || 2 * m + 1 > 256 || k < 1 || k > 32 || nr >= (size_t)INT32_MAX - 8 || nt >= (size_t)INT32_MAX - 8)
+            return ctx->fail(SCCG_E_UNSUPPORTED, "global sccg_match takes 0 <= m <= 127, 1 <= k <= 32");
         global_prepare_reset();   // buffers shared with compress: never reuse its preparation
         GET(uint8_t, R, B_RP, nr + 64);
         GET(uint8_t, T, B_TP, nt + 64);

@@ -31,6 +31,13 @@ constexpr int WPB = 4;                 // chunks (waves) per block
 constexpr int WCAP = 256;              // window positions held in LDS (2m+1 <= WCAP)
 constexpr int32_t INVALID = INT32_MIN;
 constexpr int ANCHOR_K = 32;
+// Walk keys are exact 2-bit codes of at most KEY_K bases (common.h).  For k > KEY_K (a non-parity
+// parameter override; the reference hard-codes k = 14, compression.cpp:373) every key is the code of
+// the k-mer's first KEY_K bases: a key hit is a candidate only if the extension from KEY_K reaches
+// k (ext_k), and a position whose key hits have no such candidate is a literal step.
+constexpr int KEY_K = 15;
+constexpr int KMAX = 32;              // largest k the walk takes
+constexpr int KB_COUNT = 32;          // kb: the first k bytes of T' at [0, k), their count at [32, 36)
 constexpr int ANCHOR_STEP_DEFAULT = 32;   // reference sample stride (SCCG_ANCHOR_STEP for tuning runs)
 constexpr int ANCHOR_LOAD_DEFAULT = 4;    // table slots per sample (SCCG_ANCHOR_LOAD)
 #ifndef ANCHOR_PROBE_BATCHES
@@ -82,6 +89,7 @@ struct WalkPtrs {
     const uint8_t* R;
     const uint8_t* T;
     int32_t nR, nT, k, m, S, C, cap;
+    int32_t kp;               // key length: min(k, KEY_K); k > KEY_K confirms the rest by extension (KEY_K)
     int32_t* bt[2];
     int32_t* bp[2];
     int32_t* bl[2];
@@ -300,6 +308,17 @@ __device__ int32_t wave_lce_hbm(const uint8_t* __restrict__ R, int32_t a, const 
     return maxlen > 0 ? maxlen : 0;
 }
 
+// extend_alignment (compression.cpp:27-34) of window candidate c for the target k-mer at y: its
+// length, or 0 when only the key's kp bases match (k > KEY_K: then c is no candidate at all)
+__device__ __forceinline__ int32_t ext_k(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t c, int32_t y) {
+    const int32_t kp = A.kp;
+    int32_t maxlen = A.nR - (c + kp);
+    const int32_t mt = A.nT - (y + kp);
+    if (mt < maxlen) maxlen = mt;
+    const int32_t l = kp + wave_lce(A, L, B, c + kp, y + kp, maxlen);
+    return l >= A.k ? l : 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // window of P in registers: lane l holds the keys of window indices 4l+q (q < 4), i.e. of the
 // reference k-mers starting at lo+4l+q, lo = max(0, P-m), up to hi = min(nR-k, P+m).
@@ -331,24 +350,25 @@ __device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin&
     uint64_t code;
     uint32_t bad;
     pack_codes<5>(w, code, bad);
-    const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
+    const int kp = A.kp;
+    const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        W.key[q] = (bad >> q) & KM ? exotic_key(A.R + W.lo + i0 + q, k) : (uint32_t)(code >> (2 * q)) & MASK;
+        W.key[q] = (bad >> q) & KM ? exotic_key(A.R + W.lo + i0 + q, kp) : (uint32_t)(code >> (2 * q)) & MASK;
         if (i0 + q < W.n) W.vmask |= 1u << q;
     }
 }
 
-// key of the target k-mer at y from its 16 bytes w (loaded by the caller; k <= 15)
+// key of the target k-mer at y from its 16 bytes w (loaded by the caller; kp <= 15)
 __device__ __forceinline__ uint32_t target_key_w(const WalkPtrs& A, int32_t y, const uint32_t (&w)[4]) {
-    const int k = A.k;
+    const int kp = A.kp;
     uint64_t code;
     uint32_t bad;
     pack_codes<4>(w, code, bad);
-    return bad & ((1u << k) - 1u) ? exotic_key(A.T + y, k) : (uint32_t)code & ((1u << (2 * k)) - 1u);
+    return bad & ((1u << kp) - 1u) ? exotic_key(A.T + y, kp) : (uint32_t)code & ((1u << (2 * kp)) - 1u);
 }
 
-// bit q set: window index 4*lane+q holds exactly the k-mer T[y..y+k) (key kk)
+// bit q set: window index 4*lane+q holds exactly the key's kp bases T[y..y+kp) (key kk)
 __device__ __forceinline__ uint32_t win_match(const WalkPtrs& A, const RegWin& W, uint32_t kk, int32_t y) {
     uint32_t m = 0;
 #pragma unroll
@@ -357,7 +377,7 @@ __device__ __forceinline__ uint32_t win_match(const WalkPtrs& A, const RegWin& W
     if (m && kk >= KEY_EXOTIC) {   // hash keys: confirm bytes (rare)
         const int32_t c0 = W.lo + 4 * lane_id();
         for (int q = 0; q < 4; q++)
-            if (((m >> q) & 1u) && !bytes_eq(A.R + c0 + q, A.T + y, A.k)) m &= ~(1u << q);
+            if (((m >> q) & 1u) && !bytes_eq(A.R + c0 + q, A.T + y, A.kp)) m &= ~(1u << q);
     }
     return m;
 }
@@ -385,7 +405,7 @@ __device__ void bloom_window(const RegWin& W, WalkLds& L) {
 // Bloom filter passes a superset, confirmed exactly against the register window in position order).
 constexpr int WIDE = 16;   // positions per lane per step (1024 per wave step)
 __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, const RegWin& W, int32_t x, int32_t end) {
-    const int lane = lane_id(), k = A.k;
+    const int lane = lane_id(), k = A.kp;
     const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
     uint32_t w[8];   // 32 bytes >= WIDE + k - 1; the next step's words are loaded one step ahead
     loadw<8>(A.T + x + WIDE * lane, w);
@@ -451,7 +471,6 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     const int32_t lo_j = j * A.S;
     const int32_t hi_j = (lo_j + A.S < A.nT) ? lo_j + A.S : A.nT;
     const int32_t lastk = A.nT - A.k;
-    const int k = A.k;
 
     int32_t x, P, n = 0, q = 0, ob, cb = -1, cc = 0;
     if (kind == KIND_SPEC) {
@@ -606,11 +625,9 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
                 const int cl_ = __ffsll((long long)cm) - 1;
                 cm &= cm - 1;
                 const int32_t c = W.lo + 4 * cl_ + qq;
-                int32_t maxlen = A.nR - (c + k);
-                const int32_t mt = A.nT - (y + k);
-                if (mt < maxlen) maxlen = mt;
-                const int32_t l = k + wave_lce(A, L, B, c + k, y + k, maxlen);   // extend_alignment
+                const int32_t l = ext_k(A, L, B, c, y);   // extend_alignment
                 ncand++;
+                if (!l) continue;   // (k > KEY_K) only the key's bases match
                 if (l > bl) { bl = l; bcnt = 1; bhas0 = (c == 0); bkey = c ? pick_key(c, P) : ~0ull; }
                 else if (l == bl) {
                     bcnt++;
@@ -618,6 +635,10 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
                     else { const uint64_t pk = pick_key(c, P); bkey = pk < bkey ? pk : bkey; }
                 }
             }
+        }
+        if (!bcnt) {   // (k > KEY_K) no candidate behind the key hits: a literal step
+            x = y + 1;
+            continue;
         }
         uint64_t pk;
         if (bcnt >= 2 && bhas0) pk = bkey;
@@ -967,13 +988,14 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
     for (int i = tid; i < (1 << CH_TBITS); i += 1024) tab[i] = CH_EMPTY;
     if (tid == 0) trunc_s = INT32_MAX;
     __syncthreads();
-    const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
+    const int kp = A.kp;   // (keys of the first kp bases: hits are a superset for k > KEY_K)
+    const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
     for (int32_t q = blo + tid; q <= bhi; q += 1024) {   // the band's keys
         uint32_t wv[4], bad;
         uint64_t code;
         loadw<4>(A.R + q, wv);
         pack_codes<4>(wv, code, bad);
-        uint32_t key = bad & KM ? exotic_key(A.R + q, k) : (uint32_t)code & MASK;
+        uint32_t key = bad & KM ? exotic_key(A.R + q, kp) : (uint32_t)code & MASK;
         if (key == CH_EMPTY) key = CH_EMPTY - 1;   // (exotic hash collision: a superset is fine)
         uint32_t sl = ch_slot(key);
         for (;;) {
@@ -1018,7 +1040,7 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
             pack_codes<8>(wv, code, bad);
             const int lim = b1 - p0 < 16 ? (int)(b1 - p0) : 16;
             for (int st = 0; st < lim; st++) {
-                const uint32_t key = (bad >> st) & KM ? exotic_key(A.T + p0 + st, k) : (uint32_t)(code >> (2 * st)) & MASK;
+                const uint32_t key = (bad >> st) & KM ? exotic_key(A.T + p0 + st, kp) : (uint32_t)(code >> (2 * st)) & MASK;
                 if (in_band(key)) mask |= 1u << st;
             }
         }
@@ -1040,7 +1062,7 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
             const int32_t y = (int32_t)(p0 + st);
             if (idx < CH_HCAP) {
                 oy[idx] = y;
-                ok[idx] = (bad >> st) & KM ? exotic_key(A.T + y, k) : (uint32_t)(code >> (2 * st)) & MASK;
+                ok[idx] = (bad >> st) & KM ? exotic_key(A.T + y, kp) : (uint32_t)(code >> (2 * st)) & MASK;
             } else if (idx == CH_HCAP) {
                 trunc_s = y;   // the first hit not kept: positions from here on are not covered
             }
@@ -1159,10 +1181,8 @@ __global__ __launch_bounds__(64) void k_chain_step(WalkPtrs A) {
                         const int cl_ = __ffsll((long long)cm) - 1;
                         cm &= cm - 1;
                         const int32_t c = W.lo + 4 * cl_ + qq;
-                        int32_t maxlen = A.nR - (c + k);
-                        const int32_t mt = A.nT - (y + k);
-                        if (mt < maxlen) maxlen = mt;
-                        const int32_t l = k + wave_lce(A, L, B, c + k, y + k, maxlen);
+                        const int32_t l = ext_k(A, L, B, c, y);
+                        if (!l) continue;   // (k > KEY_K) only the key's bases match
                         if (l > bl) { bl = l; bcnt = 1; bhas0 = (c == 0); bkey = c ? pick_key(c, P) : ~0ull; }
                         else if (l == bl) {
                             bcnt++;
@@ -1171,6 +1191,7 @@ __global__ __launch_bounds__(64) void k_chain_step(WalkPtrs A) {
                         }
                     }
                 }
+                if (!bcnt) continue;   // (k > KEY_K) no candidate: a literal step
                 uint64_t pk;
                 if (bcnt >= 2 && bhas0) pk = bkey;
                 else { const uint64_t k0 = bhas0 ? pick_key(0, P) : ~0ull; pk = k0 < bkey ? k0 : bkey; }
@@ -1433,15 +1454,15 @@ __device__ __forceinline__ void sweep_kmers_w(const uint8_t* __restrict__ R, int
 
 // pass 0: max extension over all candidates; pass 1: count / has0 / min pick key at that max
 __global__ void k_fullc(WalkPtrs A, int32_t y, int32_t P, int pass) {
-    const int k = A.k;
+    const int k = A.k, kp = A.kp;
     const uint8_t* kb = A.T + y;
-    const uint32_t key = walk_key(kb, k);
+    const uint32_t key = walk_key(kb, kp);
     const uint32_t lmax = (uint32_t)A.fc[0];
     const bool exo = key >= KEY_EXOTIC;
-    sweep_kmers(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) {
-        return exo ? !pure : (pure && code == key);   // exotic: candidates confirmed bytewise below
+    sweep_kmers(A.R, (int64_t)A.nR - k + 1, kp, [&](uint32_t code, bool pure) {
+        return exo ? !pure : (pure && code == key);   // exotic (or k > kp): candidates confirmed bytewise below
     }, [&](int64_t c) {
-        if (exo && !bytes_eq(A.R + c, kb, k)) return;
+        if ((exo || k > kp) && !bytes_eq(A.R + c, kb, k)) return;
         const int32_t l = serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, y, k);
         if (pass == 0) atomicMax(&A.fc[0], (unsigned long long)l);
         else if ((uint32_t)l == lmax) {
@@ -1489,8 +1510,10 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
     __shared__ uint32_t hidx[1 << PBBITS];
     __shared__ uint32_t bits[1 << (PFBITS - 5)];
     __shared__ CandBest wbest[SCCG_BLOCK / 64];
-    const int k = A.k;
-    const uint32_t key0 = walk_key(A.T + x0, k);   // exotic: no statistics (host falls back)
+    // keys of the first kp bases: for k > kp the hits are a superset (the host confirms the first
+    // with k_fullc) and x0's statistics confirm the rest of each candidate bytewise
+    const int k = A.k, kp = A.kp;
+    const uint32_t key0 = walk_key(A.T + x0, kp);   // exotic: no statistics (host falls back)
     CandBest best{0, 0, 0, ~0ull};
     for (int i = threadIdx.x; i < (1 << PBBITS); i += blockDim.x) { hkey[i] = 0xffffffffu; hidx[i] = 0xffffffffu; }
     for (int i = threadIdx.x; i < (1 << (PFBITS - 5)); i += blockDim.x) bits[i] = 0;
@@ -1500,7 +1523,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
         uint64_t cw;
         loadw<4>(A.T + x0 + i, w);
         pack_codes<4>(w, cw, bad);
-        const uint32_t key = bad & ((1u << k) - 1u) ? exotic_key(A.T + x0 + i, k) : (uint32_t)cw & ((1u << (2 * k)) - 1u);
+        const uint32_t key = bad & ((1u << kp) - 1u) ? exotic_key(A.T + x0 + i, kp) : (uint32_t)cw & ((1u << (2 * kp)) - 1u);
         if (key >= KEY_EXOTIC) { atomicMin(&A.fc[5], (unsigned long long)(x0 + i)); continue; }
         const uint32_t fb = slot_hash(key, PFBITS);
         atomicOr(&bits[fb >> 5], 1u << (fb & 31));
@@ -1513,7 +1536,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
     }
     __syncthreads();
     // the bitmap test is branch-free per position; the exact probe runs only for bitmap hits
-    sweep_kmers(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) {
+    sweep_kmers(A.R, (int64_t)A.nR - k + 1, kp, [&](uint32_t code, bool pure) {
         const uint32_t fb = slot_hash(code, PFBITS);
         return pure && ((bits[fb >> 5] >> (fb & 31)) & 1u);
     }, [&](int64_t c) {
@@ -1522,8 +1545,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
         uint32_t w[4];
         loadw<4>(A.R + c, w);
         pack_codes<4>(w, cw, bad);
-        const uint32_t code = (uint32_t)cw & ((1u << (2 * k)) - 1u);
-        if (code == key0) {
+        const uint32_t code = (uint32_t)cw & ((1u << (2 * kp)) - 1u);
+        if (code == key0 && (k == kp || bytes_eq(A.R + c + kp, A.T + x0 + kp, k - kp))) {
             const uint32_t l = (uint32_t)serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, x0, k);
             best = cb_merge(best, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key((int32_t)c, -1) : ~0ull});
         }
@@ -1553,13 +1576,14 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
 template <bool ANCH>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
     __shared__ CandBest wbest[SCCG_BLOCK / 64];
-    const int k = A.k;
-    const uint32_t key0 = walk_key(A.T + x0, k);
+    const int k = A.k, kp = A.kp;
+    const uint32_t key0 = walk_key(A.T + x0, kp);
     CandBest best{0, 0, 0, ~0ull};
     if (key0 < KEY_EXOTIC || ANCH) {   // exotic: no statistics, the caller falls back to k_presence
         const bool want = key0 < KEY_EXOTIC;
-        sweep_kmers_w(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) { return want && pure && code == key0; },
+        sweep_kmers_w(A.R, (int64_t)A.nR - k + 1, kp, [&](uint32_t code, bool pure) { return want && pure && code == key0; },
                       [&](int64_t c) {
+                          if (k > kp && !bytes_eq(A.R + c + kp, A.T + x0 + kp, k - kp)) return;
                           const uint32_t l = (uint32_t)serial_ext(A.R, A.nR, A.T, A.nT, (int32_t)c, x0, k);
                           best = cb_merge(best, CandBest{l, 1u, c == 0 ? 1u : 0u, c ? pick_key((int32_t)c, -1) : ~0ull});
                       },
@@ -1601,7 +1625,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
 // reading disagreed with T') -> the caller runs the full k_key0 sweep.  fc[13]: positions found.
 // ---------------------------------------------------------------------------------------------
 // one wave: the first k bytes of T' (strip + toupper + N erase of the target FASTA, the header line
-// [hdr[0], hdr[1]) excluded) within the first `limit` FASTA bytes -> kb[0, k), their count -> kb[16..19]
+// [hdr[0], hdr[1]) excluded) within the first `limit` FASTA bytes -> kb[0, k), their count -> kb[KB_COUNT..]
 __global__ void k_first_kmer(const uint8_t* __restrict__ fa, int64_t n, const int64_t* __restrict__ hdr, int k,
                              int64_t limit, uint8_t* __restrict__ kb) {
     const int lane = lane_id();
@@ -1625,17 +1649,18 @@ __global__ void k_first_kmer(const uint8_t* __restrict__ fa, int64_t n, const in
             if ((keep >> i) & 1u) { if (idx < k) kb[idx] = c_toupper(b[i]); idx++; }
         found += __shfl(incl, 63, 64);
     }
-    if (lane == 0) *reinterpret_cast<int32_t*>(kb + 16) = found < k ? found : k;
+    if (lane == 0) *reinterpret_cast<int32_t*>(kb + KB_COUNT) = found < k ? found : k;
 }
 
 template <bool ANCH>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
-    const int k = A.k;
-    const bool have = *reinterpret_cast<const int32_t*>(A.kb + 16) == k;
-    const uint32_t key0 = have ? walk_key(A.kb, k) : KEY_EXOTIC;
+    const int k = A.k, kp = A.kp;
+    const bool have = *reinterpret_cast<const int32_t*>(A.kb + KB_COUNT) == k;
+    const uint32_t key0 = have ? walk_key(A.kb, kp) : KEY_EXOTIC;
     const bool want = key0 < KEY_EXOTIC;
-    sweep_kmers_w(A.R, (int64_t)A.nR - k + 1, k, [&](uint32_t code, bool pure) { return want && pure && code == key0; },
+    sweep_kmers_w(A.R, (int64_t)A.nR - k + 1, kp, [&](uint32_t code, bool pure) { return want && pure && code == key0; },
                   [&](int64_t c) {
+                      if (k > kp && !bytes_eq(A.R + c + kp, A.kb + kp, k - kp)) return;
                       const unsigned long long i = atomicAdd(&A.fc[13], 1ull);
                       if (i < (unsigned long long)CAND_CAP) A.cand[i] = (int32_t)c;
                   },
@@ -1667,10 +1692,10 @@ constexpr int CAND_STATS_GRID = 256;
 // whole wave (one round trip: lane i compares byte i of the FASTA-read k-mer with T')
 __device__ __forceinline__ bool cand_stats_usable(const WalkPtrs& A) {
     const int k = A.k, lane = lane_id();
-    const bool head = *reinterpret_cast<const int32_t*>(A.kb + 16) == k && A.fc[13] <= (unsigned long long)CAND_CAP &&
+    const bool head = *reinterpret_cast<const int32_t*>(A.kb + KB_COUNT) == k && A.fc[13] <= (unsigned long long)CAND_CAP &&
                       A.nT >= k;
     const bool same = lane >= k || A.kb[lane] == A.T[lane];   // T' has readable slack past nT
-    return head && __ballot(!same) == 0 && walk_key(A.kb, k) < KEY_EXOTIC;
+    return head && __ballot(!same) == 0 && walk_key(A.kb, A.kp) < KEY_EXOTIC;
 }
 __global__ __launch_bounds__(SCCG_BLOCK) void k_cand_stats(WalkPtrs A) {
     __shared__ CandBest wbest[SCCG_BLOCK / 64];
@@ -2018,6 +2043,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     Carve c{(char*)ws, 0, ws_bytes};
     A.R = R; A.T = T;
     A.nR = (int32_t)nR; A.nT = (int32_t)nT; A.k = k; A.m = m; A.S = S;
+    A.kp = k < KEY_K ? k : KEY_K;
     A.C = (int32_t)((nT + S - 1) / S);
     if (A.C < 1) A.C = 1;
     A.cap = S / k + 4;
@@ -2320,7 +2346,7 @@ void global_prepare_reset() { g_prep = Prepared{}; g_early = Early{}; }
 int global_sweep_early(const uint8_t* Rp, int64_t nRp, const uint8_t* tgt_fa, int64_t tn, const int64_t* d_hdr, int k,
                        int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s) {
     g_early = Early{};
-    if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
+    if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
     if (nRp < k || tn <= 0) return 0;   // no walk can use it
     size_t used = 0;
     // |T'| <= tn: the carve's R'-only front (anchor table, fc, positions, kb) does not depend on it
@@ -2346,7 +2372,7 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const uint8_t* tgt_fa, in
 int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
                    size_t ws_bytes, hipStream_t s) {
     g_prep = Prepared{};
-    if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
+    if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
     size_t used = 0;
     WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
     if (used > ws_bytes) return SCCG_E_INTERNAL;
@@ -2375,7 +2401,7 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
                           void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
                           bool abs_p, const EmitTarget* late_out, bool keep_flat) {
-    if (m < 0 || 2 * m + 1 > WCAP || k > 15 || k < 1) return SCCG_E_UNSUPPORTED;
+    if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
     size_t used = 0;
     WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
     if (used > ws_bytes) return SCCG_E_INTERNAL;
@@ -2519,14 +2545,22 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 RC(dev_readback(&it, 1, s));
             }
             if (r[0] != ~0ull && r[0] < r[1]) {
-                first_y = (int32_t)r[0];
-                if (first_y == x0 && r[4] > 0) {   // statistics gathered by the same sweep
+                const int32_t y = (int32_t)r[0];
+                if (y == x0 && r[4] > 0) {   // statistics gathered by the same sweep
                     const uint64_t k0 = 1ull << 32;   // pick_key(0, -1)
                     const uint64_t pk = (r[5] >= 2 && r[6]) ? r[7] : ((r[6] && k0 < r[7]) ? k0 : r[7]);
+                    first_y = y;
                     first_p = (int32_t)(uint32_t)pk;
                     first_l = (int32_t)r[4];
+                    break;
                 }
-                break;
+                if (A.k == A.kp) { first_y = y; break; }   // exact keys: y has a candidate
+                // k > KEY_K: y's first kp bases occur in R'; the exact scan decides
+                FullC f;
+                RC(run_fullc(A, y, -1, &f, s));
+                if (f.lmax > 0) { first_y = y; first_p = f.p; first_l = (int32_t)f.lmax; break; }
+                x0 = y + 1;
+                continue;
             }
             if (r[1] != ~0ull) {
                 FullC f;

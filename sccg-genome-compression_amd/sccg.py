@@ -50,6 +50,13 @@ class Stats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class Params(ctypes.Structure):
+    """sccg_params (include/sccg.h): compression.cpp:373-379's constants; other values than the
+    defaults are non-parity overrides (local=1 takes only m; local=0 takes 1 <= k <= 32, m)."""
+    _fields_ = [("k", ctypes.c_int32), ("k2", ctypes.c_int32), ("L", ctypes.c_int32), ("m", ctypes.c_int32),
+                ("T1", ctypes.c_float), ("T2", ctypes.c_int32), ("local", ctypes.c_int32)]
+
+
 _lib = None
 
 
@@ -69,6 +76,9 @@ def load_library():
     lib.sccg_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
     lib.sccg_compress.argtypes = [vp, c, sz, c, sz, ctypes.POINTER(Buf)]
     lib.sccg_compress_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
+    lib.sccg_params_default.argtypes = [ctypes.POINTER(Params)]
+    lib.sccg_compress_ex.argtypes = [vp, ctypes.POINTER(Params), c, sz, c, sz, ctypes.POINTER(Buf)]
+    lib.sccg_compress_device_ex.argtypes = [vp, ctypes.POINTER(Params), vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
     lib.sccg_compress_bound.argtypes = [sz, sz]
     lib.sccg_compress_bound.restype = sz
     lib.sccg_match.argtypes = [vp, c, sz, c, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64,
@@ -131,10 +141,25 @@ class Context:
         self.lib.sccg_buf_free(ctypes.byref(buf))
         return data
 
-    def compress(self, ref_fa: bytes, tgt_fa: bytes) -> bytes:
-        """Bytes of compressed_genome.txt (compression.cpp:320-580, without 7z)."""
+    def params(self, **overrides) -> Params:
+        """sccg_params: the reference's constants (compression.cpp:373-379) with `overrides` applied."""
+        prm = Params()
+        self.lib.sccg_params_default(ctypes.byref(prm))
+        for name, v in overrides.items():
+            if name not in dict(Params._fields_):
+                raise TypeError(f"unknown parameter {name!r}")
+            setattr(prm, name, v)
+        return prm
+
+    def compress(self, ref_fa: bytes, tgt_fa: bytes, **overrides) -> bytes:
+        """Bytes of compressed_genome.txt (compression.cpp:320-580, without 7z).  Keyword overrides
+        (k, k2, L, m, T1, T2, local) go through sccg_compress_ex as non-parity parameters."""
         buf = Buf()
-        rc = self.lib.sccg_compress(self.ptr, ref_fa, len(ref_fa), tgt_fa, len(tgt_fa), ctypes.byref(buf))
+        if overrides:
+            rc = self.lib.sccg_compress_ex(self.ptr, ctypes.byref(self.params(**overrides)), ref_fa, len(ref_fa),
+                                           tgt_fa, len(tgt_fa), ctypes.byref(buf))
+        else:
+            rc = self.lib.sccg_compress(self.ptr, ref_fa, len(ref_fa), tgt_fa, len(tgt_fa), ctypes.byref(buf))
         if rc:
             data = self._take(buf)
             err = SccgError(rc, self.lib.sccg_last_error(self.ptr).decode(errors="replace"))
@@ -151,11 +176,15 @@ class Context:
         return self._take(buf)
 
     def compress_device(self, d_ref: int, ref_len: int, d_tgt: int, tgt_len: int, d_out: int, out_cap: int,
-                        stream: int = 0) -> int:
+                        stream: int = 0, **overrides) -> int:
         """HBM-resident compress: device pointers in, record text written to d_out; returns length."""
         n = ctypes.c_size_t()
-        rc = self.lib.sccg_compress_device(self.ptr, d_ref, ref_len, d_tgt, tgt_len, d_out, out_cap,
-                                           ctypes.byref(n), stream or None)
+        if overrides:
+            rc = self.lib.sccg_compress_device_ex(self.ptr, ctypes.byref(self.params(**overrides)), d_ref, ref_len,
+                                                  d_tgt, tgt_len, d_out, out_cap, ctypes.byref(n), stream or None)
+        else:
+            rc = self.lib.sccg_compress_device(self.ptr, d_ref, ref_len, d_tgt, tgt_len, d_out, out_cap,
+                                               ctypes.byref(n), stream or None)
         if rc:
             self._err(rc)
         return n.value

@@ -18,6 +18,12 @@ class OracleError(RuntimeError):
         self.partial = partial
 
 
+class OrcParams(ctypes.Structure):
+    """orc_params (oracle/sccg_oracle.h): compression.cpp:373-379's constants."""
+    _fields_ = [("k", ctypes.c_int), ("k2", ctypes.c_int), ("L", ctypes.c_int), ("m", ctypes.c_int),
+                ("T1", ctypes.c_float), ("T2", ctypes.c_int), ("local", ctypes.c_int)]
+
+
 class OrcRec(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("p", ctypes.c_int32), ("l", ctypes.c_int32),
                 ("t", ctypes.c_int64)]
@@ -35,6 +41,9 @@ def _load():
         lib.orc_match.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int,
                                   ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                   ctypes.POINTER(ctypes.POINTER(OrcRec)), ctypes.POINTER(ctypes.c_int64)]
+        lib.orc_compress_params.argtypes = [ctypes.POINTER(OrcParams), ctypes.c_char_p, ctypes.c_size_t,
+                                            ctypes.c_char_p, ctypes.c_size_t, pp, psz]
+        lib.orc_params_default.argtypes = [ctypes.POINTER(OrcParams)]
         lib.orc_free.argtypes = [ctypes.c_void_p]
         lib.orc_last_mode_global.restype = ctypes.c_int
         lib.orc_last_switch_segment.restype = ctypes.c_int64
@@ -57,6 +66,17 @@ def _call(fn, a: bytes, b: bytes) -> bytes:
 def compress(ref_fa: bytes, tgt_fa: bytes) -> bytes:
     """compressed_genome.txt bytes (compression.cpp:320-580, without 7z)."""
     return _call(_load().orc_compress, ref_fa, tgt_fa)
+
+
+def compress_params(ref_fa: bytes, tgt_fa: bytes, **overrides) -> bytes:
+    """compress() with compression.cpp:373-379's constants overridden (k, k2, L, m, T1, T2, local)."""
+    lib = _load()
+    prm = OrcParams()
+    lib.orc_params_default(ctypes.byref(prm))
+    for name, v in overrides.items():
+        setattr(prm, name, v)
+    return _call(lambda a, na, b, nb, o, n: lib.orc_compress_params(ctypes.byref(prm), a, na, b, nb, o, n),
+                 ref_fa, tgt_fa)
 
 
 def last_mode() -> tuple[bool, int]:

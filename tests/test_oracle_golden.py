@@ -118,3 +118,45 @@ def test_close_paren_literals_vs_reference(seed):
         assert (rc, fa) == (0, oraclelib.decompress(rec, rfa))
     except oraclelib.OracleError as e:
         assert rc != 0 and e.rc != 0
+
+
+# ---- parameter overrides (sccg_params) ----------------------------------------
+@pytest.mark.parametrize("case", goldens.param_cases(), ids=lambda c: f"k{c['k']}-m{c['m']}-{c['gen']}{c['seed']}")
+def test_param_fixtures(case):
+    """orc_compress_params reproduces the reference built with other k / m (make_param_golden.py)."""
+    rfa, tfa = goldens.param_inputs(case)
+    try:
+        rec, rc = oraclelib.compress_params(rfa, tfa, k=case["k"], m=case["m"]), 0
+    except oraclelib.OracleError as e:
+        rec, rc = e.partial, 1
+    assert rc == case["compress_rc"]
+    assert rec == case["record"]
+
+
+def _run_ref_param(k, m, rfa, tfa):
+    binary = os.path.join(REF_BIN, f"compression_k{k}_m{m}")
+    env = dict(os.environ, PATH=os.path.join(REPO, "oracle", "stub7z") + os.pathsep + os.environ["PATH"])
+    with tempfile.TemporaryDirectory() as d:
+        rp, tp = os.path.join(d, "r.fa"), os.path.join(d, "t.fa")
+        open(rp, "wb").write(rfa)
+        open(tp, "wb").write(tfa)
+        subprocess.run([binary, rp, tp, os.path.join(d, "o")], env=env, stdout=subprocess.DEVNULL,
+                       stderr=subprocess.DEVNULL, check=True)
+        return open(os.path.join(d, "o", "compressed_genome.txt"), "rb").read()
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_BIN, "compression_k21_m100")),
+                    reason="reference k=21 variant not built (make -C oracle ref-param K=21)")
+@pytest.mark.parametrize("seed", range(200, 212))
+def test_param_k21_differential_vs_reference(seed):
+    rfa, tfa = fuzzgen.global_case(seed)
+    assert oraclelib.compress_params(rfa, tfa, k=21) == _run_ref_param(21, 100, rfa, tfa)
+
+
+def test_param_local0_is_the_global_pass():
+    """local = 0 gives the global pass alone: on a case the reference switches on, the same text."""
+    for seed in range(4):
+        rfa, tfa = fuzzgen.global_case(seed)
+        rec = oraclelib.compress(rfa, tfa)
+        if oraclelib.last_mode()[0]:
+            assert oraclelib.compress_params(rfa, tfa, local=0) == rec
