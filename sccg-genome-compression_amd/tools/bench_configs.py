@@ -4,7 +4,9 @@
     UCSC lengths, synthetic, compressed one after another; the 8-GPU job LPT-shards them),
   * decompression of a chr1-sized record stream (BASELINE configs[3]),
   * compression of a T2T-like divergent pair (configs[4] shape, literal-heavy),
-  * compression of a pair that stays in local mode (no switch).
+  * compression of a pair that stays in local mode (no switch),
+  * the chr1-sized pair through the parameter overrides (sccg_params, non-parity): the global walk
+    at BASELINE configs[1]'s k = 21 and at the reference's k = 14, without the local controller.
 
     python bench_configs.py [--scale 1.0] [--steps 3]
 Prints one JSON object per workload.
@@ -47,12 +49,14 @@ def main() -> None:
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / args.steps, r
 
-    work = [("chr1_decompress", "hg", 247_249_719, 249_250_621, 1),
-            ("t2t_like_compress", "t2t", 100_000_000, 100_000_000, 7),
-            ("local_mode_compress", "local", 247_249_719, 247_249_719, 8)]
+    work = [("chr1_decompress", "hg", 247_249_719, 249_250_621, 1, {}),
+            ("t2t_like_compress", "t2t", 100_000_000, 100_000_000, 7, {}),
+            ("local_mode_compress", "local", 247_249_719, 247_249_719, 8, {}),
+            ("chr1_k21_global_compress", "hg", 247_249_719, 249_250_621, 1, {"k": 21, "local": 0}),
+            ("chr1_k14_global_compress", "hg", 247_249_719, 249_250_621, 1, {"local": 0})]
     if not args.only or args.only in "genome":
         genome(ctx, dev, stream, args, to_dev)
-    for name, prof, rl, tl, seed in work:
+    for name, prof, rl, tl, seed, over in work:
         if args.only and args.only not in name:
             continue
         rl, tl = int(rl * args.scale), int(tl * args.scale)
@@ -60,7 +64,8 @@ def main() -> None:
         d_ref, d_tgt = to_dev(rfa), to_dev(tfa)
         cap = ctx.compress_bound(len(rfa), len(tfa))
         d_rec = torch.empty(cap, dtype=torch.uint8, device=dev)
-        n_rec = ctx.compress_device(d_ref.data_ptr(), len(rfa), d_tgt.data_ptr(), len(tfa), d_rec.data_ptr(), cap, stream)
+        n_rec = ctx.compress_device(d_ref.data_ptr(), len(rfa), d_tgt.data_ptr(), len(tfa), d_rec.data_ptr(), cap, stream,
+                                    **over)
         st = ctx.stats()
         if name.endswith("decompress"):
             need = ctx.reconstruct_device(d_ref.data_ptr(), len(rfa), d_rec.data_ptr(), n_rec, 0, 0, stream)
@@ -72,11 +77,15 @@ def main() -> None:
                    "bases_per_s": st["target_bases"] / dt, "roundtrip_exact": exact}
         else:
             dt, n = timed(lambda: ctx.compress_device(d_ref.data_ptr(), len(rfa), d_tgt.data_ptr(), len(tfa),
-                                                      d_rec.data_ptr(), cap, stream))
+                                                      d_rec.data_ptr(), cap, stream, **over))
             st = ctx.stats()
             out = {"workload": name, "target_bases": st["target_bases"], "record_bytes": n, "seconds": dt,
                    "bases_per_s": st["target_bases"] / dt, "mode": "global" if st["mode_global"] else "local",
                    "switch_segment": st["switch_segment"], "walk_rounds": st["walk_rounds"], "matches": st["n_matches"]}
+            if over:
+                out["params"] = over
+                rec = d_rec[:n].cpu().numpy().tobytes()
+                out["roundtrip_exact"] = ctx.reconstruct(rec, rfa) == tfa
         print(json.dumps(out), flush=True)
         del d_ref, d_tgt, d_rec
         torch.cuda.empty_cache()
