@@ -20,16 +20,24 @@ constexpr int WPB = SCCG_BLOCK / 64;             // wave tiles per block
 // First position >= from (from = *from_slot + 1, or 0) holding `c` (mode 1) or a '>' that starts a
 // line (mode 0).  Blocks take 16 KiB chunks in increasing order from a ticket and stop as soon as a
 // chunk starts past the best match: a header at the start of the file costs one wave of chunks,
-// not a pass over the whole FASTA.  *res must hold n on entry; *ticket 0.
+// not a pass over the whole FASTA.  Every thread loads its 64 bytes at once (a byte loop with an
+// early exit issues its loads one after another: ~50 us behind a busy HBM).  *res must hold n on
+// entry; *ticket 0.
 constexpr int64_t FM_CHUNK = 16384;
+template <int NW>
+__device__ __forceinline__ uint8_t wb(const uint32_t (&w)[NW], int i) { return (uint8_t)(w[i >> 2] >> (8 * (i & 3))); }
+template <int NW>
+__device__ __forceinline__ void load_words(const uint8_t* __restrict__ buf, int64_t n, int64_t off, uint32_t (&w)[NW]);
 __global__ __launch_bounds__(SCCG_BLOCK) void k_first_match(const uint8_t* __restrict__ buf, int64_t n,
                                                             const int64_t* __restrict__ from_slot, int mode, uint8_t c,
                                                             int64_t* __restrict__ res, unsigned int* __restrict__ ticket) {
     __shared__ int64_t s_cs;
     const int64_t from = from_slot ? *from_slot + 1 : 0;
+    const int64_t base = from & ~(int64_t)63;   // chunks start 64-byte aligned; bytes before `from` are skipped
+    constexpr int PER = FM_CHUNK / SCCG_BLOCK;   // 64 bytes per thread
     for (;;) {
         if (threadIdx.x == 0) {
-            const int64_t cs = from + (int64_t)atomicAdd(ticket, 1u) * FM_CHUNK;
+            const int64_t cs = base + (int64_t)atomicAdd(ticket, 1u) * FM_CHUNK;
             const int64_t best = (int64_t)__hip_atomic_load((unsigned long long*)res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_cs = (cs >= n || cs >= best) ? -1 : cs;
         }
@@ -37,17 +45,24 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_first_match(const uint8_t* __res
         const int64_t cs = s_cs;
         __syncthreads();
         if (cs < 0) return;
-        const int64_t p0 = cs + (int64_t)threadIdx.x * (FM_CHUNK / SCCG_BLOCK);
-        int64_t hit = INT64_MAX;
-        uint8_t prev = (p0 > 0 && p0 - 1 < n) ? buf[p0 - 1] : (uint8_t)'\n';
-        for (int i = 0; i < FM_CHUNK / SCCG_BLOCK && hit == INT64_MAX; i++) {
-            const int64_t p = p0 + i;
-            if (p >= n) break;
-            const uint8_t b = buf[p];
-            if (mode == 0 ? (b == '>' && (p == 0 || prev == '\n')) : (b == c)) hit = p;
-            prev = b;
+        const int64_t p0 = cs + (int64_t)threadIdx.x * PER;
+        // (no `continue` past the barriers above: lanes of one wave would then reach them in
+        // different iterations, and the block deadlocks)
+        if (p0 < n) {
+            uint32_t w[PER / 4];
+            load_words<PER / 4>(buf, n, p0, w);
+            uint8_t prev = p0 > 0 ? buf[p0 - 1] : (uint8_t)'\n';
+            int64_t hit = INT64_MAX;
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                const uint8_t b = wb(w, i);
+                const int64_t p = p0 + i;
+                const bool ok = p >= from && p < n && (mode == 0 ? (b == '>' && (p == 0 || prev == '\n')) : (b == c));
+                if (ok && hit == INT64_MAX) hit = p;
+                prev = b;
+            }
+            if (hit != INT64_MAX) atomicMin((unsigned long long*)res, (unsigned long long)hit);
         }
-        if (hit != INT64_MAX) atomicMin((unsigned long long*)res, (unsigned long long)hit);
     }
 }
 
@@ -64,9 +79,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_first_match(const uint8_t* __res
 // kept bytes into the wave's LDS copy of the tile's output at its wave-scan offset, then the wave
 // stores the tile's output range with aligned dword stores.
 // ---------------------------------------------------------------------------------------------
-template <int NW>
-__device__ __forceinline__ uint8_t wb(const uint32_t (&w)[NW], int i) { return (uint8_t)(w[i >> 2] >> (8 * (i & 3))); }
-
 template <int NW>
 __device__ __forceinline__ void load_words(const uint8_t* __restrict__ buf, int64_t n, int64_t off, uint32_t (&w)[NW]) {
     if (off + 4 * NW <= n && (((uintptr_t)(buf + off)) & 15) == 0) {

@@ -147,9 +147,11 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 void global_prepare_reset();   // forget a preparation that will not be used
 // As soon as R' exists (before |T'| is known, tn >= |T'|): the anchor samples and the positions of
 // the target's first k-mer, read from the target FASTA (d_hdr: its header range).  A later
-// global_prepare on the same ws/R' only extends those positions once T' exists.
-int global_sweep_early(const uint8_t* Rp, int64_t nRp, const uint8_t* tgt_fa, int64_t tn, const int64_t* d_hdr, int k,
-                       int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s);
+// global_prepare on the same ws/R' only extends those positions once T' exists.  |R'| is read on
+// the device from d_nRp (no host round trip); nRp_bound >= |R'| sizes the workspace and the anchor
+// table (ws must hold walk_workspace_bytes(nRp_bound, tn, ...)).
+int global_sweep_early(const uint8_t* Rp, int64_t nRp_bound, const int64_t* d_nRp, const uint8_t* tgt_fa, int64_t tn,
+                       const int64_t* d_hdr, int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s);
 // Where the record text goes, when the caller learns it only during the walk: resolve() is called
 // once, after the rounds and before the text is written, and returns the output pointer.
 struct EmitTarget {

@@ -394,15 +394,17 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     HIPTRY(hipStreamWaitEvent(s3, ctx->ev_tstrip, 0));
     uint8_t* nline = nullptr;
     int64_t rl_len[2] = {0, 0};
-    // the worker's first readback (header range, |T|, |T'|, the '(' flag) is this thread's too
-    int64_t h4[4] = {0, 0, 0, 0};
+    // the worker's first readback (header range, |T|, |T'|, the '(' flag, |R|, |R'|) is this
+    // thread's too
+    int64_t h4[4] = {0, 0, 0, 0}, lr[2] = {0, 0};
+    HIPTRY(hipStreamWaitEvent(s3, ctx->ev_rstrip, 0));
     int32_t flags = 0;
     std::promise<int> lens_read;
     std::future<int> lens = lens_read.get_future();
     ctx->worker.submit([&, s3]() -> int {
         {
-            const RbItem it[2] = {{sc, h4, (int)sizeof h4}, {d_flags, &flags, (int)sizeof flags}};
-            const int rc = dev_readback(it, 2, s3);
+            const RbItem it[3] = {{sc, h4, (int)sizeof h4}, {d_flags, &flags, (int)sizeof flags}, {sc + 7, lr, (int)sizeof lr}};
+            const int rc = dev_readback(it, 3, s3);
             lens_read.set_value(rc);
             if (rc) return ctx->hipfail(rc);
         }
@@ -431,16 +433,14 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     } lines{&ctx->worker};
     // The walk's R'-only preparation (anchor samples, positions of the target's first k-mer read off
     // its FASTA) starts on the side stream as soon as R' exists, beside the target's strip.
-    int64_t hr[2];   // |R|, |R'|
-    {
-        TRY(d2h_i64(ctx, sc + 7, hr, 2, ctx->side));
-        if (hr[1] < INT32_MAX - 8 && tn < INT32_MAX - 8) {
-            HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
-            const size_t wsb_early = walk_workspace_bytes(hr[1], tn, kg, walk_chunk(tn));   // |T'| <= tn
-            void* ws_early = ctx->get(B_WALK, wsb_early);
-            if (!ws_early) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb_early);
-            TRY(global_sweep_early(Rp, hr[1], tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb_early, ctx->side));
-        }
+    // The walk workspace is sized by the FASTA lengths (>= |R'|, |T'|), so the early sweep needs no
+    // host read of |R'| (it reads it on the device) and the walk reuses the same carve.
+    const size_t wsb = walk_workspace_bytes(rn, tn, kg, walk_chunk(tn));
+    if (rn < INT32_MAX - 8 && tn < INT32_MAX - 8) {
+        HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
+        void* ws_early = ctx->get(B_WALK, wsb);
+        if (!ws_early) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
+        TRY(global_sweep_early(Rp, rn, sc + 8, tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb, ctx->side));
     }
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
     // ---- fork.  The local pass (compression.cpp:372-474, main stream) is latency-bound; the
@@ -468,7 +468,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, s));
     }
     TRY(lens.get());
-    const int64_t hdr[2] = {h4[0], h4[1]}, lt[2] = {h4[2], h4[3]}, lr[2] = {hr[0], hr[1]};
+    const int64_t hdr[2] = {h4[0], h4[1]}, lt[2] = {h4[2], h4[3]};
     const int64_t nT = lt[0], nR = lr[0];
     if (nT >= INT32_MAX - 8 || nR >= INT32_MAX - 8)
         return ctx->fail(SCCG_E_UNSUPPORTED, "sequence longer than the reference's int positions allow");
@@ -488,7 +488,6 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
 
     // ---- the global walk's preparation, side stream (wasted only if the pass stays local)
     const int64_t np[2] = {lt[1], lr[1]};
-    const size_t wsb = walk_workspace_bytes(np[1], np[0], kg, walk_chunk(tn));
     void* ws = ctx->get(B_WALK, wsb);
     if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
     TRY(global_prepare(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, s2));

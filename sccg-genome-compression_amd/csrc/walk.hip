@@ -39,7 +39,8 @@ constexpr int KEY_K = 15;
 constexpr int KMAX = 32;              // largest k the walk takes
 constexpr int KB_COUNT = 32;          // kb: the first k bytes of T' at [0, k), their count at [32, 36)
 constexpr int ANCHOR_STEP_DEFAULT = 32;   // reference sample stride (SCCG_ANCHOR_STEP for tuning runs)
-constexpr int ANCHOR_LOAD_DEFAULT = 4;    // table slots per sample (SCCG_ANCHOR_LOAD)
+constexpr int ANCHOR_LOAD_DEFAULT = 1;    // table slots per sample, rounded up to a power of two (SCCG_ANCHOR_LOAD):
+                                          // a 64 MiB table for chr1 stays in the MALL (4 slots/sample: 256 MiB, sweep +40 %)
 #ifndef ANCHOR_PROBE_BATCHES
 #define ANCHOR_PROBE_BATCHES 2            // 64 target probes per batch per anchor vote (measured: 2 beats 4)
 #endif
@@ -128,6 +129,7 @@ struct WalkPtrs {
     uint32_t agen;            // anchor tag generation (one per call)
     int32_t round;            // walk round of the launch (kernel argument copy)
     int32_t abits;
+    const int64_t* dnR;       // early sweep: |R'| in device memory (nR is then only a bound)
     int32_t astep;            // anchor sample stride
     int32_t amulti;           // 1: second build pass marks repeated 32-mers
     unsigned long long* fc;   // full-candidate scan scalars: [0] lmax [1] cnt [2] has0 [3] minkey [4] firsthit [5] firstexo
@@ -1624,41 +1626,61 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
 // fc[12]: 1 = early statistics valid, 2 = not usable (too many positions, exotic key, or the FASTA
 // reading disagreed with T') -> the caller runs the full k_key0 sweep.  fc[13]: positions found.
 // ---------------------------------------------------------------------------------------------
-// one wave: the first k bytes of T' (strip + toupper + N erase of the target FASTA, the header line
-// [hdr[0], hdr[1]) excluded) within the first `limit` FASTA bytes -> kb[0, k), their count -> kb[KB_COUNT..]
-__global__ void k_first_kmer(const uint8_t* __restrict__ fa, int64_t n, const int64_t* __restrict__ hdr, int k,
-                             int64_t limit, uint8_t* __restrict__ kb) {
-    const int lane = lane_id();
+// The first k bytes of T' (strip + toupper + N erase of the target FASTA, the header line
+// [hdr[0], hdr[1]) excluded) within the first `limit` FASTA bytes -> kb[0, k), their count -> kb[KB_COUNT..].
+// One block, 16 KiB per step: every thread loads its 64 bytes at once (a chromosome starts with
+// ~10 kb of N, which a one-wave byte loop crossed in ~10 dependent steps behind the busy strips).
+__global__ __launch_bounds__(SCCG_BLOCK) void k_first_kmer(const uint8_t* __restrict__ fa, int64_t n,
+                                                           const int64_t* __restrict__ hdr, int k, int64_t limit,
+                                                           uint8_t* __restrict__ kb) {
+    __shared__ int64_t tmp[5];
+    constexpr int PER = 64;
     const int64_t h = hdr[0], he = hdr[1];
     const int64_t end = n < limit ? n : limit;
-    int found = 0;
-    for (int64_t base = 0; base < end && found < k; base += 64 * 16) {
-        uint32_t keep = 0;
-        uint8_t b[16];
+    int64_t found = 0;
+    for (int64_t base = 0; base < end && found < k; base += (int64_t)SCCG_BLOCK * PER) {
+        const int64_t p0 = base + (int64_t)threadIdx.x * PER;
+        uint32_t w[PER / 4];
+        if (p0 + PER + 4 <= end) {
+            loadw<PER / 4>(fa + p0, w);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int64_t p = base + 16 * lane + i;
-            b[i] = p < end ? fa[p] : (uint8_t)' ';
-            const bool kp = p < end && !(p >= h && p < he) && !c_isspace(b[i]) && c_toupper(b[i]) != 'N';
-            keep |= (uint32_t)kp << i;
+            for (int q = 0; q < PER / 4; q++) {
+                uint32_t v = 0;
+                for (int i = 0; i < 4; i++) {
+                    const int64_t p = p0 + 4 * q + i;
+                    v |= (uint32_t)(p < end ? fa[p] : (uint8_t)' ') << (8 * i);
+                }
+                w[q] = v;
+            }
         }
-        const int cnt = __popc(keep);
-        const int incl = wave_incl_add(cnt);
-        int idx = found + incl - cnt;
-        for (int i = 0; i < 16; i++)
-            if ((keep >> i) & 1u) { if (idx < k) kb[idx] = c_toupper(b[i]); idx++; }
-        found += __shfl(incl, 63, 64);
+        uint64_t keep = 0;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const uint8_t b = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+            const int64_t p = p0 + i;
+            const bool kp = p < end && !(p >= h && p < he) && !c_isspace(b) && c_toupper(b) != 'N';
+            keep |= (uint64_t)kp << i;
+        }
+        int64_t total = 0;
+        int64_t idx = found + block_excl_add((int64_t)__popcll(keep), tmp, &total);
+        for (uint64_t m = keep; m && idx < k; m &= m - 1, idx++) {
+            const int i = __ffsll((long long)m) - 1;
+            kb[idx] = c_toupper((uint8_t)(w[i >> 2] >> (8 * (i & 3))));
+        }
+        found += total;
     }
-    if (lane == 0) *reinterpret_cast<int32_t*>(kb + KB_COUNT) = found < k ? found : k;
+    if (threadIdx.x == 0) *reinterpret_cast<int32_t*>(kb + KB_COUNT) = found < k ? (int32_t)found : k;
 }
 
 template <bool ANCH>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
     const int k = A.k, kp = A.kp;
+    const int64_t nR = A.dnR ? *A.dnR : A.nR;   // |R'| (A.nR only bounds it)
     const bool have = *reinterpret_cast<const int32_t*>(A.kb + KB_COUNT) == k;
     const uint32_t key0 = have ? walk_key(A.kb, kp) : KEY_EXOTIC;
     const bool want = key0 < KEY_EXOTIC;
-    sweep_kmers_w(A.R, (int64_t)A.nR - k + 1, kp, [&](uint32_t code, bool pure) { return want && pure && code == key0; },
+    sweep_kmers_w(A.R, nR - k + 1, kp, [&](uint32_t code, bool pure) { return want && pure && code == key0; },
                   [&](int64_t c) {
                       if (k > kp && !bytes_eq(A.R + c + kp, A.kb + kp, k - kp)) return;
                       const unsigned long long i = atomicAdd(&A.fc[13], 1ull);
@@ -1669,7 +1691,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
 #pragma unroll
                       for (int h = 0; h < 2; h++) {
                           const int64_t p = p0 + 32 * h;
-                          if (p + ANCHOR_K > A.nR) break;
+                          if (p + ANCHOR_K > nR) break;
                           uint64_t code = 0;
                           uint32_t bad = 0;
 #pragma unroll
@@ -2031,14 +2053,17 @@ int anchor_step() {
 }
 int anchor_bits(int64_t nR) {
     static const int load = [] { const int x = env_int("SCCG_ANCHOR_LOAD", ANCHOR_LOAD_DEFAULT); return x >= 1 && x <= 16 ? x : ANCHOR_LOAD_DEFAULT; }();
-    int64_t want = load * (nR / anchor_step() + 1);   // load <= 1/4: few samples lose their slot
+    // SCCG_ANCHOR_SHIFT (tuning runs): the table's size in powers of two away from `load` slots per sample
+    static const int shift = [] { const int x = env_int("SCCG_ANCHOR_SHIFT", 0); return x >= -4 && x <= 4 ? x : 0; }();
+    int64_t want = load * (nR / anchor_step() + 1);
     int b = 10;
     while ((1ll << b) < want && b < 34) b++;
-    return b;
+    b += shift;
+    return b < 10 ? 10 : b;
 }
 
 WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int k, int m,
-               int S, size_t* used) {
+               int S, size_t* used, int abits = 0) {
     WalkPtrs A{};
     Carve c{(char*)ws, 0, ws_bytes};
     A.R = R; A.T = T;
@@ -2049,7 +2074,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.cap = S / k + 4;
     const size_t C = (size_t)A.C, cap = (size_t)A.cap;
     // front: what depends on R' alone (the early sweep fills it before |T'| is known)
-    A.abits = anchor_bits(nR);
+    A.abits = abits ? abits : anchor_bits(nR);   // (an early sweep sized it from a bound of |R'|)
     A.astep = anchor_step();
     {
         static const int multi = env_int("SCCG_ANCHOR_MULTI", 0);
@@ -2270,15 +2295,17 @@ struct Prepared {
     int64_t nR = -1, nT = -1;
     int k = 0, m = 0, chunk = 0;
     uint32_t agen = 0;
+    int abits = 0;
 };
 thread_local Prepared g_prep;
 
 struct Early {   // an early sweep queued by global_sweep_early
     const void* ws = nullptr;
     const uint8_t* R = nullptr;
-    int64_t nR = -1;
+    int64_t nR = -1;   // the bound of |R'| it was sized for
     int k = 0;
     uint32_t agen = 0;
+    int abits = 0;
 };
 thread_local Early g_early;
 
@@ -2327,8 +2354,8 @@ int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
 }
 
 WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
-                   size_t ws_bytes, size_t* used) {
-    WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, used);
+                   size_t ws_bytes, size_t* used, int abits = 0) {
+    WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, used, abits);
     if (!getenv("SCCG_DEBUG")) A.dbg = nullptr;   // per-chunk counters only in diagnostic runs
     A.dbg_phases = getenv("SCCG_DEBUG_PHASES") != nullptr;
     static const int32_t sb = [] {
@@ -2343,18 +2370,20 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 
 void global_prepare_reset() { g_prep = Prepared{}; g_early = Early{}; }
 
-int global_sweep_early(const uint8_t* Rp, int64_t nRp, const uint8_t* tgt_fa, int64_t tn, const int64_t* d_hdr, int k,
-                       int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s) {
+int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, const uint8_t* tgt_fa, int64_t tn,
+                       const int64_t* d_hdr, int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s) {
     g_early = Early{};
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
     if (nRp < k || tn <= 0) return 0;   // no walk can use it
     size_t used = 0;
-    // |T'| <= tn: the carve's R'-only front (anchor table, fc, positions, kb) does not depend on it
+    // |T'| <= tn: the carve's R'-only front (anchor table, fc, positions, kb) does not depend on it;
+    // nRp bounds |R'|, which the sweep reads from d_nRp
     WalkPtrs A = make_ptrs(Rp, nRp, nullptr, tn, k, m, chunk, ws, ws_bytes, &used);
     if (used > ws_bytes) return SCCG_E_INTERNAL;
+    A.dnR = d_nRp;
     RC(anchor_generation(A, ws, s));
     RC(set_u64(A.fc + 12, {0, 0}, s));
-    hipLaunchKernelGGL(k_first_kmer, dim3(1), dim3(64), 0, s, tgt_fa, tn, d_hdr, k, (int64_t)1 << 20, A.kb);
+    hipLaunchKernelGGL(k_first_kmer, dim3(1), dim3(SCCG_BLOCK), 0, s, tgt_fa, tn, d_hdr, k, (int64_t)1 << 20, A.kb);
     const unsigned g = first_sweep_grid(A);
     if (A.astep == 32) {
         PROF_LAUNCH(PROF_ANCHOR, s, k_sweep_early<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
@@ -2365,7 +2394,7 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const uint8_t* tgt_fa, in
         PROF_LAUNCH(PROF_ANCHOR, s, k_anchor_build<false>, dim3(ga), dim3(256), 0, s, A);
     }
     SCCG_HIP(hipGetLastError());
-    g_early = Early{ws, Rp, nRp, k, A.agen};
+    g_early = Early{ws, Rp, nRp, k, A.agen, A.abits};
     return 0;
 }
 
@@ -2373,12 +2402,13 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
                    size_t ws_bytes, hipStream_t s) {
     g_prep = Prepared{};
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
-    size_t used = 0;
-    WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
-    if (used > ws_bytes) return SCCG_E_INTERNAL;
     const Early e = g_early;
     g_early = Early{};
-    if (e.ws == ws && e.R == Rp && e.nR == nRp && e.k == k) {
+    const bool early = e.ws == ws && e.R == Rp && e.nR >= nRp && e.k == k;
+    size_t used = 0;
+    WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used, early ? e.abits : 0);
+    if (used > ws_bytes) return SCCG_E_INTERNAL;
+    if (early) {
         // the early sweep already stored the anchors and the first k-mer's positions
         A.agen = e.agen;
         if (A.nR >= A.k && A.nT >= A.k) {
@@ -2394,7 +2424,7 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
     } else {
         RC(queue_prepare(A, ws, s));
     }
-    g_prep = Prepared{ws, Rp, Tp, nRp, nTp, k, m, chunk, A.agen};
+    g_prep = Prepared{ws, Rp, Tp, nRp, nTp, k, m, chunk, A.agen, A.abits};
     return 0;
 }
 
@@ -2402,8 +2432,12 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                           void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
                           bool abs_p, const EmitTarget* late_out, bool keep_flat) {
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
+    const Prepared g = g_prep;   // queued by global_prepare (the caller ordered s after it)
+    g_prep = Prepared{};
+    const bool prepared = g.ws == ws && g.R == Rp && g.T == Tp && g.nR == nRp && g.nT == nTp && g.k == k && g.m == m &&
+                          g.chunk == chunk;
     size_t used = 0;
-    WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used);
+    WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used, prepared ? g.abits : 0);
     if (used > ws_bytes) return SCCG_E_INTERNAL;
     res->rounds = 0;
     res->chains = 0;
@@ -2425,14 +2459,8 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     const bool walkable = nRp >= k && lastk >= 0;
     const unsigned gsweep = grid_for(nRp - k + 1 > 0 ? nRp - k + 1 : 1, 256 * FC_PER_T) > PRESENCE_GRID
                                 ? PRESENCE_GRID : grid_for(nRp - k + 1 > 0 ? nRp - k + 1 : 1, 256 * FC_PER_T);
-    {
-        const Prepared& g = g_prep;
-        const bool prepared = g.ws == ws && g.R == Rp && g.T == Tp && g.nR == nRp && g.nT == nTp && g.k == k &&
-                              g.m == m && g.chunk == chunk;
-        if (prepared) A.agen = g.agen;   // queued by global_prepare (the caller ordered s after it)
-        else RC(queue_prepare(A, ws, s));
-        g_prep = Prepared{};
-    }
+    if (prepared) A.agen = g.agen;
+    else RC(queue_prepare(A, ws, s));
 
     // ---- round 1 is queued before the host knows the first step: k_walk_init<true> resolves the
     //      usual start on the device, and the round's status comes back with the first-step
