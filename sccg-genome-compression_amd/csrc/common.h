@@ -95,12 +95,14 @@ __device__ __forceinline__ void pack_codes(const uint32_t (&w)[ND], uint64_t& co
         for (int i = 0; i < ND; i++) bad |= nz_bytes(d[i]) << (4 * i);
     }
 }
-// ND words from an arbitrary (global or LDS) address: ND+1 aligned dword loads
+// ND words from an arbitrary (global or LDS) address: ND+1 aligned dword loads.  The aligned base
+// is formed by pointer arithmetic on p (not through an integer): the compiler then keeps p's address
+// space and emits global loads; a pointer rebuilt from an integer is generic, and FLAT loads also
+// count against lgkmcnt, so every later LDS wait would wait for the HBM load too.
 template <int ND>
 __device__ __forceinline__ void loadw(const uint8_t* p, uint32_t (&o)[ND]) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p - sh);
     uint32_t v[ND + 1];
 #pragma unroll
     for (int i = 0; i <= ND; i++) v[i] = w[i];

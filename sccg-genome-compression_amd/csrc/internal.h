@@ -160,6 +160,9 @@ struct EmitTarget {
     // optional, polled after every walk round: nonzero = the walk's result is not wanted (the
     // caller's local pass found no switch), so global_match_and_emit stops with WALK_ABANDONED
     int (*abandon)(void* user) = nullptr;
+    // optional, called once right after round 1 is queued on the walk's stream (the caller may
+    // order other work behind it)
+    int (*round1_queued)(void* user, hipStream_t s) = nullptr;
 };
 // global_match_and_emit's return when EmitTarget::resolve/abandon gave up on the walk (not an error)
 constexpr int WALK_ABANDONED = -1;

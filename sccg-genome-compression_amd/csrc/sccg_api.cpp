@@ -128,7 +128,7 @@ struct sccg_ctx {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;       // walk preparation, overlapping the local pass
     hipStream_t side2 = nullptr;      // header + run lines, overlapping the local pass
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr, ev_tstrip = nullptr,
+    hipEvent_t ev_fork = nullptr, ev_fork2 = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr, ev_tstrip = nullptr,
                ev_local = nullptr;
     int64_t* h_switch = nullptr;      // pinned: the local pass's switch word, copied behind the pass
     std::string err;
@@ -192,10 +192,16 @@ int sccg_ctx_create(int device, sccg_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return SCCG_E_HIP;
     sccg_ctx* c = new sccg_ctx();
     c->device = device;
+    // the side stream carries the global walk's critical path (R' sweep -> walk rounds -> text):
+    // SCCG_SIDE_PRIORITY=1 (tuning runs) gives it the device's highest stream priority
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    static const bool side_prio = [] { const char* e = getenv("SCCG_SIDE_PRIORITY"); return e && atoi(e) > 0; }();
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, side_prio ? prio_hi : prio_lo) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_lines, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_tstrip, hipEventDisableTiming) != hipSuccess ||
@@ -221,6 +227,7 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     for (int i = 0; i < B_COUNT; i++)
         if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
     (void)hipEventDestroy(ctx->ev_fork);
+    (void)hipEventDestroy(ctx->ev_fork2);
     (void)hipEventDestroy(ctx->ev_join);
     (void)hipEventDestroy(ctx->ev_lines);
     (void)hipEventDestroy(ctx->ev_tstrip);
@@ -455,7 +462,20 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     GET(SegStat, stat, B_STAT, iters_max > 0 ? iters_max : 1);
     GET(int32_t, cls, B_SEGCLS, iters_max > 0 ? iters_max : 1);
     int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
-    if (iters_max > 0 && !force_global) {
+    // Where the local pass goes.  It fills every CU while it runs (LDS and VGPRs), but only the final
+    // record text needs it; the global walk (side stream) is the critical path of a switching pair.
+    //   0: right after both strips (beside the R' sweep);  1: behind the walk's preparation (the
+    //   first-step statistics);  2: behind walk round 1 (SCCG_LOCAL_ORDER, tuning runs)
+    static const int local_order = [] { const char* e = getenv("SCCG_LOCAL_ORDER"); const int v = e ? atoi(e) : 0; return v >= 0 && v <= 2 ? v : 0; }();
+    bool local_launched = false;
+    auto launch_local = [&](hipStream_t after) -> int {
+        if (local_launched) return 0;
+        local_launched = true;
+        if (after) {
+            HIPTRY(hipEventRecord(ctx->ev_fork2, after));
+            HIPTRY(hipStreamWaitEvent(s, ctx->ev_fork2, 0));
+        }
+        if (iters_max > 0 && !force_global) {
         if (cls != ctx->cls_buf || ctx->cap[B_SEGCLS] != ctx->cls_cap || ctx->cls_gen >= (1 << 28)) {
             // new buffer (or tags about to wrap): zero it once, so no stale tag can match
             HIPTRY(hipMemsetAsync(cls, 0, ctx->cap[B_SEGCLS], s));
@@ -466,7 +486,10 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         const int32_t gen = ++ctx->cls_gen;
         // one launch over every segment; segments past a detected switch are never started
         TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, s));
-    }
+        }
+        return 0;
+    };
+    if (local_order == 0) TRY(launch_local(nullptr));
     TRY(lens.get());
     const int64_t hdr[2] = {h4[0], h4[1]}, lt[2] = {h4[2], h4[3]};
     const int64_t nT = lt[0], nR = lr[0];
@@ -492,6 +515,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
     TRY(global_prepare(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, s2));
     HIPTRY(hipEventRecord(ctx->ev_join, s2));
+    if (local_order == 1 || iters <= 0 || force_global) TRY(launch_local(s2));
 
     int64_t pos = 0;
     auto join_lines = [&](hipStream_t on) -> int {   // the lowercase line's end, `on` ordered after it
@@ -511,8 +535,17 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         sw_known = true;
         return 0;
     };
-    if (iters > 0 && !force_global) HIPTRY(hipMemcpyAsync(ctx->h_switch, sc + 21, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HIPTRY(hipEventRecord(ctx->ev_local, s));
+    auto local_tail = [&]() -> int {   // the switch word behind the local pass, and its event
+        if (iters > 0 && !force_global) HIPTRY(hipMemcpyAsync(ctx->h_switch, sc + 21, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPTRY(hipEventRecord(ctx->ev_local, s));
+        return 0;
+    };
+    if (local_launched) TRY(local_tail());
+    auto ensure_local = [&](hipStream_t after) -> int {   // (order 2 when the walk never queued round 1)
+        if (local_launched) return 0;
+        TRY(launch_local(after));
+        return local_tail();
+    };
 
     // ---- global (compression.cpp:484-574), speculatively: the walk runs on the side stream right
     //      behind its preparation, beside the local pass, and is abandoned if the pass finds no
@@ -527,7 +560,10 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
             std::function<int()> poll;
             static int call(void* u, uint8_t** o) { return static_cast<Late*>(u)->f(o); }
             static int abandon(void* u) { return static_cast<Late*>(u)->poll(); }
+            std::function<int(hipStream_t)> r1;
+            static int round1(void* u, hipStream_t st) { return static_cast<Late*>(u)->r1(st); }
         } late{[&](uint8_t** o) -> int {
+                   TRY(ensure_local(s2));
                    TRY(read_switch());
                    if (sw < 0 && !force_global) return WALK_ABANDONED;
                    TRY(join_lines(s2));
@@ -543,12 +579,13 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
                    return 0;
                },
                [&]() -> int {
-                   if (force_global) return 0;
+                   if (force_global || !local_launched) return 0;
                    if (!sw_known && hipEventQuery(ctx->ev_local) != hipSuccess) return 0;   // pass still running
                    if (read_switch()) return 0;   // the resolve step reports the error
                    return sw < 0;
-               }};
-        const EmitTarget target{&Late::call, &late, &Late::abandon};
+               },
+               [&](hipStream_t st) -> int { return local_order == 2 ? ensure_local(st) : 0; }};
+        const EmitTarget target{&Late::call, &late, &Late::abandon, &Late::round1};
         const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
                                              s2, paren, &target, /*keep_flat=*/false);
         if (rc != WALK_ABANDONED) {
@@ -557,6 +594,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
             global_done = true;
         }
     }
+    TRY(ensure_local(s2));
     HIPTRY(hipEventRecord(ctx->ev_join, s2));   // all side work (preparation, walk) before anything reuses it
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_join, 0));
     TRY(read_switch());

@@ -212,6 +212,20 @@ __device__ __forceinline__ void loadw_lds(const uint8_t* lds, int32_t off, uint3
     for (int i = 0; i < ND; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
 }
 
+// ND words at byte offset lds_off of an LDS copy (in_lds) or at g in global memory.  The empty asm
+// after the global load keeps the compiler from merging the two loads into one FLAT load through a
+// selected pointer (FLAT loads count against lgkmcnt: every later LDS wait would wait for HBM).
+template <int ND>
+__device__ __forceinline__ void loadw_sel(bool in_lds, const uint8_t* lds, int32_t lds_off, const uint8_t* g,
+                                          uint32_t (&o)[ND]) {
+    if (in_lds) {
+        loadw_lds<ND>(lds, lds_off, o);
+    } else {
+        loadw<ND>(g, o);
+        asm volatile("" ::: "memory");
+    }
+}
+
 // first differing byte of two 32-byte stretches (32: none)
 __device__ __forceinline__ int first_diff32(const uint32_t (&r)[8], const uint32_t (&t)[8]) {
     int pos = 32;
@@ -347,8 +361,7 @@ __device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin&
     const int i0 = 4 * lane;
     if (i0 >= W.n) return;
     uint32_t w[5];   // 20 bytes >= 3 + k
-    if (lds) loadw_lds<5>(L->rbuf, W.lo - B->rb0 + i0, w);
-    else loadw<5>(A.R + W.lo + i0, w);
+    loadw_sel<5>(lds, lds ? L->rbuf : nullptr, lds ? W.lo - B->rb0 + i0 : 0, A.R + W.lo + i0, w);
     uint64_t code;
     uint32_t bad;
     pack_codes<5>(w, code, bad);
@@ -571,8 +584,8 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         const int32_t y_l = x + lane;
         const bool valid = y_l < scan_end;
         uint32_t tw[4];
-        if (B.has_t(x, 64 + 16)) loadw_lds<4>(L.tbuf, y_l - B.tb0, tw);
-        else loadw<4>(A.T + y_l, tw);   // 4 KiB readable slack after T: no bound needed for the load
+        // (4 KiB readable slack after T: no bound needed for the global load)
+        loadw_sel<4>(B.has_t(x, 64 + 16), L.tbuf, y_l - B.tb0, A.T + y_l, tw);
         if (W.P != P) { reg_window(A, P, W, &L, &B); if (DBG) dbg_c[3]++; }
         if (DBG) tick(6);
         if (W.n <= 0) { x = scan_end; break; }
@@ -2493,6 +2506,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                            A, 0, 0);
         A.round = 1;
         RC(queue_round(FROZEN_FIRST, false));
+        if (late_out && late_out->round1_queued) RC(late_out->round1_queued(late_out->user, s));
         A.round = 2;
         RC(queue_round(FROZEN_FIRST, true));
         pre_round = true;
