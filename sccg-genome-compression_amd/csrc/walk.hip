@@ -909,22 +909,41 @@ __global__ __launch_bounds__(1024) void k_round_tail(WalkPtrs A, int fbase, int 
     if (threadIdx.x == 0) { A.scal[0] = 0; ntrig = 0; }
     __syncthreads();
     const int32_t next = A.round + 1;
-    for (int32_t j = (int32_t)threadIdx.x; j < A.C; j += (int32_t)blockDim.x) {
-        const int32_t ex = j ? A.exitX[j - 1] : A.scal[2];
-        const int32_t ep = j ? A.exitP[j - 1] : A.scal[3];
-        const bool pend = ex != INVALID && !(ex == A.usedX[j] && ep == A.usedP[j]);
-        if (!pend) {
-            if (A.lround[j] == next) A.lround[j] = A.round;   // listed by an earlier batch of this round
-            continue;
+    // RT_U chunks per thread and step, their state loaded together (one memory round trip per step
+    // instead of one per chunk: the loop is latency-bound)
+    constexpr int RT_U = 8;
+    const int32_t nthr = (int32_t)blockDim.x;
+    for (int32_t jb = (int32_t)threadIdx.x; jb < A.C; jb += nthr * RT_U) {
+        int32_t ex[RT_U], ep[RT_U], ux[RT_U], up[RT_U], lr[RT_U];
+#pragma unroll
+        for (int u = 0; u < RT_U; u++) {
+            const int32_t j = jb + u * nthr;
+            if (j < A.C) {
+                ex[u] = j ? A.exitX[j - 1] : A.scal[2];
+                ep[u] = j ? A.exitP[j - 1] : A.scal[3];
+                ux[u] = A.usedX[j];
+                up[u] = A.usedP[j];
+                lr[u] = A.lround[j];
+            }
         }
-        A.snapX[j] = ex;
-        A.snapP[j] = ep;
-        A.kind[j] = KIND_FIX;
-        A.lround[j] = next;
-        A.plist[atomicAdd(&A.scal[0], 1)] = j;
-        if (j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round) {
-            const int t = atomicAdd(&ntrig, 1);
-            if (t < RESPEC_MAX_TRIGGERS) trig[t] = j;
+#pragma unroll
+        for (int u = 0; u < RT_U; u++) {
+            const int32_t j = jb + u * nthr;
+            if (j >= A.C) break;
+            const bool pend = ex[u] != INVALID && !(ex[u] == ux[u] && ep[u] == up[u]);
+            if (!pend) {
+                if (lr[u] == next) A.lround[j] = A.round;   // listed by an earlier batch of this round
+                continue;
+            }
+            A.snapX[j] = ex[u];
+            A.snapP[j] = ep[u];
+            A.kind[j] = KIND_FIX;
+            A.lround[j] = next;
+            A.plist[atomicAdd(&A.scal[0], 1)] = j;
+            if (j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round) {
+                const int t = atomicAdd(&ntrig, 1);
+                if (t < RESPEC_MAX_TRIGGERS) trig[t] = j;
+            }
         }
     }
     __syncthreads();
@@ -1935,6 +1954,53 @@ __global__ void k_chunk_meta(WalkPtrs A) {
     }
 }
 
+// k_chunk_meta + both exclusive scans (+ the long-gap counter reset) in one 1024-thread block, for
+// up to CP_MAX chunks: cprev[j] = last chunk before j holding a match (-1: none), flat_off[j] =
+// matches of the chunks before j, scal64[0] = all of them, scal64[2] = 0 (three launches fewer at
+// the end of every round that queues the record text)
+constexpr int CP_PER = 16, CP_MAX = 1024 * CP_PER;
+__global__ __launch_bounds__(1024) void k_chunk_prefix(WalkPtrs A) {
+    __shared__ int64_t wsum[16], wmax[16];
+    if (A.scal[9]) return;
+    const int tid = (int)threadIdx.x, lane = lane_id(), w = wave_in_block();
+    const int32_t per = (A.C + 1023) / 1024, base = tid * per;
+    int64_t n[CP_PER];
+    int64_t s = 0, mx = -1;
+#pragma unroll
+    for (int i = 0; i < CP_PER; i++) {
+        const int32_t j = base + i;
+        n[i] = (i < per && j < A.C) ? A.cnt[A.cur[j]][j] : 0;
+        s += n[i];
+        if (n[i] > 0) mx = j;
+    }
+    // inclusive wave scans, then across the 16 waves
+    int64_t is = s, im = mx;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t os = __shfl_up(is, d, 64), om = __shfl_up(im, d, 64);
+        if (lane >= d) { is += os; im = om > im ? om : im; }
+    }
+    if (lane == 63) { wsum[w] = is; wmax[w] = im; }
+    __syncthreads();
+    int64_t cs = 0, cm = -1;
+    for (int i = 0; i < w; i++) { cs += wsum[i]; cm = wmax[i] > cm ? wmax[i] : cm; }
+    int64_t es = cs + is - s;                                       // exclusive sum before this thread
+    int64_t em = __shfl_up(im, 1, 64);                              // exclusive max before this thread
+    if (lane == 0) em = -1;
+    em = cm > em ? cm : em;
+#pragma unroll
+    for (int i = 0; i < CP_PER; i++) {
+        const int32_t j = base + i;
+        if (i < per && j < A.C) {
+            A.flat_off[j] = es;
+            A.cprev[j] = em;
+            es += n[i];
+            if (n[i] > 0) em = j;
+        }
+    }
+    if (tid == 1023) { A.scal64[0] = es; A.scal64[2] = 0; }
+}
+
 __device__ __forceinline__ int64_t token_len(int32_t d, int32_t l) { return 3 + ndigits_i32(d) + ndigits_i32(l); }
 __device__ __forceinline__ int write_token(uint8_t* o, int32_t d, int32_t l) {
     uint8_t* q = o;
@@ -2524,11 +2590,15 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     // (dev_first: the first match is the device's resolution of the usual first step, see k_chunk_text)
     auto queue_text = [&](bool long_copy, bool dev_first) -> int {
         const int32_t nf = dev_first ? 2 : first_y != INVALID ? 1 : 0;
-        const unsigned gc = grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256);
-        hipLaunchKernelGGL(k_chunk_meta, dim3(gc), dim3(256), 0, s, A);
-        RC(dev_excl_max(A.cprev, A.cprev, A.C, nullptr, A.partial, s));
-        RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
-        RC(set_u64(reinterpret_cast<unsigned long long*>(A.scal64 + 2), {0}, s));
+        if (A.C <= CP_MAX) {
+            hipLaunchKernelGGL(k_chunk_prefix, dim3(1), dim3(1024), 0, s, A);
+        } else {
+            const unsigned gc = grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256);
+            hipLaunchKernelGGL(k_chunk_meta, dim3(gc), dim3(256), 0, s, A);
+            RC(dev_excl_max(A.cprev, A.cprev, A.C, nullptr, A.partial, s));
+            RC(dev_excl_sum(A.flat_off, A.flat_off, A.C, A.scal64, A.partial, s));
+            RC(set_u64(reinterpret_cast<unsigned long long*>(A.scal64 + 2), {0}, s));
+        }
         const FirstMatch F{first_y, first_p, first_l, nf};
         hipLaunchKernelGGL(k_chunk_text<false>, dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, F, (int)abs_p, out);
         RC(dev_excl_sum(A.ctext, A.ctext, A.C, A.scal64 + 1, A.partial, s));
