@@ -85,6 +85,11 @@ constexpr int CH_MAX_GENS = 4096;      // generations per chain
 constexpr int64_t CH_DENSE_HITS = 32768;  // band hits of one generation that switch the chain to find-first generations
 constexpr int CH_DENSE_N = 32;         // hand back to the chunk rounds when CH_DENSE_N matches
 constexpr int32_t CH_DENSE_SPAN = 8192;   // fall within this many target bases (the walk is aligned again)
+// A chain is for frozen stretches (a chance hit every ~100 kb: T2T-like targets).  One that keeps
+// finding matches is a trapped walk (chance hits in a low-complexity window nudging P every few kb,
+// e.g. the synthetic chr22 from 45.8 Mb): one wave then walks them serially (~4 us each), which the
+// rounds' trapped re-speculation resolves faster, so the chain hands back after this many matches.
+constexpr int CH_HANDBACK_N = 64;
 
 struct WalkPtrs {
     const uint8_t* R;
@@ -1230,7 +1235,8 @@ __global__ __launch_bounds__(64) void k_chain_step(WalkPtrs A) {
                 if (bcnt >= 2 && bhas0) pk = bkey;
                 else { const uint64_t k0 = bhas0 ? pick_key(0, P) : ~0ull; pk = k0 < bkey ? k0 : bkey; }
                 const int32_t p = (int32_t)(uint32_t)pk;
-                if (p == 0 || nm >= A.chm_cap) { reason = 2; break; }   // pn2 == 0 or list full: the rounds take over at (x, P)
+                // pn2 == 0, list full or a trapped (match-rich) chain: the rounds take over at (x, P)
+                if (p == 0 || nm >= A.chm_cap || nm >= CH_HANDBACK_N) { reason = 2; break; }
                 if (lane == 0) { A.chm_t[nm] = y; A.chm_p[nm] = p; A.chm_l[nm] = bl; }
                 const int slot = nm % CH_DENSE_N;
                 const int32_t old = lane_val(rt, slot);
@@ -2262,8 +2268,9 @@ int h2d_sync(void* dst, const void* src, size_t bytes, hipStream_t s) {
 
 // The frozen chain from the earliest frozen chunk committed in this round (k_chain_*): generations
 // are queued CH_GENS_PER_SYNC at a time (a finished chain turns the rest into no-ops), then the
-// covered chunks are filled.  *gens: generations run.
-int run_chain(WalkPtrs& A, hipStream_t s, int* gens) {
+// covered chunks are filled.  *gens: generations run; *trapped: it handed back as a trapped
+// (match-rich) chain.
+int run_chain(WalkPtrs& A, hipStream_t s, int* gens, bool* trapped) {
     hipLaunchKernelGGL(k_chain_init, dim3(1), dim3(64), 0, s, A);
     SCCG_HIP(hipGetLastError());
     int32_t st[2] = {0, 0};
@@ -2288,6 +2295,7 @@ int run_chain(WalkPtrs& A, hipStream_t s, int* gens) {
         if (rc) return rc;
     }
     *gens = cs[8];
+    *trapped = cs[5] == 2 && cs[3] >= CH_HANDBACK_N;
     if (getenv("SCCG_DEBUG"))
         fprintf(stderr, "[chain] from chunk %d (x %d, P %d): %d generations, %d matches, end x %d P %d, reason %d\n", cs[4], cs[9],
                 cs[10], cs[8], cs[3], cs[1], cs[2], cs[5]);
@@ -2706,7 +2714,8 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         mark("anchors");
         int32_t nlist = A.C;
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
-        static const bool chains_on = getenv("SCCG_NO_CHAINS") == nullptr;   // (A/B and tests)
+        static const bool chains_env = getenv("SCCG_NO_CHAINS") == nullptr;   // (A/B and tests)
+        bool chains_on = chains_env;   // off for the rest of the call after a trapped chain
         // with the device first step, rounds 1 and 2 went out before the first readback
         const int64_t round0 = pre_round ? 2 : 1;
         for (int64_t round = round0;; round++) {
@@ -2741,14 +2750,20 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 RC(dev_readback(&rs_item, 1, s));
             }
             // A chain pays where rounds would resolve a frozen stretch hit by hit: a frozen chunk in
-            // round 1 (only chunk 0 is exact there, so the true walk froze at once), more frozen chunks
-            // than the blind batch covers, or frozen chunks still turning up from round 3 on.  A few
-            // frozen chunks in round 2 (N gaps of aligned pairs) stay with the blind batch.
-            const bool chain_now = chains_on && rs[5] > 0 && (round == 1 || round >= 3 || rs[5] > FROZEN_FIRST);
+            // round 1 (only chunk 0 is exact there, so the true walk froze at once), or frozen chunks
+            // still turning up from round SCCG_CHAIN_ROUND (default 10) on.  Earlier frozen chunks (N
+            // gaps of aligned pairs, short frozen stretches) stay with the blind batches.  Measured
+            // (start round 3 / 6 / 10): synthetic chr22 2.3 / 1.7 / 1.7 ms, 20 Mb T2T-like pair 5.5 /
+            // 5.7 / 5.7 ms, 100 Mb T2T-like pair 14.0 / 14.4-17.6 / 12.4 ms (23 ms without chains).
+            static const int chain_round = [] { const char* e = getenv("SCCG_CHAIN_ROUND"); const int v = e ? atoi(e) : 10; return v >= 2 ? v : 10; }();
+            const bool chain_now = chains_on && rs[5] > 0 && (round == 1 || round >= chain_round);
             if (chain_now) {
                 // a frozen chain: walk it on over the rest of the target, then the pending list again
                 int gens = 0;
-                RC(run_chain(A, s, &gens));
+                bool trapped = false;
+                RC(run_chain(A, s, &gens, &trapped));
+                static const bool keep_chains = getenv("SCCG_KEEP_CHAINS") != nullptr;   // (A/B)
+                if (trapped && !keep_chains) chains_on = false;   // a trapped walk: the rounds' re-speculation resolves it
                 RC(frozen_batch(0, 0, false));
                 RC(dev_readback(&rs_item, 1, s));
                 spec_text = false;   // the chain rewrote chunks after the round's text was queued

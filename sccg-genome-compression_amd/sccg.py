@@ -76,9 +76,10 @@ def load_library():
     lib.sccg_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
     lib.sccg_compress.argtypes = [vp, c, sz, c, sz, ctypes.POINTER(Buf)]
     lib.sccg_compress_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
-    lib.sccg_params_default.argtypes = [ctypes.POINTER(Params)]
-    lib.sccg_compress_ex.argtypes = [vp, ctypes.POINTER(Params), c, sz, c, sz, ctypes.POINTER(Buf)]
-    lib.sccg_compress_device_ex.argtypes = [vp, ctypes.POINTER(Params), vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
+    if hasattr(lib, "sccg_params_default"):   # (absent from builds older than the overrides: A/B runs)
+        lib.sccg_params_default.argtypes = [ctypes.POINTER(Params)]
+        lib.sccg_compress_ex.argtypes = [vp, ctypes.POINTER(Params), c, sz, c, sz, ctypes.POINTER(Buf)]
+        lib.sccg_compress_device_ex.argtypes = [vp, ctypes.POINTER(Params), vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
     lib.sccg_compress_bound.argtypes = [sz, sz]
     lib.sccg_compress_bound.restype = sz
     lib.sccg_match.argtypes = [vp, c, sz, c, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64,
