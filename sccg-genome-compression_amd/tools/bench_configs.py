@@ -28,6 +28,8 @@ def main() -> None:
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--only", default="")
+    ap.add_argument("--contexts", type=int, default=1,
+                    help="genome: contexts (host threads) per GPU compressing chromosomes concurrently")
     args = ap.parse_args()
     import torch
     import sccg
@@ -95,6 +97,7 @@ def genome(ctx, dev, stream, args, to_dev) -> None:
     """BASELINE configs[2] on one GPU: every chromosome pair resident in HBM, compressed in turn."""
     import torch
     import multigpu
+    import sccg
     import synth
     t0 = time.perf_counter()
     pairs = []
@@ -107,21 +110,50 @@ def genome(ctx, dev, stream, args, to_dev) -> None:
     d_rec = torch.empty(cap, dtype=torch.uint8, device=dev)
     ctx.compress_device(pairs[20][0].data_ptr(), pairs[20][1], pairs[20][2].data_ptr(), pairs[20][3],
                         d_rec.data_ptr(), cap, stream)   # warm-up (chr21)
+    # several contexts on the one GPU, each driven by its own host thread (ctypes drops the GIL):
+    # one chromosome's host round trips and serial phases overlap another's kernels
+    import queue
+    import threading
+    ctxs = [ctx] + [sccg.Context(0) for _ in range(max(0, args.contexts - 1))]
+    outs = [d_rec] + [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in ctxs[1:]]
+    streams = [torch.cuda.Stream(dev) for _ in ctxs]
+    order = sorted(range(len(pairs)), key=lambda i: -pairs[i][3])   # largest first
+
+    def run_all():
+        q = queue.Queue()
+        for i in order:
+            q.put(i)
+        res = {}
+
+        def worker(c, o, sm):
+            torch.cuda.set_device(dev)
+            while True:
+                try:
+                    i = q.get_nowait()
+                except queue.Empty:
+                    return
+                dr, rn, dt_, tn = pairs[i]
+                n = c.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, o.data_ptr(), cap, sm.cuda_stream)
+                res[i] = (c.stats()["target_bases"], n)
+
+        th = [threading.Thread(target=worker, args=(c, o, sm)) for c, o, sm in zip(ctxs, outs, streams)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return res
+
     best = None
     for _ in range(args.steps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        bases = rec_bytes = 0
-        per = []
-        for dr, rn, dt_, tn in pairs:
-            n = ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, d_rec.data_ptr(), cap, stream)
-            st = ctx.stats()
-            bases += st["target_bases"]
-            rec_bytes += n
-            per.append(st["target_bases"])
+        res = run_all()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         best = dt if best is None or dt < best else best
+        bases = sum(v[0] for v in res.values())
+        rec_bytes = sum(v[1] for v in res.values())
+        per = [res[i][0] for i in range(len(pairs))]
     # per chromosome (synchronised individually; diagnostics)
     per_s = []
     for dr, rn, dt_, tn in pairs:
@@ -131,7 +163,9 @@ def genome(ctx, dev, stream, args, to_dev) -> None:
         st = ctx.stats()
         per_s.append({"ms": round((time.perf_counter() - t1) * 1e3, 2), "rounds": st["walk_rounds"],
                       "switch": st["switch_segment"], "matches": st["n_matches"]})
-    print(json.dumps({"workload": "hg19_vs_hg18_genome_1gpu", "chromosomes": len(pairs), "target_bases": bases,
+    for c in ctxs[1:]:
+        c.close()
+    print(json.dumps({"workload": "hg19_vs_hg18_genome_1gpu", "contexts": len(ctxs), "chromosomes": len(pairs), "target_bases": bases,
                       "record_bytes": rec_bytes, "seconds": best, "bases_per_s": bases / best,
                       "lpt_max_over_mean_8gpu": multigpu.max_over_mean(per, 8), "generate_seconds": gen_s,
                       "per_chromosome": dict(zip(multigpu.CHROMS, per_s))}),
