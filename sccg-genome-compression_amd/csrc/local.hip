@@ -660,9 +660,12 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_local_all<false>, SCCG_BLOCK, 0) != hipSuccess || per < 1)
             per = 4;
-        // SCCG_LOCAL_BPC: fewer resident blocks per CU (leaves LDS for the walk that runs beside it)
+        // Fewer resident blocks per CU than fit (4) leave room for the global walk's preparation and
+        // round 1, which otherwise wait for the whole pass (it fills every CU's VGPRs and LDS).
+        // Measured (blocks/CU 4 / 3 / 2): whole genome on 1 GPU 28.5 / 27.3 / 27.2 ms, chr1 pair
+        // 1.57 / 1.55 / 1.54 ms, local-mode pair 2.84 / 2.90 / 2.97 ms.  SCCG_LOCAL_BPC overrides.
         const char* e = getenv("SCCG_LOCAL_BPC");
-        const int bpc = e ? atoi(e) : 0;
+        const int bpc = e ? atoi(e) : 3;
         if (bpc >= 1 && bpc < per) per = bpc;
         return (unsigned)(cus * per);
     }();
