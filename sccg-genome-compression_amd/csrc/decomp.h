@@ -25,5 +25,8 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
                       int64_t* d_dsum, int64_t nref, int64_t* d_partial, int32_t* d_err, int64_t* d_total, hipStream_t s);
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
                    const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s);
-// N insertion + lowercase + 50-column wrap of nres result bytes into d_out (no final '\n')
-int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, uint8_t* d_out, hipStream_t s);
+// N insertion + lowercase + 50-column wrap of nres result bytes into d_out (no final '\n');
+// d_span: scratch of dc_format_span_words(nres) int64 (per-span run indices)
+int64_t dc_format_span_words(int64_t nres);
+int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out,
+              hipStream_t s);

@@ -155,6 +155,32 @@ __global__ void k_len_to_i64(const int32_t* __restrict__ len, int64_t n, int64_t
 }
 
 constexpr int WPB = 4;
+// dst[0, l) = src[0, l) by one wave: bytes up to dst's next 16-byte boundary and after its last one
+// one per lane, the rest 16 bytes per lane as aligned stores built from five dword loads of the
+// (unaligned) source combined with v_alignbyte.  The source may be read up to 19 bytes past
+// src + l (the reference buffers carry 64 bytes of slack).
+__device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t l, int lane) {
+    const int64_t h = ((16 - ((uintptr_t)dst & 15)) & 15) < l ? ((16 - ((uintptr_t)dst & 15)) & 15) : l;
+    const int64_t nb = (l - h) >> 4;
+    const int64_t t0 = h + (nb << 4);
+    if (lane < h) dst[lane] = src[lane];
+    if (lane < l - t0) dst[t0 + lane] = src[t0 + lane];
+    const uint8_t* s0 = src + h;
+    const unsigned sh = (unsigned)((uintptr_t)s0 & 3);
+    const uint32_t* sa = reinterpret_cast<const uint32_t*>((uintptr_t)s0 & ~(uintptr_t)3);
+    uint4* d = reinterpret_cast<uint4*>(dst + h);
+    for (int64_t c = lane; c < nb; c += 64) {
+        const uint32_t* w = sa + 4 * c;
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+        uint4 v;
+        v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        v.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        d[c] = v;
+    }
+}
+
 __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill(const uint8_t* __restrict__ s, int64_t n,
                                                          const int64_t* __restrict__ lp, const int64_t* __restrict__ off,
                                                          const int64_t* __restrict__ dsum, const int64_t* __restrict__ dlt,
@@ -166,19 +192,25 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill(const uint8_t* __restri
     const int lane = lane_id();
     const int64_t i = base + lane;
     bool tok = false;
+    int64_t p = 0, l = 0, o = 0;
     if (i < n) {
         const uint8_t c = s[i];
         const bool inside = lp[i] >= 0 && s[lp[i]] == '(';
-        if (c == '(') tok = true;
-        else if (!inside) dec[off[i]] = c;   // literals, a stray ')' included
+        if (c == '(') {
+            tok = true;
+            p = dsum[i] + dlt[i];
+            l = contrib[i];
+            o = off[i];
+        } else if (!inside) {
+            dec[off[i]] = c;   // literals, a stray ')' included
+        }
     }
     unsigned long long tm = __ballot(tok);
     while (tm) {
         const int j = __ffsll((long long)tm) - 1;
         tm &= tm - 1;
-        const int64_t ij = base + j;
-        const int64_t p = dsum[ij] + dlt[ij], l = contrib[ij], o = off[ij];
-        for (int64_t q = lane; q < l; q += 64) dec[o + q] = R[p + q];
+        const int64_t pj = __shfl(p, j), lj = __shfl(l, j), oj = __shfl(o, j);
+        wave_copy(dec + oj, R + pj, lj, lane);
     }
 }
 
@@ -202,65 +234,176 @@ __device__ __forceinline__ int64_t first_run_ending_after(const int32_t* st, con
 // thread-per-64-positions writer straight to HBM, lanes 64 bytes apart, took 4.6 ms for a
 // chr1-sized FASTA.)
 constexpr int FPER = 16, FSPAN = 256 * FPER;
-// N positions before j (j inside an N run: those of the run before j included)
-__device__ __forceinline__ int64_t n_before(const int32_t* ns, const int32_t* nl, const int64_t* ncum, int64_t nn, int64_t j) {
-    const int64_t r = first_run_ending_after(ns, nl, nn, j);
+// N positions before j (j inside an N run: those of the run before j included), given
+// r = first_run_ending_after(ns, nl, nn, j)
+__device__ __forceinline__ int64_t n_before_at(const int32_t* ns, const int32_t* nl, const int64_t* ncum, int64_t nn,
+                                               int64_t r, int64_t j) {
     if (r < nn) return ncum[r] + (ns[r] <= j ? j - ns[r] : 0);
     return nn ? ncum[nn - 1] + nl[nn - 1] : 0;
 }
+
+// Span boundaries J_b = min(b * FSPAN, nres), b = 0..nspan: the first N run and the first
+// lowercase run ending after J_b, and J_b minus the N positions before it (the decoded-byte offset
+// of J_b).  One thread per (boundary, run list), all independent: the dependent binary-search loads
+// overlap across the grid instead of sitting at the head of every format block (a per-block search
+// chain of ~36 loads x 30 block generations took 0.79 ms of a chr1 reconstruction).
+__global__ void k_span_index(int64_t nres, int64_t nspan, const int32_t* __restrict__ ns, const int32_t* __restrict__ nl,
+                             const int64_t* __restrict__ ncum, int64_t nn, const int32_t* __restrict__ ls,
+                             const int32_t* __restrict__ ll, int64_t nlr, int64_t* __restrict__ tab) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * (nspan + 1); i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = i >> 1;
+        const int64_t J = b * FSPAN < nres ? b * FSPAN : nres;
+        if (i & 1) {
+            tab[3 * b + 2] = first_run_ending_after(ls, ll, nlr, J);
+        } else {
+            const int64_t r = first_run_ending_after(ns, nl, nn, J);
+            tab[3 * b + 0] = J - n_before_at(ns, nl, ncum, nn, r, J);
+            tab[3 * b + 1] = r;
+        }
+    }
+}
+
+// Run-list views for format_positions: starts, ends and (N runs) the N count before each run,
+// read from the span's LDS copies or from the global lists.
+struct LdsRuns {
+    const int32_t* s;
+    const int32_t* e;
+    const int64_t* b;
+    __device__ int64_t st(int64_t r) const { return s[r]; }
+    __device__ int64_t en(int64_t r) const { return e[r]; }
+    __device__ int64_t nb(int64_t r) const { return b[r]; }
+};
+struct GlobalRuns {
+    const int32_t* s;
+    const int32_t* l;
+    const int64_t* b;
+    __device__ int64_t st(int64_t r) const { return s[r]; }
+    __device__ int64_t en(int64_t r) const { return (int64_t)s[r] + l[r]; }
+    __device__ int64_t nb(int64_t r) const { return b[r]; }
+};
+
+// Formats positions [j0, j0 + FPER) of a span (j < J1) into sout; rn / rl enter as the first
+// N / lowercase run ending after j0 (runs past the views' counts: none left, ntot N before).
+template <typename V>
+__device__ __forceinline__ void format_positions(int64_t j0, int64_t J1, int64_t nres, int64_t O0, int64_t dbase,
+                                                 const uint8_t* sdec, uint8_t* sout, V N, int64_t nn, int64_t ntot, V L,
+                                                 int64_t nlr, int64_t rn, int64_t rl) {
+    int64_t n_s = INT64_MAX, n_e = INT64_MAX, n_b = ntot, l_s = INT64_MAX, l_e = INT64_MAX;
+    if (rn < nn) { n_s = N.st(rn); n_e = N.en(rn); n_b = N.nb(rn); }
+    if (rl < nlr) { l_s = L.st(rl); l_e = L.en(rl); }
+    // output offset of j = j + j / 50 - O0, kept as a running column (no 64-bit division per base)
+    int64_t o = j0 + j0 / 50 - O0;
+    int col = (int)(j0 % 50);
+    const int64_t je = j0 + FPER < J1 ? j0 + FPER : J1;
+    for (int64_t j = j0; j < je; j++) {
+        while (j >= n_e) {
+            rn++;
+            if (rn < nn) { n_s = N.st(rn); n_e = N.en(rn); n_b = N.nb(rn); }
+            else { n_s = n_e = INT64_MAX; n_b = ntot; }
+        }
+        while (j >= l_e) {
+            rl++;
+            if (rl < nlr) { l_s = L.st(rl); l_e = L.en(rl); }
+            else l_s = l_e = INT64_MAX;
+        }
+        uint8_t c = j >= n_s ? (uint8_t)'N' : sdec[j - n_b - dbase];
+        if (j >= l_s) c = c_tolower(c);
+        sout[o++] = c;
+        if (++col == 50) {
+            col = 0;
+            if (j != nres - 1) sout[o++] = '\n';
+        }
+    }
+}
+
+// first r in [a, b) with V::en(r) > j, ends ascending
+template <typename V>
+__device__ __forceinline__ int64_t first_end_after(const V& v, int64_t a, int64_t b, int64_t j) {
+    while (a < b) {
+        const int64_t m = (a + b) >> 1;
+        if (v.en(m) > j) b = m; else a = m + 1;
+    }
+    return a;
+}
+
+// One block per span.  The span's decoded bytes (dword loads), and when they are few (<= FRUNS
+// each, the usual case) the N and lowercase runs it touches, are staged in LDS in one round trip
+// behind the span table; every thread then formats FPER positions from LDS only, and the block
+// stores its output range with dword stores.  Spans with dense run alternation read the run
+// lists from global memory instead.
+constexpr int FRUNS = 384;
 __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__ dec, int64_t nres,
                                                      const int32_t* __restrict__ ns, const int32_t* __restrict__ nl,
                                                      const int64_t* __restrict__ ncum, int64_t nn,
                                                      const int32_t* __restrict__ ls, const int32_t* __restrict__ ll,
-                                                     int64_t nlr, uint8_t* __restrict__ out) {
-    __shared__ uint8_t sdec[FSPAN];
-    __shared__ uint8_t sout[FSPAN + FSPAN / 50 + 2];
-    __shared__ int64_t sd[6];
-    const int64_t J0 = (int64_t)blockIdx.x * FSPAN;
+                                                     int64_t nlr, const int64_t* __restrict__ tab, uint8_t* __restrict__ out) {
+    __shared__ uint32_t sdec_w[FSPAN / 4 + 2];
+    __shared__ uint8_t sout[FSPAN + FSPAN / 50 + 8];
+    __shared__ int32_t s_ns[FRUNS], s_ne[FRUNS], s_ls[FRUNS], s_le[FRUNS];
+    __shared__ int64_t s_nb[FRUNS];
+    __shared__ int64_t st[7];
+    const int64_t b = blockIdx.x;
+    const int64_t J0 = b * FSPAN;
     if (J0 >= nres) return;
     const int64_t J1 = J0 + FSPAN < nres ? J0 + FSPAN : nres;
-    // one search per block for each run list bounds the runs the span touches: [sd[2], sd[4]] for
-    // N, [sd[3], sd[5]] for lowercase; each thread then searches only that range (a span with dense
-    // case or N alternation holds up to FSPAN/2 runs, too many to walk forward through)
-    if (threadIdx.x == 0) sd[0] = J0 - n_before(ns, nl, ncum, nn, J0);
-    if (threadIdx.x == 64) sd[1] = J1 - n_before(ns, nl, ncum, nn, J1);
-    if (threadIdx.x == 128) { sd[2] = first_run_ending_after(ns, nl, nn, J0); sd[4] = first_run_ending_after(ns, nl, nn, J1 - 1); }
-    if (threadIdx.x == 192) { sd[3] = first_run_ending_after(ls, ll, nlr, J0); sd[5] = first_run_ending_after(ls, ll, nlr, J1 - 1); }
+    const int tid = threadIdx.x;
+    if (tid < 6) st[tid] = tab[3 * b + tid];
+    if (tid == 6) st[6] = nn ? ncum[nn - 1] + nl[nn - 1] : 0;
     __syncthreads();
-    const int64_t d0 = sd[0], dn = sd[1] - d0;
-    for (int64_t i = threadIdx.x; i < dn; i += 256) sdec[i] = dec[d0 + i];
-    const int64_t O0 = J0 + J0 / 50;
-    const int64_t jl = J1 - 1;
-    const int64_t On = jl + jl / 50 + 1 + ((jl % 50 == 49 && jl != nres - 1) ? 1 : 0) - O0;
-    __syncthreads();
-    const int64_t j0 = J0 + (int64_t)threadIdx.x * FPER;
-    if (j0 < J1) {
-        // the current N run [n_s, n_e) with the N count before it, the current lowercase run [l_s, l_e)
-        int64_t rn = first_run_ending_after(ns, nl, sd[4] < nn ? sd[4] + 1 : nn, j0, sd[2]);
-        int64_t rl = first_run_ending_after(ls, ll, sd[5] < nlr ? sd[5] + 1 : nlr, j0, sd[3]);
-        int64_t n_s, n_e, n_b, l_s, l_e;
-        auto load_n = [&]() {
-            if (rn < nn) { n_s = ns[rn]; n_e = n_s + nl[rn]; n_b = ncum[rn]; }
-            else { n_s = n_e = INT64_MAX; n_b = nn ? ncum[nn - 1] + nl[nn - 1] : 0; }
-        };
-        auto load_l = [&]() {
-            if (rl < nlr) { l_s = ls[rl]; l_e = l_s + ll[rl]; }
-            else l_s = l_e = INT64_MAX;
-        };
-        load_n();
-        load_l();
-        for (int64_t j = j0; j < j0 + FPER && j < J1; j++) {
-            while (j >= n_e) { rn++; load_n(); }
-            while (j >= l_e) { rl++; load_l(); }
-            uint8_t c = j >= n_s ? (uint8_t)'N' : sdec[j - n_b - d0];
-            if (j >= l_s) c = c_tolower(c);
-            const int64_t o = j + j / 50 - O0;
-            sout[o] = c;
-            if (j % 50 == 49 && j != nres - 1) sout[o + 1] = '\n';
+    // the runs this span touches lie in [first(J0), first(J1)] (first = first run ending after)
+    const int64_t d0 = st[0], dn = st[3] - d0;
+    const int64_t n_lo = st[1], n_hi = st[4] < nn ? st[4] + 1 : nn;
+    const int64_t l_lo = st[2], l_hi = st[5] < nlr ? st[5] + 1 : nlr;
+    const int64_t ntot = st[6];
+    const bool lds_runs = n_hi - n_lo <= FRUNS && l_hi - l_lo <= FRUNS;
+    const int64_t a0 = d0 & ~(int64_t)3;
+    const int64_t nw = (d0 + dn - a0 + 3) >> 2;
+    const uint32_t* decw = reinterpret_cast<const uint32_t*>(dec + a0);
+    for (int64_t i = tid; i < nw; i += 256) sdec_w[i] = decw[i];
+    if (lds_runs) {
+        for (int64_t r = n_lo + tid; r < n_hi; r += 256) {
+            const int32_t x = ns[r];
+            s_ns[r - n_lo] = x;
+            s_ne[r - n_lo] = x + nl[r];
+            s_nb[r - n_lo] = ncum[r];
+        }
+        for (int64_t r = l_lo + tid; r < l_hi; r += 256) {
+            const int32_t x = ls[r];
+            s_ls[r - l_lo] = x;
+            s_le[r - l_lo] = x + ll[r];
         }
     }
     __syncthreads();
-    for (int64_t i = threadIdx.x; i < On; i += 256) out[O0 + i] = sout[i];
+    const uint8_t* sdec = reinterpret_cast<const uint8_t*>(sdec_w);
+    const int64_t O0 = J0 + J0 / 50;
+    const int64_t jl = J1 - 1;
+    const int64_t On = jl + jl / 50 + 1 + ((jl % 50 == 49 && jl != nres - 1) ? 1 : 0) - O0;
+    const int64_t j0 = J0 + (int64_t)tid * FPER;
+    if (j0 < J1) {
+        if (lds_runs) {
+            const int64_t cn = n_hi - n_lo, cl = l_hi - l_lo;
+            const LdsRuns N{s_ns, s_ne, s_nb}, L{s_ls, s_le, nullptr};
+            format_positions(j0, J1, nres, O0, a0, sdec, sout, N, cn, ntot, L, cl, first_end_after(N, 0, cn, j0),
+                             first_end_after(L, 0, cl, j0));
+        } else {
+            const GlobalRuns N{ns, nl, ncum}, L{ls, ll, nullptr};
+            format_positions(j0, J1, nres, O0, a0, sdec, sout, N, nn, ntot, L, nlr, first_end_after(N, n_lo, n_hi, j0),
+                             first_end_after(L, l_lo, l_hi, j0));
+        }
+    }
+    __syncthreads();
+    // store [O0, O0 + On): bytes up to the first 4-byte boundary and after the last, dwords between
+    uint8_t* o = out + O0;
+    const int64_t h = ((4 - ((uintptr_t)o & 3)) & 3) < On ? ((4 - ((uintptr_t)o & 3)) & 3) : On;
+    const int64_t nbw = (On - h) >> 2;
+    const int64_t t0 = h + (nbw << 2);
+    if (tid < h) o[tid] = sout[tid];
+    if (tid < On - t0) o[t0 + tid] = sout[t0 + tid];
+    uint32_t* ow = reinterpret_cast<uint32_t*>(o + h);
+    for (int64_t i = tid; i < nbw; i += 256) {
+        const uint8_t* q = sout + h + 4 * i;
+        ow[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+    }
 }
 
 }  // namespace
@@ -348,11 +491,19 @@ int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int
     return 0;
 }
 
-int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, uint8_t* d_out, hipStream_t s) {
+int64_t dc_format_span_words(int64_t nres) { return 3 * ((nres + FSPAN - 1) / FSPAN + 2); }
+
+int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out,
+              hipStream_t s) {
     if (nres <= 0) return 0;
-    PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_span, dim3(grid_for(nres, FSPAN)), dim3(256), 0, s, d_dec, nres,
+    const int64_t nspan = (nres + FSPAN - 1) / FSPAN;
+    hipLaunchKernelGGL(k_span_index, dim3(grid_for(2 * (nspan + 1), 256)), dim3(256), 0, s, nres, nspan,
                        (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
-                       (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, d_out);
+                       (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, d_span);
+    SCCG_HIP(hipGetLastError());
+    PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_span, dim3((unsigned)nspan), dim3(256), 0, s, d_dec, nres,
+                       (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
+                       (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

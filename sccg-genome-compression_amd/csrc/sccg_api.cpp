@@ -43,7 +43,7 @@ enum Slot {
     B_SCAL, B_PARTIAL,
     B_RUN_S, B_RUN_E, B_TMP64, B_RUN_SN, B_RUN_EN, B_TMP64N, B_NLINE, B_RECS, B_STAT, B_SEGCLS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
     // decompression
-    B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC,
+    B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC, B_D_SPAN,
     // delta_encode's own token scan (targets holding '(')
     B_DX, B_DELTA,
     // a second FASTA-strip scratch set (the reference strips beside the target, on the side stream)
@@ -748,7 +748,8 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     TRY(dc_decode_fill(enc, nenc, lp, doff, dsum, dlt, contrib, Rp, dec, s));
     if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
     TRY(dev_put_bytes(out + hlen, "\n", 1, s));
-    TRY(dc_format(dec, nres, nr, lr, out + hlen + 1, s));
+    GET(int64_t, span, B_D_SPAN, dc_format_span_words(nres));
+    TRY(dc_format(dec, nres, nr, lr, span, out + hlen + 1, s));
     TRY(dev_put_bytes(out + total - 1, "\n", 1, s));
     HIPTRY(hipStreamSynchronize(s));
     ctx->stats.target_bases = nres;

@@ -250,6 +250,27 @@ def test_dense_case_and_n_alternation(ctx, period):
     assert fa == oraclelib.decompress(want, rfa)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_token_copy_alignments(ctx, seed):
+    """Record lines built by hand: tokens of length 0..70 (and some to 3000) at every source and
+    destination alignment between literal runs of 1-5 bases, so the wave copy's byte head, 16-byte
+    body and byte tail all meet every offset (decompression.cpp:210-236)."""
+    rng = random.Random(700 + seed)
+    ref = "".join(rng.choice("ACGT") for _ in range(20_000))
+    rfa = fuzzgen.to_fasta(ref)
+    toks, prev = [], 0
+    for _ in range(3000):
+        if rng.random() < 0.3:
+            toks.append(rng.choice("ACGT") * rng.randint(1, 5))
+        else:
+            ln = rng.randint(0, 70) if rng.random() < 0.8 else rng.randint(70, 3000)
+            p = rng.randint(0, len(ref) - ln)
+            toks.append(f"({p - prev},{ln})")
+            prev = p
+    rec = ("\n\n" + "".join(toks)).encode()
+    assert ctx.reconstruct(rec, rfa) == oraclelib.decompress(rec, rfa)
+
+
 @pytest.mark.parametrize("pieces", ["safe", "mixed"])
 def test_paren_large_vs_oracle(ctx, pieces):
     """Multi-tile scans of the paren path: a 3 Mb global-mode pair with punctuation literals."""
