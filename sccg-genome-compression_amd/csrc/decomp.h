@@ -20,9 +20,11 @@ int dc_last_paren(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_parti
 int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
                   int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s);
 // record line: per-byte output contribution / token deltas, output offsets, absolute p, range
-// check (d_err bit1 = token beyond the reference); *d_total = decoded length
+// check against *d_nref (d_err bit1 = token beyond the reference; the check waits for nref_ready
+// when given); *d_total = decoded length
 int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,
-                      int64_t* d_dsum, int64_t nref, int64_t* d_partial, int32_t* d_err, int64_t* d_total, hipStream_t s);
+                      int64_t* d_dsum, const int64_t* d_nref, hipEvent_t nref_ready, int64_t* d_partial, int32_t* d_err,
+                      int64_t* d_total, hipStream_t s);
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
                    const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s);
 // N insertion + lowercase + 50-column wrap of nres result bytes into d_out (no final '\n');

@@ -140,8 +140,9 @@ __global__ void k_tok_parse(const uint8_t* __restrict__ s, int64_t n, const int6
 
 // absolute p = running sum of deltas over tokens (decompression.cpp:220-222); range check :223
 __global__ void k_tok_check(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ dsum,
-                            const int64_t* __restrict__ dlt, const int64_t* __restrict__ contrib, int64_t nref,
-                            int32_t* __restrict__ err) {
+                            const int64_t* __restrict__ dlt, const int64_t* __restrict__ contrib,
+                            const int64_t* __restrict__ d_nref, int32_t* __restrict__ err) {
+    const int64_t nref = *d_nref;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (s[i] != '(') continue;
         const int64_t p = dsum[i] + dlt[i];
@@ -462,7 +463,8 @@ int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64
 }
 
 int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,
-                      int64_t* d_dsum, int64_t nref, int64_t* d_partial, int32_t* d_err, int64_t* d_total, hipStream_t s) {
+                      int64_t* d_dsum, const int64_t* d_nref, hipEvent_t nref_ready, int64_t* d_partial, int32_t* d_err,
+                      int64_t* d_total, hipStream_t s) {
     if (n <= 0) {
         SCCG_HIP(hipMemsetAsync(d_total, 0, sizeof(int64_t), s));
         return 0;
@@ -476,8 +478,9 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
     if (rc) return rc;
     rc = dev_excl_sum(d_dlt, d_dsum, n, nullptr, d_partial, s);
     if (rc) return rc;
+    if (nref_ready) SCCG_HIP(hipStreamWaitEvent(s, nref_ready, 0));
     hipLaunchKernelGGL(k_tok_check, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_dsum, (const int64_t*)d_dlt,
-                       (const int64_t*)d_contrib, nref, d_err);
+                       (const int64_t*)d_contrib, d_nref, d_err);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

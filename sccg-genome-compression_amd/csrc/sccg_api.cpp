@@ -694,10 +694,13 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
         TRY(dev_readback(&it, 1, s));
         n_is_comma = c == ',';
     }
-    int64_t rl[2];
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 8, nullptr, rl,
-              n_is_comma ? FILTER_UPPER : FILTER_DROP_UPPERN_ONLY, Rp));
-    const int64_t nRp = rl[1];
+    // the reference strips on the side stream beside the run-line and record-line parses (its
+    // length |R'| stays on the device, sc[9], until the range check and the parse's readback)
+    HIPTRY(hipEventRecord(ctx->ev_fork, s));
+    HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 8, nullptr, nullptr,
+              n_is_comma ? FILTER_UPPER : FILTER_DROP_UPPERN_ONLY, Rp, 1, ctx->side));
+    HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
 
     // ---- run lines + record line
     const int64_t nmax = (nlower > nnl ? nlower : nnl) > nenc ? (nlower > nnl ? nlower : nnl) : nenc;
@@ -723,12 +726,13 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     GET(int64_t, contrib, B_D_CONTRIB, nenc + 1);
     GET(int64_t, doff, B_D_OFF, nenc + 1);
     GET(int64_t, dsum, B_D_DSUM, nenc + 1);
-    TRY(dc_decode_prepare(enc, nenc, lp, contrib, dlt, doff, dsum, nRp, part, d_err, sc + 12, s));
-    int64_t D = 0;
+    TRY(dc_decode_prepare(enc, nenc, lp, contrib, dlt, doff, dsum, sc + 9, ctx->ev_rstrip, part, d_err, sc + 12, s));
+    HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // n <= 0 skips the range check's wait
+    int64_t D = 0, nRp = 0;
     int32_t err = 0;
     {
-        const RbItem it[2] = {{sc + 12, &D, (int)sizeof D}, {d_err, &err, (int)sizeof err}};
-        TRY(dev_readback(it, 2, s));
+        const RbItem it[3] = {{sc + 12, &D, (int)sizeof D}, {d_err, &err, (int)sizeof err}, {sc + 9, &nRp, (int)sizeof nRp}};
+        TRY(dev_readback(it, 3, s));
     }
     if (err & 1) return ctx->fail(SCCG_E_PARSE, "record text outside the run/token grammar");
     if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
