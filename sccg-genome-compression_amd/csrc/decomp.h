@@ -10,6 +10,10 @@ struct DcRuns {
     int64_t total;    // sum of len
 };
 
+// every '\n' of the record text, unordered: d_buf[0] = their count, d_buf[1, 1 + DC_NL_CAP) the
+// first DC_NL_CAP found (one pass; the caller sorts them, or uses dc_find_lines when there are more)
+constexpr int DC_NL_CAP = 32;
+int dc_newlines(const uint8_t* d_rec, int64_t n, int64_t* d_buf, hipStream_t s);
 // positions of the first four '\n' of the record text (n when absent) -> d_nl[0..3]
 int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl, hipStream_t s);
 // exclusive max-scan of parenthesis positions: d_lp[i] = last '(' or ')' strictly before i

@@ -38,6 +38,17 @@ __device__ __forceinline__ bool parse_int(const uint8_t* s, int64_t n, int64_t a
     return true;
 }
 
+// every '\n' of the record text into nl[0, NL_CAP) in any order, their count in *cnt (a record
+// file holds 2-3 of them; the caller falls back to ordered searches when there are more)
+__global__ void k_newlines(const uint8_t* __restrict__ s, int64_t n, unsigned long long* __restrict__ cnt,
+                           int64_t* __restrict__ nl) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (s[i] == '\n') {
+            const unsigned long long k = atomicAdd(cnt, 1ull);
+            if (k < (unsigned long long)DC_NL_CAP) nl[k] = i;
+        }
+}
+
 // positions of '(' / ')' -> value i, else -1 (for a max-scan: last parenthesis at or before i)
 __global__ void k_paren_pos(const uint8_t* __restrict__ s, int64_t n, int64_t* __restrict__ v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -415,6 +426,15 @@ int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl /*8: 4 results 
         int rc = launch_first_match(d_rec, n, i ? (const int64_t*)(d_nl + i - 1) : nullptr, 1, '\n', d_nl + i, d_nl + 4 + i, s);
         if (rc) return rc;
     }
+    return 0;
+}
+
+int dc_newlines(const uint8_t* d_rec, int64_t n, int64_t* d_buf, hipStream_t s) {
+    SCCG_HIP(hipMemsetAsync(d_buf, 0, sizeof(int64_t), s));
+    if (n <= 0) return 0;
+    const unsigned g = grid_for(n, 256) > 4096 ? 4096 : grid_for(n, 256);
+    hipLaunchKernelGGL(k_newlines, dim3(g), dim3(256), 0, s, d_rec, n, reinterpret_cast<unsigned long long*>(d_buf), d_buf + 1);
+    SCCG_HIP(hipGetLastError());
     return 0;
 }
 

@@ -11,6 +11,7 @@
 // delta_encode (:222-304) is folded into the emitters: each "(p," is written as "(p-p_prev,".
 // When the target holds '(' bytes, literals can fool delta_encode's token scan; then the record
 // line is written with absolute p (the text before delta_encode) and delta.hip runs that scan.
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -43,7 +44,7 @@ enum Slot {
     B_SCAL, B_PARTIAL,
     B_RUN_S, B_RUN_E, B_TMP64, B_RUN_SN, B_RUN_EN, B_TMP64N, B_NLINE, B_RECS, B_STAT, B_SEGCLS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
     // decompression
-    B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC, B_D_SPAN,
+    B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC, B_D_SPAN, B_D_NLPOS,
     // delta_encode's own token scan (targets holding '(')
     B_DX, B_DELTA,
     // a second FASTA-strip scratch set (the reference strips beside the target, on the side stream)
@@ -658,12 +659,24 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
                      int64_t out_cap, int64_t* out_len, bool size_only) {
     hipStream_t s = ctx->stream;
     GET(int64_t, sc, B_SCAL, 64);
+    // the line ends: one pass collects every '\n' (a record file holds 2-3); more than DC_NL_CAP
+    // of them -> four ordered first-match searches
     int64_t nl[4];
-    TRY(dc_find_lines(rec, n, sc, s));
+    int64_t nlb[1 + DC_NL_CAP];
     uint8_t first = 0;
+    GET(int64_t, dnl, B_D_NLPOS, 1 + DC_NL_CAP);
+    TRY(dc_newlines(rec, n, dnl, s));
     {
-        const RbItem it[2] = {{sc, nl, (int)sizeof nl}, {rec, &first, n > 0 ? 1 : 0}};
+        const RbItem it[2] = {{dnl, nlb, (int)sizeof nlb}, {rec, &first, n > 0 ? 1 : 0}};
         TRY(dev_readback(it, 2, s));
+    }
+    if (nlb[0] <= DC_NL_CAP) {
+        std::sort(nlb + 1, nlb + 1 + nlb[0]);
+        for (int i = 0; i < 4; i++) nl[i] = i < nlb[0] ? nlb[1 + i] : n;
+    } else {
+        TRY(dc_find_lines(rec, n, sc, s));
+        const RbItem it{sc, nl, (int)sizeof nl};
+        TRY(dev_readback(&it, 1, s));
     }
     // getline semantics: line i spans [start_i, nl_i); it exists iff start_i < n  (:68-97)
     int64_t start[4], end[4];

@@ -13,6 +13,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 T=$(find $OUT/tr -name '*kernel_trace.csv' | head -n 1)
 S=$(find $OUT/tr -name '*kernel_stats.csv' | head -n 1)
 cp "$S" $OUT/kernel_stats.csv
-python3 sccg-genome-compression_amd/tools/trace_streams.py "$T" --start-kernel k_first_match --n 120 > $OUT/timeline.txt
+python3 sccg-genome-compression_amd/tools/trace_streams.py "$T" --start-kernel k_newlines --n 120 > $OUT/timeline.txt
 rm -rf $OUT/tr
 timeout -k 10 200 python3 sccg-genome-compression_amd/tools/bench_configs.py --only chr1_decompress --steps 20 > $OUT/out.json
