@@ -44,7 +44,7 @@ enum Slot {
     B_SCAL, B_PARTIAL,
     B_RUN_S, B_RUN_E, B_TMP64, B_RUN_SN, B_RUN_EN, B_TMP64N, B_NLINE, B_RECS, B_STAT, B_SEGCLS, B_SEG_A, B_SEG_B, B_RP, B_TP, B_WALK, B_OUT,
     // decompression
-    B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC, B_D_SPAN, B_D_NLPOS,
+    B_D_LP, B_D_FLAG, B_D_DLT, B_D_CONTRIB, B_D_OFF, B_D_DSUM, B_D_LS, B_D_LL, B_D_LC, B_D_NS, B_D_NL, B_D_NC, B_D_DEC, B_D_SPAN, B_D_NLPOS, B_D_LP2, B_D_DLT2, B_PARTIAL2,
     // delta_encode's own token scan (targets holding '(')
     B_DX, B_DELTA,
     // a second FASTA-strip scratch set (the reference strips beside the target, on the side stream)
@@ -715,31 +715,37 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
               n_is_comma ? FILTER_UPPER : FILTER_DROP_UPPERN_ONLY, Rp, 1, ctx->side));
     HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
 
-    // ---- run lines + record line
-    const int64_t nmax = (nlower > nnl ? nlower : nnl) > nenc ? (nlower > nnl ? nlower : nnl) : nenc;
+    // ---- record line on side2 (own scratch) beside the run-line parses, which read counts back
+    int32_t* d_err = reinterpret_cast<int32_t*>(sc + 40);
+    HIPTRY(hipMemsetAsync(d_err, 0, sizeof(int32_t), s));
+    GET(int64_t, lp2, B_D_LP2, nenc + 1);
+    GET(int64_t, dlt2, B_D_DLT2, nenc + 1);
+    GET(int64_t, part2, B_PARTIAL2, scan_partials_needed(nenc + 1) + 16);
+    GET(int64_t, contrib, B_D_CONTRIB, nenc + 1);
+    GET(int64_t, doff, B_D_OFF, nenc + 1);
+    GET(int64_t, dsum, B_D_DSUM, nenc + 1);
+    const int64_t nmax = nlower > nnl ? nlower : nnl;
     GET(int64_t, lp, B_D_LP, nmax + 1);
     GET(int64_t, flag, B_D_FLAG, nmax + 1);
     GET(int64_t, dlt, B_D_DLT, nmax + 1);
     GET(int64_t, part, B_PARTIAL, scan_partials_needed(nmax + 1) + 16);
-    int32_t* d_err = reinterpret_cast<int32_t*>(sc + 40);
-    HIPTRY(hipMemsetAsync(d_err, 0, sizeof(int32_t), s));
+    GET(int32_t, ls, B_D_LS, nlower / 2 + 2);
+    GET(int32_t, ll, B_D_LL, nlower / 2 + 2);
+    GET(int64_t, lc, B_D_LC, nlower / 2 + 2);
+    GET(int32_t, ns, B_D_NS, nnl / 2 + 2);
+    GET(int32_t, nlr, B_D_NL, nnl / 2 + 2);
+    GET(int64_t, nc, B_D_NC, nnl / 2 + 2);
+    HIPTRY(hipEventRecord(ctx->ev_fork2, s));
+    HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
+    TRY(dc_decode_prepare(enc, nenc, lp2, contrib, dlt2, doff, dsum, sc + 9, ctx->ev_rstrip, part2, d_err, sc + 12,
+                          ctx->side2));
+    HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
     DcRuns lr{}, nr{};
-    {
-        GET(int32_t, ls, B_D_LS, nlower / 2 + 2);
-        GET(int32_t, ll, B_D_LL, nlower / 2 + 2);
-        GET(int64_t, lc, B_D_LC, nlower / 2 + 2);
-        lr.start = ls; lr.len = ll; lr.cum = lc;
-        TRY(dc_parse_runs(lower, nlower, &lr, lp, flag, dlt, part, d_err, sc + 10, s));
-        GET(int32_t, ns, B_D_NS, nnl / 2 + 2);
-        GET(int32_t, nlr, B_D_NL, nnl / 2 + 2);
-        GET(int64_t, nc, B_D_NC, nnl / 2 + 2);
-        nr.start = ns; nr.len = nlr; nr.cum = nc;
-        TRY(dc_parse_runs(nline, nnl, &nr, lp, flag, dlt, part, d_err, sc + 11, s));
-    }
-    GET(int64_t, contrib, B_D_CONTRIB, nenc + 1);
-    GET(int64_t, doff, B_D_OFF, nenc + 1);
-    GET(int64_t, dsum, B_D_DSUM, nenc + 1);
-    TRY(dc_decode_prepare(enc, nenc, lp, contrib, dlt, doff, dsum, sc + 9, ctx->ev_rstrip, part, d_err, sc + 12, s));
+    lr.start = ls; lr.len = ll; lr.cum = lc;
+    TRY(dc_parse_runs(lower, nlower, &lr, lp, flag, dlt, part, d_err, sc + 10, s));
+    nr.start = ns; nr.len = nlr; nr.cum = nc;
+    TRY(dc_parse_runs(nline, nnl, &nr, lp, flag, dlt, part, d_err, sc + 11, s));
+    HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // n <= 0 skips the range check's wait
     int64_t D = 0, nRp = 0;
     int32_t err = 0;
@@ -762,7 +768,7 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     if (size_only) return SCCG_OK;
     if (total > out_cap) return ctx->fail(SCCG_E_NOMEM, "output needs %lld bytes", (long long)total);
     GET(uint8_t, dec, B_D_DEC, D + 64);
-    TRY(dc_decode_fill(enc, nenc, lp, doff, dsum, dlt, contrib, Rp, dec, s));
+    TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s));
     if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
     TRY(dev_put_bytes(out + hlen, "\n", 1, s));
     GET(int64_t, span, B_D_SPAN, dc_format_span_words(nres));
