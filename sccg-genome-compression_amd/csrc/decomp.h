@@ -20,9 +20,14 @@ int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl, hipStream_t s)
 // (negative when none)
 int dc_last_paren(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_partial, hipStream_t s);
 // parse a lowercase / N run line (decompression.cpp:126-207) into r (arrays pre-allocated with
-// capacity n/2+1); d_err bit0 set on text outside the grammar
+// capacity dc_run_cap(n)); d_err bit0 set on text outside the grammar.  No host wait: d_count[0]
+// = runs, d_count[1] = total run length stay on the device (the caller reads them into r->n /
+// r->total); d_lp, d_flag, d_dlt hold >= max(n, dc_run_cap(n)) + 1 entries.
+int64_t dc_run_cap(int64_t n);
 int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
                   int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s);
+// d_err bit2: the last N run (count d_ncnt[0]) ends past the decoded length *d_D + N count d_ncnt[1]
+int dc_n_check(const DcRuns& nr, const int64_t* d_ncnt, const int64_t* d_D, int32_t* d_err, hipStream_t s);
 // record line: per-byte output contribution / token deltas, output offsets, absolute p, range
 // check against *d_nref (d_err bit1 = token beyond the reference; the check waits for nref_ready
 // when given); *d_total = decoded length

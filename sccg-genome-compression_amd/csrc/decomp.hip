@@ -106,16 +106,29 @@ __global__ void k_run_items_parse(const uint8_t* __restrict__ s, int64_t n, cons
     }
 }
 
-// starts = inclusive prefix of deltas (exclusive scan + own delta); runs must be ascending & disjoint
+// starts = inclusive prefix of deltas (exclusive scan + own delta); runs must be ascending & disjoint.
+// Also the run lengths as int64 for the N-count prefix, 0 past the *d_nr parsed runs (the scans run
+// to the capacity, so the host never waits for the count).
 __global__ void k_run_finish(const int64_t* __restrict__ dex, const int64_t* __restrict__ dlt, const int32_t* __restrict__ len,
-                             int64_t nr, int32_t* __restrict__ start, int32_t* __restrict__ err) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nr; r += (int64_t)gridDim.x * blockDim.x) {
+                             int64_t cap, const int64_t* __restrict__ d_nr, int32_t* __restrict__ start,
+                             int64_t* __restrict__ len64, int32_t* __restrict__ err) {
+    const int64_t nr = *d_nr;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < cap; r += (int64_t)gridDim.x * blockDim.x) {
+        if (r >= nr) { len64[r] = 0; continue; }
         const int64_t st = dex[r] + dlt[r];
         const int64_t pst = r ? dex[r - 1] + dlt[r - 1] : INT64_MIN;
         const int64_t pend = r ? pst + len[r - 1] : 0;
         if (st < 0 || st > INT32_MAX || (r && st < pend)) atomicOr(err, 1);
         start[r] = (int32_t)st;
+        len64[r] = len[r];
     }
+}
+
+// the last N run must end within the sequence: decoded length (*d_D) + N count (d_ncnt[1])
+__global__ void k_n_check(const int32_t* __restrict__ ns, const int32_t* __restrict__ nl, const int64_t* __restrict__ d_ncnt,
+                          const int64_t* __restrict__ d_D, int32_t* __restrict__ err) {
+    const int64_t n = d_ncnt[0];
+    if (threadIdx.x == 0 && n > 0 && (int64_t)ns[n - 1] + nl[n - 1] > *d_D + d_ncnt[1]) atomicOr(err, 4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -159,11 +172,6 @@ __global__ void k_tok_check(const uint8_t* __restrict__ s, int64_t n, const int6
         const int64_t p = dsum[i] + dlt[i];
         if (p < 0 || p + contrib[i] > nref) atomicOr(err, 2);
     }
-}
-
-__global__ void k_len_to_i64(const int32_t* __restrict__ len, int64_t n, int64_t* __restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = len[i];
 }
 
 constexpr int WPB = 4;
@@ -447,39 +455,41 @@ int dc_last_paren(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_parti
     return dev_excl_max(d_lp, d_lp, n, nullptr, d_partial, s);
 }
 
+int64_t dc_run_cap(int64_t n) { return n / 2 + 2; }
+
 int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
                   int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s) {
-    if (n <= 0) { r->n = 0; return 0; }
+    if (n <= 0) {
+        SCCG_HIP(hipMemsetAsync(d_count, 0, 2 * sizeof(int64_t), s));
+        return 0;
+    }
+    const int64_t cap = dc_run_cap(n);
     int rc = dc_last_paren(d_s, n, d_lp, d_partial, s);
     if (rc) return rc;
+    SCCG_HIP(hipMemsetAsync(d_dlt, 0, (size_t)cap * sizeof(int64_t), s));   // deltas past the runs scan as 0
     const unsigned g = grid_for(n, 256) > 8192 ? 8192 : grid_for(n, 256);
     hipLaunchKernelGGL(k_run_items_flag, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_lp, d_flag, d_err);
-    rc = dev_excl_sum(d_flag, d_flag, n, d_count, d_partial, s);
+    rc = dev_excl_sum(d_flag, d_flag, n, d_count, d_partial, s);   // item ranks; d_count[0] = runs
     if (rc) return rc;
     hipLaunchKernelGGL(k_run_items_parse, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_lp,
                        (const int64_t*)d_flag, d_dlt, r->len, d_err);
     SCCG_HIP(hipGetLastError());
-    int64_t nr = 0;
-    {
-        const RbItem it{d_count, &nr, (int)sizeof nr};
-        rc = dev_readback(&it, 1, s);
-        if (rc) return rc;
-    }
-    r->n = nr;
-    if (nr == 0) return 0;
-    // exclusive sum of deltas into d_flag (free now), then starts
-    rc = dev_excl_sum(d_dlt, d_flag, nr, nullptr, d_partial, s);
+    // exclusive sum of deltas into d_flag (free now), then starts and int64 lengths, then the
+    // N-count prefix; d_count[1] = total run length
+    rc = dev_excl_sum(d_dlt, d_flag, cap, nullptr, d_partial, s);
     if (rc) return rc;
-    const unsigned g2 = grid_for(nr, 256) > 8192 ? 8192 : grid_for(nr, 256);
+    const unsigned g2 = grid_for(cap, 256) > 8192 ? 8192 : grid_for(cap, 256);
     hipLaunchKernelGGL(k_run_finish, dim3(g2), dim3(256), 0, s, (const int64_t*)d_flag, (const int64_t*)d_dlt,
-                       (const int32_t*)r->len, nr, r->start, d_err);
-    // cumulative lengths (for N: count of N positions before a run)
-    hipLaunchKernelGGL(k_len_to_i64, dim3(g2), dim3(256), 0, s, (const int32_t*)r->len, nr, r->cum);
+                       (const int32_t*)r->len, cap, (const int64_t*)d_count, r->start, r->cum, d_err);
     SCCG_HIP(hipGetLastError());
-    rc = dev_excl_sum(r->cum, r->cum, nr, d_count, d_partial, s);
-    if (rc) return rc;
-    const RbItem it{d_count, &r->total, (int)sizeof r->total};
-    return dev_readback(&it, 1, s);
+    return dev_excl_sum(r->cum, r->cum, cap, d_count + 1, d_partial, s);
+}
+
+int dc_n_check(const DcRuns& nr, const int64_t* d_ncnt, const int64_t* d_D, int32_t* d_err, hipStream_t s) {
+    hipLaunchKernelGGL(k_n_check, dim3(1), dim3(64), 0, s, (const int32_t*)nr.start, (const int32_t*)nr.len, d_ncnt, d_D,
+                       d_err);
+    SCCG_HIP(hipGetLastError());
+    return 0;
 }
 
 int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,

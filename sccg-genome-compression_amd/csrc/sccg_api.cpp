@@ -724,17 +724,17 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     GET(int64_t, contrib, B_D_CONTRIB, nenc + 1);
     GET(int64_t, doff, B_D_OFF, nenc + 1);
     GET(int64_t, dsum, B_D_DSUM, nenc + 1);
-    const int64_t nmax = nlower > nnl ? nlower : nnl;
-    GET(int64_t, lp, B_D_LP, nmax + 1);
-    GET(int64_t, flag, B_D_FLAG, nmax + 1);
-    GET(int64_t, dlt, B_D_DLT, nmax + 1);
-    GET(int64_t, part, B_PARTIAL, scan_partials_needed(nmax + 1) + 16);
-    GET(int32_t, ls, B_D_LS, nlower / 2 + 2);
-    GET(int32_t, ll, B_D_LL, nlower / 2 + 2);
-    GET(int64_t, lc, B_D_LC, nlower / 2 + 2);
-    GET(int32_t, ns, B_D_NS, nnl / 2 + 2);
-    GET(int32_t, nlr, B_D_NL, nnl / 2 + 2);
-    GET(int64_t, nc, B_D_NC, nnl / 2 + 2);
+    const int64_t nmax = nlower > nnl ? nlower : nnl;   // >= dc_run_cap of either line but for n <= 3
+    GET(int64_t, lp, B_D_LP, nmax + 4);
+    GET(int64_t, flag, B_D_FLAG, nmax + 4);
+    GET(int64_t, dlt, B_D_DLT, nmax + 4);
+    GET(int64_t, part, B_PARTIAL, scan_partials_needed(nmax + 4) + 16);
+    GET(int32_t, ls, B_D_LS, dc_run_cap(nlower));
+    GET(int32_t, ll, B_D_LL, dc_run_cap(nlower));
+    GET(int64_t, lc, B_D_LC, dc_run_cap(nlower));
+    GET(int32_t, ns, B_D_NS, dc_run_cap(nnl));
+    GET(int32_t, nlr, B_D_NL, dc_run_cap(nnl));
+    GET(int64_t, nc, B_D_NC, dc_run_cap(nnl));
     HIPTRY(hipEventRecord(ctx->ev_fork2, s));
     HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
     TRY(dc_decode_prepare(enc, nenc, lp2, contrib, dlt2, doff, dsum, sc + 9, ctx->ev_rstrip, part2, d_err, sc + 12,
@@ -742,26 +742,26 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
     DcRuns lr{}, nr{};
     lr.start = ls; lr.len = ll; lr.cum = lc;
-    TRY(dc_parse_runs(lower, nlower, &lr, lp, flag, dlt, part, d_err, sc + 10, s));
+    TRY(dc_parse_runs(lower, nlower, &lr, lp, flag, dlt, part, d_err, sc + 14, s));
     nr.start = ns; nr.len = nlr; nr.cum = nc;
-    TRY(dc_parse_runs(nline, nnl, &nr, lp, flag, dlt, part, d_err, sc + 11, s));
+    TRY(dc_parse_runs(nline, nnl, &nr, lp, flag, dlt, part, d_err, sc + 16, s));
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // n <= 0 skips the range check's wait
-    int64_t D = 0, nRp = 0;
+    TRY(dc_n_check(nr, sc + 16, sc + 12, d_err, s));
+    // one readback: decoded length, error bits, |R'|, both run lines' counts and totals
+    int64_t D = 0, nRp = 0, cnt[4] = {0, 0, 0, 0};
     int32_t err = 0;
     {
-        const RbItem it[3] = {{sc + 12, &D, (int)sizeof D}, {d_err, &err, (int)sizeof err}, {sc + 9, &nRp, (int)sizeof nRp}};
-        TRY(dev_readback(it, 3, s));
+        const RbItem it[4] = {{sc + 12, &D, (int)sizeof D}, {d_err, &err, (int)sizeof err}, {sc + 9, &nRp, (int)sizeof nRp},
+                              {sc + 14, cnt, (int)sizeof cnt}};
+        TRY(dev_readback(it, 4, s));
     }
+    lr.n = cnt[0]; lr.total = cnt[1];
+    nr.n = cnt[2]; nr.total = cnt[3];
     if (err & 1) return ctx->fail(SCCG_E_PARSE, "record text outside the run/token grammar");
     if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
     const int64_t nres = D + nr.total;
-    if (nr.n > 0) {
-        int32_t ls_last = 0, ll_last = 0;
-        const RbItem it[2] = {{nr.start + nr.n - 1, &ls_last, 4}, {nr.len + nr.n - 1, &ll_last, 4}};
-        TRY(dev_readback(it, 2, s));
-        if ((int64_t)ls_last + ll_last > nres) return ctx->fail(SCCG_E_PARSE, "N positions beyond the sequence");
-    }
+    if (err & 4) return ctx->fail(SCCG_E_PARSE, "N positions beyond the sequence");
     const int64_t hlen = has_hdr ? end[0] : 0;
     const int64_t total = hlen + 1 + nres + (nres > 0 ? (nres - 1) / 50 : 0) + 1;
     *out_len = total;
