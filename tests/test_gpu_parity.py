@@ -271,6 +271,33 @@ def test_token_copy_alignments(ctx, seed):
     assert ctx.reconstruct(rec, rfa) == oraclelib.decompress(rec, rfa)
 
 
+_RUN_LINE_CASES = {
+    "empty_lines": b"\n\n(0,10)", "one_n": b"\n(5,3)\n(0,10)", "lower_and_n": b"(2,4)\n(5,3)\n(0,10)AC",
+    "n_tail": b"\n(10,2)\n(0,10)", "n_past": b"\n(20,5)\n(0,3)", "lower_singleton": b"7\n\n(0,10)",
+    "n_items": b"\n1,3,2\n(0,10)", "hdr": b">chrX\n(1,2)\n(3,1)\n(0,10)", "lower_all": b"(0,10)\n\n(0,10)",
+    "n_only": b"\n(0,4)\n", "many_runs": ("".join(f"{1 if i else 0}," for i in range(40))[:-1] + "\n\n(0,100)").encode(),
+}
+
+
+@pytest.mark.parametrize("name", sorted(_RUN_LINE_CASES))
+def test_run_line_edges(ctx, name):
+    """Hand-built run lines (decompression.cpp:126-207, :241-262): empty lines, singletons, a run at
+    the sequence end, one past it (an error on both sides), a header; the run counts stay on the
+    device and are read back once with the record line's."""
+    rng = random.Random(1)
+    rfa = fuzzgen.to_fasta("".join(rng.choice("ACGT") for _ in range(200)))
+    rec = _RUN_LINE_CASES[name]
+    try:
+        want = oraclelib.decompress(rec, rfa)
+    except oraclelib.OracleError:   # the reference exits 1 (or its behaviour is undefined)
+        want = None
+    if want is None:
+        with pytest.raises(sccg.SccgError):
+            ctx.reconstruct(rec, rfa)
+    else:
+        assert ctx.reconstruct(rec, rfa) == want
+
+
 @pytest.mark.parametrize("pieces", ["safe", "mixed"])
 def test_paren_large_vs_oracle(ctx, pieces):
     """Multi-tile scans of the paren path: a 3 Mb global-mode pair with punctuation literals."""
