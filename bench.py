@@ -1,22 +1,29 @@
 #!/usr/bin/env python3
 """bench.py -- target bases compressed per second on MI355X (BASELINE.json metric).
 
-Workload (configs[1]): a chr1-sized hg19-vs-hg18 pair (|R| = 247,249,719, |T| = 249,250,621),
-synthetic (tools/synth.c "hg" profile; real FASTA is not available offline).  One step = the whole
-hot path on resident inputs: both FASTA texts already in HBM -> compressed_genome.txt bytes in
-HBM (ingest, lowercase line, local segments + switch, N line, N erase, global walk, delta-encoded
-record text).  7z is outside the path, as in the reference's own timing split.
+Workload (BASELINE configs[2], the north-star job): the whole hg19-vs-hg18 genome -- the 24
+chromosome pairs chr1..22, X, Y at their UCSC lengths (hg18 = reference, hg19 = target,
+multigpu.HG18 / HG19), synthetic (tools/synth.c "hg" profile, seed = chromosome index 1..24; real
+FASTA is not available offline).  One compression.cpp invocation per pair, exactly as the
+reference runs it (compression.cpp:584-610), at the reference's own parameters (k = 14, m = 100,
+compression.cpp:373-379).
+
+One step = every pair of this rank's LPT shard compressed on its GPU (FASTA texts already resident
+in HBM -> compressed_genome.txt bytes in HBM: ingest, lowercase line, local segments + switch, N
+line, N erase, global walk, delta-encoded record text), then the per-chromosome record streams
+gathered to rank 0 over RCCL (the job's only exchange).  7z is outside the path, as in the
+reference's own timing split.  `--contexts C` runs C library contexts per GPU, each driven by its
+own host thread, so one pair's host round trips overlap another pair's kernels.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-Multi-GPU: chromosomes are independent, so every rank compresses its own chr1-shaped pair
-(seed 1+rank; weak scaling) and the per-chromosome record streams are gathered to rank 0 over
-RCCL inside the step, as the whole-genome driver does.
-
-Printed (rank 0): one JSON line with value = all ranks' target bases / max-over-ranks time, the
-roofline of the dominant kernel (HIP events on the library's stream, algorithmic bytes from
-DESIGN.md §4) and the reference CPU path timed on a bounded sample on this host.
+Printed (rank 0): one JSON line.  value = the genome's target bases / max-over-ranks step time
+(strong scaling: the job is fixed, N GPUs share it); roofline of the dominant kernel (HIP events
+on the launching streams, SURVEY §8(d) algorithmic bytes) and of the whole job; the reference
+compression.cpp timed on this host on BASELINE configs[0] (the chr21 pair); the chr1 record
+stream reconstructed on the GPU (configs[3]); per-chromosome sha256 checked against the
+reference's, pinned in tests/golden/genome_manifest.json.
 """
 from __future__ import annotations
 
@@ -28,41 +35,65 @@ import shutil
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(REPO, "sccg-genome-compression_amd")
 sys.path.insert(0, PKG_DIR)
 
-CHR1 = (247_249_719, 249_250_621)   # hg18 / hg19 chr1 (UCSC chromInfo)
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "target bases compressed/sec at 1/2/4/8 GPUs; bit-exact record stream vs CPU ref"
+MANIFEST = os.path.join(REPO, "tests", "golden", "genome_manifest.json")
+# Hardware queues per process for the default run: C contexts x 3 streams + torch's stream must not
+# share queues (a queue serialises its streams' kernels).  HIP's default is 4; at most 32 here.
+HW_QUEUES_DEFAULT = 12
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes(kernel: str, shape: dict) -> float | None:
-    """Algorithmic HBM bytes of ONE launch of `kernel` for this workload."""
-    nT, nR = shape["target_bases"], shape["reference_bases"]
-    if kernel == "fasta_strip":       # read the FASTA, write the kept bytes (target and reference launch)
-        return (shape["tgt_fa"] + nT + shape["ref_fa"] + nR) / 2.0
-    if kernel == "local_segments":    # both segment strings once + records and stats
-        lead = min(nR, nT)
-        return 2.0 * lead + (lead / 1000.0) * (1024 + 32)
-    if kernel == "walk":              # every target base once + the matched reference bases once
-        return None                   # per-launch bytes vary by round; see walk_bytes below
-    if kernel in ("run_extract", "n_filter"):
-        return float(nT + nT)
-    if kernel == "first_sweep_anchors":   # R' once + one 8-byte anchor slot per 32 reference bases
-        return float(nR + nR / 32 * 8)
+def walk_alg_bytes(nT: int) -> float:
+    """the walk's share of B_global, 0.5 B per target base (packed target + packed
+    reference along the matches)."""
+    return 0.5 * nT
+
+
+def job_alg_bytes(nT: int, nR: int, nRp: int, out: int) -> float:
+    """SURVEY §8(d) B_global = 1.25(|T|+|R|) + 0.25|R| + 4|R'| + 0.5|T| + |out|."""
+    return 1.25 * (nT + nR) + 0.25 * nR + 4.0 * nRp + 0.5 * nT + out
+
+
+def kernel_alg_bytes(kernel: str, tot: dict) -> float | None:
+    """Algorithmic HBM bytes of one STEP of `kernel` summed over the step's pairs."""
+    if kernel == "walk":
+        return walk_alg_bytes(tot["target_bases"])
+    if kernel == "fasta_strip":          # read the FASTA, write the stripped and the N-erased copies
+        return tot["tgt_fa"] + tot["ref_fa"] + 2.0 * (tot["target_bases"] + tot["reference_bases"])
+    if kernel == "run_extract":          # T once
+        return float(tot["target_bases"])
+    if kernel == "first_sweep_anchors":  # R' once + one 8-byte anchor slot per 32 reference bases
+        return tot["reference_bases"] * (1.0 + 8.0 / 32.0)
+    if kernel == "local_segments":       # both segment strings (up to the switch, bounded by all of them)
+        return 2.0 * min(tot["target_bases"], tot["reference_bases"])
     return None
 
 
-def cpu_baseline(sample_bases: int) -> dict | None:
-    """The reference compression.cpp (oracle/_ref, built from /root/reference) on a bounded
-    sample of the same workload shape, single-threaded, stub 7z, stdout discarded."""
+def load_manifest() -> dict:
+    try:
+        return {e["name"]: e for e in json.load(open(MANIFEST))}
+    except Exception:
+        return {}
+
+
+def cpu_baseline(timeout_s: int) -> dict | None:
+    """The reference compression.cpp (oracle/_ref, compiled from /root/reference's sources) on
+    BASELINE configs[0]: the chr21 pair (hg18 chr21 = 46,944,323 vs hg19 chr21 = 48,129,895,
+    seed 21 -- the same pair the genome job compresses), single-threaded, stub 7z, stdout to
+    /dev/null.  Falls back to the C restatement (oracle/sccg_oracle) if the reference binary is
+    absent.  The record sha256 is compared with the pinned manifest."""
+    import multigpu
     import synth
     ref_bin = os.path.join(REPO, "oracle", "_ref", "compression")
     kind = "reference"
@@ -71,57 +102,81 @@ def cpu_baseline(sample_bases: int) -> dict | None:
         kind = "port"
         if not os.path.exists(ref_bin):
             return None
-    rl, tl = sample_bases, sample_bases + sample_bases // 400
-    rfa, tfa = synth.synth_pair("hg", rl, tl, 101)
+    i = multigpu.CHROMS.index("chr21")
+    rl, tl = multigpu.HG18[i], multigpu.HG19[i]
+    rfa, tfa = synth.synth_pair("hg", rl, tl, i + 1)
     d = tempfile.mkdtemp(prefix="sccg_cpu_")
     try:
         rp, tp = os.path.join(d, "ref.fa"), os.path.join(d, "tgt.fa")
         open(rp, "wb").write(rfa)
         open(tp, "wb").write(tfa)
+        del rfa, tfa
         env = dict(os.environ, PATH=os.path.join(REPO, "oracle", "stub7z") + os.pathsep + os.environ.get("PATH", ""))
         if kind == "reference":
-            cmd = [ref_bin, rp, tp, os.path.join(d, "out")]
+            outp = os.path.join(d, "out")
+            cmd = [ref_bin, rp, tp, outp]
+            rec_path = os.path.join(outp, "compressed_genome.txt")
         else:
-            cmd = [ref_bin, "compress", rp, tp, os.path.join(d, "out.txt")]
+            rec_path = os.path.join(d, "out.txt")
+            cmd = [ref_bin, "compress", rp, tp, rec_path]
         t0 = time.perf_counter()
-        p = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600)
+        p = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout_s)
         dt = time.perf_counter() - t0
         if p.returncode != 0:
             return None
+        sha = hashlib.sha256(open(rec_path, "rb").read()).hexdigest()
+    except subprocess.TimeoutExpired:
+        return None
     finally:
         shutil.rmtree(d, ignore_errors=True)
-    return {"value": tl / dt, "unit": "target bases/s", "cores": 1, "kind": kind,
-            "sample": f"hg-profile synthetic pair |R|={rl:,} |T|={tl:,} (seed 101), wall {dt:.2f} s, "
-                      f"single-threaded, stub 7z, stdout to /dev/null"}
-
-
-def load_pmc(kernel: str) -> float | None:
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary, if any."""
-    path = os.path.join(REPO, "profiles", "pmc_summary.json")
-    if not os.path.exists(path):
-        return None
+    pin = load_manifest().get("chr21", {}).get("record_sha256")
+    cpu = "unknown"
     try:
-        doc = json.load(open(path))
-        return doc.get(kernel, {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": tl / dt, "unit": "target bases/s", "cores": 1, "kind": kind,
+            "sample": f"BASELINE configs[0]: hg19-vs-hg18 chr21-sized synthetic pair |R|={rl:,} |T|={tl:,} (seed 21), "
+                      f"wall {dt:.1f} s, single-threaded ({cpu}), stub 7z, stdout to /dev/null",
+            "record_matches_pinned": (sha == pin) if pin else None}
+
+
+class Lane:
+    """One library context + its stream, output buffer and host thread."""
+
+    def __init__(self, sccg, torch, dev, cap: int, device_index: int):
+        self.ctx = sccg.Context(device_index)
+        self.stream = torch.cuda.Stream(dev)
+        self.out = torch.empty(cap, dtype=torch.uint8, device=dev)
+        self.cap = cap
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--cpu-sample", type=int, default=10_000_000, help="reference CPU sample size (bases)")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--contexts", type=int, default=2, help="library contexts (host threads) per GPU")
+    ap.add_argument("--hw-queues", type=int, default=HW_QUEUES_DEFAULT,
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
+    ap.add_argument("--workload", choices=["genome", "chr1"], default="genome",
+                    help="genome: BASELINE configs[2] (default); chr1: one chr1-sized pair per rank (configs[1] shape)")
+    ap.add_argument("--names", default="", help="comma-separated subset of chromosomes (diagnostics)")
+    ap.add_argument("--cpu-timeout", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-check", action="store_true", help="skip the round-trip parity check")
-    ap.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events in the timed region (A/B of their cost)")
-    ap.add_argument("--ref-len", type=int, default=CHR1[0])
-    ap.add_argument("--tgt-len", type=int, default=CHR1[1])
+    ap.add_argument("--no-check", action="store_true", help="skip the pinned sha256 checks")
+    ap.add_argument("--no-decomp", action="store_true", help="skip the configs[3] reconstruction")
+    ap.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events in the timed region")
     args = ap.parse_args()
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))   # before HIP initialises
 
     import torch
     import torch.distributed as dist
+    import multigpu
     import sccg
     import synth
 
@@ -133,86 +188,228 @@ def main() -> None:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    t0 = time.perf_counter()
-    rfa, tfa = synth.synth_pair("hg", args.ref_len, args.tgt_len, 1 + rank)
-    log(f"[rank {rank}] generated pair in {time.perf_counter() - t0:.1f} s "
-        f"({len(rfa):,} + {len(tfa):,} FASTA bytes)")
-    d_ref = torch.frombuffer(bytearray(rfa), dtype=torch.uint8).to(dev)
-    d_tgt = torch.frombuffer(bytearray(tfa), dtype=torch.uint8).to(dev)
-    ctx = sccg.Context(local)
-    cap = ctx.compress_bound(len(rfa), len(tfa))
-    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # ---- the job: chromosome pairs, LPT-sharded by target size (multigpu.lpt_shard)
+    if args.workload == "genome":
+        jobs = [(n, multigpu.HG18[i], multigpu.HG19[i], i + 1) for i, n in enumerate(multigpu.CHROMS)]
+        if args.names:
+            keep = set(args.names.split(","))
+            jobs = [j for j in jobs if j[0] in keep]
+        mine = [jobs[i] for i in multigpu.lpt_shard([j[2] for j in jobs], world)[rank]]
+    else:
+        jobs = [(f"chr1_r{r}", multigpu.HG18[0], multigpu.HG19[0], 1 + r) for r in range(world)]
+        mine = [jobs[rank]]
 
-    import multigpu
+    # ---- inputs: generated on the host (threads: the C generator releases the GIL), then resident
+    t0 = time.perf_counter()
+    pairs: dict = {}
+    host_fa: dict = {}
+    lock = threading.Lock()
+
+    def gen(job):
+        name, rl, tl, seed = job
+        rfa, tfa = synth.synth_pair("hg", rl, tl, seed)
+        with lock:
+            host_fa[name] = (rfa, tfa)
+
+    ths = [threading.Thread(target=gen, args=(j,)) for j in mine]
+    nthr = 8
+    for b in range(0, len(ths), nthr):
+        for t in ths[b:b + nthr]:
+            t.start()
+        for t in ths[b:b + nthr]:
+            t.join()
+    for name, rl, tl, seed in mine:
+        rfa, tfa = host_fa[name]
+        pairs[name] = (torch.frombuffer(bytearray(rfa), dtype=torch.uint8).to(dev), len(rfa),
+                       torch.frombuffer(bytearray(tfa), dtype=torch.uint8).to(dev), len(tfa))
+    keep_chr1 = host_fa.get("chr1") or host_fa.get(f"chr1_r{rank}")
+    tgt_fa_bytes = sum(len(v[1]) for v in host_fa.values())
+    ref_fa_bytes = sum(len(v[0]) for v in host_fa.values())
+    host_fa.clear()
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] {len(mine)} pairs generated and resident in {time.perf_counter() - t0:.1f} s "
+        f"({ref_fa_bytes + tgt_fa_bytes:,} FASTA bytes)")
+
+    n_lanes = max(1, min(args.contexts, len(mine)))
+    cap = max(sccg.Context.compress_bound_static(p[1], p[3]) for p in pairs.values())
+    lanes = [Lane(sccg, torch, dev, cap, local) for _ in range(n_lanes)]
+    order = sorted(pairs, key=lambda n: -pairs[n][3])   # largest first onto the first free lane
+    results: dict = {}      # name -> (device tensor of its record text, stats)
+    errors: list = []
+
+    def run_shard() -> None:
+        nxt = [0]
+        qlock = threading.Lock()
+
+        def worker(lane: Lane) -> None:
+            try:
+                torch.cuda.set_device(dev)
+                while True:
+                    with qlock:
+                        if nxt[0] >= len(order):
+                            return
+                        name = order[nxt[0]]
+                        nxt[0] += 1
+                    dr, rn, dt_, tn = pairs[name]
+                    n = lane.ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, lane.out.data_ptr(), lane.cap,
+                                                 lane.stream.cuda_stream)
+                    st = lane.ctx.stats()
+                    prev = results.get(name)
+                    with torch.cuda.stream(lane.stream):
+                        buf = prev[0] if prev is not None and prev[0].numel() == n else \
+                            torch.empty(n, dtype=torch.uint8, device=dev)
+                        buf.copy_(lane.out[:n])   # the pair's record stream, kept for the gather
+                    results[name] = (buf, st)
+            except Exception as e:   # noqa: BLE001 -- reported after the join
+                errors.append(e)
+
+        ths = [threading.Thread(target=worker, args=(ln,)) for ln in lanes]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errors:
+            raise errors[0]
+
     gathered: list = [None]
 
-    def step() -> int:
-        n = ctx.compress_device(d_ref.data_ptr(), len(rfa), d_tgt.data_ptr(), len(tfa), d_out.data_ptr(), cap, stream)
+    def step() -> None:
+        run_shard()
+        for ln in lanes:
+            ln.stream.synchronize()
         if world > 1:
-            # per-chromosome record streams -> rank 0 over RCCL (multigpu.gather_to_root, the
-            # genome driver's exchange): one size all-gather, then a gather of each rank's output
-            # prefix straight out of d_out; only rank 0 receives
-            gathered[0] = multigpu.gather_to_root(d_out, n)
-        return n
+            # per-chromosome record streams -> rank 0 over RCCL (multigpu.gather_records): one size
+            # all-gather, then one gather of each rank's packed streams; only rank 0 receives
+            gathered[0] = multigpu.gather_records({n: results[n][0] for n in order}, device=dev)
 
     for _ in range(args.warmup):
-        n_out = step()
-    ctx.profile(not args.no_prof)
+        step()
+    lanes[0].ctx.profile(not args.no_prof)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        n_out = step()
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    prof = ctx.profile_get()
-    ctx.profile(False)
-    st = ctx.stats()
+    prof = lanes[0].ctx.profile_get()
+    lanes[0].ctx.profile(False)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    gather_ok = None
-    if world > 1 and rank == 0:
-        parts = gathered[0]
-        gather_ok = all(p.numel() > 0 for p in parts) and torch.equal(parts[0], d_out[:n_out])
-        if not gather_ok:
-            raise SystemExit("bench: gathered record streams are wrong (empty part or rank 0 mismatch)")
+    # ---- per-rank totals (all ranks' target bases make up the whole job)
+    tot = {"target_bases": sum(results[n][1]["target_bases"] for n in order),
+           "reference_bases": sum(results[n][1]["reference_bases"] for n in order),
+           "record_bytes": sum(int(results[n][0].numel()) for n in order),
+           "tgt_fa": tgt_fa_bytes, "ref_fa": ref_fa_bytes}
+    totals = [tot]
+    if world > 1:
+        got = [None] * world
+        dist.all_gather_object(got, tot)
+        totals = got
+    job = {k: sum(t[k] for t in totals) for k in tot}
+
+    # ---- parity: every chromosome's record stream against the reference's pinned sha256
     parity = None
     if not args.no_check:
-        rec = d_out[:n_out].cpu().numpy().tobytes()
-        fa = ctx.reconstruct(rec, rfa)
-        parity = {"roundtrip_exact": fa == tfa, "record_sha256": hashlib.sha256(rec).hexdigest(),
-                  "record_bytes": len(rec)}
+        streams = {}
+        if world > 1:
+            if rank == 0:
+                streams = gathered[0]
+        else:
+            streams = {n: results[n][0].cpu().numpy().tobytes() for n in order}
+        if rank == 0:
+            pins = load_manifest()
+            checked = [n for n in streams if n in pins and args.workload == "genome"]
+            bad = [n for n in checked if hashlib.sha256(streams[n]).hexdigest() != pins[n]["record_sha256"]]
+            parity = {"chromosomes": len(streams), "pinned_checked": len(checked), "pinned_mismatch": bad,
+                      "reference": "oracle/_ref (compression.cpp compiled unchanged), tests/golden/genome_manifest.json"}
+            if args.workload == "chr1":
+                parity["record_sha256"] = hashlib.sha256(next(iter(streams.values()))).hexdigest()
+            if bad:
+                raise SystemExit(f"bench: record streams differ from the reference for {bad}")
+
+    # ---- configs[3]: the chr1 record stream back to FASTA on this GPU (rank 0, outside the step)
+    decomp = None
+    if rank == 0 and not args.no_decomp and keep_chr1 is not None:
+        name = "chr1" if "chr1" in results else f"chr1_r{rank}"
+        rfa_h, tfa_h = keep_chr1
+        dr, rn, _, _ = pairs[name]
+        rec = results[name][0]
+        ctx = lanes[0].ctx
+        s = lanes[0].stream
+        need = ctx.reconstruct_device(dr.data_ptr(), rn, rec.data_ptr(), rec.numel(), 0, 0, s.cuda_stream)
+        d_fa = torch.empty(need + 64, dtype=torch.uint8, device=dev)
+        ks = max(3, args.steps)
+        ctx.reconstruct_device(dr.data_ptr(), rn, rec.data_ptr(), rec.numel(), d_fa.data_ptr(), need + 64, s.cuda_stream)
+        ctx.profile(not args.no_prof)
+        s.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(ks):
+            n_fa = ctx.reconstruct_device(dr.data_ptr(), rn, rec.data_ptr(), rec.numel(), d_fa.data_ptr(), need + 64,
+                                          s.cuda_stream)
+        s.synchronize()
+        ddt = (time.perf_counter() - t1) / ks
+        dprof = ctx.profile_get()
+        ctx.profile(False)
+        exact = d_fa[:n_fa].cpu().numpy().tobytes() == tfa_h
+        nTd = ctx.stats()["target_bases"]
+        b_dec = rec.numel() + rn + n_fa + nTd   # SURVEY §8(d) B_decomp = |rec| + |R| + |T_fa| + |T_matched| (<= |T|)
+        decomp = {"workload": "BASELINE configs[3]: chr1 record stream -> FASTA on 1 GPU", "target_bases": nTd,
+                  "ms": ddt * 1e3, "bases_per_s": nTd / ddt, "roundtrip_exact": exact,
+                  "roofline_job": {"bound": "hbm", "alg_bytes": b_dec, "achieved": b_dec / ddt / 1e9,
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": b_dec / ddt / 1e9 / HBM_PEAK_GBS},
+                  "kernels": {k: {"ms_per_call": v[0] / ks, "launches_per_call": v[1] / ks} for k, v in dprof.items()}}
+        if not exact:
+            raise SystemExit("bench: chr1 reconstruction differs from the target FASTA")
 
     if rank == 0:
-        nT = st["target_bases"]
-        value = world * nT * args.steps / dt
-        shape = {"target_bases": nT, "reference_bases": st["reference_bases"], "tgt_fa": len(tfa), "ref_fa": len(rfa)}
+        value = job["target_bases"] * args.steps / dt
+        ms_step = dt * 1e3 / args.steps
         kernels = {k: {"ms_per_step": v[0] / args.steps, "launches_per_step": v[1] / args.steps,
                        "avg_launch_ms": v[0] / v[1]} for k, v in prof.items()}
         roof = None
         if prof:
             dom = max(prof, key=lambda k: prof[k][0])
-            avg_ms = prof[dom][0] / prof[dom][1]
-            alg = algorithmic_bytes(dom, shape)
-            if dom == "walk":
-                # whole-walk algorithmic bytes (2 B per target base: T' once + R' along matches)
-                alg = 2.0 * nT * args.steps / prof[dom][1]
-            if alg is not None:
+            alg_step = kernel_alg_bytes(dom, tot)
+            if alg_step is not None:
+                launches_step = prof[dom][1] / args.steps
+                avg_ms = prof[dom][0] / prof[dom][1]
+                alg = alg_step / launches_step
                 achieved = alg / (avg_ms * 1e-3) / 1e9
-                traffic = load_pmc(dom)
                 roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                        "traffic": traffic, "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms}
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                        "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms,
+                        "alg_model": "SURVEY §8(d): walk = 0.5 B per target base (packed T' + packed R' along matches)"
+                        if dom == "walk" else "DESIGN.md §4"}
+                pmc = load_pmc(dom)
+                if pmc:
+                    roof["traffic"] = pmc["hbm_bytes_per_launch"]
+                    roof["traffic_over_alg"] = round(pmc["hbm_bytes_per_launch"] / alg, 3)
+                    roof["traffic_source"] = pmc["source"]
+        nRp = sum(results[n][1]["reference_bases"] for n in order)   # |R'| <= |R| (N erased); bound
+        b_job = sum(job_alg_bytes(results[n][1]["target_bases"], results[n][1]["reference_bases"],
+                                  results[n][1]["reference_bases"], int(results[n][0].numel())) for n in order)
+        if world > 1:
+            b_job = b_job * job["target_bases"] / max(1, tot["target_bases"])   # other ranks: same model per base
+        roof_job = {"bound": "hbm", "alg_bytes_per_step": b_job, "achieved": b_job / (ms_step * 1e-3) / 1e9,
+                    "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                    "frac": b_job / (ms_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
+                    "model": "SURVEY §8(d) B_global = 1.25(|T|+|R|) + 0.25|R| + 4|R'| + 0.5|T| + |out| (|R'| taken as |R|)"}
+        del nRp
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.cpu_sample)
+            cpu = cpu_baseline(args.cpu_timeout)
+        per = {n: {"mode": "global" if results[n][1]["mode_global"] else "local",
+                   "rounds": results[n][1]["walk_rounds"], "matches": results[n][1]["n_matches"],
+                   "record_bytes": int(results[n][0].numel())} for n in order}
+        wl = ("hg19-vs-hg18 whole genome: 24 chromosome pairs at UCSC lengths (BASELINE configs[2])"
+              if args.workload == "genome" else "hg19-vs-hg18 chr1-sized pair per GPU (BASELINE configs[1] shape)")
         line = {
             "metric": METRIC,
             "value": value,
@@ -220,26 +417,42 @@ def main() -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": dt * 1e3 / args.steps,
+            "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.workload == "genome" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (tools/synth.c hg profile, seed 1+rank); real hg18/hg19 unavailable offline",
-            "config": {"workload": "hg19-vs-hg18 chr1-sized pair (BASELINE configs[1]), one pair per GPU",
-                       "reference_bases": st["reference_bases"], "target_bases": nT,
-                       "mode": "global" if st["mode_global"] else "local",
-                       "switch_segment": st["switch_segment"], "matches": st["n_matches"],
-                       "walk_rounds": st["walk_rounds"], "walk_chunks": st["walk_chunks"],
-                       "parallelism": f"chromosome-sharded x{world}, RCCL gather of record streams"},
+            "data": "synthetic (tools/synth.c hg profile, seed = chromosome index); real hg18/hg19 unavailable offline",
+            "config": {"workload": wl, "chromosomes": len(jobs), "pairs_rank0": len(order),
+                       "target_bases": job["target_bases"], "reference_bases": job["reference_bases"],
+                       "k": 14, "m": 100, "params": "reference constants (compression.cpp:373-379), local controller on",
+                       "contexts_per_gpu": n_lanes, "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                       "parallelism": f"LPT chromosome shard x{world}, RCCL gather of record streams to rank 0",
+                       "record_bytes": job["record_bytes"]},
             "roofline": roof,
+            "roofline_job": roof_job,
             "cpu_baseline": cpu,
             "parity": parity,
+            "decompress": decomp,
             "kernels": kernels,
+            "per_chromosome_rank0": per,
         }
         print(json.dumps(line), flush=True)
+    for ln in lanes:
+        ln.ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def load_pmc(kernel: str) -> dict | None:
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of this bench."""
+    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        doc = json.load(open(path))
+        v = doc.get(kernel, {}).get("hbm_bytes_per_launch")
+        return {"hbm_bytes_per_launch": v, "source": doc.get("_source", path)} if v else None
+    except Exception:
+        return None
 
 
 if __name__ == "__main__":

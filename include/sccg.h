@@ -9,6 +9,8 @@
  * Entry point                         replaces (reference file:line)
  * ----------------------------------  -------------------------------------------------------------
  * sccg_compress / _device             compress_genome up to the 7z call  compression.cpp:320-580
+ * sccg_compress_files                 the same from FASTA files to the   compression.cpp:181-220,
+ *                                     record file                         :320-331
  *   (_ex: with parameter overrides      of its constants                   compression.cpp:373-379)
  *                                     (read_genomes_from_files :181-220, lowercase/N run lines
  *                                     :341-368/:495-555, local loop :372-481, global pass
@@ -44,6 +46,9 @@ extern "C" {
 #define SCCG_E_PARSE        7  /* malformed run line / token (decompression.cpp:309-311) */
 #define SCCG_E_UNSUPPORTED  8  /* shape outside what sccg_match accepts (see below) */
 #define SCCG_E_INTERNAL     9  /* internal consistency check failed */
+#define SCCG_E_OPEN_REF    10  /* reference FASTA cannot be opened / read (compression.cpp:187-191) */
+#define SCCG_E_OPEN_TGT    11  /* target FASTA cannot be opened / read (compression.cpp:202-206) */
+#define SCCG_E_WRITE       12  /* the record file cannot be written (compression.cpp:329-331) */
 
 typedef struct sccg_ctx sccg_ctx;
 
@@ -117,6 +122,15 @@ int sccg_compress_ex(sccg_ctx* ctx, const sccg_params* params, const char* ref_f
 int sccg_compress_device_ex(sccg_ctx* ctx, const sccg_params* params, const void* d_ref_fa,
                             size_t ref_len, const void* d_tgt_fa, size_t tgt_len, void* d_out,
                             size_t out_cap, size_t* out_len, void* stream);
+
+/* Files in, record file out (compression.cpp:320-580 up to, excluding, the 7z call): reads both
+ * FASTA files (host threads, pinned staging, the copies to HBM overlapped with the reading and the
+ * reference's GPU work), compresses on the GPU and writes `out_path` (the bytes sccg_compress
+ * returns).  params NULL = the reference's constants.  *out_len (optional) = bytes written.
+ * SCCG_E_OPEN_REF / _OPEN_TGT when an input cannot be opened (nothing written), SCCG_E_WRITE when
+ * the output cannot; SCCG_E_DELTA_STOI writes the un-delta'd text as the reference does. */
+int sccg_compress_files(sccg_ctx* ctx, const sccg_params* params, const char* ref_path, const char* tgt_path,
+                        const char* out_path, size_t* out_len);
 
 /* match_sequences(Sr, St, k, m, global, offset) on already-uppercased byte strings.  Accepted
  * shapes: global == 0 with |Sr| <= 1000 and |St| <= 1000 (the local-segment kernel), or

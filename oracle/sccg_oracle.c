@@ -45,9 +45,10 @@ static void sb_reserve(sb_t* b, size_t extra) {
     b->cap = nc;
 }
 static void sb_put(sb_t* b, const char* s, size_t n) {
+    if (!n && b->d) return;
     sb_reserve(b, n);
     if (b->oom) return;
-    memcpy(b->d + b->n, s, n);
+    if (n) memcpy(b->d + b->n, s, n);
     b->n += n;
     b->d[b->n] = 0;
 }
@@ -195,11 +196,13 @@ static int kindex_build(kindex_t* ix, const char* s, int64_t n, int k) {
         else if (wide) { ix->pure2[ix->npure].code = code; ix->pure2[ix->npure++].pos = (int32_t)st; }
         else ix->pure[ix->npure++] = (code << 32) | (uint64_t)st;
     }
-    if (wide) qsort(ix->pure2, (size_t)ix->npure, sizeof(kpos_t), cmp_kpos);
-    else if (ix->npure < 4096) qsort(ix->pure, (size_t)ix->npure, sizeof(uint64_t), cmp_u64);
-    else radix_sort_u64_hi(ix->pure, ix->npure, 2 * k);
+    if (ix->npure > 1) {   /* (the arrays may be NULL when empty) */
+        if (wide) qsort(ix->pure2, (size_t)ix->npure, sizeof(kpos_t), cmp_kpos);
+        else if (ix->npure < 4096) qsort(ix->pure, (size_t)ix->npure, sizeof(uint64_t), cmp_u64);
+        else radix_sort_u64_hi(ix->pure, ix->npure, 2 * k);
+    }
     g_cmp_s = s; g_cmp_k = k;
-    qsort(ix->exo, (size_t)ix->nexo, sizeof(int32_t), cmp_exo);
+    if (ix->nexo > 1) qsort(ix->exo, (size_t)ix->nexo, sizeof(int32_t), cmp_exo);
     return ORC_OK;
 }
 
@@ -656,7 +659,7 @@ static int parse_positions(const char* s, size_t n, ivec_t* out) {
         }
     }
     if (out->oom) return ORC_E_ALLOC;
-    qsort(out->v, (size_t)out->n, sizeof(int), cmp_int);
+    if (out->n > 1) qsort(out->v, (size_t)out->n, sizeof(int), cmp_int);   /* (v may be NULL when empty) */
     return ORC_OK;
 }
 

@@ -47,35 +47,32 @@ int main(int argc, char* argv[]) {
     }
     std::cout << "Successfully created output folder: " << out_dir << "\n";
     const auto t0 = std::chrono::high_resolution_clock::now();
-    std::string ref, tgt;
-    if (!slurp(ref_path, ref)) {
-        std::cerr << "Error opening reference file: " << ref_path << "\n";
-        return 1;
-    }
-    if (!slurp(tgt_path, tgt)) {
-        std::cerr << "Error opening target file: " << tgt_path << "\n";
-        return 1;
-    }
     sccg_ctx* ctx = nullptr;
     int rc = sccg_ctx_create(cli_device(), &ctx);
     if (rc) {
         std::cerr << "Error: no usable GPU (sccg_ctx_create rc=" << rc << ")\n";
         return 1;
     }
-    sccg_buf text{};
-    rc = sccg_compress_ex(ctx, &prm, ref.data(), ref.size(), tgt.data(), tgt.size(), &text);
+    // files -> record file in the library (pinned staging, reads overlapped with the GPU work)
+    std::filesystem::create_directories(out_dir);
+    const std::string txt = out_dir + "/compressed_genome.txt";
+    rc = sccg_compress_files(ctx, &prm, ref_path.c_str(), tgt_path.c_str(), txt.c_str(), nullptr);
+    if (rc == SCCG_E_OPEN_REF || rc == SCCG_E_OPEN_TGT) {   // compression.cpp:189 / :204
+        std::cerr << (rc == SCCG_E_OPEN_REF ? "Error opening reference file: " : "Error opening target file: ")
+                  << (rc == SCCG_E_OPEN_REF ? ref_path : tgt_path) << "\n";
+        sccg_ctx_destroy(ctx);
+        return 1;
+    }
+    if (rc == SCCG_E_WRITE) {
+        std::cerr << "Greska pri otvaranju datoteke: " << txt << "\n";
+        sccg_ctx_destroy(ctx);
+        return 1;
+    }
     if (rc && rc != SCCG_E_DELTA_STOI) {
         std::cerr << "Error: " << sccg_last_error(ctx) << " (rc=" << rc << ")\n";
         sccg_ctx_destroy(ctx);
         return 1;
     }
-    std::filesystem::create_directories(out_dir);
-    const std::string txt = out_dir + "/compressed_genome.txt";
-    if (!spit(txt, text.data, text.len)) {
-        std::cerr << "Greska pri otvaranju datoteke: " << txt << "\n";
-        return 1;
-    }
-    sccg_buf_free(&text);
     sccg_stats st{};
     sccg_last_stats(ctx, &st);
     sccg_ctx_destroy(ctx);

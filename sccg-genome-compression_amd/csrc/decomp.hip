@@ -118,7 +118,8 @@ __global__ void k_run_finish(const int64_t* __restrict__ dex, const int64_t* __r
         const int64_t st = dex[r] + dlt[r];
         const int64_t pst = r ? dex[r - 1] + dlt[r - 1] : INT64_MIN;
         const int64_t pend = r ? pst + len[r - 1] : 0;
-        if (st < 0 || st > INT32_MAX || (r && st < pend)) atomicOr(err, 1);
+        // (the formatter keeps run ends in int32: a run must also END within int32)
+        if (st < 0 || st + (int64_t)len[r] > INT32_MAX || (r && st < pend)) atomicOr(err, 1);
         start[r] = (int32_t)st;
         len64[r] = len[r];
     }

@@ -26,7 +26,7 @@ struct Registry {
     std::vector<Pending> pending;
     double ms[PROF_COUNT] = {};
     int64_t n[PROF_COUNT] = {};
-    hipEvent_t open[PROF_COUNT] = {};
+    uint64_t epoch = 0;   // bumped by sccg_profile: begin events of an earlier epoch are dropped
 
     hipEvent_t take() {
         if (!pool.empty()) {
@@ -64,6 +64,13 @@ const char* const NAMES[PROF_COUNT] = {
     "dc_decode", "dc_format",
 };
 
+// each host thread brackets its own launches (several contexts may launch the same family at once)
+struct Open {
+    hipEvent_t e[PROF_COUNT] = {};
+    uint64_t epoch[PROF_COUNT] = {};
+};
+thread_local Open t_open;
+
 }  // namespace
 
 void prof_begin(hipStream_t s, int id) {
@@ -72,18 +79,20 @@ void prof_begin(hipStream_t s, int id) {
     std::lock_guard<std::mutex> g(r.mu);
     hipEvent_t e = r.take();
     (void)hipEventRecord(e, s);
-    r.open[id] = e;
+    t_open.e[id] = e;
+    t_open.epoch[id] = r.epoch;
 }
 
 void prof_end(hipStream_t s, int id) {
     Registry& r = reg();
     if (!r.on) return;
     std::lock_guard<std::mutex> g(r.mu);
-    if (!r.open[id]) return;
+    if (!t_open.e[id]) return;
+    if (t_open.epoch[id] != r.epoch) { r.pool.push_back(t_open.e[id]); t_open.e[id] = nullptr; return; }
     hipEvent_t e = r.take();
     (void)hipEventRecord(e, s);
-    r.pending.push_back({id, r.open[id], e});
-    r.open[id] = nullptr;
+    r.pending.push_back({id, t_open.e[id], e});
+    t_open.e[id] = nullptr;
     if (r.pending.size() > 4096) r.drain();
 }
 
@@ -94,7 +103,8 @@ int sccg_profile(sccg_ctx* /*ctx*/, int enable) {
     std::lock_guard<std::mutex> g(r.mu);
     r.drain();
     r.on = enable != 0;
-    for (int i = 0; i < PROF_COUNT; i++) { r.ms[i] = 0; r.n[i] = 0; r.open[i] = nullptr; }
+    r.epoch++;
+    for (int i = 0; i < PROF_COUNT; i++) { r.ms[i] = 0; r.n[i] = 0; }
     return SCCG_OK;
 }
 

@@ -14,6 +14,11 @@
 #include <algorithm>
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
@@ -136,6 +141,12 @@ struct sccg_ctx {
     sccg_stats stats{};
     void* buf[B_COUNT] = {};
     size_t cap[B_COUNT] = {};
+    // sccg_compress_files: pinned staging slots (STAGE_THREADS readers x STAGE_SLOTS), one copy
+    // stream per input file, allocated on first use
+    uint8_t* stage[16] = {};
+    hipEvent_t stage_ev[16] = {};
+    hipStream_t copy_ref = nullptr, copy_tgt = nullptr;
+    hipEvent_t ev_ref_in = nullptr, ev_tgt_in = nullptr;
     void* cls_buf = nullptr;   // local segment classes: buffer the generation tags refer to
     size_t cls_cap = 0;
     int32_t cls_gen = 0;
@@ -236,6 +247,14 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_hdr);
     (void)hipEventDestroy(ctx->ev_local);
     if (ctx->h_switch) (void)hipHostFree(ctx->h_switch);
+    for (int i = 0; i < 16; i++) {
+        if (ctx->stage[i]) (void)hipHostFree(ctx->stage[i]);
+        if (ctx->stage_ev[i]) (void)hipEventDestroy(ctx->stage_ev[i]);
+    }
+    if (ctx->copy_ref) (void)hipStreamDestroy(ctx->copy_ref);
+    if (ctx->copy_tgt) (void)hipStreamDestroy(ctx->copy_tgt);
+    if (ctx->ev_ref_in) (void)hipEventDestroy(ctx->ev_ref_in);
+    if (ctx->ev_tgt_in) (void)hipEventDestroy(ctx->ev_tgt_in);
     (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->side2);
     (void)hipStreamDestroy(ctx->stream);
@@ -351,8 +370,18 @@ int check_params(sccg_ctx* ctx, const sccg_params& P) {
     return 0;
 }
 
+// Host-side readiness of the two FASTA texts (sccg_compress_files): each hook blocks until that
+// file's bytes are all queued on a copy stream and returns an event behind them; the pipeline waits
+// on it right before the first kernel that reads the file, so the reference's strip (and the R'
+// sweep behind it) run while the target is still being read.
+struct InputReady {
+    int (*ref)(void* user, hipEvent_t* ev);
+    int (*tgt)(void* user, hipEvent_t* ev);
+    void* user;
+};
+
 int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa, int64_t rn, const uint8_t* tfa,
-                         int64_t tn, uint8_t* out, int64_t out_cap, int64_t* out_len) {
+                         int64_t tn, uint8_t* out, int64_t out_cap, int64_t* out_len, const InputReady* rdy = nullptr) {
     hipStream_t s = ctx->stream;
     if (const int rc = check_params(ctx, P)) return rc;
     // local = 0: no local pass, the global pass from the start (compression.cpp:378, :484)
@@ -388,8 +417,18 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     global_prepare_reset();
     HIPTRY(hipEventRecord(ctx->ev_fork, s));
     HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    if (rdy) {
+        hipEvent_t e = nullptr;
+        if (const int rc = rdy->ref(rdy->user, &e)) return rc;
+        HIPTRY(hipStreamWaitEvent(ctx->side, e, 0));
+    }
     TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side));
     HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
+    if (rdy) {
+        hipEvent_t e = nullptr;
+        if (const int rc = rdy->tgt(rdy->user, &e)) return rc;
+        HIPTRY(hipStreamWaitEvent(s, e, 0));
+    }
     TRY(launch_find_header(tfa, tn, sc, s));
     HIPTRY(hipEventRecord(ctx->ev_hdr, s));
     TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
@@ -652,6 +691,186 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     return SCCG_OK;
 }
 
+
+// -------------------------------------------------------------------------------------------
+// FASTA files -> compressed_genome.txt (read_genomes_from_files, compression.cpp:181-220, up to the
+// record file of :329, without 7z).  STAGE_THREADS host threads read both files in STAGE_PIECE
+// pieces with pread() into pinned slots (two per thread), and each piece goes to HBM on its file's
+// copy stream as soon as it is read; the reference is read first, so its strip and the R' sweep
+// run on the GPU while the target is still being read.  The record text comes back through the
+// same pinned slots, a piece at a time, and is written as it arrives.
+// -------------------------------------------------------------------------------------------
+constexpr int STAGE_THREADS = 4, STAGE_SLOTS = 2;
+constexpr size_t STAGE_PIECE = (size_t)16 << 20;
+static_assert(STAGE_THREADS * STAGE_SLOTS <= 16, "sccg_ctx::stage");
+
+int staging_init(sccg_ctx* ctx) {
+    if (ctx->copy_ref) return 0;
+    for (int i = 0; i < STAGE_THREADS * STAGE_SLOTS; i++) {
+        HIPTRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->stage[i]), STAGE_PIECE, hipHostMallocDefault));
+        HIPTRY(hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming));
+    }
+    HIPTRY(hipEventCreateWithFlags(&ctx->ev_ref_in, hipEventDisableTiming));
+    HIPTRY(hipEventCreateWithFlags(&ctx->ev_tgt_in, hipEventDisableTiming));
+    HIPTRY(hipStreamCreateWithFlags(&ctx->copy_tgt, hipStreamNonBlocking));
+    HIPTRY(hipStreamCreateWithFlags(&ctx->copy_ref, hipStreamNonBlocking));
+    return 0;
+}
+
+struct FileLoad {
+    sccg_ctx* ctx;
+    int fd[2];                 // 0 reference, 1 target
+    int64_t len[2];
+    uint8_t* dst[2];           // device
+    int64_t npiece[2];
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t queued[2] = {0, 0};
+    int err = 0;               // first failure: SCCG_E_OPEN_REF / SCCG_E_OPEN_TGT / SCCG_E_HIP
+    std::string msg;
+
+    void fail(int code, const std::string& m) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!err) { err = code; msg = m; }
+        cv.notify_all();
+    }
+    // reader t: pieces t, t + STAGE_THREADS, ... of the sequence (reference pieces, then target's)
+    void reader(int t) {
+        (void)hipSetDevice(ctx->device);
+        const int64_t total = npiece[0] + npiece[1];
+        int k = 0;
+        for (int64_t p = t; p < total; p += STAGE_THREADS) {
+            { std::lock_guard<std::mutex> g(mu); if (err) return; }
+            const int f = p < npiece[0] ? 0 : 1;
+            const int64_t q = f ? p - npiece[0] : p;
+            const int64_t off = q * (int64_t)STAGE_PIECE;
+            const size_t n = (size_t)(len[f] - off < (int64_t)STAGE_PIECE ? len[f] - off : (int64_t)STAGE_PIECE);
+            const int si = t * STAGE_SLOTS + (k++ % STAGE_SLOTS);
+            if (hipEventSynchronize(ctx->stage_ev[si]) != hipSuccess) { fail(SCCG_E_HIP, "staging event"); return; }
+            size_t got = 0;
+            while (got < n) {
+                const ssize_t r = pread(fd[f], ctx->stage[si] + got, n - got, (off_t)(off + (int64_t)got));
+                if (r <= 0) {
+                    if (r < 0 && errno == EINTR) continue;
+                    fail(f ? SCCG_E_OPEN_TGT : SCCG_E_OPEN_REF, f ? "short read of the target file" : "short read of the reference file");
+                    return;
+                }
+                got += (size_t)r;
+            }
+            hipStream_t cs = f ? ctx->copy_tgt : ctx->copy_ref;
+            std::lock_guard<std::mutex> g(mu);   // the count and the copy's place on the stream together
+            if (hipMemcpyAsync(dst[f] + off, ctx->stage[si], n, hipMemcpyHostToDevice, cs) != hipSuccess ||
+                hipEventRecord(ctx->stage_ev[si], cs) != hipSuccess) {
+                if (!err) { err = SCCG_E_HIP; msg = "staging copy"; }
+                cv.notify_all();
+                return;
+            }
+            queued[f]++;
+            cv.notify_all();
+        }
+    }
+    // blocks until every piece of file f is queued; records ev behind them on f's copy stream
+    int ready(int f, hipEvent_t ev) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return err || queued[f] == npiece[f]; });
+        if (err) return err;
+        if (hipEventRecord(ev, f ? ctx->copy_tgt : ctx->copy_ref) != hipSuccess) return SCCG_E_HIP;
+        return 0;
+    }
+    static int ref_ready(void* u, hipEvent_t* e) {
+        FileLoad* L = static_cast<FileLoad*>(u);
+        *e = L->ctx->ev_ref_in;
+        return L->ready(0, *e);
+    }
+    static int tgt_ready(void* u, hipEvent_t* e) {
+        FileLoad* L = static_cast<FileLoad*>(u);
+        *e = L->ctx->ev_tgt_in;
+        return L->ready(1, *e);
+    }
+};
+
+int write_all(int fd, const uint8_t* p, size_t n) {
+    while (n) {
+        const ssize_t w = write(fd, p, n);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return -1;
+        }
+        p += w;
+        n -= (size_t)w;
+    }
+    return 0;
+}
+
+int compress_files_impl(sccg_ctx* ctx, const sccg_params& P, const char* ref_path, const char* tgt_path,
+                        const char* out_path, int64_t* out_len) {
+    // open both inputs first, in the reference's order and with its failure points (:187-191, :202-206)
+    struct Fd {
+        int v = -1;
+        ~Fd() { if (v >= 0) close(v); }
+    } fr, ft;
+    fr.v = open(ref_path, O_RDONLY);
+    if (fr.v < 0) return ctx->fail(SCCG_E_OPEN_REF, "Error opening reference file: %s", ref_path);
+    ft.v = open(tgt_path, O_RDONLY);
+    if (ft.v < 0) return ctx->fail(SCCG_E_OPEN_TGT, "Error opening target file: %s", tgt_path);
+    struct stat sr{}, stt{};
+    if (fstat(fr.v, &sr) || !S_ISREG(sr.st_mode)) return ctx->fail(SCCG_E_OPEN_REF, "reference is not a regular file: %s", ref_path);
+    if (fstat(ft.v, &stt) || !S_ISREG(stt.st_mode)) return ctx->fail(SCCG_E_OPEN_TGT, "target is not a regular file: %s", tgt_path);
+    TRY(staging_init(ctx));
+    const int64_t rn = (int64_t)sr.st_size, tn = (int64_t)stt.st_size;
+    uint8_t* drf = reinterpret_cast<uint8_t*>(ctx->get(B_RFA, (size_t)rn + 16));
+    uint8_t* dtf = reinterpret_cast<uint8_t*>(ctx->get(B_TFA, (size_t)tn + 16));
+    const size_t cap = sccg_compress_bound((size_t)rn, (size_t)tn);
+    uint8_t* dout = reinterpret_cast<uint8_t*>(ctx->get(B_OUT, cap));
+    if (!drf || !dtf || !dout) return ctx->fail(SCCG_E_NOMEM, "device allocation failed");
+
+    FileLoad L;
+    L.ctx = ctx;
+    L.fd[0] = fr.v; L.fd[1] = ft.v;
+    L.len[0] = rn; L.len[1] = tn;
+    L.dst[0] = drf; L.dst[1] = dtf;
+    L.npiece[0] = (rn + (int64_t)STAGE_PIECE - 1) / (int64_t)STAGE_PIECE;
+    L.npiece[1] = (tn + (int64_t)STAGE_PIECE - 1) / (int64_t)STAGE_PIECE;
+    std::vector<std::thread> th;
+    for (int t = 0; t < STAGE_THREADS; t++) th.emplace_back([&L, t] { L.reader(t); });
+    struct Join {
+        std::vector<std::thread>& th;
+        FileLoad& L;
+        ~Join() {
+            for (auto& x : th) if (x.joinable()) x.join();
+        }
+    } join{th, L};
+    const InputReady rdy{&FileLoad::ref_ready, &FileLoad::tgt_ready, &L};
+    int64_t len = 0;
+    int rc = compress_device_impl(ctx, P, drf, rn, dtf, tn, dout, (int64_t)cap, &len, &rdy);
+    for (auto& x : th) x.join();
+    if (L.err) return ctx->fail(L.err, "%s", L.msg.c_str());
+    if (rc && rc != SCCG_E_DELTA_STOI) return rc;   // DELTA_STOI still writes the file's text
+    // the record file (compression.cpp:329-331): a piece at a time through the pinned slots
+    Fd fo;
+    fo.v = open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fo.v < 0) return ctx->fail(SCCG_E_WRITE, "cannot open %s for writing", out_path);
+    const int64_t np = (len + (int64_t)STAGE_PIECE - 1) / (int64_t)STAGE_PIECE;
+    for (int64_t p = 0; p < np + 1; p++) {
+        if (p < np) {   // copy piece p while piece p - 1 is written
+            const int64_t off = p * (int64_t)STAGE_PIECE;
+            const size_t n = (size_t)(len - off < (int64_t)STAGE_PIECE ? len - off : (int64_t)STAGE_PIECE);
+            HIPTRY(hipMemcpyAsync(ctx->stage[p & 1], dout + off, n, hipMemcpyDeviceToHost, ctx->stream));
+            HIPTRY(hipEventRecord(ctx->stage_ev[p & 1], ctx->stream));
+        }
+        if (p > 0) {
+            const int64_t q = p - 1, off = q * (int64_t)STAGE_PIECE;
+            const size_t n = (size_t)(len - off < (int64_t)STAGE_PIECE ? len - off : (int64_t)STAGE_PIECE);
+            HIPTRY(hipEventSynchronize(ctx->stage_ev[q & 1]));
+            if (write_all(fo.v, ctx->stage[q & 1], n)) return ctx->fail(SCCG_E_WRITE, "write to %s failed", out_path);
+        }
+    }
+    if (close(fo.v)) { fo.v = -1; return ctx->fail(SCCG_E_WRITE, "closing %s failed", out_path); }
+    fo.v = -1;
+    *out_len = len;
+    return rc;
+}
+
 // -------------------------------------------------------------------------------------------
 // reconstruction (decompression.cpp)
 // -------------------------------------------------------------------------------------------
@@ -839,6 +1058,19 @@ int sccg_compress_ex(sccg_ctx* ctx, const sccg_params* params, const char* ref_f
     h[len] = 0;
     out_text->data = h;
     out_text->len = (size_t)len;
+    return rc;
+}
+
+int sccg_compress_files(sccg_ctx* ctx, const sccg_params* params, const char* ref_path, const char* tgt_path,
+                        const char* out_path, size_t* out_len) {
+    if (!ctx || !ref_path || !tgt_path || !out_path) return SCCG_E_INVALID;
+    sccg_params p;
+    sccg_params_default(&p);
+    if (params) p = *params;
+    HIPTRY(hipSetDevice(ctx->device));
+    int64_t len = 0;
+    const int rc = compress_files_impl(ctx, p, ref_path, tgt_path, out_path, &len);
+    if (out_len) *out_len = (size_t)len;
     return rc;
 }
 

@@ -1014,6 +1014,7 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
     __shared__ uint32_t tab[1 << CH_TBITS];
     __shared__ int32_t wsum[17];
     __shared__ int32_t trunc_s;
+    __shared__ int32_t s_first;
     if (!A.chs[0]) return;
     const int tid = (int)threadIdx.x, lane = lane_id(), w = wave_in_block(), k = A.k;
     const int32_t x = A.chs[1], P = A.chs[2];
@@ -1065,9 +1066,17 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
     int32_t cnt = 0;
     int64_t covered = b1;   // first position of the span not covered (b1: all of it)
     for (int64_t base = b0; base < b1; base += 16 * 1024) {
-        if (first_only && base > (int64_t)__hip_atomic_load(&A.chs[13], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            covered = base;   // a hit lies before this block's rest: the step never gets here
-            break;
+        if (first_only) {
+            // block-uniform decision: one load of the shared first hit, seen by every wave (a
+            // per-thread load could split the block between breaking and meeting the barriers)
+            if (tid == 0) s_first = __hip_atomic_load(&A.chs[13], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            const bool stop = base > (int64_t)s_first;
+            __syncthreads();   // s_first is rewritten next step
+            if (stop) {
+                covered = base;   // a hit lies before this block's rest: the step never gets here
+                break;
+            }
         }
         const int64_t p0 = base + 16 * tid;
         uint32_t mask = 0;
@@ -2205,8 +2214,10 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.ctext = c.take<int64_t>(C + 1);
     A.chs = c.take<int32_t>(16);
     {
+        // k_chain_step hands back at CH_HANDBACK_N matches, so no chain stores more than that
         const int64_t mc = nT / k + 2;
-        A.chm_cap = (int32_t)(mc < CHAIN_MCAP ? mc : CHAIN_MCAP);
+        const int64_t lim = CH_HANDBACK_N + 1 < CHAIN_MCAP ? CH_HANDBACK_N + 1 : CHAIN_MCAP;
+        A.chm_cap = (int32_t)(mc < lim ? mc : lim);
     }
     A.chm_t = c.take<int32_t>((size_t)A.chm_cap);
     A.chm_p = c.take<int32_t>((size_t)A.chm_cap);
@@ -2749,12 +2760,15 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 RC(frozen_batch(0, FROZEN_FIRST, false));   // fy was set by k_commit
                 RC(dev_readback(&rs_item, 1, s));
             }
-            // A chain pays where rounds would resolve a frozen stretch hit by hit: a frozen chunk in
-            // round 1 (only chunk 0 is exact there, so the true walk froze at once), or frozen chunks
-            // still turning up from round SCCG_CHAIN_ROUND (default 10) on.  Earlier frozen chunks (N
-            // gaps of aligned pairs, short frozen stretches) stay with the blind batches.  Measured
-            // (start round 3 / 6 / 10): synthetic chr22 2.3 / 1.7 / 1.7 ms, 20 Mb T2T-like pair 5.5 /
-            // 5.7 / 5.7 ms, 100 Mb T2T-like pair 14.0 / 14.4-17.6 / 12.4 ms (23 ms without chains).
+            // A chain pays where rounds would resolve a frozen stretch hit by hit: frozen chunks still
+            // turning up from round SCCG_CHAIN_ROUND (default 10) on.  (A frozen chunk in round 1 --
+            // only chunk 0 is exact there, so the true walk froze at once -- starts one too, but only
+            // on the host-first-step path: the default device-first path queues rounds 1 and 2
+            // before its first readback and starts this loop at round 2, where round 2's frozen
+            // chunks stay with the blind batches.)  Earlier frozen chunks (N gaps of aligned pairs,
+            // short frozen stretches) stay with the blind batches.  Measured (start round 3 / 6 /
+            // 10): synthetic chr22 2.3 / 1.7 / 1.7 ms, 20 Mb T2T-like pair 5.5 / 5.7 / 5.7 ms, 100 Mb
+            // T2T-like pair 14.0 / 14.4-17.6 / 12.4 ms (23 ms without chains).
             static const int chain_round = [] { const char* e = getenv("SCCG_CHAIN_ROUND"); const int v = e ? atoi(e) : 10; return v >= 2 ? v : 10; }();
             const bool chain_now = chains_on && rs[5] > 0 && (round == 1 || round >= chain_round);
             if (chain_now) {

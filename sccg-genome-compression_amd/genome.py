@@ -23,6 +23,8 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+SCCG_E_IO = 100   # a FASTA file could not be read (host side; no library call was made)
+
 
 class Emitter:
     """Rank 0's output side: <out>/<name>/compressed_genome.txt (compression.cpp:329) and the
@@ -39,10 +41,18 @@ class Emitter:
         self.done: set[str] = set()
 
     def emit(self, name: str, rec: bytes, rc_n: int) -> None:
+        try:
+            self._emit(name, rec, rc_n)
+        except OSError as e:   # an unwritable output folder: this chromosome fails, the job goes on
+            print(f"Error: {name}: {e}", file=sys.stderr)
+            self.rc = 1
+
+    def _emit(self, name: str, rec: bytes, rc_n: int) -> None:
         import sccg
         self.done.add(name)
         if rc_n and rc_n != sccg.SCCG_E_DELTA_STOI:
-            print(f"Error: {name}: {sccg.ERRORS.get(rc_n, rc_n)}", file=sys.stderr)
+            what = "cannot read the FASTA files" if rc_n == SCCG_E_IO else sccg.ERRORS.get(rc_n, rc_n)
+            print(f"Error: {name}: {what}", file=sys.stderr)
             self.rc = 1
             return
         d = os.path.join(self.out_dir, name)
@@ -67,6 +77,80 @@ class Emitter:
                 self.rc = 1
         self.procs = []
         return self.rc
+
+
+def compress_shard(mine: list[str], ref_dir: str, tgt_dir: str, make_ctx, em: Emitter | None,
+                   err_hip: int) -> tuple[dict, dict]:
+    """Compress this rank's pairs.  Never raises: a rank that fails (no context, an unreadable
+    file, a failing pair) must still enter the gather, or every other rank would hang in the
+    collective.  Failures become per-pair error codes (rc) that travel with the stats; rank 0
+    reports them as the reference CLI would (compression.cpp:188-191, 203-206: exit 1).
+    `make_ctx()` returns an object with compress(ref, tgt) / stats() / close() (sccg.Context)."""
+    import sccg
+    parts: dict[str, bytes] = {}
+    stats: dict[str, dict] = {}
+    ctx = None
+    try:
+        ctx = make_ctx()
+    except Exception as e:   # noqa: BLE001
+        print(f"Error: no context: {e}", file=sys.stderr)
+    for n in mine:
+        rec, rc_n, st = b"", 0, {}
+        try:
+            ref = open(os.path.join(ref_dir, n + ".fa"), "rb").read()
+            tgt = open(os.path.join(tgt_dir, n + ".fa"), "rb").read()
+        except OSError as e:
+            print(f"Error: {n}: {e}", file=sys.stderr)
+            rc_n = SCCG_E_IO
+        if not rc_n and ctx is None:
+            rc_n = err_hip
+        if not rc_n:
+            # keep a failing pair's rc and whatever text it produced, as the reference CLI does
+            try:
+                rec = ctx.compress(ref, tgt)
+                st = ctx.stats()
+            except sccg.SccgError as e:
+                rec, rc_n = getattr(e, "partial", None) or b"", e.rc
+            except Exception as e:   # noqa: BLE001
+                print(f"Error: {n}: {e}", file=sys.stderr)
+                rec, rc_n = b"", err_hip
+        stats[n] = dict(st, rc=rc_n)
+        if em is not None:
+            em.emit(n, rec, rc_n)      # rank 0's own chromosomes: 7z starts now
+        else:
+            parts[n] = rec
+    if ctx is not None:
+        try:
+            ctx.close()
+        except Exception:   # noqa: BLE001
+            pass
+    return parts, stats
+
+
+def collect(names: list[str], parts: dict, stats: dict, em: Emitter | None, dev, world: int) -> dict:
+    """The job's exchange: every rank's record texts and stats to rank 0 (multigpu.gather_records
+    + gather_to_root); rank 0 emits the chromosomes it did not compress itself (a pair no rank
+    reported counts as failed).  Returns all stats on rank 0, this rank's elsewhere."""
+    import torch
+    import multigpu
+    if world <= 1:
+        return stats
+    merged = multigpu.gather_records(parts, device=dev)
+    st_blob = json.dumps(stats).encode()
+    got = multigpu.gather_to_root(torch.frombuffer(bytearray(st_blob), dtype=torch.uint8).to(dev), len(st_blob))
+    if got is None:
+        return stats
+    all_stats: dict = {}
+    for g in got:
+        all_stats.update(json.loads(g.cpu().numpy().tobytes()))
+    for n in names:
+        if n not in em.done:
+            if n in merged and n in all_stats:
+                em.emit(n, merged[n], all_stats[n]["rc"])
+            else:
+                print(f"Error: {n}: no rank reported it", file=sys.stderr)
+                em.rc = 1
+    return all_stats
 
 
 def main(argv=None) -> int:
@@ -101,37 +185,10 @@ def main(argv=None) -> int:
     em = Emitter(args.out, not args.no_7z) if rank == 0 else None
 
     t0 = time.perf_counter()
-    parts: dict[str, bytes] = {}
-    stats: dict[str, dict] = {}
-    with sccg.Context(local) as ctx:
-        for n in mine:
-            ref = open(os.path.join(args.ref_dir, n + ".fa"), "rb").read()
-            tgt = open(os.path.join(args.tgt_dir, n + ".fa"), "rb").read()
-            # a failing pair must not leave this rank out of the gather (the others would hang):
-            # keep its rc and whatever text it produced, as the reference CLI does
-            try:
-                rec, rc_n = ctx.compress(ref, tgt), 0
-            except sccg.SccgError as e:
-                rec, rc_n = getattr(e, "partial", None) or b"", e.rc
-            stats[n] = dict(ctx.stats(), rc=rc_n)
-            if em is not None:
-                em.emit(n, rec, rc_n)      # rank 0's own chromosomes: 7z starts now
-            else:
-                parts[n] = rec
+    parts, stats = compress_shard(mine, args.ref_dir, args.tgt_dir, lambda: sccg.Context(local), em,
+                                  sccg.ERR_CODES["SCCG_E_HIP"])
     t_comp = time.perf_counter() - t0
-    all_stats = stats
-    if world > 1:
-        merged = multigpu.gather_records(parts, device=dev)
-        st_blob = json.dumps(stats).encode()
-        got = multigpu.gather_to_root(torch.frombuffer(bytearray(st_blob), dtype=torch.uint8).to(dev),
-                                      len(st_blob))
-        if got is not None:
-            all_stats = {}
-            for g in got:
-                all_stats.update(json.loads(g.cpu().numpy().tobytes()))
-            for n in names:
-                if n not in em.done:
-                    em.emit(n, merged[n], all_stats[n]["rc"])
+    all_stats = collect(names, parts, stats, em, dev, world)
     rc = 0
     if rank == 0:
         rc = em.wait()

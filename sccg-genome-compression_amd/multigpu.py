@@ -3,8 +3,8 @@
 SCCG compresses one chromosome pair per invocation and pairs are independent,
 so the multi-GPU job is: LPT-assign pairs to ranks (largest target first onto the least-loaded
 rank), compress locally, then move every rank's record texts to rank 0 -- the job's only data
-exchange -- with one size all-gather and one padded all-gather (RCCL over xGMI with the "nccl"
-backend on GPUs; "gloo" on CPU for tests).
+exchange -- with one all-gather of the int64 sizes and one gather of the (max-size) packed streams
+to rank 0 only (RCCL over xGMI with the "nccl" backend on GPUs; "gloo" on CPU for tests).
 """
 from __future__ import annotations
 

@@ -20,7 +20,8 @@ SCCG_OK = 0
 SCCG_E_DELTA_STOI = 4
 ERRORS = {1: "SCCG_E_INVALID", 2: "SCCG_E_HIP", 3: "SCCG_E_NOMEM", 4: "SCCG_E_DELTA_STOI",
           5: "SCCG_E_FORMAT", 6: "SCCG_E_RANGE", 7: "SCCG_E_PARSE", 8: "SCCG_E_UNSUPPORTED",
-          9: "SCCG_E_INTERNAL"}
+          9: "SCCG_E_INTERNAL", 10: "SCCG_E_OPEN_REF", 11: "SCCG_E_OPEN_TGT", 12: "SCCG_E_WRITE"}
+ERR_CODES = {v: k for k, v in ERRORS.items()}
 
 
 class SccgError(RuntimeError):
@@ -80,6 +81,8 @@ def load_library():
         lib.sccg_params_default.argtypes = [ctypes.POINTER(Params)]
         lib.sccg_compress_ex.argtypes = [vp, ctypes.POINTER(Params), c, sz, c, sz, ctypes.POINTER(Buf)]
         lib.sccg_compress_device_ex.argtypes = [vp, ctypes.POINTER(Params), vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
+    if hasattr(lib, "sccg_compress_files"):
+        lib.sccg_compress_files.argtypes = [vp, ctypes.POINTER(Params), c, c, c, ctypes.POINTER(sz)]
     lib.sccg_compress_bound.argtypes = [sz, sz]
     lib.sccg_compress_bound.restype = sz
     lib.sccg_match.argtypes = [vp, c, sz, c, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64,
@@ -168,6 +171,17 @@ class Context:
             raise err
         return self._take(buf)
 
+    def compress_files(self, ref_path: str, tgt_path: str, out_path: str, **overrides) -> int:
+        """FASTA files -> record file out_path (sccg_compress_files: compression.cpp:181-220, :320-331,
+        without 7z); returns the bytes written.  SCCG_E_DELTA_STOI raises after writing the file."""
+        n = ctypes.c_size_t()
+        prm = ctypes.byref(self.params(**overrides)) if overrides else None
+        rc = self.lib.sccg_compress_files(self.ptr, prm, os.fsencode(ref_path), os.fsencode(tgt_path),
+                                          os.fsencode(out_path), ctypes.byref(n))
+        if rc:
+            self._err(rc)
+        return n.value
+
     def reconstruct(self, record: bytes, ref_fa: bytes) -> bytes:
         """Bytes of reconstructed_genome.fa (decompression.cpp after 7z)."""
         buf = Buf()
@@ -218,6 +232,11 @@ class Context:
 
     def compress_bound(self, ref_len: int, tgt_len: int) -> int:
         return self.lib.sccg_compress_bound(ref_len, tgt_len)
+
+    @staticmethod
+    def compress_bound_static(ref_len: int, tgt_len: int) -> int:
+        """sccg_compress_bound without a context (it needs no device)."""
+        return load_library().sccg_compress_bound(ref_len, tgt_len)
 
     def match(self, sr: bytes, st: bytes, k: int, m: int, glob: bool, offset: int = 0):
         """match_sequences (compression.cpp:36) -> [(kind, p, l, t)] like the oracle's records."""

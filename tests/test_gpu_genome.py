@@ -1,0 +1,91 @@
+"""GPU parity at full size: BASELINE configs[2] (the whole hg19-vs-hg18 genome, 24 pairs) and the
+100 Mb T2T-like pair (configs[4]'s stuck / literal-heavy path), each record stream against the
+sha256 of the REAL reference's output (oracle/_ref = compression.cpp compiled unchanged, run in the
+build container by tests/golden/pin_genome.py -> tests/golden/genome_manifest.json).
+
+Each pair goes through the device-resident C ABI (sccg_compress_device), as bench.py runs it, and
+the chr21 / T2T pairs also through the host API and the round trip (sccg_reconstruct).
+"""
+import hashlib
+import json
+import os
+import threading
+
+import pytest
+
+import synthlib
+from pkg import sccg
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+MANIFEST = os.path.join(HERE, "golden", "genome_manifest.json")
+
+
+def _manifest():
+    if not os.path.exists(MANIFEST):
+        return []
+    return json.load(open(MANIFEST))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = sccg.Context(0)
+    yield c
+    c.close()
+
+
+def _device_compress(ctx, rfa, tfa):
+    import torch
+    dev = torch.device("cuda", 0)
+    d_r = torch.frombuffer(bytearray(rfa), dtype=torch.uint8).to(dev)
+    d_t = torch.frombuffer(bytearray(tfa), dtype=torch.uint8).to(dev)
+    cap = ctx.compress_bound(len(rfa), len(tfa))
+    d_o = torch.empty(cap, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream(dev)
+    n = ctx.compress_device(d_r.data_ptr(), len(rfa), d_t.data_ptr(), len(tfa), d_o.data_ptr(), cap, s.cuda_stream)
+    rec = d_o[:n].cpu().numpy().tobytes()
+    del d_r, d_t, d_o
+    return rec
+
+
+def test_genome_24_pairs_vs_reference(ctx):
+    pins = [e for e in _manifest() if e["profile"] == "hg"]
+    if len(pins) < 24:
+        pytest.skip("genome manifest incomplete")
+    # generate in a few threads (the C generator releases the GIL), compress in order
+    bad, done = [], {}
+
+    def gen(e):
+        done[e["name"]] = synthlib.synth_pair("hg", e["ref_len"], e["tgt_len"], e["seed"])
+
+    for b in range(0, len(pins), 6):
+        ths = [threading.Thread(target=gen, args=(e,)) for e in pins[b:b + 6]]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        for e in pins[b:b + 6]:
+            rfa, tfa = done.pop(e["name"])
+            assert hashlib.sha256(tfa).hexdigest() == e["tgt_fa_sha256"], e["name"]
+            rec = _device_compress(ctx, rfa, tfa)
+            if len(rec) != e["record_len"] or hashlib.sha256(rec).hexdigest() != e["record_sha256"]:
+                bad.append(e["name"])
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["chr21", "t2t100"])
+def test_pinned_pair_host_api_and_roundtrip(ctx, name):
+    e = {m["name"]: m for m in _manifest()}.get(name)
+    if e is None:
+        pytest.skip(f"{name} not pinned")
+    rfa, tfa = synthlib.synth_pair(e["profile"], e["ref_len"], e["tgt_len"], e["seed"])
+    rec = ctx.compress(rfa, tfa)
+    assert hashlib.sha256(rec).hexdigest() == e["record_sha256"]
+    if name == "t2t100":
+        st = ctx.stats()
+        assert st["mode_global"] == 1
+        # the walk rounds stay bounded on the stuck path (compression.cpp:83-101)
+        assert st["walk_rounds"] < 64, st
+    fa = ctx.reconstruct(rec, rfa)
+    assert hashlib.sha256(fa).hexdigest() == e["fasta_sha256"]

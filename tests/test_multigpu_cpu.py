@@ -137,3 +137,79 @@ def test_emitter_status_and_7z(tmp_path):
     em2 = genome.Emitter(str(out), True, str(fake))
     em2.emit("chr4", b"x", 0)
     assert em2.wait() == 0
+
+
+class _FakeCtx:
+    """Stands in for sccg.Context on CPU: the record text is a function of the two inputs."""
+
+    def compress(self, ref, tgt):
+        return b"REC:" + tgt[::-1] + b"|" + ref[:3]
+
+    def stats(self):
+        return {"target_bases": 0}
+
+    def close(self):
+        pass
+
+
+def _genome_worker(rank, world, port, q, root):
+    import torch
+    import torch.distributed as dist
+    import genome
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names = ["chrA", "chrB", "chrC", "chrD", "chrE"]
+        sizes = [os.path.getsize(os.path.join(root, "tgt", n + ".fa")) for n in names]
+        mine = [names[i] for i in multigpu.lpt_shard(sizes, world)[rank]]
+        em = genome.Emitter(os.path.join(root, "out"), False) if rank == 0 else None
+
+        def make_ctx():
+            if rank == 1:
+                raise RuntimeError("no usable GPU (injected)")
+            return _FakeCtx()
+
+        parts, stats = genome.compress_shard(mine, os.path.join(root, "ref"), os.path.join(root, "tgt"), make_ctx, em, 2)
+        all_stats = genome.collect(names, parts, stats, em, torch.device("cpu"), world)
+        rc = em.wait() if rank == 0 else None
+        q.put((rank, mine, rc, {n: v["rc"] for n, v in all_stats.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_genome_failing_rank_gloo_world2(tmp_path):
+    """A rank whose context cannot be created still enters the gather: no hang; its chromosomes
+    come back failed (rc), the healthy rank's are written, and the job's rc is 1 (genome.py)."""
+    root = tmp_path
+    for d in ("ref", "tgt"):
+        (root / d).mkdir()
+    for i, n in enumerate(["chrA", "chrB", "chrC", "chrD", "chrE"]):
+        (root / "ref" / f"{n}.fa").write_bytes(b">r\nACGT" * (i + 1))
+        (root / "tgt" / f"{n}.fa").write_bytes(b">t\nTTGCA" * (5 - i) * 3)
+    (root / "tgt" / "chrE.fa").write_bytes(b">t\nAC")
+    os.remove(root / "ref" / "chrE.fa")   # an unreadable pair on whichever rank holds it
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_genome_worker, args=(r, 2, port, q, str(root))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (mine, rc, st) for r, mine, rc, st in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    mine0, rc0, st0 = res[0]
+    mine1, _, _ = res[1]
+    assert rc0 == 1
+    import genome
+    for n in mine1:
+        assert st0[n] != 0   # rank 1 had no context (or the file is missing)
+        assert not (root / "out" / n).exists()
+    for n in mine0:
+        if n == "chrE":
+            assert st0[n] == genome.SCCG_E_IO
+            continue
+        assert st0[n] == 0
+        tgt = (root / "tgt" / f"{n}.fa").read_bytes()
+        ref = (root / "ref" / f"{n}.fa").read_bytes()
+        assert (root / "out" / n / "compressed_genome.txt").read_bytes() == _FakeCtx().compress(ref, tgt)
