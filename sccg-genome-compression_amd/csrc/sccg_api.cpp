@@ -54,6 +54,8 @@ enum Slot {
     B_DX, B_DELTA,
     // a second FASTA-strip scratch set (the reference strips beside the target, on the side stream)
     B_TILE2_A, B_TILE2_B, B_TILE2_FA, B_TILE2_FB, B_TILE2_LAST, B_TILE2_OFF, B_TILE2_OFF2, B_TILE2_CARRY, B_TILE2_BSUM,
+    // 2-bit packed R' / T' (codes, exception bits) for the global walk
+    B_RQ, B_RX, B_TQ, B_TX,
     B_COUNT
 };
 
@@ -424,6 +426,13 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     }
     TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side));
     HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
+    // R' and T' 2-bit packed for the walk (|R'|, |T'| read on the device; FASTA lengths bound them)
+    GET(uint32_t, rq, B_RQ, pack_q_words(rn));
+    GET(uint32_t, rx, B_RX, pack_x_words(rn));
+    GET(uint32_t, tq, B_TQ, pack_q_words(tn));
+    GET(uint32_t, tx, B_TX, pack_x_words(tn));
+    const PackedSeq pr{rq, rx}, pt{tq, tx};
+    TRY(launch_pack_seq(Rp, rn, sc + 8, rq, rx, ctx->side));
     if (rdy) {
         hipEvent_t e = nullptr;
         if (const int rc = rdy->tgt(rdy->user, &e)) return rc;
@@ -432,6 +441,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     TRY(launch_find_header(tfa, tn, sc, s));
     HIPTRY(hipEventRecord(ctx->ev_hdr, s));
     TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
+    TRY(launch_pack_seq(Tp, tn, sc + 3, tq, tx, s));
     // ---- header + lowercase line (compression.cpp:337-368) and the N line: side2, driven by the
     //      context's host worker (its launches wait on run counts).  They need only T, so they are
     //      queued right behind the target's strip -- ahead of the local pass and the walk, which
@@ -553,7 +563,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     const int64_t np[2] = {lt[1], lr[1]};
     void* ws = ctx->get(B_WALK, wsb);
     if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
-    TRY(global_prepare(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, s2));
+    TRY(global_prepare(Rp, np[1], Tp, np[0], pr, pt, kg, mg, walk_chunk(tn), ws, wsb, s2));
     HIPTRY(hipEventRecord(ctx->ev_join, s2));
     if (local_order == 1 || iters <= 0 || force_global) TRY(launch_local(s2));
 
@@ -626,7 +636,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
                },
                [&](hipStream_t st) -> int { return local_order == 2 ? ensure_local(st) : 0; }};
         const EmitTarget target{&Late::call, &late, &Late::abandon, &Late::round1};
-        const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
+        const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], pr, pt, kg, mg, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
                                              s2, paren, &target, /*keep_flat=*/false);
         if (rc != WALK_ABANDONED) {
             TRY(rc);
@@ -1160,13 +1170,20 @@ int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, s
         GET(uint8_t, T, B_TP, nt + 64);
         if (nr) HIPTRY(hipMemcpyAsync(R, sr, nr, hipMemcpyHostToDevice, s));
         if (nt) HIPTRY(hipMemcpyAsync(T, st, nt, hipMemcpyHostToDevice, s));
+        GET(uint32_t, rq, B_RQ, pack_q_words((int64_t)nr));
+        GET(uint32_t, rx, B_RX, pack_x_words((int64_t)nr));
+        GET(uint32_t, tq, B_TQ, pack_q_words((int64_t)nt));
+        GET(uint32_t, tx, B_TX, pack_x_words((int64_t)nt));
+        TRY(launch_pack_seq(R, (int64_t)nr, nullptr, rq, rx, s));
+        TRY(launch_pack_seq(T, (int64_t)nt, nullptr, tq, tx, s));
+        const PackedSeq pr{rq, rx}, pt{tq, tx};
         const size_t wsb = walk_workspace_bytes((int64_t)nr, (int64_t)nt, k, walk_chunk((int64_t)nt));
         void* ws = ctx->get(B_WALK, wsb);
         GET(uint8_t, txt, B_OUT, 4 * nt + 64);
         if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace");
         WalkResult wr{};
         int64_t tl = 0;
-        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, k, m, walk_chunk((int64_t)nt), ws, wsb, txt, &tl, &wr, s));
+        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, pr, pt, k, m, walk_chunk((int64_t)nt), ws, wsb, txt, &tl, &wr, s));
         const int32_t *dt, *dp, *dl;
         int64_t nm;
         global_matches(ws, &dt, &dp, &dl, &nm);
