@@ -45,9 +45,10 @@ sys.path.insert(0, PKG_DIR)
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "target bases compressed/sec at 1/2/4/8 GPUs; bit-exact record stream vs CPU ref"
 MANIFEST = os.path.join(REPO, "tests", "golden", "genome_manifest.json")
-# Hardware queues per process for the default run: C contexts x 3 streams + torch's stream must not
-# share queues (a queue serialises its streams' kernels).  HIP's default is 4; at most 32 here.
-HW_QUEUES_DEFAULT = 12
+# GPU_MAX_HW_QUEUES for the run: 0 keeps the environment's (HIP's default, 4).  Measured on the
+# genome bench (profiles/r03_ab.txt): 2 contexts with 4 queues 24.1-24.5 ms per step, with 8 queues
+# 28.0-28.3 ms, 3 contexts with 8-12 queues 26.0-31.3 ms, 1 context 29.8-29.9 ms.
+HW_QUEUES_DEFAULT = 0
 
 
 def log(*a):
@@ -267,17 +268,25 @@ def main() -> None:
     results: dict = {}      # name -> (device tensor of its record text, stats)
     errors: list = []
 
-    def run_shard() -> None:
-        nxt = [0]
-        qlock = threading.Lock()
+    # persistent lane threads: a step releases them through one barrier and joins them at another
+    # (no thread start per step)
+    nxt = [0]
+    qlock = threading.Lock()
+    go = threading.Barrier(n_lanes + 1)
+    done = threading.Barrier(n_lanes + 1)
+    stop = [False]
 
-        def worker(lane: Lane) -> None:
+    def worker(lane: Lane) -> None:
+        torch.cuda.set_device(dev)
+        while True:
+            go.wait()
+            if stop[0]:
+                return
             try:
-                torch.cuda.set_device(dev)
                 while True:
                     with qlock:
                         if nxt[0] >= len(order):
-                            return
+                            break
                         name = order[nxt[0]]
                         nxt[0] += 1
                     dr, rn, dt_, tn = pairs[name]
@@ -290,14 +299,18 @@ def main() -> None:
                             torch.empty(n, dtype=torch.uint8, device=dev)
                         buf.copy_(lane.out[:n])   # the pair's record stream, kept for the gather
                     results[name] = (buf, st)
-            except Exception as e:   # noqa: BLE001 -- reported after the join
+            except Exception as e:   # noqa: BLE001 -- reported after the step
                 errors.append(e)
+            done.wait()
 
-        ths = [threading.Thread(target=worker, args=(ln,)) for ln in lanes]
-        for t in ths:
-            t.start()
-        for t in ths:
-            t.join()
+    lane_threads = [threading.Thread(target=worker, args=(ln,), daemon=True) for ln in lanes]
+    for t in lane_threads:
+        t.start()
+
+    def run_shard() -> None:
+        nxt[0] = 0
+        go.wait()
+        done.wait()
         if errors:
             raise errors[0]
 
@@ -474,6 +487,10 @@ def main() -> None:
             "per_chromosome_rank0": per,
         }
         print(json.dumps(line), flush=True)
+    stop[0] = True
+    go.wait()
+    for t in lane_threads:
+        t.join()
     for ln in lanes:
         ln.ctx.close()
     if world > 1:

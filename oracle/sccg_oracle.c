@@ -339,6 +339,65 @@ static int match_core(const kindex_t* H, const char* sr, int nr, const char* st,
     return out->oom ? ORC_E_ALLOC : ORC_OK;
 }
 
+/* The global walk of match_core (compression.cpp:64-161, global = 1) from an arbitrary state
+ * (index = x0, prev_match_end = P0) up to the first state with index >= x_end: its match records
+ * (kind 1, t = target index; literals are the gaps) and that exit state.  Two walks that reach the
+ * same (index, P) are identical afterwards -- the property the chunked GPU walk and the
+ * cross-GPU split of one chromosome rest on.  TEST INFRASTRUCTURE ONLY. */
+int orc_walk_range(const char* sr, int64_t nr, const char* st, int64_t nt, int k, int m, int64_t x0, int64_t P0,
+                   int64_t x_end, orc_rec** recs, int64_t* nrec, int64_t* exit_x, int64_t* exit_P) {
+    kindex_t H;
+    recv_t v = {0};
+    int rc = kindex_build(&H, sr, nr, k);
+    if (rc != ORC_OK) { *recs = NULL; *nrec = 0; return rc; }
+    int index = (int)x0, pme = (int)P0;
+    const int ntk = (int)nt - k + 1;
+    while (index < ntk && index < x_end) {
+        int64_t lo, hi; int pm;
+        kindex_lookup(&H, st + index, &lo, &hi, &pm);
+        int take_literal = (lo == hi);
+        if (!take_literal) {
+            int in_range = 0;
+            for (int64_t j = lo; j < hi; j++) {
+                int p = kindex_pos(&H, pm, j);
+                if (pme == -1 || iabs(p - pme) <= m) { in_range = 1; break; }
+            }
+            take_literal = !in_range;
+        }
+        if (take_literal) { index++; continue; }
+        int lmax1 = 0, lmax2 = 0, pn1 = 0, pn2 = 0, ln1 = 0, ln2 = 0;
+        for (int64_t j = lo; j < hi; j++) {
+            int p = kindex_pos(&H, pm, j);
+            int l = extend_len(sr, (int)nr, st, (int)nt, p, index, k);
+            if (pme == -1 || iabs(p - pme) <= m) {
+                if (l == lmax2) {
+                    if (pn2 == 0 || iabs(p - pme) < iabs(pn2 - pme)) pn2 = p;
+                } else if (l > lmax2) {
+                    lmax2 = l; pn2 = p; ln2 = l;
+                }
+            }
+            if (l == lmax1) {
+                if (pn1 == 0 || iabs(p - pme) < iabs(pn1 - pme)) pn1 = p;
+            } else if (l > lmax1) {
+                lmax1 = l; pn1 = p; ln1 = l;
+            }
+        }
+        int fp, fl;
+        if (pn2 != 0) { fp = pn2; fl = ln2; }
+        else { fp = pn1; fl = ln1; }
+        pme = fp + fl - 1;
+        rec_push(&v, 1, fp, fl, index);
+        index += fl;
+    }
+    kindex_free(&H);
+    if (v.oom) { free(v.r); *recs = NULL; *nrec = 0; return ORC_E_ALLOC; }
+    *recs = v.r;
+    *nrec = v.n;
+    *exit_x = index;   /* >= x_end, or the walk ran out of k-mers (index >= |St| - k + 1) */
+    *exit_P = pme;
+    return ORC_OK;
+}
+
 int orc_match(const char* sr, int64_t nr, const char* st, int64_t nt, int k, int m, int global,
               int64_t offset, orc_rec** recs, int64_t* nrec) {
     kindex_t H;

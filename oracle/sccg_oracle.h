@@ -44,6 +44,11 @@ int orc_match(const char* sr, int64_t nr, const char* st, int64_t nt, int k, int
 
 /* compression.cpp:320-582 compress_genome up to (excluding) the 7z call: the exact bytes of
  * <out>/compressed_genome.txt.  On ORC_E_DELTA_STOI *out holds the un-delta'd text. */
+/* The global walk (match_sequences with global = true) from state (index x0, prev_match_end P0)
+ * until index >= x_end: match records only (literals are the gaps) and the exit state. */
+int orc_walk_range(const char* sr, int64_t nr, const char* st, int64_t nt, int k, int m, int64_t x0, int64_t P0,
+                   int64_t x_end, orc_rec** recs, int64_t* nrec, int64_t* exit_x, int64_t* exit_P);
+
 int orc_compress(const char* ref_fa, size_t ref_len, const char* tgt_fa, size_t tgt_len,
                  char** out, size_t* out_len);
 

@@ -409,6 +409,40 @@ __global__ void k_strip_scan_apply(int64_t ntiles, const int64_t* __restrict__ t
     }
 }
 
+// The wave's staged filter output (cnt bytes for positions [g0, g0 + cnt)) 2-bit packed into pq / px
+// (internal.h PackedSeq): every lane takes 32-base groups (one exception word, two code words);
+// groups wholly inside the range are stored, the two edge groups shared with the neighbouring
+// tiles are OR-ed into the zero-filled arrays (launch_fasta_strip clears them first).
+__device__ __forceinline__ void stage_pack(const uint8_t* __restrict__ st, int cnt, int64_t g0, uint32_t* __restrict__ pq,
+                                           uint32_t* __restrict__ px) {
+    if (cnt <= 0) return;
+    const int64_t g1 = g0 + cnt;
+    for (int64_t W = (g0 >> 5) + lane_id(); W <= ((g1 - 1) >> 5); W += 64) {
+        const int64_t b = W << 5;
+        uint32_t c0 = 0, c1 = 0, xb = 0;
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            const int64_t g = b + i;
+            if (g < g0 || g >= g1) continue;
+            const uint32_t c = st[g - g0];
+            const uint32_t code = ((c >> 1) ^ (c >> 2)) & 3u;
+            const bool acgt = c == 'A' || c == 'C' || c == 'G' || c == 'T';
+            if (i < 16) c0 |= code << (2 * i);
+            else c1 |= code << (2 * (i - 16));
+            if (!acgt) xb |= 1u << i;
+        }
+        if (b >= g0 && b + 32 <= g1) {
+            pq[2 * W] = c0;
+            pq[2 * W + 1] = c1;
+            px[W] = xb;
+        } else {
+            if (c0) atomicOr(&pq[2 * W], c0);
+            if (c1) atomicOr(&pq[2 * W + 1], c1);
+            if (xb) atomicOr(&px[W], xb);
+        }
+    }
+}
+
 template <IngestMode MODE>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n,
                                                             const int64_t* __restrict__ hdr,
@@ -416,7 +450,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
                                                             const int64_t* __restrict__ toff2,
                                                             const int32_t* __restrict__ tcarry,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
-                                                            int32_t* __restrict__ flags) {
+                                                            int32_t* __restrict__ flags, uint32_t* __restrict__ pq,
+                                                            uint32_t* __restrict__ px) {
     __shared__ uint32_t stage_all[WPB][STAGE_WORDS];
     __shared__ uint32_t tab[16];
     if (threadIdx.x < 16) tab[threadIdx.x] = compact_sel(threadIdx.x);
@@ -446,6 +481,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
         stage_lane<true>(s1, tab, w, fkeep, (int)(ex >> 16));
         wave_sync();
         stage_out(st4, (int)(tot >> 16), out2, toff2[tile]);
+        if (pq) stage_pack(s1, (int)(tot >> 16), toff2[tile], pq, px);
     }
 }
 
@@ -584,7 +620,7 @@ int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t
 
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,
                        int64_t* d_len, int32_t* d_flags, const IngestScratch& sc, hipStream_t s, FilterMode fmode,
-                       uint8_t* out2, int64_t* d_len2) {
+                       uint8_t* out2, int64_t* d_len2, uint32_t* pq, uint32_t* px) {
     if (n <= 0) {
         SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));
         if (d_len2) SCCG_HIP(hipMemsetAsync(d_len2, 0, sizeof(int64_t), s));
@@ -608,13 +644,20 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     hipLaunchKernelGGL(k_strip_scan_apply, dim3(grid_for(ntiles, 256)), dim3(256), 0, s, ntiles, sc.tile_a, sc.tile_b,
                        sc.tile_fa, sc.tile_fb, sc.tile_last, btot, sc.tile_off, sc.tile_off2, sc.tile_carry, d_len,
                        d_len2);
+    if (!out2) pq = px = nullptr;
+    if (pq) {   // edge groups are OR-ed in: zero the blocks the strip can reach (<= n bases)
+        SCCG_HIP(hipMemsetAsync(pq, 0, (size_t)pack_q_words(n) * 4, s));
+        SCCG_HIP(hipMemsetAsync(px, 0, (size_t)pack_x_words(n) * 4, s));
+    }
     if (mode == INGEST_TGT)
         PROF_LAUNCH(PROF_STRIP, s, k_strip_write<INGEST_TGT>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, pq, px);
     else
         PROF_LAUNCH(PROF_STRIP, s, k_strip_write<INGEST_REF>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, pq, px);
     SCCG_HIP(hipGetLastError());
+    // the block holding the sequence end and the padding: exception bits past the end
+    if (pq) return launch_pack_seq_from(out2, n, d_len2, pq, px, 64, s);
     return 0;
 }
 

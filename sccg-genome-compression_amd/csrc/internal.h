@@ -89,7 +89,7 @@ int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, 
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header,
                        uint8_t* out, int64_t* d_len, int32_t* d_flags, const IngestScratch& sc,
                        hipStream_t s, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
-                       int64_t* d_len2 = nullptr);
+                       int64_t* d_len2 = nullptr, uint32_t* pq = nullptr, uint32_t* px = nullptr);
 // maximal runs of lowercase bytes (rs_l/re_l) and of N/n bytes (rs_n/re_n), start/end inclusive,
 // in one pass; d_nruns[0..1] = their counts
 int launch_runs2(const uint8_t* s_in, int64_t n, int32_t* rs_l, int32_t* re_l, int32_t* rs_n, int32_t* re_n,
@@ -144,6 +144,10 @@ __host__ __device__ inline int64_t pack_q_words(int64_t n) { return 4 * pack_blo
 __host__ __device__ inline int64_t pack_x_words(int64_t n) { return 2 * pack_blocks(n); }
 // packs s[0, n) (n = *d_n when d_n is given; n_bound >= it sizes the grid and the padding) into q / x
 int launch_pack_seq(const uint8_t* s, int64_t n_bound, const int64_t* d_n, uint32_t* q, uint32_t* x, hipStream_t st);
+// the same for the blocks from the first one at or past position n - kfrom + 1 only (kfrom = 64: the
+// block holding position n on; the strip packs the blocks before it)
+int launch_pack_seq_from(const uint8_t* s, int64_t n_bound, const int64_t* d_n, uint32_t* q, uint32_t* x, int kfrom,
+                         hipStream_t st);
 struct WalkWorkspace;  // defined in walk.hip
 struct WalkResult {
     int64_t n_matches;
@@ -166,7 +170,9 @@ void global_prepare_reset();   // forget a preparation that will not be used
 // global_prepare on the same ws/R' only extends those positions once T' exists.  |R'| is read on
 // the device from d_nRp (no host round trip); nRp_bound >= |R'| sizes the workspace and the anchor
 // table (ws must hold walk_workspace_bytes(nRp_bound, tn, ...)).
-int global_sweep_early(const uint8_t* Rp, int64_t nRp_bound, const int64_t* d_nRp, const uint8_t* tgt_fa, int64_t tn,
+// It also writes R' 2-bit packed into rq / rx (PackedSeq, sized for nRp_bound).
+int global_sweep_early(const uint8_t* Rp, int64_t nRp_bound, const int64_t* d_nRp, uint32_t* rq, uint32_t* rx,
+                       const uint8_t* tgt_fa, int64_t tn,
                        const int64_t* d_hdr, int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s);
 // Where the record text goes, when the caller learns it only during the walk: resolve() is called
 // once, after the rounds and before the text is written, and returns the output pointer.

@@ -304,7 +304,7 @@ int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n, hipStream_t s = 
 // (set 1: the second scratch set, so two strips can run at once; s: stream, default the context's)
 int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const int64_t* d_hdr, uint8_t* out,
           int64_t* d_len, int32_t* d_flags, int64_t* h_len, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
-          int set = 0, hipStream_t s = nullptr) {
+          int set = 0, hipStream_t s = nullptr, uint32_t* pq = nullptr, uint32_t* px = nullptr) {
     const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE + 1;
     const int o = set ? B_TILE2_A - B_TILE_A : 0;
     static_assert(B_TILE_BSUM - B_TILE_A == B_TILE2_BSUM - B_TILE2_A, "scratch sets line up");
@@ -321,7 +321,7 @@ int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const in
     sc.tile_a = ta; sc.tile_b = tb; sc.tile_fa = tfa; sc.tile_fb = tfb; sc.tile_last = tl; sc.tile_off = to;
     sc.tile_off2 = to2; sc.tile_carry = tc; sc.block_sums = bs; sc.scalars = nullptr;
     TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, s ? s : ctx->stream, fmode, out2,
-                           out2 ? d_len + 1 : nullptr));
+                           out2 ? d_len + 1 : nullptr, pq, px));
     return h_len ? d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1, s) : 0;   // h_len null: the caller reads d_len later
 }
 
@@ -426,13 +426,13 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     }
     TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side));
     HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
-    // R' and T' 2-bit packed for the walk (|R'|, |T'| read on the device; FASTA lengths bound them)
+    // R' and T' 2-bit packed for the walk (|R'|, |T'| read on the device; FASTA lengths bound them):
+    // R' by the early sweep (global_sweep_early), T' behind its strip
     GET(uint32_t, rq, B_RQ, pack_q_words(rn));
     GET(uint32_t, rx, B_RX, pack_x_words(rn));
     GET(uint32_t, tq, B_TQ, pack_q_words(tn));
     GET(uint32_t, tx, B_TX, pack_x_words(tn));
     const PackedSeq pr{rq, rx}, pt{tq, tx};
-    TRY(launch_pack_seq(Rp, rn, sc + 8, rq, rx, ctx->side));
     if (rdy) {
         hipEvent_t e = nullptr;
         if (const int rc = rdy->tgt(rdy->user, &e)) return rc;
@@ -440,8 +440,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     }
     TRY(launch_find_header(tfa, tn, sc, s));
     HIPTRY(hipEventRecord(ctx->ev_hdr, s));
-    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
-    TRY(launch_pack_seq(Tp, tn, sc + 3, tq, tx, s));
+    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp, 0, nullptr, tq, tx));
     // ---- header + lowercase line (compression.cpp:337-368) and the N line: side2, driven by the
     //      context's host worker (its launches wait on run counts).  They need only T, so they are
     //      queued right behind the target's strip -- ahead of the local pass and the walk, which
@@ -497,7 +496,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
         void* ws_early = ctx->get(B_WALK, wsb);
         if (!ws_early) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
-        TRY(global_sweep_early(Rp, rn, sc + 8, tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb, ctx->side));
+        TRY(global_sweep_early(Rp, rn, sc + 8, rq, rx, tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb, ctx->side));
     }
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
     // ---- fork.  The local pass (compression.cpp:372-474, main stream) is latency-bound; the

@@ -501,12 +501,16 @@ __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L
 // loads, the SWAR codes of common.h, one 16-byte code store and one 8-byte exception store.
 // HBM: 1 B read + 0.375 B written per base.
 // ---------------------------------------------------------------------------------------------
+// (kfrom > 0: only the blocks a k_sweep_early<true> with k = kfrom did not pack: from the first
+// block at or past its last k-mer start on)
 __global__ __launch_bounds__(SCCG_BLOCK) void k_pack_seq(const uint8_t* __restrict__ s, int64_t n_bound,
                                                          const int64_t* __restrict__ d_n, uint32_t* __restrict__ q,
-                                                         uint32_t* __restrict__ x) {
+                                                         uint32_t* __restrict__ x, int kfrom) {
     const int64_t n = d_n ? *d_n : n_bound;
     const int64_t nblk = pack_blocks(n_bound);
-    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t npos = n - kfrom + 1 > 0 ? n - kfrom + 1 : 0;
+    const int64_t b0 = kfrom > 0 ? (npos + 63) / 64 : 0;
+    for (int64_t b = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += (int64_t)gridDim.x * blockDim.x) {
         const int64_t p0 = 64 * b;
         uint32_t cw[4] = {0, 0, 0, 0}, xw[2] = {~0u, ~0u};
         if (p0 < n) {
@@ -1800,6 +1804,20 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
                   },
                   [&](int64_t p0, const uint32_t (&cw)[20], const uint32_t (&dw)[20], uint32_t acc) {
                       if (!ANCH) return;
+                      if (A.Rq) {   // the 2-bit packed R' of this 64-base block (k_pack_seq's layout)
+                          uint32_t q4[4];
+#pragma unroll
+                          for (int j = 0; j < 4; j++)
+                              q4[j] = cw[4 * j] | (cw[4 * j + 1] << 8) | (cw[4 * j + 2] << 16) | (cw[4 * j + 3] << 24);
+                          uint64_t bad = 0;
+                          if (acc) {
+#pragma unroll
+                              for (int i = 0; i < 16; i++) bad |= (uint64_t)nz_bytes(dw[i]) << (4 * i);
+                          }
+                          if (nR - p0 < 64) bad |= ~0ull << (nR - p0);   // past R'
+                          reinterpret_cast<uint4*>(const_cast<uint32_t*>(A.Rq))[p0 >> 6] = make_uint4(q4[0], q4[1], q4[2], q4[3]);
+                          reinterpret_cast<uint2*>(const_cast<uint32_t*>(A.Rx))[p0 >> 6] = make_uint2((uint32_t)bad, (uint32_t)(bad >> 32));
+                      }
 #pragma unroll
                       for (int h = 0; h < 2; h++) {
                           const int64_t p = p0 + 32 * h;
@@ -2428,7 +2446,14 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s, std::vector<int32_t>* resume
 int launch_pack_seq(const uint8_t* s, int64_t n_bound, const int64_t* d_n, uint32_t* q, uint32_t* x, hipStream_t st) {
     const int64_t nblk = pack_blocks(n_bound);
     const unsigned g = grid_for(nblk, SCCG_BLOCK) > 16384 ? 16384 : grid_for(nblk, SCCG_BLOCK);
-    hipLaunchKernelGGL(k_pack_seq, dim3(g), dim3(SCCG_BLOCK), 0, st, s, n_bound, d_n, q, x);
+    hipLaunchKernelGGL(k_pack_seq, dim3(g), dim3(SCCG_BLOCK), 0, st, s, n_bound, d_n, q, x, 0);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_pack_seq_from(const uint8_t* s, int64_t n_bound, const int64_t* d_n, uint32_t* q, uint32_t* x, int kfrom,
+                         hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_seq, dim3(64), dim3(SCCG_BLOCK), 0, st, s, n_bound, d_n, q, x, kfrom);
     SCCG_HIP(hipGetLastError());
     return 0;
 }
@@ -2541,11 +2566,12 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 
 void global_prepare_reset() { g_prep = Prepared{}; g_early = Early{}; }
 
-int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, const uint8_t* tgt_fa, int64_t tn,
-                       const int64_t* d_hdr, int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s) {
+int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, uint32_t* rq, uint32_t* rx,
+                       const uint8_t* tgt_fa, int64_t tn, const int64_t* d_hdr, int k, int m, int chunk, void* ws,
+                       size_t ws_bytes, hipStream_t s) {
     g_early = Early{};
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
-    if (nRp < k || tn <= 0) return 0;   // no walk can use it
+    if (nRp < k || tn <= 0) return launch_pack_seq(Rp, nRp, d_nRp, rq, rx, s);   // no walk can use the sweep
     size_t used = 0;
     // |T'| <= tn: the carve's R'-only front (anchor table, fc, positions, kb) does not depend on it;
     // nRp bounds |R'|, which the sweep reads from d_nRp
@@ -2557,8 +2583,14 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, con
     hipLaunchKernelGGL(k_first_kmer, dim3(1), dim3(SCCG_BLOCK), 0, s, tgt_fa, tn, d_hdr, k, (int64_t)1 << 20, A.kb);
     const unsigned g = first_sweep_grid(A);
     if (A.astep == 32) {
+        // the sweep packs R' as it reads it; the blocks past its last k-mer start (and the padding)
+        // are packed behind it
+        A.Rq = rq;
+        A.Rx = rx;
         PROF_LAUNCH(PROF_ANCHOR, s, k_sweep_early<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
+        hipLaunchKernelGGL(k_pack_seq, dim3(64), dim3(SCCG_BLOCK), 0, s, Rp, nRp, d_nRp, rq, rx, k);
     } else {
+        RC(launch_pack_seq(Rp, nRp, d_nRp, rq, rx, s));
         hipLaunchKernelGGL(k_sweep_early<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
         const int64_t ns = (int64_t)A.nR / A.astep + 1;
         const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);

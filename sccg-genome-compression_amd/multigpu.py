@@ -121,3 +121,73 @@ def gather_records(parts: dict[str, bytes | torch.Tensor], device: torch.device 
     for part in got:
         merged.update(unpack_records(part.cpu().numpy().tobytes()))
     return merged
+
+
+# -------------------------------------------------------------------------------------------------
+# One chromosome's global walk split across ranks.
+#
+# The reference's global pass is ONE sequential walk over T' (compression.cpp:561, :64-161) with
+# state (index, P = prev_match_end).  Two walks that reach the same state coincide afterwards, so
+# the target can be cut into per-rank ranges exactly as the GPU walk cuts it into chunks:
+#   1. rank r walks its range [h_r, h_{r+1}) from a guessed entry state (rank 0: the true start);
+#   2. rounds: every rank's exit state goes to its successor (one all-gather of 2 int64 per rank);
+#      a rank whose trajectory was not walked from its predecessor's current exit re-walks from it
+#      and splices onto its old trajectory at the first common match (after a common match the
+#      states are equal); the loop ends when no entry changed -- at most world - 1 rounds;
+#   3. the per-rank match lists go to rank 0 (the record-stream gather of the genome job).
+# The result is the single sequential walk exactly, whatever the guesses were.  `walker` is the
+# per-rank engine: walker(x0, P0, x_end) -> (matches [(t, p, l)], (exit_x, exit_P)), the walk from
+# state (x0, P0) until index >= x_end.
+# -------------------------------------------------------------------------------------------------
+def split_ranges(n_target: int, world: int) -> list[int]:
+    """Range starts h_0 = 0 < ... < h_world = n_target (equal shares)."""
+    return [n_target * r // world for r in range(world)] + [n_target]
+
+
+def splice(new: list, old: list, new_exit: tuple, old_exit: tuple) -> tuple[list, tuple, bool]:
+    """The re-walk `new` joined onto the old trajectory at their first common match: from there on
+    the two walks coincide, so the old suffix (and exit) stand.  Returns (trajectory, exit, changed)."""
+    pos = {m: i for i, m in enumerate(old)}
+    for j, m in enumerate(new):
+        i = pos.get(m)
+        if i is not None:
+            return new[:j] + old[i:], old_exit, False
+    return new, new_exit, new_exit != old_exit
+
+
+def split_walk(walker, n_target: int, guess_entry, group=None) -> list | None:
+    """Run this rank's share of one chromosome's global walk and return the whole walk's match list
+    on rank 0 (None elsewhere).  guess_entry(h) -> P: the speculative entry of a range starting at
+    h (rank 0 uses the true start, P = -1)."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    h = split_ranges(n_target, world)
+    lo, hi = h[rank], h[rank + 1]
+    entry = (0, -1) if rank == 0 else (lo, int(guess_entry(lo)))
+    traj, exit_state = walker(entry[0], entry[1], hi)
+    for _ in range(world):
+        ex = torch.tensor([exit_state[0], exit_state[1]], dtype=torch.int64)
+        exits = [torch.empty(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(exits, ex, group=group)
+        changed = 0
+        if rank > 0:
+            want = (int(exits[rank - 1][0]), int(exits[rank - 1][1]))
+            if want != entry:
+                new, new_exit = walker(want[0], want[1], hi)
+                traj, new_exit2, ch = splice(new, traj, new_exit, exit_state)
+                entry, exit_state = want, new_exit2
+                changed = int(ch) | 1   # walked again: the successors must re-check next round
+        flag = torch.tensor([changed], dtype=torch.int64)
+        dist.all_reduce(flag, group=group)
+        if int(flag.item()) == 0:
+            break
+    # gather the trajectories to rank 0 (a gatherv of int32 triples)
+    flat = torch.tensor([v for m in traj for v in m], dtype=torch.int64)
+    got = gather_to_root(flat.view(torch.uint8), flat.numel() * 8, group=group)
+    if got is None:
+        return None
+    out: list = []
+    for part in got:
+        a = part.view(torch.int64).tolist() if part.numel() else []
+        out.extend(tuple(a[i:i + 3]) for i in range(0, len(a), 3))
+    return out

@@ -99,3 +99,40 @@ def match(sr: bytes, st: bytes, k: int, m: int, glob: bool, offset: int = 0):
     out = [(recs[i].kind, recs[i].p, recs[i].l, recs[i].t) for i in range(n.value)]
     lib.orc_free(recs)
     return out
+
+
+def walk_range(sr: bytes, st: bytes, k: int, m: int, x0: int, p0: int, x_end: int):
+    """The global walk from state (x0, P0) until index >= x_end (orc_walk_range): ([(t, p, l)], (x, P))."""
+    lib = _load()
+    fn = lib.orc_walk_range
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.POINTER(OrcRec)),
+                   ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    recs, n, ex, ep = ctypes.POINTER(OrcRec)(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = fn(sr, len(sr), st, len(st), k, m, x0, p0, x_end, ctypes.byref(recs), ctypes.byref(n), ctypes.byref(ex),
+            ctypes.byref(ep))
+    if rc:
+        raise OracleError(rc)
+    out = [(recs[i].t, recs[i].p, recs[i].l) for i in range(n.value)]
+    lib.orc_free(recs)
+    return out, (ex.value, ep.value)
+
+
+def global_sequences(ref_fa: bytes, tgt_fa: bytes) -> tuple[bytes, bytes]:
+    """R', T' of the global pass: FASTA ingest (compression.cpp:181-220), toupper, N erase (:556-557)."""
+    def seq(fa: bytes, target: bool) -> bytes:
+        out, seen_hdr = [], False
+        for line in fa.split(b"\n"):
+            if target:
+                if not line:
+                    continue
+                if not seen_hdr and line[:1] == b">":
+                    seen_hdr = True
+                    continue
+            elif not line or line[:1] == b">":
+                continue
+            out.append(line)
+        s = b"".join(out)
+        s = bytes(c for c in s if c not in b" \t\n\v\f\r") if any(c in s for c in b" \t\v\f\r") else s
+        return s.upper().replace(b"N", b"")
+    return seq(ref_fa, False), seq(tgt_fa, True)
