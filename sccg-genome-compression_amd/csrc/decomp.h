@@ -34,8 +34,12 @@ int dc_n_check(const DcRuns& nr, const int64_t* d_ncnt, const int64_t* d_D, int3
 int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,
                       int64_t* d_dsum, const int64_t* d_nref, hipEvent_t nref_ready, int64_t* d_partial, int32_t* d_err,
                       int64_t* d_total, hipStream_t s);
+// (tiled path, dc_tok_tiled(): the range check against *d_nref happens here, d_err bit 2)
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
-                   const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s);
+                   const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s,
+                   const int64_t* d_nref, int32_t* d_err);
+// true: the record line takes the per-block path (its range errors are known only after the fill)
+bool dc_tok_tiled();
 // N insertion + lowercase + 50-column wrap of nres result bytes into d_out (no final '\n');
 // d_span: scratch of dc_format_span_words(nres) int64 (per-span run indices)
 int64_t dc_format_span_words(int64_t nres);

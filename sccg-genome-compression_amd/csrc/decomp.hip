@@ -12,6 +12,8 @@
 // lowercase membership found by binary search over the (sorted, disjoint) run lists.
 // Inputs the reference's own compressor can produce are handled exactly; text outside that
 // grammar is reported as SCCG_E_PARSE instead of reproducing the reference's undefined paths.
+#include <cstdlib>
+
 #include "internal.h"
 #include "decomp.h"
 
@@ -104,6 +106,183 @@ __global__ void k_run_items_parse(const uint8_t* __restrict__ s, int64_t n, cons
         dlt[r] = d;
         len[r] = (int32_t)l;
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// run lines, tiled (the usual path): one wave per 4 KiB tile, 64 bytes per lane.  A run line's
+// parentheses only open "(d,len)" items of at most 25 bytes, so the "inside an item" state at a
+// lane's first byte follows from the last parenthesis before it: in the lanes before it (a wave
+// max-scan), else in the 32 bytes before the tile (text outside the compressor's grammar is flagged
+// by the item parses either way).  Three launches per line instead of a parenthesis max-scan, an
+// item-rank scan and three prefix sums (decompression.cpp:126-207 per item, running start, sorted).
+// ---------------------------------------------------------------------------------------------
+constexpr int RL_TILE = 4096, RL_LANE = RL_TILE / 64;
+
+// one item at i: "(d,l)" or a bare "d" followed by ',' or the end (decompression.cpp:126-164)
+__device__ __forceinline__ bool rl_item(const uint8_t* s, int64_t n, int64_t i, int64_t* d, int64_t* l) {
+    *l = 1;
+    if (s[i] == '(') {
+        int64_t comma = -1, close = -1;
+        for (int64_t q = i + 1; q < n && q < i + 32; q++) {
+            if (s[q] == ',' && comma < 0) comma = q;
+            if (s[q] == ')') { close = q; break; }
+            if (s[q] == '(') break;
+        }
+        return comma > 0 && close > comma && parse_int(s, n, i + 1, comma, d) && parse_int(s, n, comma + 1, close, l) &&
+               *l >= 0;
+    }
+    int64_t e = i;
+    while (e < n && is_num(s[e])) e++;
+    return (e == n || s[e] == ',') && parse_int(s, n, i, e, d);
+}
+
+// the "inside an item" state at the first byte of each lane's 64 (wave-uniform tile t)
+__device__ __forceinline__ bool rl_lane_inside(const uint8_t* s, int64_t n, int64_t t0, int64_t a) {
+    const int lane = lane_id();
+    // this lane's last parenthesis (2 * position + open), -1: none
+    int64_t last = -1;
+    for (int64_t i = a; i < a + RL_LANE && i < n; i++)
+        if (s[i] == '(' || s[i] == ')') last = 2 * i + (s[i] == '(');
+    int64_t ex = __shfl_up(last, 1, 64);
+    if (lane == 0) ex = -1;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {   // exclusive max-scan over the lanes before
+        const int64_t o = __shfl_up(ex, d, 64);
+        if (lane >= d && o > ex) ex = o;
+    }
+    // before the tile: the last parenthesis among its 32 preceding bytes
+    const int64_t b = t0 - 32 + (lane & 31);
+    const bool par = lane < 32 && b >= 0 && b < n && (s[b] == '(' || s[b] == ')');
+    const unsigned long long pm = __ballot(par);
+    bool tile_in = false;
+    if (pm) {
+        const int l = 63 - __clzll((long long)pm);
+        tile_in = s[t0 - 32 + l] == '(';
+    }
+    return ex >= 0 ? (ex & 1) != 0 : tile_in;
+}
+
+struct RlLane {
+    int64_t cnt, dsum, lsum, lastlen;   // items starting in the lane, their deltas, lengths, the last length (-1)
+};
+
+// walk the lane's bytes: item starts (in order) to f(i, d, l); byte-class errors to err
+template <typename F>
+__device__ __forceinline__ RlLane rl_lane(const uint8_t* s, int64_t n, int64_t a, bool inside, int32_t* err, F&& f) {
+    RlLane r{0, 0, 0, -1};
+    bool bad = false;
+    uint8_t prev = a > 0 ? s[a - 1] : (uint8_t)',';
+    for (int64_t i = a; i < a + RL_LANE && i < n; i++) {
+        const uint8_t c = s[i];
+        bool start = false;
+        if (c == '(') { start = true; inside = true; }
+        else if (c == ')') { inside = false; }
+        else if (!inside) {
+            if (is_num(c)) start = !(i > 0 && is_num(prev));
+            else if (c != ',') bad = true;
+        }
+        if (start) {
+            int64_t d = 0, l = 1;
+            if (!rl_item(s, n, i, &d, &l)) bad = true;
+            f(i, d, l, r);
+            r.cnt++;
+            r.dsum += d;
+            r.lsum += l;
+            r.lastlen = l;
+        }
+        prev = c;
+    }
+    if (bad) atomicOr(err, 1);
+    return r;
+}
+
+// pass 1: per tile (count, delta sum, length sum, last length) -> tsum[4 * t]
+__global__ __launch_bounds__(256) void k_rl_tiles(const uint8_t* __restrict__ s, int64_t n, int64_t* __restrict__ tsum,
+                                                  int32_t* __restrict__ err) {
+    const int64_t t = (int64_t)blockIdx.x * 4 + wave_in_block();
+    const int64_t t0 = t * RL_TILE;
+    if (t0 >= n) return;
+    const int lane = lane_id();
+    const int64_t a = t0 + (int64_t)lane * RL_LANE;
+    const bool inside = rl_lane_inside(s, n, t0, a);
+    const RlLane r = rl_lane(s, n, a, inside, err, [](int64_t, int64_t, int64_t, const RlLane&) {});
+    const int64_t c = wave_sum(r.cnt), d = wave_sum(r.dsum), l = wave_sum(r.lsum);
+    const unsigned long long hm = __ballot(r.cnt > 0);
+    const int64_t last = hm ? __shfl(r.lastlen, 63 - __clzll((long long)hm), 64) : -1;
+    if (lane == 0) { tsum[4 * t] = c; tsum[4 * t + 1] = d; tsum[4 * t + 2] = l; tsum[4 * t + 3] = last; }
+}
+
+// pass 2 (one block): exclusive prefix over tiles of (count, deltas, lengths) and the last item
+// length before each tile (-1: none); the totals -> d_count[0..1]
+__global__ __launch_bounds__(1024) void k_rl_scan(int64_t ntiles, int64_t* __restrict__ tsum, int64_t* __restrict__ d_count) {
+    __shared__ int64_t wc[16], wd[16], wl[16], wlast[16];
+    const int tid = (int)threadIdx.x, lane = lane_id(), w = wave_in_block();
+    const int64_t per = (ntiles + 1023) / 1024, b0 = tid * per;
+    int64_t c = 0, d = 0, l = 0, last = -1;
+    for (int64_t t = b0; t < b0 + per && t < ntiles; t++) {
+        c += tsum[4 * t]; d += tsum[4 * t + 1]; l += tsum[4 * t + 2];
+        if (tsum[4 * t + 3] >= 0) last = tsum[4 * t + 3];
+    }
+    int64_t ic = c, id = d, il = l, ilast = last;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t xc = __shfl_up(ic, o, 64), xd = __shfl_up(id, o, 64), xl = __shfl_up(il, o, 64),
+                      xlast = __shfl_up(ilast, o, 64);
+        if (lane >= o) { ic += xc; id += xd; il += xl; if (ilast < 0) ilast = xlast; }
+    }
+    if (lane == 63) { wc[w] = ic; wd[w] = id; wl[w] = il; wlast[w] = ilast; }
+    __syncthreads();
+    int64_t pc = 0, pd = 0, pl = 0, plast = -1;
+    for (int i = 0; i < w; i++) { pc += wc[i]; pd += wd[i]; pl += wl[i]; if (wlast[i] >= 0) plast = wlast[i]; }
+    int64_t ec = pc + ic - c, ed = pd + id - d, el = pl + il - l;
+    int64_t elast = __shfl_up(ilast, 1, 64);
+    if (lane == 0 || elast < 0) elast = lane == 0 ? plast : (elast < 0 ? plast : elast);
+    for (int64_t t = b0; t < b0 + per && t < ntiles; t++) {
+        const int64_t tc = tsum[4 * t], td = tsum[4 * t + 1], tl = tsum[4 * t + 2], tlast = tsum[4 * t + 3];
+        tsum[4 * t] = ec; tsum[4 * t + 1] = ed; tsum[4 * t + 2] = el; tsum[4 * t + 3] = elast;
+        ec += tc; ed += td; el += tl;
+        if (tlast >= 0) elast = tlast;
+    }
+    if (tid == 1023) { d_count[0] = ec; d_count[1] = el; }
+}
+
+// pass 3: every item's start (running sum of deltas), length and the exclusive prefix of lengths;
+// starts must be >= 0, ascending and disjoint, and end within int32 (k_run_finish's checks)
+__global__ __launch_bounds__(256) void k_rl_write(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ tsum,
+                                                  int32_t* __restrict__ start, int32_t* __restrict__ len,
+                                                  int64_t* __restrict__ cum, int32_t* __restrict__ err) {
+    const int64_t t = (int64_t)blockIdx.x * 4 + wave_in_block();
+    const int64_t t0 = t * RL_TILE;
+    if (t0 >= n) return;
+    const int lane = lane_id();
+    const int64_t a = t0 + (int64_t)lane * RL_LANE;
+    const bool inside = rl_lane_inside(s, n, t0, a);
+    // the lane's totals first (a dry pass), then its exclusive prefixes over the wave
+    int32_t dummy = 0;
+    const RlLane tot = rl_lane(s, n, a, inside, &dummy, [](int64_t, int64_t, int64_t, const RlLane&) {});
+    const int64_t ic = wave_incl_add(tot.cnt), id = wave_incl_add(tot.dsum), il = wave_incl_add(tot.lsum);
+    // the last item length before this lane (in earlier lanes, else before the tile)
+    const unsigned long long hm = __ballot(tot.cnt > 0) & ((1ull << lane) - 1ull);
+    const int64_t prevlen = hm ? __shfl(tot.lastlen, 63 - __clzll((long long)hm), 64) : tsum[4 * t + 3];
+    const int64_t hm2 = __shfl(tot.lastlen, hm ? 63 - __clzll((long long)hm) : 0, 64);
+    (void)hm2;
+    const int64_t rank0 = tsum[4 * t] + ic - tot.cnt;
+    int64_t run_start = tsum[4 * t + 1] + id - tot.dsum;   // start of the last item before this lane's first
+    int64_t run_cum = tsum[4 * t + 2] + il - tot.lsum;
+    int64_t prev_end = rank0 > 0 ? run_start + (prevlen >= 0 ? prevlen : 0) : INT64_MIN;
+    bool bad = false;
+    rl_lane(s, n, a, inside, &dummy, [&](int64_t, int64_t d, int64_t l, const RlLane& r) {
+        const int64_t rank = rank0 + r.cnt;
+        const int64_t st = run_start + d;
+        if (st < 0 || st + l > INT32_MAX || (rank > 0 && st < prev_end)) bad = true;
+        start[rank] = (int32_t)st;
+        len[rank] = (int32_t)l;
+        cum[rank] = run_cum;
+        run_start = st;
+        run_cum += l;
+        prev_end = st + l;
+    });
+    if (bad) atomicOr(err, 1);
 }
 
 // starts = inclusive prefix of deltas (exclusive scan + own delta); runs must be ascending & disjoint.
@@ -231,6 +410,114 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill(const uint8_t* __restri
         const int j = __ffsll((long long)tm) - 1;
         tm &= tm - 1;
         const int64_t pj = __shfl(p, j), lj = __shfl(l, j), oj = __shfl(o, j);
+        wave_copy(dec + oj, R + pj, lj, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// record line, per 64-byte block (the usual path).  A token "(dp,l)" is at most 25 bytes, so the
+// "inside a token" state at a block's first byte follows from the last parenthesis before it (the
+// lanes before it in the 4 KiB tile, else the 32 bytes before the tile; rl_lane_inside).  Pass 1
+// stores per block its state and its sums of output bytes (literal 1, token l) and token deltas;
+// two exclusive scans over the blocks give every block's output offset and running p; the fill
+// recomputes a block's bytes from those (decompression.cpp:210-236), with the range check of
+// :223-229 (d_err bit 2) in the same pass.  (The per-byte arrays of the scan-based path -- last
+// parenthesis, contribution, delta, their prefix sums: 40 B per record byte -- are gone.)
+// ---------------------------------------------------------------------------------------------
+constexpr int TK_B = 64;   // record bytes per block (one lane in pass 1, one wave in the fill)
+
+__global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ s, int64_t n, int64_t* __restrict__ bin,
+                                                    int64_t* __restrict__ bcontrib, int64_t* __restrict__ bdelta,
+                                                    int32_t* __restrict__ err) {
+    const int64_t t = (int64_t)blockIdx.x * 4 + wave_in_block();
+    const int64_t t0 = t * (64 * TK_B);
+    if (t0 >= n) return;
+    const int lane = lane_id();
+    const int64_t a = t0 + (int64_t)lane * TK_B;
+    bool inside = rl_lane_inside(s, n, t0, a);
+    const int64_t b = a / TK_B;
+    if (a >= n) return;
+    const bool in0 = inside;
+    int64_t cs = 0, ds = 0;
+    bool bad = false;
+    for (int64_t i = a; i < a + TK_B && i < n; i++) {
+        const uint8_t c = s[i];
+        if (c == '(') {
+            int64_t comma = -1, close = -1, d = 0, l = 0;
+            for (int64_t q = i + 1; q < n && q < i + 32; q++) {
+                if (s[q] == ',' && comma < 0) comma = q;
+                if (s[q] == ')') { close = q; break; }
+                if (s[q] == '(') break;
+            }
+            if (!(comma > 0 && close > comma && parse_int(s, n, i + 1, comma, &d) && parse_int(s, n, comma + 1, close, &l)) ||
+                l < 0)
+                bad = true;
+            cs += l;
+            ds += d;
+            inside = true;
+        } else if (c == ')') {
+            cs += inside ? 0 : 1;   // a ')' outside a token is a literal (decompression.cpp:231-234)
+            inside = false;
+        } else if (!inside) {
+            cs += 1;
+        }
+    }
+    if (bad) atomicOr(err, 1);
+    bin[b] = in0;
+    bcontrib[b] = cs;
+    bdelta[b] = ds;
+}
+
+// one wave per block: literals and token copies into dec at the block's offsets; tokens beyond
+// the reference (p < 0 or p + l > |R'|, decompression.cpp:223-229) set d_err bit 2 and copy nothing
+__global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restrict__ s, int64_t n,
+                                                          const int64_t* __restrict__ bin, const int64_t* __restrict__ boff,
+                                                          const int64_t* __restrict__ bdsum, const int64_t* __restrict__ d_nref,
+                                                          const uint8_t* __restrict__ R, uint8_t* __restrict__ dec,
+                                                          int32_t* __restrict__ err) {
+    const int64_t b = (int64_t)blockIdx.x * WPB + wave_in_block();
+    const int64_t base = b * TK_B;
+    if (base >= n) return;
+    const int lane = lane_id();
+    const int64_t i = base + lane;
+    const uint8_t c = i < n ? s[i] : (uint8_t)',';
+    const bool par = i < n && (c == '(' || c == ')');
+    // the last parenthesis strictly before this byte inside the block, else the block's state
+    const unsigned long long pm = __ballot(par) & ((1ull << lane) - 1ull);
+    const bool inside = pm ? s[base + 63 - __clzll((long long)pm)] == '(' : bin[b] != 0;
+    int64_t contrib = 0, d = 0;
+    bool tok = false;
+    if (i < n) {
+        if (c == '(') {
+            int64_t comma = -1, close = -1, l = 0;
+            for (int64_t q = i + 1; q < n && q < i + 32; q++) {
+                if (s[q] == ',' && comma < 0) comma = q;
+                if (s[q] == ')') { close = q; break; }
+                if (s[q] == '(') break;
+            }
+            if (comma > 0 && close > comma && parse_int(s, n, i + 1, comma, &d) && parse_int(s, n, comma + 1, close, &l) && l >= 0) {
+                tok = true;
+                contrib = l;
+            }
+        } else if (c == ')') {
+            contrib = inside ? 0 : 1;
+        } else if (!inside) {
+            contrib = 1;
+        }
+    }
+    const int64_t o = boff[b] + wave_incl_add(contrib) - contrib;
+    const int64_t p = bdsum[b] + wave_incl_add(d);   // running p, this token included
+    const int64_t nref = *d_nref;
+    if (tok && (p < 0 || p + contrib > nref)) {
+        atomicOr(err, 2);
+        tok = false;
+    }
+    if (!tok && contrib == 1 && c != '(') dec[o] = c;   // literals, a stray ')' included
+    unsigned long long tm = __ballot(tok);
+    while (tm) {
+        const int j = __ffsll((long long)tm) - 1;
+        tm &= tm - 1;
+        const int64_t pj = __shfl(p, j), lj = __shfl(contrib, j), oj = __shfl(o, j);
         wave_copy(dec + oj, R + pj, lj, lane);
     }
 }
@@ -465,6 +752,18 @@ int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64
         return 0;
     }
     const int64_t cap = dc_run_cap(n);
+    const int64_t ntiles = (n + RL_TILE - 1) / RL_TILE;
+    static const bool old_path = getenv("SCCG_RL_SCAN") != nullptr;   // (A/B: the scan-based parser)
+    if (!old_path && ntiles <= 64 * 1024 && 4 * ntiles <= 2 * (n + 4)) {
+        // tiled: d_flag holds the per-tile summaries (4 per tile), d_dlt is unused
+        const unsigned g = (unsigned)((ntiles + 3) / 4);
+        hipLaunchKernelGGL(k_rl_tiles, dim3(g), dim3(256), 0, s, d_s, n, d_flag, d_err);
+        hipLaunchKernelGGL(k_rl_scan, dim3(1), dim3(1024), 0, s, ntiles, d_flag, d_count);
+        hipLaunchKernelGGL(k_rl_write, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_flag, r->start, r->len, r->cum,
+                           d_err);
+        SCCG_HIP(hipGetLastError());
+        return 0;
+    }
     int rc = dc_last_paren(d_s, n, d_lp, d_partial, s);
     if (rc) return rc;
     SCCG_HIP(hipMemsetAsync(d_dlt, 0, (size_t)cap * sizeof(int64_t), s));   // deltas past the runs scan as 0
@@ -500,6 +799,19 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
         SCCG_HIP(hipMemsetAsync(d_total, 0, sizeof(int64_t), s));
         return 0;
     }
+    if (dc_tok_tiled()) {
+        // per 64-byte block: state, output bytes, deltas; their exclusive prefixes -> d_off, d_dsum
+        const int64_t nb = (n + TK_B - 1) / TK_B;
+        const unsigned g = (unsigned)((n + 4 * 64 * TK_B - 1) / (4 * 64 * TK_B));
+        hipLaunchKernelGGL(k_tok_blocks, dim3(g), dim3(256), 0, s, d_s, n, d_lp, d_contrib, d_dlt, d_err);
+        SCCG_HIP(hipGetLastError());
+        int rc = dev_excl_sum(d_contrib, d_off, nb, d_total, d_partial, s);
+        if (rc) return rc;
+        rc = dev_excl_sum(d_dlt, d_dsum, nb, nullptr, d_partial, s);
+        (void)d_nref;
+        (void)nref_ready;
+        return rc;   // (the range check is in the fill, dc_decode_fill)
+    }
     int rc = dc_last_paren(d_s, n, d_lp, d_partial, s);
     if (rc) return rc;
     const unsigned g = grid_for(n, 256) > 8192 ? 8192 : grid_for(n, 256);
@@ -516,9 +828,21 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
     return 0;
 }
 
+bool dc_tok_tiled() {
+    static const bool v = getenv("SCCG_TOK_SCAN") == nullptr;   // (A/B: the scan-based record-line path)
+    return v;
+}
+
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
-                   const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s) {
+                   const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s,
+                   const int64_t* d_nref, int32_t* d_err) {
     if (n <= 0) return 0;
+    if (dc_tok_tiled()) {
+        PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_fill2, dim3(grid_for((n + TK_B - 1) / TK_B, WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n,
+                    d_lp, d_off, d_dsum, d_nref, d_R, d_dec, d_err);
+        SCCG_HIP(hipGetLastError());
+        return 0;
+    }
     PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_fill, dim3(grid_for(n, 64 * WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n, d_lp, d_off, d_dsum, d_dlt,
                        d_contrib, d_R, d_dec);
     SCCG_HIP(hipGetLastError());

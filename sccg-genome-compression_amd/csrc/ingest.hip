@@ -410,35 +410,57 @@ __global__ void k_strip_scan_apply(int64_t ntiles, const int64_t* __restrict__ t
 }
 
 // The wave's staged filter output (cnt bytes for positions [g0, g0 + cnt)) 2-bit packed into pq / px
-// (internal.h PackedSeq): every lane takes 32-base groups (one exception word, two code words);
-// groups wholly inside the range are stored, the two edge groups shared with the neighbouring
-// tiles are OR-ed into the zero-filled arrays (launch_fasta_strip clears them first).
-__device__ __forceinline__ void stage_pack(const uint8_t* __restrict__ st, int cnt, int64_t g0, uint32_t* __restrict__ pq,
+// (internal.h PackedSeq).  Lane i of a pass takes the 4-base slot s = s0 + i (global positions
+// [4s, 4s + 4), s0 32-base aligned): one aligned pair of stage dwords per lane (consecutive lanes,
+// consecutive dwords: no LDS bank conflicts), SWAR codes and exception bits, then 4 lanes OR their
+// bytes into a code word and 8 lanes their nibbles into an exception word (xor shuffles).  Words
+// wholly inside the range are stored; the edge words shared with the neighbouring tiles are OR-ed
+// into the zero-filled arrays (launch_fasta_strip clears them first).
+__device__ __forceinline__ void stage_pack(const uint32_t* __restrict__ st4, int cnt, int64_t g0, uint32_t* __restrict__ pq,
                                            uint32_t* __restrict__ px) {
     if (cnt <= 0) return;
+    const int lane = lane_id();
     const int64_t g1 = g0 + cnt;
-    for (int64_t W = (g0 >> 5) + lane_id(); W <= ((g1 - 1) >> 5); W += 64) {
-        const int64_t b = W << 5;
-        uint32_t c0 = 0, c1 = 0, xb = 0;
+    const int64_t s0 = (g0 >> 5) << 3;
+    const int r = (int)(g0 - 4 * s0);   // [0, 32): stage offset of slot s0 is -r
+    const int npass = (int)((((g1 - 1) >> 2) - s0) >> 6) + 1;
+    for (int it = 0; it < npass; it++) {
+        const int i = it * 64 + lane;
+        const int o = 4 * i - r;   // stage offset of the slot's first base
+        const int sh = o & 3, wlo = (o - sh) >> 2;
+        // clamped reads: the bytes they misplace lie outside [0, cnt) and are masked below
+        const int wl = min(max(wlo, 0), STAGE_WORDS - 1), wh = min(max(wlo + 1, 0), STAGE_WORDS - 1);
+        const uint32_t lo = st4[wl], hi = st4[wh];
+        const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
+        uint32_t vm = 0;   // bytes of the slot inside [0, cnt)
 #pragma unroll
-        for (int i = 0; i < 32; i++) {
-            const int64_t g = b + i;
-            if (g < g0 || g >= g1) continue;
-            const uint32_t c = st[g - g0];
-            const uint32_t code = ((c >> 1) ^ (c >> 2)) & 3u;
-            const bool acgt = c == 'A' || c == 'C' || c == 'G' || c == 'T';
-            if (i < 16) c0 |= code << (2 * i);
-            else c1 |= code << (2 * (i - 16));
-            if (!acgt) xb |= 1u << i;
+        for (int j = 0; j < 4; j++) vm |= (o + j >= 0 && o + j < cnt) ? (1u << j) : 0u;
+        const uint32_t t = ((v >> 1) ^ (v >> 2)) & 0x03030303u;
+        const uint32_t spread = (vm & 1 ? 0x03u : 0u) | (vm & 2 ? 0x0cu : 0u) | (vm & 4 ? 0x30u : 0u) | (vm & 8 ? 0xc0u : 0u);
+        const uint32_t c8 = (t | (t >> 6) | (t >> 12) | (t >> 18)) & spread;
+        const uint32_t acgt = sw_eq(v, 'A') | sw_eq(v, 'C') | sw_eq(v, 'G') | sw_eq(v, 'T');
+        const uint32_t x4 = sw_bits(~acgt & 0x80808080u) & vm;
+        uint32_t qw = c8 << (8 * (lane & 3));
+        qw |= __shfl_xor(qw, 1);
+        qw |= __shfl_xor(qw, 2);
+        uint32_t xw = x4 << (4 * (lane & 7));
+        xw |= __shfl_xor(xw, 1);
+        xw |= __shfl_xor(xw, 2);
+        xw |= __shfl_xor(xw, 4);
+        const int64_t s = s0 + i;
+        if ((lane & 3) == 0) {
+            const int64_t b = 4 * s;   // 16 bases of code word s / 4
+            if (b < g1) {
+                if (b >= g0 && b + 16 <= g1) pq[s >> 2] = qw;
+                else if (qw) atomicOr(&pq[s >> 2], qw);
+            }
         }
-        if (b >= g0 && b + 32 <= g1) {
-            pq[2 * W] = c0;
-            pq[2 * W + 1] = c1;
-            px[W] = xb;
-        } else {
-            if (c0) atomicOr(&pq[2 * W], c0);
-            if (c1) atomicOr(&pq[2 * W + 1], c1);
-            if (xb) atomicOr(&px[W], xb);
+        if ((lane & 7) == 0) {
+            const int64_t b = 4 * s;   // 32 bases of exception word s / 8
+            if (b < g1) {
+                if (b >= g0 && b + 32 <= g1) px[s >> 3] = xw;
+                else if (xw) atomicOr(&px[s >> 3], xw);
+            }
         }
     }
 }
@@ -481,7 +503,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
         stage_lane<true>(s1, tab, w, fkeep, (int)(ex >> 16));
         wave_sync();
         stage_out(st4, (int)(tot >> 16), out2, toff2[tile]);
-        if (pq) stage_pack(s1, (int)(tot >> 16), toff2[tile], pq, px);
+        if (pq) stage_pack(st4, (int)(tot >> 16), toff2[tile], pq, px);
     }
 }
 

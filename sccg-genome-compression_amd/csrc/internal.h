@@ -171,7 +171,8 @@ void global_prepare_reset();   // forget a preparation that will not be used
 // the device from d_nRp (no host round trip); nRp_bound >= |R'| sizes the workspace and the anchor
 // table (ws must hold walk_workspace_bytes(nRp_bound, tn, ...)).
 // It also writes R' 2-bit packed into rq / rx (PackedSeq, sized for nRp_bound).
-int global_sweep_early(const uint8_t* Rp, int64_t nRp_bound, const int64_t* d_nRp, uint32_t* rq, uint32_t* rx,
+// (packed: rq / rx hold R' already -- its strip packed it -- and the sweep reads them instead)
+int global_sweep_early(const uint8_t* Rp, int64_t nRp_bound, const int64_t* d_nRp, uint32_t* rq, uint32_t* rx, bool packed,
                        const uint8_t* tgt_fa, int64_t tn,
                        const int64_t* d_hdr, int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s);
 // Where the record text goes, when the caller learns it only during the walk: resolve() is called

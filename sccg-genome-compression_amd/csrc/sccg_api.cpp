@@ -325,6 +325,34 @@ int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const in
     return h_len ? d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1, s) : 0;   // h_len null: the caller reads d_len later
 }
 
+// SCCG_CHECK_PACK=1 (GPU tests): the strip-packed q / x of s (|s| = *d_n <= nb) against a separate
+// k_pack_seq pass over the same bytes, whole arrays (padding included); syncs the stream.
+bool check_pack_on() {   // read per call: a test switches it on for some pairs only
+    const char* e = getenv("SCCG_CHECK_PACK");
+    return e && atoi(e) != 0;
+}
+int check_pack(const uint8_t* s, int64_t nb, const int64_t* d_n, const uint32_t* q, const uint32_t* x, hipStream_t st) {
+    const size_t nq = (size_t)pack_q_words(nb), nx = (size_t)pack_x_words(nb);
+    uint32_t* t = nullptr;
+    if (hipMalloc(&t, (nq + nx) * 4) != hipSuccess) return SCCG_E_NOMEM;
+    std::vector<uint32_t> a(nq + nx), b(nq + nx);
+    int rc = launch_pack_seq(s, nb, d_n, t, t + nq, st);
+    if (!rc && (hipMemcpyAsync(a.data(), q, nq * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(a.data() + nq, x, nx * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(b.data(), t, (nq + nx) * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess))
+        rc = SCCG_E_HIP;
+    (void)hipFree(t);
+    if (!rc && a != b) {
+        size_t i = 0;
+        while (a[i] == b[i]) i++;
+        fprintf(stderr, "check_pack: word %zu of %zu (%s) strip %08x pack %08x\n", i < nq ? i : i - nq, i < nq ? nq : nx,
+                i < nq ? "q" : "x", a[i], b[i]);
+        rc = SCCG_E_INTERNAL;
+    }
+    return rc;
+}
+
 // Both run lines of the stripped target (compression.cpp:341-368 lowercase, :495-522 N) in two
 // syncs: run extraction for both predicates, one read of both run counts, run text for both, one
 // read of both text lengths.  The lowercase line goes to out_lower, the N line to out_n.
@@ -424,15 +452,18 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         if (const int rc = rdy->ref(rdy->user, &e)) return rc;
         HIPTRY(hipStreamWaitEvent(ctx->side, e, 0));
     }
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side));
-    HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
-    // R' and T' 2-bit packed for the walk (|R'|, |T'| read on the device; FASTA lengths bound them):
-    // R' by the early sweep (global_sweep_early), T' behind its strip
+    // R' and T' 2-bit packed for the walk, each by its own strip (the write pass packs the bytes it
+    // stages; |R'|, |T'| stay on the device, the FASTA lengths bound them)
     GET(uint32_t, rq, B_RQ, pack_q_words(rn));
     GET(uint32_t, rx, B_RX, pack_x_words(rn));
     GET(uint32_t, tq, B_TQ, pack_q_words(tn));
     GET(uint32_t, tx, B_TX, pack_x_words(tn));
     const PackedSeq pr{rq, rx}, pt{tq, tx};
+    // (SCCG_RPACK_SWEEP=1, A/B runs: the byte sweep packs R' instead of its strip)
+    static const bool rpack_sweep = [] { const char* e = getenv("SCCG_RPACK_SWEEP"); return e && atoi(e) != 0; }();
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side,
+              rpack_sweep ? nullptr : rq, rpack_sweep ? nullptr : rx));
+    HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
     if (rdy) {
         hipEvent_t e = nullptr;
         if (const int rc = rdy->tgt(rdy->user, &e)) return rc;
@@ -441,6 +472,11 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     TRY(launch_find_header(tfa, tn, sc, s));
     HIPTRY(hipEventRecord(ctx->ev_hdr, s));
     TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp, 0, nullptr, tq, tx));
+    if (check_pack_on()) {   // (tests) the strips' packing against k_pack_seq of the same bytes
+        HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
+        if (!rpack_sweep && check_pack(Rp, rn, sc + 8, rq, rx, s)) return ctx->fail(SCCG_E_INTERNAL, "strip-packed R' differs");
+        if (check_pack(Tp, tn, sc + 3, tq, tx, s)) return ctx->fail(SCCG_E_INTERNAL, "strip-packed T' differs");
+    }
     // ---- header + lowercase line (compression.cpp:337-368) and the N line: side2, driven by the
     //      context's host worker (its launches wait on run counts).  They need only T, so they are
     //      queued right behind the target's strip -- ahead of the local pass and the walk, which
@@ -496,7 +532,8 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
         void* ws_early = ctx->get(B_WALK, wsb);
         if (!ws_early) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
-        TRY(global_sweep_early(Rp, rn, sc + 8, rq, rx, tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb, ctx->side));
+        TRY(global_sweep_early(Rp, rn, sc + 8, rq, rx, !rpack_sweep, tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb,
+                               ctx->side));
     }
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
     // ---- fork.  The local pass (compression.cpp:372-474, main stream) is latency-bound; the
@@ -996,13 +1033,19 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     if (size_only) return SCCG_OK;
     if (total > out_cap) return ctx->fail(SCCG_E_NOMEM, "output needs %lld bytes", (long long)total);
     GET(uint8_t, dec, B_D_DEC, D + 64);
-    TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s));
+    TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s, sc + 9, d_err));
     if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
     TRY(dev_put_bytes(out + hlen, "\n", 1, s));
     GET(int64_t, span, B_D_SPAN, dc_format_span_words(nres));
     TRY(dc_format(dec, nres, nr, lr, span, out + hlen + 1, s));
     TRY(dev_put_bytes(out + total - 1, "\n", 1, s));
-    HIPTRY(hipStreamSynchronize(s));
+    if (dc_tok_tiled()) {   // the range check ran with the fill: read the error bits behind the output
+        const RbItem it{d_err, &err, (int)sizeof err};
+        TRY(dev_readback(&it, 1, s));
+        if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
+    } else {
+        HIPTRY(hipStreamSynchronize(s));
+    }
     ctx->stats.target_bases = nres;
     ctx->stats.reference_bases = nRp;
     return SCCG_OK;

@@ -75,8 +75,11 @@ constexpr int32_t CAND_CAP = 65536;  // early sweep: first-k-mer occurrences kep
 // Frozen chains (k_chain_*): a committed frozen chunk's exit state is walked on over the rest of the
 // target by one wave that visits only "band hits" -- target positions whose k-mer occurs among the
 // reference k-mers within CH_BAND of the generation's P -- found by a grid scan.
-constexpr int CH_BAND = 512;           // band half-width (reference positions around P)
-constexpr int CH_TBITS = 13;           // band key table: 8192 LDS slots (load <= 1/2)
+#ifndef SCCG_CH_BAND
+#define SCCG_CH_BAND 512
+#endif
+constexpr int CH_BAND = SCCG_CH_BAND;   // band half-width (reference positions around P)
+constexpr int CH_TBITS = CH_BAND <= 2048 ? 13 : 14;   // band key table: 8192 / 16384 LDS slots (load <= 1/2)
 constexpr int CH_GRID = 512;           // scan blocks (1024 threads, 16 positions each per step)
 constexpr int CH_HCAP = 4096;          // band hits kept per block and generation
 constexpr int32_t CHAIN_MCAP = 1 << 22;   // matches a chain may take
@@ -89,7 +92,10 @@ constexpr int32_t CH_DENSE_SPAN = 8192;   // fall within this many target bases 
 // finding matches is a trapped walk (chance hits in a low-complexity window nudging P every few kb,
 // e.g. the synthetic chr22 from 45.8 Mb): one wave then walks them serially (~4 us each), which the
 // rounds' trapped re-speculation resolves faster, so the chain hands back after this many matches.
-constexpr int CH_HANDBACK_N = 64;
+#ifndef SCCG_CH_HANDBACK
+#define SCCG_CH_HANDBACK 64
+#endif
+constexpr int CH_HANDBACK_N = SCCG_CH_HANDBACK;
 
 struct WalkPtrs {
     const uint8_t* R;
@@ -547,6 +553,7 @@ constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cand
 #ifndef WALK_WAVES_PER_EU
 #define WALK_WAVES_PER_EU 5
 #endif
+// nlist_dev (optional): the list length from device memory (a round queued before the host knows it)
 // nlist_dev (optional): the list length from device memory (a round queued before the host knows it)
 template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
@@ -1836,6 +1843,57 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
                   });
 }
 
+// The same sweep over the 2-bit packed R' (the strip packed it): 0.375 B per base instead of 1, one
+// thread per 64-base block -- its four code words and the next one (the k-mers overhanging the
+// block), its two exception words and the next one.  The anchor samples at every 32nd position are
+// exactly the block's two 64-bit code words.
+__global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_packed(WalkPtrs A) {
+    const int k = A.k, kp = A.kp;
+    const int64_t nR = A.dnR ? *A.dnR : A.nR;   // |R'| (A.nR only bounds it)
+    const bool have = *reinterpret_cast<const int32_t*>(A.kb + KB_COUNT) == k;
+    const uint32_t key0 = have ? walk_key(A.kb, kp) : KEY_EXOTIC;
+    const bool want = key0 < KEY_EXOTIC;
+    const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
+    const int64_t npos = nR - k + 1;
+    const int64_t nblk = (nR + 63) / 64;
+    const uint4* q4 = reinterpret_cast<const uint4*>(A.Rq);
+    const uint2* x2 = reinterpret_cast<const uint2*>(A.Rx);
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p0 = 64 * b;
+        const uint4 qa = q4[b];
+        const uint2 xa = x2[b];
+        const uint32_t qn = A.Rq[4 * b + 4], xn = A.Rx[2 * b + 2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {   // anchors (astep 32)
+            const int64_t p = p0 + 32 * h;
+            if (p + ANCHOR_K > nR || (h ? xa.y : xa.x)) continue;
+            const uint64_t code = h ? ((uint64_t)qa.w << 32 | qa.z) : ((uint64_t)qa.y << 32 | qa.x);
+            const uint64_t key = mix64(code);
+            A.atab[key >> (64 - A.abits)] = ((uint64_t)anchor_tag(key, A.agen) << 32) | (uint32_t)p;
+        }
+        if (!want || p0 >= npos) continue;
+        const uint32_t w[5] = {qa.x, qa.y, qa.z, qa.w, qn};
+        const uint32_t xw[3] = {xa.x, xa.y, xn};
+        uint64_t hits = 0;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint64_t code = ((uint64_t)w[g + 1] << 32) | w[g];
+            const uint32_t bad = __builtin_amdgcn_alignbit(xw[(g >> 1) + 1], xw[g >> 1], 16u * (uint32_t)(g & 1));
+#pragma unroll
+            for (int st = 0; st < 16; st++)
+                if (((uint32_t)(code >> (2 * st)) & MASK) == key0 && !((bad >> st) & KM)) hits |= 1ull << (16 * g + st);
+        }
+        if (npos - p0 < 64) hits &= (1ull << (npos - p0)) - 1;
+        while (hits) {
+            const int64_t c = p0 + __builtin_ctzll(hits);
+            hits &= hits - 1;
+            if (k > kp && !bytes_eq(A.R + c + kp, A.kb + kp, k - kp)) continue;
+            const unsigned long long i = atomicAdd(&A.fc[13], 1ull);
+            if (i < (unsigned long long)CAND_CAP) A.cand[i] = (int32_t)c;
+        }
+    }
+}
+
 // after T' exists: statistics of x0 = 0 over the early sweep's positions (as k_key0 +
 // k_cand_reduce would leave them in fc[4..11]).  Grid-wide: every wave extends one position at a
 // time (wave_lce: 2 KiB per round trip), per-block results go to fcb and k_cand_stats_fin merges
@@ -2317,6 +2375,9 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
 // SCCG_DEBUG runs take the instrumented walk
 using WalkKernel = void (*)(WalkPtrs, const int32_t*, int32_t, const int32_t*);
 WalkKernel walk_kernel(const WalkPtrs& A) { return A.dbg ? k_walk<true> : k_walk<false>; }
+// blocks of a walk launch over nlist chunks: no more than fit on the GPU at once (its waves take the
+// chunks from a queue)
+unsigned walk_grid(int64_t nlist) { return grid_for(nlist, WPB); }
 
 struct FullC {
     int64_t lmax;
@@ -2435,7 +2496,7 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s, std::vector<int32_t>* resume
         int rc = dev_set_i32(A.scal + 1, 1, {0}, s);
         if (rc) return rc;
         if ((rc = h2d_sync(A.rlist, rl.data(), rl.size() * 4, s))) return rc;
-        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
+        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(walk_grid((int64_t)rl.size())), dim3(SCCG_BLOCK), 0, s, A,
                     (const int32_t*)A.rlist, (int32_t)rl.size(), (const int32_t*)nullptr);
         SCCG_HIP(hipGetLastError());
     }
@@ -2566,12 +2627,12 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 
 void global_prepare_reset() { g_prep = Prepared{}; g_early = Early{}; }
 
-int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, uint32_t* rq, uint32_t* rx,
+int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, uint32_t* rq, uint32_t* rx, bool packed,
                        const uint8_t* tgt_fa, int64_t tn, const int64_t* d_hdr, int k, int m, int chunk, void* ws,
                        size_t ws_bytes, hipStream_t s) {
     g_early = Early{};
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
-    if (nRp < k || tn <= 0) return launch_pack_seq(Rp, nRp, d_nRp, rq, rx, s);   // no walk can use the sweep
+    if (nRp < k || tn <= 0) return packed ? 0 : launch_pack_seq(Rp, nRp, d_nRp, rq, rx, s);   // no walk can use the sweep
     size_t used = 0;
     // |T'| <= tn: the carve's R'-only front (anchor table, fc, positions, kb) does not depend on it;
     // nRp bounds |R'|, which the sweep reads from d_nRp
@@ -2582,7 +2643,12 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, uin
     RC(set_u64(A.fc + 12, {0, 0}, s));
     hipLaunchKernelGGL(k_first_kmer, dim3(1), dim3(SCCG_BLOCK), 0, s, tgt_fa, tn, d_hdr, k, (int64_t)1 << 20, A.kb);
     const unsigned g = first_sweep_grid(A);
-    if (A.astep == 32) {
+    if (A.astep == 32 && packed) {
+        // R' is packed already (by its strip): the sweep reads the packed words
+        A.Rq = rq;
+        A.Rx = rx;
+        PROF_LAUNCH(PROF_ANCHOR, s, k_sweep_packed, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
+    } else if (A.astep == 32) {
         // the sweep packs R' as it reads it; the blocks past its last k-mer start (and the padding)
         // are packed behind it
         A.Rq = rq;
@@ -2590,7 +2656,7 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, uin
         PROF_LAUNCH(PROF_ANCHOR, s, k_sweep_early<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
         hipLaunchKernelGGL(k_pack_seq, dim3(64), dim3(SCCG_BLOCK), 0, s, Rp, nRp, d_nRp, rq, rx, k);
     } else {
-        RC(launch_pack_seq(Rp, nRp, d_nRp, rq, rx, s));
+        if (!packed) RC(launch_pack_seq(Rp, nRp, d_nRp, rq, rx, s));
         hipLaunchKernelGGL(k_sweep_early<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
         const int64_t ns = (int64_t)A.nR / A.astep + 1;
         const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
@@ -2675,7 +2741,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     // (dev_nlist: the list length is the previous round tail's pending count, scal[0])
     auto queue_round = [&](int fbase_cap, bool dev_nlist) -> int {
         const int32_t* nd = dev_nlist ? A.scal : nullptr;
-        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist,
+        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(walk_grid(A.C)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist,
                     A.C, nd);
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
@@ -2841,7 +2907,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             A.round = (int32_t)round;   // every kernel of the round gets it by value
             const bool queued = pre_round && round == round0;
             if (!queued) {
-                PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A,
+                PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(walk_grid(nlist)), dim3(SCCG_BLOCK), 0, s, A,
                             (const int32_t*)A.plist, nlist, (const int32_t*)nullptr);
                 SCCG_HIP(hipGetLastError());
             }

@@ -89,3 +89,33 @@ def test_pinned_pair_host_api_and_roundtrip(ctx, name):
         assert st["walk_rounds"] < 64, st
     fa = ctx.reconstruct(rec, rfa)
     assert hashlib.sha256(fa).hexdigest() == e["fasta_sha256"]
+
+
+def test_compress_files_vs_reference(ctx, tmp_path):
+    """sccg_compress_files (files -> record file, pinned staging) on the chr21 pair: the pinned
+    reference bytes, and the reference's failure points (compression.cpp:187-191, :202-206)."""
+    e = {m["name"]: m for m in _manifest()}.get("chr21")
+    if e is None:
+        pytest.skip("chr21 not pinned")
+    rfa, tfa = synthlib.synth_pair(e["profile"], e["ref_len"], e["tgt_len"], e["seed"])
+    rp, tp, op = tmp_path / "ref.fa", tmp_path / "tgt.fa", tmp_path / "compressed_genome.txt"
+    rp.write_bytes(rfa)
+    tp.write_bytes(tfa)
+    n = ctx.compress_files(str(rp), str(tp), str(op))
+    rec = op.read_bytes()
+    assert n == len(rec) == e["record_len"]
+    assert hashlib.sha256(rec).hexdigest() == e["record_sha256"]
+    for args, code in (((str(tmp_path / "nope.fa"), str(tp)), "SCCG_E_OPEN_REF"),
+                       ((str(rp), str(tmp_path / "nope.fa")), "SCCG_E_OPEN_TGT")):
+        with pytest.raises(sccg.SccgError) as ei:
+            ctx.compress_files(*args, str(tmp_path / "x.txt"))
+        assert ei.value.rc == sccg.ERR_CODES[code]
+    with pytest.raises(sccg.SccgError) as ei:
+        ctx.compress_files(str(rp), str(tp), str(tmp_path / "no_dir" / "x.txt"))
+    assert ei.value.rc == sccg.ERR_CODES["SCCG_E_WRITE"]
+    # a small pair through both paths
+    rfa2, tfa2 = synthlib.synth_pair("hg", 300_000, 301_000, 5)
+    rp.write_bytes(rfa2)
+    tp.write_bytes(tfa2)
+    ctx.compress_files(str(rp), str(tp), str(op))
+    assert op.read_bytes() == ctx.compress(rfa2, tfa2)
