@@ -409,62 +409,6 @@ __global__ void k_strip_scan_apply(int64_t ntiles, const int64_t* __restrict__ t
     }
 }
 
-// The wave's staged filter output (cnt bytes for positions [g0, g0 + cnt)) 2-bit packed into pq / px
-// (internal.h PackedSeq).  Lane i of a pass takes the 4-base slot s = s0 + i (global positions
-// [4s, 4s + 4), s0 32-base aligned): one aligned pair of stage dwords per lane (consecutive lanes,
-// consecutive dwords: no LDS bank conflicts), SWAR codes and exception bits, then 4 lanes OR their
-// bytes into a code word and 8 lanes their nibbles into an exception word (xor shuffles).  Words
-// wholly inside the range are stored; the edge words shared with the neighbouring tiles are OR-ed
-// into the zero-filled arrays (launch_fasta_strip clears them first).
-__device__ __forceinline__ void stage_pack(const uint32_t* __restrict__ st4, int cnt, int64_t g0, uint32_t* __restrict__ pq,
-                                           uint32_t* __restrict__ px) {
-    if (cnt <= 0) return;
-    const int lane = lane_id();
-    const int64_t g1 = g0 + cnt;
-    const int64_t s0 = (g0 >> 5) << 3;
-    const int r = (int)(g0 - 4 * s0);   // [0, 32): stage offset of slot s0 is -r
-    const int npass = (int)((((g1 - 1) >> 2) - s0) >> 6) + 1;
-    for (int it = 0; it < npass; it++) {
-        const int i = it * 64 + lane;
-        const int o = 4 * i - r;   // stage offset of the slot's first base
-        const int sh = o & 3, wlo = (o - sh) >> 2;
-        // clamped reads: the bytes they misplace lie outside [0, cnt) and are masked below
-        const int wl = min(max(wlo, 0), STAGE_WORDS - 1), wh = min(max(wlo + 1, 0), STAGE_WORDS - 1);
-        const uint32_t lo = st4[wl], hi = st4[wh];
-        const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
-        uint32_t vm = 0;   // bytes of the slot inside [0, cnt)
-#pragma unroll
-        for (int j = 0; j < 4; j++) vm |= (o + j >= 0 && o + j < cnt) ? (1u << j) : 0u;
-        const uint32_t t = ((v >> 1) ^ (v >> 2)) & 0x03030303u;
-        const uint32_t spread = (vm & 1 ? 0x03u : 0u) | (vm & 2 ? 0x0cu : 0u) | (vm & 4 ? 0x30u : 0u) | (vm & 8 ? 0xc0u : 0u);
-        const uint32_t c8 = (t | (t >> 6) | (t >> 12) | (t >> 18)) & spread;
-        const uint32_t acgt = sw_eq(v, 'A') | sw_eq(v, 'C') | sw_eq(v, 'G') | sw_eq(v, 'T');
-        const uint32_t x4 = sw_bits(~acgt & 0x80808080u) & vm;
-        uint32_t qw = c8 << (8 * (lane & 3));
-        qw |= __shfl_xor(qw, 1);
-        qw |= __shfl_xor(qw, 2);
-        uint32_t xw = x4 << (4 * (lane & 7));
-        xw |= __shfl_xor(xw, 1);
-        xw |= __shfl_xor(xw, 2);
-        xw |= __shfl_xor(xw, 4);
-        const int64_t s = s0 + i;
-        if ((lane & 3) == 0) {
-            const int64_t b = 4 * s;   // 16 bases of code word s / 4
-            if (b < g1) {
-                if (b >= g0 && b + 16 <= g1) pq[s >> 2] = qw;
-                else if (qw) atomicOr(&pq[s >> 2], qw);
-            }
-        }
-        if ((lane & 7) == 0) {
-            const int64_t b = 4 * s;   // 32 bases of exception word s / 8
-            if (b < g1) {
-                if (b >= g0 && b + 32 <= g1) px[s >> 3] = xw;
-                else if (xw) atomicOr(&px[s >> 3], xw);
-            }
-        }
-    }
-}
-
 template <IngestMode MODE>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n,
                                                             const int64_t* __restrict__ hdr,
@@ -472,8 +416,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
                                                             const int64_t* __restrict__ toff2,
                                                             const int32_t* __restrict__ tcarry,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
-                                                            int32_t* __restrict__ flags, uint32_t* __restrict__ pq,
-                                                            uint32_t* __restrict__ px) {
+                                                            int32_t* __restrict__ flags) {
     __shared__ uint32_t stage_all[WPB][STAGE_WORDS];
     __shared__ uint32_t tab[16];
     if (threadIdx.x < 16) tab[threadIdx.x] = compact_sel(threadIdx.x);
@@ -503,7 +446,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
         stage_lane<true>(s1, tab, w, fkeep, (int)(ex >> 16));
         wave_sync();
         stage_out(st4, (int)(tot >> 16), out2, toff2[tile]);
-        if (pq) stage_pack(st4, (int)(tot >> 16), toff2[tile], pq, px);
     }
 }
 
@@ -642,7 +584,7 @@ int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t
 
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,
                        int64_t* d_len, int32_t* d_flags, const IngestScratch& sc, hipStream_t s, FilterMode fmode,
-                       uint8_t* out2, int64_t* d_len2, uint32_t* pq, uint32_t* px) {
+                       uint8_t* out2, int64_t* d_len2) {
     if (n <= 0) {
         SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));
         if (d_len2) SCCG_HIP(hipMemsetAsync(d_len2, 0, sizeof(int64_t), s));
@@ -666,20 +608,13 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     hipLaunchKernelGGL(k_strip_scan_apply, dim3(grid_for(ntiles, 256)), dim3(256), 0, s, ntiles, sc.tile_a, sc.tile_b,
                        sc.tile_fa, sc.tile_fb, sc.tile_last, btot, sc.tile_off, sc.tile_off2, sc.tile_carry, d_len,
                        d_len2);
-    if (!out2) pq = px = nullptr;
-    if (pq) {   // edge groups are OR-ed in: zero the blocks the strip can reach (<= n bases)
-        SCCG_HIP(hipMemsetAsync(pq, 0, (size_t)pack_q_words(n) * 4, s));
-        SCCG_HIP(hipMemsetAsync(px, 0, (size_t)pack_x_words(n) * 4, s));
-    }
     if (mode == INGEST_TGT)
         PROF_LAUNCH(PROF_STRIP, s, k_strip_write<INGEST_TGT>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, pq, px);
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
     else
         PROF_LAUNCH(PROF_STRIP, s, k_strip_write<INGEST_REF>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, pq, px);
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
     SCCG_HIP(hipGetLastError());
-    // the block holding the sequence end and the padding: exception bits past the end
-    if (pq) return launch_pack_seq_from(out2, n, d_len2, pq, px, 64, s);
     return 0;
 }
 

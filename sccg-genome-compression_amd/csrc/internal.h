@@ -89,7 +89,7 @@ int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, 
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header,
                        uint8_t* out, int64_t* d_len, int32_t* d_flags, const IngestScratch& sc,
                        hipStream_t s, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
-                       int64_t* d_len2 = nullptr, uint32_t* pq = nullptr, uint32_t* px = nullptr);
+                       int64_t* d_len2 = nullptr);
 // maximal runs of lowercase bytes (rs_l/re_l) and of N/n bytes (rs_n/re_n), start/end inclusive,
 // in one pass; d_nruns[0..1] = their counts
 int launch_runs2(const uint8_t* s_in, int64_t n, int32_t* rs_l, int32_t* re_l, int32_t* rs_n, int32_t* re_n,
@@ -129,25 +129,6 @@ int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_
                       int64_t* d_tmp_b, int64_t* d_partial, hipStream_t s, bool abs_p = false);
 
 // ---- walk.hip ---------------------------------------------------------------------------------
-// 2-bit packed sequence (north star: the walk reads 2-bit-packed T' and R'): q = codes, 16 bases
-// per u32 word, base i of a word at bits 2i..2i+1 (A,C,G,T = 0,1,2,3; the walk-key order of
-// common.h); x = exception bitmap, 32 bases per u32 word, bit set where the byte is not A/C/G/T
-// (its code is then meaningless and the byte array decides).  Both are written in blocks of 64
-// bases and carry PACK_PAD_BLOCKS blocks past the sequence (codes 0, exception bits 1).
-struct PackedSeq {
-    const uint32_t* q;
-    const uint32_t* x;
-};
-constexpr int64_t PACK_PAD_BLOCKS = 160;   // >= the walk's LDS copy (walk.hip LBV) past the end
-__host__ __device__ inline int64_t pack_blocks(int64_t n) { return (n + 63) / 64 + PACK_PAD_BLOCKS; }
-__host__ __device__ inline int64_t pack_q_words(int64_t n) { return 4 * pack_blocks(n); }
-__host__ __device__ inline int64_t pack_x_words(int64_t n) { return 2 * pack_blocks(n); }
-// packs s[0, n) (n = *d_n when d_n is given; n_bound >= it sizes the grid and the padding) into q / x
-int launch_pack_seq(const uint8_t* s, int64_t n_bound, const int64_t* d_n, uint32_t* q, uint32_t* x, hipStream_t st);
-// the same for the blocks from the first one at or past position n - kfrom + 1 only (kfrom = 64: the
-// block holding position n on; the strip packs the blocks before it)
-int launch_pack_seq_from(const uint8_t* s, int64_t n_bound, const int64_t* d_n, uint32_t* q, uint32_t* x, int kfrom,
-                         hipStream_t st);
 struct WalkWorkspace;  // defined in walk.hip
 struct WalkResult {
     int64_t n_matches;
@@ -161,19 +142,15 @@ size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk);
 // Queues the walk's input-only work (first-step key sweep, anchor index, chunk guesses) on s with
 // no host sync; a later global_match_and_emit with the same ws and inputs skips it (the caller
 // orders its stream after s).
-// (pr / pt: R' and T' 2-bit packed by launch_pack_seq, ordered before s)
-int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, const PackedSeq& pr, const PackedSeq& pt,
-                   int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s);
+int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
+                   size_t ws_bytes, hipStream_t s);
 void global_prepare_reset();   // forget a preparation that will not be used
 // As soon as R' exists (before |T'| is known, tn >= |T'|): the anchor samples and the positions of
 // the target's first k-mer, read from the target FASTA (d_hdr: its header range).  A later
 // global_prepare on the same ws/R' only extends those positions once T' exists.  |R'| is read on
 // the device from d_nRp (no host round trip); nRp_bound >= |R'| sizes the workspace and the anchor
 // table (ws must hold walk_workspace_bytes(nRp_bound, tn, ...)).
-// It also writes R' 2-bit packed into rq / rx (PackedSeq, sized for nRp_bound).
-// (packed: rq / rx hold R' already -- its strip packed it -- and the sweep reads them instead)
-int global_sweep_early(const uint8_t* Rp, int64_t nRp_bound, const int64_t* d_nRp, uint32_t* rq, uint32_t* rx, bool packed,
-                       const uint8_t* tgt_fa, int64_t tn,
+int global_sweep_early(const uint8_t* Rp, int64_t nRp_bound, const int64_t* d_nRp, const uint8_t* tgt_fa, int64_t tn,
                        const int64_t* d_hdr, int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s);
 // Where the record text goes, when the caller learns it only during the walk: resolve() is called
 // once, after the rounds and before the text is written, and returns the output pointer.
@@ -192,8 +169,7 @@ constexpr int WALK_ABANDONED = -1;
 // (abs_p: absolute p on the record line, the text before delta_encode; late_out: out is ignored
 // and resolved through it; keep_flat: also keep the flat match list for global_matches, else the
 // text is written straight from the chunks' trajectories)
-int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, const PackedSeq& pr,
-                          const PackedSeq& pt, int k, int m,
+int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m,
                           int chunk, void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len,
                           WalkResult* res, hipStream_t s, bool abs_p = false, const EmitTarget* late_out = nullptr,
                           bool keep_flat = true);

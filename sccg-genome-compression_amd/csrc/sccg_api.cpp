@@ -54,8 +54,6 @@ enum Slot {
     B_DX, B_DELTA,
     // a second FASTA-strip scratch set (the reference strips beside the target, on the side stream)
     B_TILE2_A, B_TILE2_B, B_TILE2_FA, B_TILE2_FB, B_TILE2_LAST, B_TILE2_OFF, B_TILE2_OFF2, B_TILE2_CARRY, B_TILE2_BSUM,
-    // 2-bit packed R' / T' (codes, exception bits) for the global walk
-    B_RQ, B_RX, B_TQ, B_TX,
     B_COUNT
 };
 
@@ -304,7 +302,7 @@ int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n, hipStream_t s = 
 // (set 1: the second scratch set, so two strips can run at once; s: stream, default the context's)
 int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const int64_t* d_hdr, uint8_t* out,
           int64_t* d_len, int32_t* d_flags, int64_t* h_len, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
-          int set = 0, hipStream_t s = nullptr, uint32_t* pq = nullptr, uint32_t* px = nullptr) {
+          int set = 0, hipStream_t s = nullptr) {
     const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE + 1;
     const int o = set ? B_TILE2_A - B_TILE_A : 0;
     static_assert(B_TILE_BSUM - B_TILE_A == B_TILE2_BSUM - B_TILE2_A, "scratch sets line up");
@@ -321,36 +319,8 @@ int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const in
     sc.tile_a = ta; sc.tile_b = tb; sc.tile_fa = tfa; sc.tile_fb = tfb; sc.tile_last = tl; sc.tile_off = to;
     sc.tile_off2 = to2; sc.tile_carry = tc; sc.block_sums = bs; sc.scalars = nullptr;
     TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, s ? s : ctx->stream, fmode, out2,
-                           out2 ? d_len + 1 : nullptr, pq, px));
+                           out2 ? d_len + 1 : nullptr));
     return h_len ? d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1, s) : 0;   // h_len null: the caller reads d_len later
-}
-
-// SCCG_CHECK_PACK=1 (GPU tests): the strip-packed q / x of s (|s| = *d_n <= nb) against a separate
-// k_pack_seq pass over the same bytes, whole arrays (padding included); syncs the stream.
-bool check_pack_on() {   // read per call: a test switches it on for some pairs only
-    const char* e = getenv("SCCG_CHECK_PACK");
-    return e && atoi(e) != 0;
-}
-int check_pack(const uint8_t* s, int64_t nb, const int64_t* d_n, const uint32_t* q, const uint32_t* x, hipStream_t st) {
-    const size_t nq = (size_t)pack_q_words(nb), nx = (size_t)pack_x_words(nb);
-    uint32_t* t = nullptr;
-    if (hipMalloc(&t, (nq + nx) * 4) != hipSuccess) return SCCG_E_NOMEM;
-    std::vector<uint32_t> a(nq + nx), b(nq + nx);
-    int rc = launch_pack_seq(s, nb, d_n, t, t + nq, st);
-    if (!rc && (hipMemcpyAsync(a.data(), q, nq * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(a.data() + nq, x, nx * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(b.data(), t, (nq + nx) * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess))
-        rc = SCCG_E_HIP;
-    (void)hipFree(t);
-    if (!rc && a != b) {
-        size_t i = 0;
-        while (a[i] == b[i]) i++;
-        fprintf(stderr, "check_pack: word %zu of %zu (%s) strip %08x pack %08x\n", i < nq ? i : i - nq, i < nq ? nq : nx,
-                i < nq ? "q" : "x", a[i], b[i]);
-        rc = SCCG_E_INTERNAL;
-    }
-    return rc;
 }
 
 // Both run lines of the stripped target (compression.cpp:341-368 lowercase, :495-522 N) in two
@@ -452,17 +422,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         if (const int rc = rdy->ref(rdy->user, &e)) return rc;
         HIPTRY(hipStreamWaitEvent(ctx->side, e, 0));
     }
-    // R' and T' 2-bit packed for the walk, each by its own strip (the write pass packs the bytes it
-    // stages; |R'|, |T'| stay on the device, the FASTA lengths bound them)
-    GET(uint32_t, rq, B_RQ, pack_q_words(rn));
-    GET(uint32_t, rx, B_RX, pack_x_words(rn));
-    GET(uint32_t, tq, B_TQ, pack_q_words(tn));
-    GET(uint32_t, tx, B_TX, pack_x_words(tn));
-    const PackedSeq pr{rq, rx}, pt{tq, tx};
-    // (SCCG_RPACK_SWEEP=1, A/B runs: the byte sweep packs R' instead of its strip)
-    static const bool rpack_sweep = [] { const char* e = getenv("SCCG_RPACK_SWEEP"); return e && atoi(e) != 0; }();
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side,
-              rpack_sweep ? nullptr : rq, rpack_sweep ? nullptr : rx));
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side));
     HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
     if (rdy) {
         hipEvent_t e = nullptr;
@@ -471,12 +431,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     }
     TRY(launch_find_header(tfa, tn, sc, s));
     HIPTRY(hipEventRecord(ctx->ev_hdr, s));
-    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp, 0, nullptr, tq, tx));
-    if (check_pack_on()) {   // (tests) the strips' packing against k_pack_seq of the same bytes
-        HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
-        if (!rpack_sweep && check_pack(Rp, rn, sc + 8, rq, rx, s)) return ctx->fail(SCCG_E_INTERNAL, "strip-packed R' differs");
-        if (check_pack(Tp, tn, sc + 3, tq, tx, s)) return ctx->fail(SCCG_E_INTERNAL, "strip-packed T' differs");
-    }
+    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
     // ---- header + lowercase line (compression.cpp:337-368) and the N line: side2, driven by the
     //      context's host worker (its launches wait on run counts).  They need only T, so they are
     //      queued right behind the target's strip -- ahead of the local pass and the walk, which
@@ -532,8 +487,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_hdr, 0));
         void* ws_early = ctx->get(B_WALK, wsb);
         if (!ws_early) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
-        TRY(global_sweep_early(Rp, rn, sc + 8, rq, rx, !rpack_sweep, tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb,
-                               ctx->side));
+        TRY(global_sweep_early(Rp, rn, sc + 8, tfa, tn, sc, kg, mg, walk_chunk(tn), ws_early, wsb, ctx->side));
     }
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
     // ---- fork.  The local pass (compression.cpp:372-474, main stream) is latency-bound; the
@@ -599,7 +553,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     const int64_t np[2] = {lt[1], lr[1]};
     void* ws = ctx->get(B_WALK, wsb);
     if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace of %zu bytes", wsb);
-    TRY(global_prepare(Rp, np[1], Tp, np[0], pr, pt, kg, mg, walk_chunk(tn), ws, wsb, s2));
+    TRY(global_prepare(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, s2));
     HIPTRY(hipEventRecord(ctx->ev_join, s2));
     if (local_order == 1 || iters <= 0 || force_global) TRY(launch_local(s2));
 
@@ -672,7 +626,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
                },
                [&](hipStream_t st) -> int { return local_order == 2 ? ensure_local(st) : 0; }};
         const EmitTarget target{&Late::call, &late, &Late::abandon, &Late::round1};
-        const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], pr, pt, kg, mg, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
+        const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
                                              s2, paren, &target, /*keep_flat=*/false);
         if (rc != WALK_ABANDONED) {
             TRY(rc);
@@ -1212,20 +1166,13 @@ int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, s
         GET(uint8_t, T, B_TP, nt + 64);
         if (nr) HIPTRY(hipMemcpyAsync(R, sr, nr, hipMemcpyHostToDevice, s));
         if (nt) HIPTRY(hipMemcpyAsync(T, st, nt, hipMemcpyHostToDevice, s));
-        GET(uint32_t, rq, B_RQ, pack_q_words((int64_t)nr));
-        GET(uint32_t, rx, B_RX, pack_x_words((int64_t)nr));
-        GET(uint32_t, tq, B_TQ, pack_q_words((int64_t)nt));
-        GET(uint32_t, tx, B_TX, pack_x_words((int64_t)nt));
-        TRY(launch_pack_seq(R, (int64_t)nr, nullptr, rq, rx, s));
-        TRY(launch_pack_seq(T, (int64_t)nt, nullptr, tq, tx, s));
-        const PackedSeq pr{rq, rx}, pt{tq, tx};
         const size_t wsb = walk_workspace_bytes((int64_t)nr, (int64_t)nt, k, walk_chunk((int64_t)nt));
         void* ws = ctx->get(B_WALK, wsb);
         GET(uint8_t, txt, B_OUT, 4 * nt + 64);
         if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace");
         WalkResult wr{};
         int64_t tl = 0;
-        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, pr, pt, k, m, walk_chunk((int64_t)nt), ws, wsb, txt, &tl, &wr, s));
+        TRY(global_match_and_emit(R, (int64_t)nr, T, (int64_t)nt, k, m, walk_chunk((int64_t)nt), ws, wsb, txt, &tl, &wr, s));
         const int32_t *dt, *dp, *dl;
         int64_t nm;
         global_matches(ws, &dt, &dp, &dl, &nm);

@@ -100,10 +100,6 @@ constexpr int CH_HANDBACK_N = SCCG_CH_HANDBACK;
 struct WalkPtrs {
     const uint8_t* R;
     const uint8_t* T;
-    const uint32_t* Rq;       // 2-bit packed R' / T' (internal.h PackedSeq): the walk's reads
-    const uint32_t* Rx;
-    const uint32_t* Tq;
-    const uint32_t* Tx;
     int32_t nR, nT, k, m, S, C, cap;
     int32_t kp;               // key length: min(k, KEY_K); k > KEY_K confirms the rest by extension (KEY_K)
     int32_t* bt[2];
@@ -180,72 +176,27 @@ struct WalkPtrs {
     int32_t dbg_phases;       // SCCG_DEBUG_PHASES: also per-phase clocks
 };
 
-// 32 bases from base position pos (pos >= 0): their codes, base pos at bits 0-1 (three dword loads,
-// two funnel shifts); Q is a global or an LDS word array
-template <typename Q>
-__device__ __forceinline__ uint64_t q_bits64(Q q, int64_t pos) {
-    const int64_t w = pos >> 4;
-    const uint32_t sh = 2u * (uint32_t)(pos & 15);
-    const uint32_t w0 = q[w], w1 = q[w + 1], w2 = q[w + 2];
-    return ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32) | __builtin_amdgcn_alignbit(w1, w0, sh);
-}
-// exception bits of the 32 bases from pos
-__device__ __forceinline__ uint32_t x_bits32(const uint32_t* __restrict__ x, int64_t pos) {
-    const int64_t w = pos >> 5;
-    return __builtin_amdgcn_alignbit(x[w + 1], x[w], (uint32_t)(pos & 31));
-}
-// 1 bit per base: bit i set where 2-bit group i of d is nonzero
-__device__ __forceinline__ uint32_t nz_groups(uint64_t d) {
-    uint64_t t = (d | (d >> 1)) & 0x5555555555555555ull;
-    t = (t | (t >> 1)) & 0x3333333333333333ull;
-    t = (t | (t >> 2)) & 0x0f0f0f0f0f0f0f0full;
-    t = (t | (t >> 4)) & 0x00ff00ff00ff00ffull;
-    t = (t | (t >> 8)) & 0x0000ffff0000ffffull;
-    t = (t | (t >> 16)) & 0x00000000ffffffffull;
-    return (uint32_t)t;
-}
-// first base i < 32 where two 32-base stretches differ (32: none): codes cr / ct, exception bits xr /
-// xt, bytes pr / pt (consulted only where both bases are exceptions -- IUPAC codes, '>' lines)
-__device__ __forceinline__ int first_diff_q(uint64_t cr, uint64_t ct, uint32_t xr, uint32_t xt, const uint8_t* pr,
-                                            const uint8_t* pt) {
-    const uint64_t d = cr ^ ct;
-    const uint32_t e = xr | xt;
-    if (!e) return d ? (int)(__builtin_ctzll(d) >> 1) : 32;
-    uint32_t mm = nz_groups(d) | e;
-    const uint32_t both = xr & xt;
-    while (mm) {
-        const int i = __builtin_ctz(mm);
-        if (!((both >> i) & 1u) || pr[i] != pt[i]) return i;
-        mm &= mm - 1;
-    }
-    return 32;
-}
-
-// Per-wave LDS: the window's Bloom filter (wide literal scans) and a copy of the last LBV bases the
-// extension loaded from R' and from T', 2-bit packed (2 KiB each).  A match step reads its next
-// window (R' around the new P), its next probe (T' right after the match) and usually the start of
-// its next extension from that copy: after a match the walk continues on the same diagonal, inside
-// the bases it just compared.  So most steps make no dependent HBM round trip at all; only an
-// extension that runs past the copy loads (and refreshes it).  The copy holds codes only: a flag
-// per side says whether its range holds any exception base (then those bits come from HBM).
+// Per-wave LDS: the window's Bloom filter (wide literal scans) and a copy of the last 2 KiB the
+// extension loaded from R' and from T'.  A match step reads its next window (R' around the new P),
+// its next probe (T' right after the match) and usually the start of its next extension from that
+// copy: after a match the walk continues on the same diagonal, inside the bytes it just compared.
+// So most steps make no dependent HBM round trip at all; only an extension that runs past the copy
+// loads (and refreshes it).
 constexpr int WFBITS = 14;             // window pre-filter: 16384-bit Bloom filter, 3 hashes
-constexpr int LBV = 8192;              // bases of R' and of T' kept per wave
-constexpr int LBQ = LBV / 16;          // their packed words
-constexpr int LEAD = 128;              // bases before the extension's start (the next window reaches back m)
-static_assert(LBV + 4 * LEAD <= PACK_PAD_BLOCKS * 64, "a copy past the sequence end stays in the padding");
+constexpr int LBV = 2048;              // bytes of R' and of T' kept per wave
+constexpr int LEAD = 128;              // of which before the extension's start (the next window reaches back m)
 __device__ __forceinline__ uint32_t wf_h1(uint32_t key) { return slot_hash(key, WFBITS); }
 __device__ __forceinline__ uint32_t wf_h2(uint32_t key) { return (key * 0x85EBCA77u) >> (32 - WFBITS); }
 __device__ __forceinline__ uint32_t wf_h3(uint32_t key) { return (key * 0xC2B2AE3Du + 0x27D4EB2Fu) >> (32 - WFBITS); }
 struct WalkLds {
     uint32_t wbits[1 << (WFBITS - 5)];
-    uint32_t rq[LBQ + 4];   // packed R'[rb0, rb0 + LBV)  (+ words read by the funnel shifts)
-    uint32_t tq[LBQ + 4];   // packed T'[tb0, tb0 + LBV)
+    uint8_t rbuf[LBV + 64];   // R'[rb0, rb0 + LBV)  (+ slack read by the unaligned word loads)
+    uint8_t tbuf[LBV + 64];   // T'[tb0, tb0 + LBV)
 };
-// the copy's bases (wave-uniform, multiples of 128); NO_BUF: nothing copied yet
+// the copy's bases (wave-uniform); NO_BUF: nothing copied yet
 constexpr int32_t NO_BUF = INT32_MIN / 2;
 struct BufPos {
     int32_t rb0 = NO_BUF, tb0 = NO_BUF;
-    bool rx = true, tx = true;   // the copy's range may hold exception bases
     __device__ __forceinline__ bool has_r(int32_t a, int32_t n) const { return a >= rb0 && a + n <= rb0 + LBV; }
     __device__ __forceinline__ bool has_t(int32_t a, int32_t n) const { return a >= tb0 && a + n <= tb0 + LBV; }
 };
@@ -260,74 +211,29 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int
     return true;
 }
 
-// 32 packed bases at base offset off of an LDS copy (in_lds) or at base pos of a global array.  The
-// empty asm after the global loads keeps the compiler from merging the two paths into FLAT loads
-// through a selected pointer (FLAT loads count against lgkmcnt: every later LDS wait would wait for
-// HBM).
-__device__ __forceinline__ uint64_t q_sel(bool in_lds, const uint32_t* lds, int32_t off, const uint32_t* __restrict__ g,
-                                          int64_t pos) {
-    uint64_t v;
-    if (in_lds) {
-        v = q_bits64(lds, off);
-    } else {
-        v = q_bits64(g, pos);
-        asm volatile("" ::: "memory");
-    }
-    return v;
+// ND words at byte offset off of an LDS byte array (ND + 1 aligned ds_read_b32)
+template <int ND>
+__device__ __forceinline__ void loadw_lds(const uint8_t* lds, int32_t off, uint32_t (&o)[ND]) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (off >> 2);
+    const uint32_t sh = (uint32_t)(off & 3);
+    uint32_t v[ND + 1];
+#pragma unroll
+    for (int i = 0; i <= ND; i++) v[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < ND; i++) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
 }
 
-// longest common extension of R'[a..] and T'[b..], at most maxlen bases (extend_alignment,
-// compression.cpp:27-34); whole wave, 32 bases per lane per step (64-bit XOR of packed codes).
-// From the LDS copy while both starts lie in it; past it, the copy is refilled from HBM: LBV bases
-// of each side from up to 2 * LEAD before the next compare (two 16-byte loads per lane and side).
-__device__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a, int32_t b, int32_t maxlen) {
-    const int lane = lane_id();
-    if (maxlen <= 0) return 0;
-    int32_t off = 0;
-    for (;;) {
-        const int32_t ra0 = a + off, tb0 = b + off;
-        if (ra0 >= B.rb0 && tb0 >= B.tb0 && ra0 < B.rb0 + LBV && tb0 < B.tb0 + LBV) {
-            int32_t avail = B.rb0 + LBV - ra0 < B.tb0 + LBV - tb0 ? B.rb0 + LBV - ra0 : B.tb0 + LBV - tb0;
-            if (avail > maxlen - off) avail = maxlen - off;
-            for (int32_t o = 0; o < avail; o += 64 * 32) {
-                const int32_t i = o + 32 * lane;   // this lane's 32 bases from ra0 / tb0
-                int32_t e = INT32_MAX;
-                if (i < avail) {
-                    const int32_t ra = ra0 + i, tb = tb0 + i;
-                    const uint64_t cr = q_bits64(L.rq, ra - B.rb0), ct = q_bits64(L.tq, tb - B.tb0);
-                    const uint32_t xr = B.rx ? x_bits32(A.Rx, ra) : 0u, xt = B.tx ? x_bits32(A.Tx, tb) : 0u;
-                    const int pos = first_diff_q(cr, ct, xr, xt, A.R + ra, A.T + tb);
-                    if (pos < 32 && i + pos < avail) e = off + i + pos;   // (at or past avail: undecided here)
-                }
-                const unsigned long long sm = __ballot(e != INT32_MAX);
-                if (sm) {
-                    const int32_t m = lane_val(e, first_lane(sm));
-                    return m < maxlen ? m : maxlen;
-                }
-            }
-            off += avail;
-            if (off >= maxlen) return maxlen;
-            continue;
-        }
-        // refill: LBV bases of each side from LEAD..LEAD+127 before the next compare, 128-aligned
-        const int32_t sa = (ra0 >= LEAD ? ra0 - LEAD : 0) & ~127, sb = (tb0 >= LEAD ? tb0 - LEAD : 0) & ~127;
-        const uint4* gr = reinterpret_cast<const uint4*>(A.Rq + (sa >> 4)) + 2 * lane;
-        const uint4* gt = reinterpret_cast<const uint4*>(A.Tq + (sb >> 4)) + 2 * lane;
-        const uint4 r0 = gr[0], r1 = gr[1], t0 = gt[0], t1 = gt[1];
-        const uint4 xr4 = reinterpret_cast<const uint4*>(A.Rx + (sa >> 5))[lane];
-        const uint4 xt4 = reinterpret_cast<const uint4*>(A.Tx + (sb >> 5))[lane];
-        wave_sync();   // the copy's previous readers are done
-        {
-            uint4* dr = reinterpret_cast<uint4*>(L.rq) + 2 * lane;
-            uint4* dt = reinterpret_cast<uint4*>(L.tq) + 2 * lane;
-            dr[0] = r0; dr[1] = r1;
-            dt[0] = t0; dt[1] = t1;
-        }
-        wave_sync();
-        B.rb0 = sa;
-        B.tb0 = sb;
-        B.rx = __ballot((xr4.x | xr4.y | xr4.z | xr4.w) != 0) != 0;
-        B.tx = __ballot((xt4.x | xt4.y | xt4.z | xt4.w) != 0) != 0;
+// ND words at byte offset lds_off of an LDS copy (in_lds) or at g in global memory.  The empty asm
+// after the global load keeps the compiler from merging the two loads into one FLAT load through a
+// selected pointer (FLAT loads count against lgkmcnt: every later LDS wait would wait for HBM).
+template <int ND>
+__device__ __forceinline__ void loadw_sel(bool in_lds, const uint8_t* lds, int32_t lds_off, const uint8_t* g,
+                                          uint32_t (&o)[ND]) {
+    if (in_lds) {
+        loadw_lds<ND>(lds, lds_off, o);
+    } else {
+        loadw<ND>(g, o);
+        asm volatile("" ::: "memory");
     }
 }
 
@@ -342,7 +248,70 @@ __device__ __forceinline__ int first_diff32(const uint32_t (&r)[8], const uint32
     return pos;
 }
 
-// the same from HBM bytes only (no copy kept; 2 KiB per round trip): the first step's statistics
+// longest common extension of R[a..] and T[b..], at most maxlen bytes (extend_alignment,
+// compression.cpp:27-34); whole wave.  First from the LDS copy when both starts lie in it; then
+// from HBM, 2 KiB per round trip (lanes 0-3 load the LEAD bytes before the stretch compared), every
+// HBM step leaving its bytes in the copy.
+__device__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a, int32_t b, int32_t maxlen) {
+    const int lane = lane_id();
+    if (maxlen <= 0) return 0;
+    int32_t off = 0;
+    if (a >= B.rb0 && b >= B.tb0 && a < B.rb0 + LBV && b < B.tb0 + LBV) {
+        int32_t avail = B.rb0 + LBV - a < B.tb0 + LBV - b ? B.rb0 + LBV - a : B.tb0 + LBV - b;
+        if (avail > maxlen) avail = maxlen;
+        const int32_t my = 32 * lane;
+        int32_t e = INT32_MAX;
+        if (my < avail) {
+            uint32_t r[8], t[8];
+            loadw_lds<8>(L.rbuf, a - B.rb0 + my, r);
+            loadw_lds<8>(L.tbuf, b - B.tb0 + my, t);
+            int pos = first_diff32(r, t);
+            if (avail - my < 32 && pos >= avail - my) pos = avail - my == maxlen - my ? avail - my : 32;
+            if (pos < 32) e = my + pos;
+        }
+        const unsigned long long sm = __ballot(e != INT32_MAX);
+        if (sm) {
+            const int32_t m = lane_val(e, first_lane(sm));
+            return m < maxlen ? m : maxlen;
+        }
+        if (avail >= maxlen) return maxlen;
+        off = avail;
+    }
+    while (off < maxlen) {
+        const int32_t lead = (a + off >= LEAD && b + off >= LEAD) ? LEAD : 0;
+        const int32_t sa = a + off - lead, sb = b + off - lead;
+        uint32_t r[8], t[8];
+        loadw<8>(A.R + sa + 32 * lane, r);
+        loadw<8>(A.T + sb + 32 * lane, t);
+        wave_sync();   // the copy's previous readers are done
+        {
+            uint4* dr = reinterpret_cast<uint4*>(L.rbuf) + 2 * lane;
+            uint4* dt = reinterpret_cast<uint4*>(L.tbuf) + 2 * lane;
+            dr[0] = make_uint4(r[0], r[1], r[2], r[3]); dr[1] = make_uint4(r[4], r[5], r[6], r[7]);
+            dt[0] = make_uint4(t[0], t[1], t[2], t[3]); dt[1] = make_uint4(t[4], t[5], t[6], t[7]);
+        }
+        wave_sync();
+        B.rb0 = sa;
+        B.tb0 = sb;
+        const int32_t rel = 32 * lane - lead;   // this lane's bytes, from a + off
+        int32_t e = INT32_MAX;
+        if (rel >= 0 && rel < maxlen - off) {
+            int pos = first_diff32(r, t);
+            const int32_t lim = maxlen - off - rel;
+            if (lim < 32 && pos > lim) pos = lim;
+            if (pos < 32) e = off + rel + pos;
+        }
+        const unsigned long long sm = __ballot(e != INT32_MAX);
+        if (sm) {
+            const int32_t m = lane_val(e, first_lane(sm));
+            return m < maxlen ? m : maxlen;
+        }
+        off += LBV - lead;
+    }
+    return maxlen;
+}
+
+// the same from HBM only (no copy kept; 2 KiB per round trip)
 __device__ int32_t wave_lce_hbm(const uint8_t* __restrict__ R, int32_t a, const uint8_t* __restrict__ T, int32_t b,
                                 int32_t maxlen) {
     const int lane = lane_id();
@@ -402,21 +371,26 @@ __device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin&
     const bool lds = L && B->has_r(W.lo, W.n + 20);
     const int i0 = 4 * lane;
     if (i0 >= W.n) return;
-    const int32_t pos = W.lo + i0;
-    const uint64_t code = q_sel(lds, lds ? L->rq : nullptr, lds ? pos - B->rb0 : 0, A.Rq, pos);
-    const uint32_t bad = (lds && !B->rx) ? 0u : x_bits32(A.Rx, pos);
+    uint32_t w[5];   // 20 bytes >= 3 + k
+    loadw_sel<5>(lds, lds ? L->rbuf : nullptr, lds ? W.lo - B->rb0 + i0 : 0, A.R + W.lo + i0, w);
+    uint64_t code;
+    uint32_t bad;
+    pack_codes<5>(w, code, bad);
     const int kp = A.kp;
     const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        W.key[q] = (bad >> q) & KM ? exotic_key(A.R + pos + q, kp) : (uint32_t)(code >> (2 * q)) & MASK;
+        W.key[q] = (bad >> q) & KM ? exotic_key(A.R + W.lo + i0 + q, kp) : (uint32_t)(code >> (2 * q)) & MASK;
         if (i0 + q < W.n) W.vmask |= 1u << q;
     }
 }
 
-// key of the target k-mer at y from its packed codes (32 bases from y) and exception bits (kp <= 15)
-__device__ __forceinline__ uint32_t target_key_q(const WalkPtrs& A, int32_t y, uint64_t code, uint32_t bad) {
+// key of the target k-mer at y from its 16 bytes w (loaded by the caller; kp <= 15)
+__device__ __forceinline__ uint32_t target_key_w(const WalkPtrs& A, int32_t y, const uint32_t (&w)[4]) {
     const int kp = A.kp;
+    uint64_t code;
+    uint32_t bad;
+    pack_codes<4>(w, code, bad);
     return bad & ((1u << kp) - 1u) ? exotic_key(A.T + y, kp) : (uint32_t)code & ((1u << (2 * kp)) - 1u);
 }
 
@@ -459,17 +433,14 @@ constexpr int WIDE = 16;   // positions per lane per step (1024 per wave step)
 __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, const RegWin& W, int32_t x, int32_t end) {
     const int lane = lane_id(), k = A.kp;
     const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
-    // 32 packed bases >= WIDE + k - 1 per lane; the next step's are loaded one step ahead
-    uint64_t ncode = q_bits64(A.Tq, (int64_t)x + WIDE * lane);
-    uint32_t nbad = x_bits32(A.Tx, (int64_t)x + WIDE * lane);
+    uint32_t w[8];   // 32 bytes >= WIDE + k - 1; the next step's words are loaded one step ahead
+    loadw<8>(A.T + x + WIDE * lane, w);
     for (int32_t base = x; base < end; base += 64 * WIDE) {
         const int32_t p0 = base + WIDE * lane;
-        const uint64_t code = ncode;
-        const uint32_t bad = nbad;
-        if (base + 64 * WIDE < end) {
-            ncode = q_bits64(A.Tq, (int64_t)p0 + 64 * WIDE);
-            nbad = x_bits32(A.Tx, (int64_t)p0 + 64 * WIDE);
-        }
+        uint64_t code;
+        uint32_t bad;
+        pack_codes<8>(w, code, bad);
+        if (base + 64 * WIDE < end) loadw<8>(A.T + p0 + 64 * WIDE, w);
         // Bloom test for all 16 positions (independent LDS reads)
         uint32_t cand = 0;
 #pragma unroll
@@ -503,48 +474,6 @@ __device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L
 }
 
 // ---------------------------------------------------------------------------------------------
-// 2-bit packed sequence (internal.h PackedSeq): one thread per 64 bases -- four aligned 16-byte
-// loads, the SWAR codes of common.h, one 16-byte code store and one 8-byte exception store.
-// HBM: 1 B read + 0.375 B written per base.
-// ---------------------------------------------------------------------------------------------
-// (kfrom > 0: only the blocks a k_sweep_early<true> with k = kfrom did not pack: from the first
-// block at or past its last k-mer start on)
-__global__ __launch_bounds__(SCCG_BLOCK) void k_pack_seq(const uint8_t* __restrict__ s, int64_t n_bound,
-                                                         const int64_t* __restrict__ d_n, uint32_t* __restrict__ q,
-                                                         uint32_t* __restrict__ x, int kfrom) {
-    const int64_t n = d_n ? *d_n : n_bound;
-    const int64_t nblk = pack_blocks(n_bound);
-    const int64_t npos = n - kfrom + 1 > 0 ? n - kfrom + 1 : 0;
-    const int64_t b0 = kfrom > 0 ? (npos + 63) / 64 : 0;
-    for (int64_t b = b0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t p0 = 64 * b;
-        uint32_t cw[4] = {0, 0, 0, 0}, xw[2] = {~0u, ~0u};
-        if (p0 < n) {
-            const uint4* src = reinterpret_cast<const uint4*>(s + p0);
-            uint32_t w[16];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint4 v = src[i];
-                w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
-            }
-            uint64_t bad = 0;
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                uint32_t d;
-                const uint32_t c = swar_codes(w[i], d);
-                cw[i >> 2] |= c << (8 * (i & 3));
-                if (d) bad |= (uint64_t)nz_bytes(d) << (4 * i);
-            }
-            if (n - p0 < 64) bad |= ~0ull << (n - p0);   // past the sequence
-            xw[0] = (uint32_t)bad;
-            xw[1] = (uint32_t)(bad >> 32);
-        }
-        reinterpret_cast<uint4*>(q)[b] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-        reinterpret_cast<uint2*>(x)[b] = make_uint2(xw[0], xw[1]);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // the chunk walk (one wave per chunk)
 // ---------------------------------------------------------------------------------------------
 __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0);   // anchors, below
@@ -553,7 +482,6 @@ constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cand
 #ifndef WALK_WAVES_PER_EU
 #define WALK_WAVES_PER_EU 5
 #endif
-// nlist_dev (optional): the list length from device memory (a round queued before the host knows it)
 // nlist_dev (optional): the list length from device memory (a round queued before the host knows it)
 template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
@@ -666,16 +594,15 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         // the probe: keys of the 64 target positions from x (from the LDS copy when it holds them)
         const int32_t y_l = x + lane;
         const bool valid = y_l < scan_end;
-        // (the packed arrays carry padding past T': no bound needed for the global loads)
-        const bool tin = B.has_t(x, 64 + 16);
-        const uint64_t tcode = q_sel(tin, L.tq, y_l - B.tb0, A.Tq, y_l);
-        const uint32_t tbad = (tin && !B.tx) ? 0u : x_bits32(A.Tx, y_l);
+        uint32_t tw[4];
+        // (4 KiB readable slack after T: no bound needed for the global load)
+        loadw_sel<4>(B.has_t(x, 64 + 16), L.tbuf, y_l - B.tb0, A.T + y_l, tw);
         if (W.P != P) { reg_window(A, P, W, &L, &B); if (DBG) dbg_c[3]++; }
         if (DBG) tick(6);
         if (W.n <= 0) { x = scan_end; break; }
         if (DBG) dbg_c[1]++;
         // ---- literal steps: first y in [x, scan_end) whose k-mer has a candidate in the window
-        const uint32_t key_l = valid ? target_key_q(A, y_l, tcode, tbad) : 0u;
+        const uint32_t key_l = valid ? target_key_w(A, y_l, tw) : 0u;
         int hl = -1;
         const int nb = scan_end - x < 64 ? scan_end - x : 64;
         for (int yy = 0; yy < nb; yy++) {
@@ -1110,8 +1037,10 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
     const int kp = A.kp;   // (keys of the first kp bases: hits are a superset for k > KEY_K)
     const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
     for (int32_t q = blo + tid; q <= bhi; q += 1024) {   // the band's keys
-        const uint64_t code = q_bits64(A.Rq, q);
-        const uint32_t bad = x_bits32(A.Rx, q);
+        uint32_t wv[4], bad;
+        uint64_t code;
+        loadw<4>(A.R + q, wv);
+        pack_codes<4>(wv, code, bad);
         uint32_t key = bad & KM ? exotic_key(A.R + q, kp) : (uint32_t)code & MASK;
         if (key == CH_EMPTY) key = CH_EMPTY - 1;   // (exotic hash collision: a superset is fine)
         uint32_t sl = ch_slot(key);
@@ -1160,8 +1089,9 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
         uint64_t code = 0;
         uint32_t bad = 0;
         if (p0 < b1) {
-            code = q_bits64(A.Tq, p0);   // (padding after packed T')
-            bad = x_bits32(A.Tx, p0);
+            uint32_t wv[8];
+            loadw<8>(A.T + p0, wv);   // 4 KiB readable slack after T'
+            pack_codes<8>(wv, code, bad);
             const int lim = b1 - p0 < 16 ? (int)(b1 - p0) : 16;
             for (int st = 0; st < lim; st++) {
                 const uint32_t key = (bad >> st) & KM ? exotic_key(A.T + p0 + st, kp) : (uint32_t)(code >> (2 * st)) & MASK;
@@ -1474,8 +1404,8 @@ __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0) {
     for (int b = 0; b < NB; b++) {
         const int32_t y = y0 + b * 64 + lane;
         dg[b] = INVALID;
-        if (y + ANCHOR_K <= A.nT && x_bits32(A.Tx, y) == 0) {
-            const uint64_t code = q_bits64(A.Tq, y);
+        uint64_t code;
+        if (y + ANCHOR_K <= A.nT && code32<false>(A.T + y, code)) {
             const uint64_t key = mix64(code);
             const uint64_t v = A.atab[key >> (64 - A.abits)];
             if ((uint32_t)(v >> 32) == anchor_tag(key, A.agen) && (uint32_t)v != A_MULTI) dg[b] = (int32_t)(uint32_t)v - y;
@@ -1811,20 +1741,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
                   },
                   [&](int64_t p0, const uint32_t (&cw)[20], const uint32_t (&dw)[20], uint32_t acc) {
                       if (!ANCH) return;
-                      if (A.Rq) {   // the 2-bit packed R' of this 64-base block (k_pack_seq's layout)
-                          uint32_t q4[4];
-#pragma unroll
-                          for (int j = 0; j < 4; j++)
-                              q4[j] = cw[4 * j] | (cw[4 * j + 1] << 8) | (cw[4 * j + 2] << 16) | (cw[4 * j + 3] << 24);
-                          uint64_t bad = 0;
-                          if (acc) {
-#pragma unroll
-                              for (int i = 0; i < 16; i++) bad |= (uint64_t)nz_bytes(dw[i]) << (4 * i);
-                          }
-                          if (nR - p0 < 64) bad |= ~0ull << (nR - p0);   // past R'
-                          reinterpret_cast<uint4*>(const_cast<uint32_t*>(A.Rq))[p0 >> 6] = make_uint4(q4[0], q4[1], q4[2], q4[3]);
-                          reinterpret_cast<uint2*>(const_cast<uint32_t*>(A.Rx))[p0 >> 6] = make_uint2((uint32_t)bad, (uint32_t)(bad >> 32));
-                      }
 #pragma unroll
                       for (int h = 0; h < 2; h++) {
                           const int64_t p = p0 + 32 * h;
@@ -1841,57 +1757,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
                           A.atab[key >> (64 - A.abits)] = ((uint64_t)anchor_tag(key, A.agen) << 32) | (uint32_t)p;
                       }
                   });
-}
-
-// The same sweep over the 2-bit packed R' (the strip packed it): 0.375 B per base instead of 1, one
-// thread per 64-base block -- its four code words and the next one (the k-mers overhanging the
-// block), its two exception words and the next one.  The anchor samples at every 32nd position are
-// exactly the block's two 64-bit code words.
-__global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_packed(WalkPtrs A) {
-    const int k = A.k, kp = A.kp;
-    const int64_t nR = A.dnR ? *A.dnR : A.nR;   // |R'| (A.nR only bounds it)
-    const bool have = *reinterpret_cast<const int32_t*>(A.kb + KB_COUNT) == k;
-    const uint32_t key0 = have ? walk_key(A.kb, kp) : KEY_EXOTIC;
-    const bool want = key0 < KEY_EXOTIC;
-    const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
-    const int64_t npos = nR - k + 1;
-    const int64_t nblk = (nR + 63) / 64;
-    const uint4* q4 = reinterpret_cast<const uint4*>(A.Rq);
-    const uint2* x2 = reinterpret_cast<const uint2*>(A.Rx);
-    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t p0 = 64 * b;
-        const uint4 qa = q4[b];
-        const uint2 xa = x2[b];
-        const uint32_t qn = A.Rq[4 * b + 4], xn = A.Rx[2 * b + 2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {   // anchors (astep 32)
-            const int64_t p = p0 + 32 * h;
-            if (p + ANCHOR_K > nR || (h ? xa.y : xa.x)) continue;
-            const uint64_t code = h ? ((uint64_t)qa.w << 32 | qa.z) : ((uint64_t)qa.y << 32 | qa.x);
-            const uint64_t key = mix64(code);
-            A.atab[key >> (64 - A.abits)] = ((uint64_t)anchor_tag(key, A.agen) << 32) | (uint32_t)p;
-        }
-        if (!want || p0 >= npos) continue;
-        const uint32_t w[5] = {qa.x, qa.y, qa.z, qa.w, qn};
-        const uint32_t xw[3] = {xa.x, xa.y, xn};
-        uint64_t hits = 0;
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const uint64_t code = ((uint64_t)w[g + 1] << 32) | w[g];
-            const uint32_t bad = __builtin_amdgcn_alignbit(xw[(g >> 1) + 1], xw[g >> 1], 16u * (uint32_t)(g & 1));
-#pragma unroll
-            for (int st = 0; st < 16; st++)
-                if (((uint32_t)(code >> (2 * st)) & MASK) == key0 && !((bad >> st) & KM)) hits |= 1ull << (16 * g + st);
-        }
-        if (npos - p0 < 64) hits &= (1ull << (npos - p0)) - 1;
-        while (hits) {
-            const int64_t c = p0 + __builtin_ctzll(hits);
-            hits &= hits - 1;
-            if (k > kp && !bytes_eq(A.R + c + kp, A.kb + kp, k - kp)) continue;
-            const unsigned long long i = atomicAdd(&A.fc[13], 1ull);
-            if (i < (unsigned long long)CAND_CAP) A.cand[i] = (int32_t)c;
-        }
-    }
 }
 
 // after T' exists: statistics of x0 = 0 over the early sweep's positions (as k_key0 +
@@ -2375,9 +2240,6 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
 // SCCG_DEBUG runs take the instrumented walk
 using WalkKernel = void (*)(WalkPtrs, const int32_t*, int32_t, const int32_t*);
 WalkKernel walk_kernel(const WalkPtrs& A) { return A.dbg ? k_walk<true> : k_walk<false>; }
-// blocks of a walk launch over nlist chunks: no more than fit on the GPU at once (its waves take the
-// chunks from a queue)
-unsigned walk_grid(int64_t nlist) { return grid_for(nlist, WPB); }
 
 struct FullC {
     int64_t lmax;
@@ -2496,28 +2358,13 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s, std::vector<int32_t>* resume
         int rc = dev_set_i32(A.scal + 1, 1, {0}, s);
         if (rc) return rc;
         if ((rc = h2d_sync(A.rlist, rl.data(), rl.size() * 4, s))) return rc;
-        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(walk_grid((int64_t)rl.size())), dim3(SCCG_BLOCK), 0, s, A,
+        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
                     (const int32_t*)A.rlist, (int32_t)rl.size(), (const int32_t*)nullptr);
         SCCG_HIP(hipGetLastError());
     }
 }
 
 }  // namespace
-
-int launch_pack_seq(const uint8_t* s, int64_t n_bound, const int64_t* d_n, uint32_t* q, uint32_t* x, hipStream_t st) {
-    const int64_t nblk = pack_blocks(n_bound);
-    const unsigned g = grid_for(nblk, SCCG_BLOCK) > 16384 ? 16384 : grid_for(nblk, SCCG_BLOCK);
-    hipLaunchKernelGGL(k_pack_seq, dim3(g), dim3(SCCG_BLOCK), 0, st, s, n_bound, d_n, q, x, 0);
-    SCCG_HIP(hipGetLastError());
-    return 0;
-}
-
-int launch_pack_seq_from(const uint8_t* s, int64_t n_bound, const int64_t* d_n, uint32_t* q, uint32_t* x, int kfrom,
-                         hipStream_t st) {
-    hipLaunchKernelGGL(k_pack_seq, dim3(64), dim3(SCCG_BLOCK), 0, st, s, n_bound, d_n, q, x, kfrom);
-    SCCG_HIP(hipGetLastError());
-    return 0;
-}
 
 size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk) {
     size_t used = 0;
@@ -2627,12 +2474,11 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
 
 void global_prepare_reset() { g_prep = Prepared{}; g_early = Early{}; }
 
-int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, uint32_t* rq, uint32_t* rx, bool packed,
-                       const uint8_t* tgt_fa, int64_t tn, const int64_t* d_hdr, int k, int m, int chunk, void* ws,
-                       size_t ws_bytes, hipStream_t s) {
+int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, const uint8_t* tgt_fa, int64_t tn,
+                       const int64_t* d_hdr, int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s) {
     g_early = Early{};
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
-    if (nRp < k || tn <= 0) return packed ? 0 : launch_pack_seq(Rp, nRp, d_nRp, rq, rx, s);   // no walk can use the sweep
+    if (nRp < k || tn <= 0) return 0;   // no walk can use it
     size_t used = 0;
     // |T'| <= tn: the carve's R'-only front (anchor table, fc, positions, kb) does not depend on it;
     // nRp bounds |R'|, which the sweep reads from d_nRp
@@ -2643,20 +2489,9 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, uin
     RC(set_u64(A.fc + 12, {0, 0}, s));
     hipLaunchKernelGGL(k_first_kmer, dim3(1), dim3(SCCG_BLOCK), 0, s, tgt_fa, tn, d_hdr, k, (int64_t)1 << 20, A.kb);
     const unsigned g = first_sweep_grid(A);
-    if (A.astep == 32 && packed) {
-        // R' is packed already (by its strip): the sweep reads the packed words
-        A.Rq = rq;
-        A.Rx = rx;
-        PROF_LAUNCH(PROF_ANCHOR, s, k_sweep_packed, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
-    } else if (A.astep == 32) {
-        // the sweep packs R' as it reads it; the blocks past its last k-mer start (and the padding)
-        // are packed behind it
-        A.Rq = rq;
-        A.Rx = rx;
+    if (A.astep == 32) {
         PROF_LAUNCH(PROF_ANCHOR, s, k_sweep_early<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
-        hipLaunchKernelGGL(k_pack_seq, dim3(64), dim3(SCCG_BLOCK), 0, s, Rp, nRp, d_nRp, rq, rx, k);
     } else {
-        if (!packed) RC(launch_pack_seq(Rp, nRp, d_nRp, rq, rx, s));
         hipLaunchKernelGGL(k_sweep_early<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
         const int64_t ns = (int64_t)A.nR / A.astep + 1;
         const unsigned ga = grid_for(ns, 256) > 8192 ? 8192 : grid_for(ns, 256);
@@ -2667,8 +2502,8 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, uin
     return 0;
 }
 
-int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, const PackedSeq& pr, const PackedSeq& pt,
-                   int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s) {
+int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
+                   size_t ws_bytes, hipStream_t s) {
     g_prep = Prepared{};
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
     const Early e = g_early;
@@ -2676,7 +2511,6 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
     const bool early = e.ws == ws && e.R == Rp && e.nR >= nRp && e.k == k;
     size_t used = 0;
     WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used, early ? e.abits : 0);
-    A.Rq = pr.q; A.Rx = pr.x; A.Tq = pt.q; A.Tx = pt.x;
     if (used > ws_bytes) return SCCG_E_INTERNAL;
     if (early) {
         // the early sweep already stored the anchors and the first k-mer's positions
@@ -2698,8 +2532,7 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
     return 0;
 }
 
-int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, const PackedSeq& pr,
-                          const PackedSeq& pt, int k, int m, int chunk,
+int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
                           void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
                           bool abs_p, const EmitTarget* late_out, bool keep_flat) {
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
@@ -2709,7 +2542,6 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                           g.chunk == chunk;
     size_t used = 0;
     WalkPtrs A = make_ptrs(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, &used, prepared ? g.abits : 0);
-    A.Rq = pr.q; A.Rx = pr.x; A.Tq = pt.q; A.Tx = pt.x;
     if (used > ws_bytes) return SCCG_E_INTERNAL;
     res->rounds = 0;
     res->chains = 0;
@@ -2741,7 +2573,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     // (dev_nlist: the list length is the previous round tail's pending count, scal[0])
     auto queue_round = [&](int fbase_cap, bool dev_nlist) -> int {
         const int32_t* nd = dev_nlist ? A.scal : nullptr;
-        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(walk_grid(A.C)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist,
+        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist,
                     A.C, nd);
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
@@ -2907,7 +2739,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             A.round = (int32_t)round;   // every kernel of the round gets it by value
             const bool queued = pre_round && round == round0;
             if (!queued) {
-                PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(walk_grid(nlist)), dim3(SCCG_BLOCK), 0, s, A,
+                PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A,
                             (const int32_t*)A.plist, nlist, (const int32_t*)nullptr);
                 SCCG_HIP(hipGetLastError());
             }

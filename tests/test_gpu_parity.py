@@ -79,33 +79,6 @@ def test_fuzz_vs_oracle(ctx, kind, seed):
     assert _gpu_reconstruct(ctx, got, rfa) == _oracle_reconstruct(want, rfa)
 
 
-@pytest.mark.parametrize("kind,seed", [("local", s) for s in range(300, 306)] + [("global", s) for s in range(300, 306)] +
-                         [("iupac", s) for s in range(6)])
-def test_strip_pack_vs_pack_seq(ctx, kind, seed, monkeypatch):
-    """The 2-bit packing fused into the strip's write pass (ingest.hip stage_pack: tile-edge words
-    OR-ed, exception bits for non-ACGT bytes) equals a separate k_pack_seq over the stripped bytes,
-    padding included (SCCG_CHECK_PACK makes sccg_api.cpp compare them; a difference fails the call)."""
-    if kind == "iupac":   # exotic bytes (IUPAC codes, lowercase, N runs) at every tile phase
-        rng = random.Random(seed)
-        body = bytes(rng.choice(b"ACGTACGTACGTNRYKMacgtn") for _ in range(rng.randint(1, 40000)))
-        tb = bytearray(body)
-        for i in range(len(tb)):
-            if rng.random() < 0.01:
-                tb[i] = ord(rng.choice("ACGTNWS"))
-        rfa = b">r\n" + b"\n".join(body[i:i + 60] for i in range(0, len(body), 60)) + b"\n"
-        tfa = b">t\n" + b"\n".join(bytes(tb[i:i + 61]) for i in range(0, len(tb), 61)) + b"\n"
-    else:
-        rfa, tfa = (fuzzgen.local_case if kind == "local" else fuzzgen.global_case)(seed)
-    monkeypatch.setenv("SCCG_CHECK_PACK", "1")
-    try:
-        got = ctx.compress(rfa, tfa)
-    except sccg.SccgError as e:
-        assert e.rc != sccg.ERR_CODES["SCCG_E_INTERNAL"], str(e)
-        got = getattr(e, "partial", None)
-    monkeypatch.delenv("SCCG_CHECK_PACK")
-    assert got == oraclelib.compress(rfa, tfa)
-
-
 def _gpu_reconstruct(ctx, rec, rfa):
     try:
         return 0, ctx.reconstruct(rec, rfa)
