@@ -28,6 +28,12 @@
 namespace {
 
 constexpr int WPB = 4;                 // chunks (waves) per block
+// k_walk's waves per block (SCCG_WALK_WPB for A/B builds): a block's LDS is released only when all
+// its waves are done, so fewer waves per block let the dispatcher start the next chunk sooner
+#ifndef SCCG_WALK_WPB
+#define SCCG_WALK_WPB 4
+#endif
+constexpr int WWPB = SCCG_WALK_WPB;
 constexpr int WCAP = 256;              // window positions held in LDS (2m+1 <= WCAP)
 constexpr int32_t INVALID = INT32_MIN;
 constexpr int ANCHOR_K = 32;
@@ -484,11 +490,11 @@ constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cand
 #endif
 // nlist_dev (optional): the list length from device memory (a round queued before the host knows it)
 template <bool DBG>
-__global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
+__global__ __launch_bounds__(64 * WWPB) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
 void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const int32_t* __restrict__ nlist_dev) {
-    __shared__ WalkLds lds_all[WPB];
+    __shared__ WalkLds lds_all[WWPB];
     const int w = wave_in_block(), lane = lane_id();
-    const int32_t li = (int32_t)blockIdx.x * WPB + w;
+    const int32_t li = (int32_t)blockIdx.x * WWPB + w;
     if (nlist_dev) nlist = *nlist_dev;
     if (li >= nlist || A.scal[9]) return;
     WalkLds& L = lds_all[w];
@@ -2358,7 +2364,7 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s, std::vector<int32_t>* resume
         int rc = dev_set_i32(A.scal + 1, 1, {0}, s);
         if (rc) return rc;
         if ((rc = h2d_sync(A.rlist, rl.data(), rl.size() * 4, s))) return rc;
-        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for((int64_t)rl.size(), WPB)), dim3(SCCG_BLOCK), 0, s, A,
+        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for((int64_t)rl.size(), WWPB)), dim3(64 * WWPB), 0, s, A,
                     (const int32_t*)A.rlist, (int32_t)rl.size(), (const int32_t*)nullptr);
         SCCG_HIP(hipGetLastError());
     }
@@ -2573,7 +2579,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     // (dev_nlist: the list length is the previous round tail's pending count, scal[0])
     auto queue_round = [&](int fbase_cap, bool dev_nlist) -> int {
         const int32_t* nd = dev_nlist ? A.scal : nullptr;
-        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(A.C, WPB)), dim3(SCCG_BLOCK), 0, s, A, (const int32_t*)A.plist,
+        PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(A.C, WWPB)), dim3(64 * WWPB), 0, s, A, (const int32_t*)A.plist,
                     A.C, nd);
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
@@ -2739,7 +2745,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             A.round = (int32_t)round;   // every kernel of the round gets it by value
             const bool queued = pre_round && round == round0;
             if (!queued) {
-                PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WPB)), dim3(SCCG_BLOCK), 0, s, A,
+                PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WWPB)), dim3(64 * WWPB), 0, s, A,
                             (const int32_t*)A.plist, nlist, (const int32_t*)nullptr);
                 SCCG_HIP(hipGetLastError());
             }
