@@ -26,6 +26,11 @@ int dc_last_paren(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_parti
 int64_t dc_run_cap(int64_t n);
 int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
                   int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s);
+// both run lines (line 0 -> r0 / d_count0, line 1 -> r1 / d_count1) in one launch set when both take
+// the tiled parser (d_flag and d_dlt then hold their tile summaries), else one after the other
+int dc_parse_runs2(const uint8_t* s0, int64_t n0, DcRuns* r0, int64_t* d_count0, const uint8_t* s1, int64_t n1, DcRuns* r1,
+                   int64_t* d_count1, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt, int64_t* d_partial, int32_t* d_err,
+                   hipStream_t s);
 // d_err bit2: the last N run (count d_ncnt[0]) ends past the decoded length *d_D + N count d_ncnt[1]
 int dc_n_check(const DcRuns& nr, const int64_t* d_ncnt, const int64_t* d_D, int32_t* d_err, hipStream_t s);
 // record line: per-byte output contribution / token deltas, output offsets, absolute p, range

@@ -109,40 +109,83 @@ __global__ void k_run_items_parse(const uint8_t* __restrict__ s, int64_t n, cons
 }
 
 // ---------------------------------------------------------------------------------------------
-// run lines, tiled (opt-in, SCCG_RL_TILED): one wave per 4 KiB tile, 64 bytes per lane.  A run line's
-// parentheses only open "(d,len)" items of at most 25 bytes, so the "inside an item" state at a
-// lane's first byte follows from the last parenthesis before it: in the lanes before it (a wave
-// max-scan), else in the 32 bytes before the tile (text outside the compressor's grammar is flagged
-// by the item parses either way).  Three launches per line instead of a parenthesis max-scan, an
-// item-rank scan and three prefix sums (decompression.cpp:126-207 per item, running start, sorted).
+// run lines, tiled: one wave per 1 KiB tile, 16 bytes per lane, the tile staged in LDS with the 32
+// bytes before it and the 64 after it (every byte read of the parse is an LDS read; coalesced HBM
+// loads once per pass).  A run line's parentheses only open "(d,len)" items of at most 25 bytes, so
+// the "inside an item" state at a lane's first byte follows from the last parenthesis before it:
+// in the lanes before it (a wave max-scan), else in the 32 bytes before the tile (text outside the
+// compressor's grammar is flagged by the item parses either way).  Three launches per line instead
+// of a parenthesis max-scan, an item-rank scan and three prefix sums (decompression.cpp:126-207 per
+// item, running start, sorted).
 // ---------------------------------------------------------------------------------------------
-constexpr int RL_TILE = 4096, RL_LANE = RL_TILE / 64;
+constexpr int RL_LANE = 16, RL_TILE = 64 * RL_LANE, RL_BEHIND = 32, RL_AHEAD = 64;
+constexpr int RL_STAGE = RL_BEHIND + RL_TILE + RL_AHEAD;
 
-// one item at i: "(d,l)" or a bare "d" followed by ',' or the end (decompression.cpp:126-164)
-__device__ __forceinline__ bool rl_item(const uint8_t* s, int64_t n, int64_t i, int64_t* d, int64_t* l) {
+// the wave's staged bytes: global positions [t0 - RL_BEHIND, t0 + tile + RL_AHEAD), 0 outside [0, n)
+struct RlView {
+    const uint8_t* b;
+    int64_t t0, n, tile;
+    __device__ __forceinline__ uint8_t at(int64_t i) const { return b[i - t0 + RL_BEHIND]; }
+    __device__ __forceinline__ int64_t lim() const { return t0 + tile + RL_AHEAD; }
+};
+
+template <int TILE>
+__device__ __forceinline__ RlView rl_stage(const uint8_t* __restrict__ s, int64_t n, int64_t t0, uint8_t* st) {
+    for (int k = lane_id(); k < RL_BEHIND + TILE + RL_AHEAD; k += 64) {
+        const int64_t g = t0 - RL_BEHIND + k;
+        st[k] = (g >= 0 && g < n) ? s[g] : (uint8_t)0;
+    }
+    wave_sync();
+    return RlView{st, t0, n, TILE};
+}
+
+__device__ __forceinline__ bool parse_int_v(const RlView& v, int64_t a, int64_t e, int64_t* out) {
+    if (a >= e) return false;
+    bool neg = false;
+    if (v.at(a) == '-' || v.at(a) == '+') { neg = v.at(a) == '-'; a++; }
+    if (a >= e || e - a > 10) return false;
+    int64_t x = 0;
+    for (int64_t i = a; i < e; i++) {
+        const uint8_t c = v.at(i);
+        if (c < '0' || c > '9') return false;
+        x = x * 10 + (c - '0');
+    }
+    x = neg ? -x : x;
+    if (x > INT32_MAX || x < INT32_MIN) return false;
+    *out = x;
+    return true;
+}
+
+// one item at i (inside the tile): "(d,l)" or a bare "d" followed by ',' or the end
+// (decompression.cpp:126-164); a bare number running past the staged bytes is not the compressor's
+__device__ __forceinline__ bool rl_item(const RlView& v, int64_t i, int64_t* d, int64_t* l) {
+    const int64_t n = v.n, lim = v.lim();
     *l = 1;
-    if (s[i] == '(') {
+    if (v.at(i) == '(') {
         int64_t comma = -1, close = -1;
         for (int64_t q = i + 1; q < n && q < i + 32; q++) {
-            if (s[q] == ',' && comma < 0) comma = q;
-            if (s[q] == ')') { close = q; break; }
-            if (s[q] == '(') break;
+            const uint8_t c = v.at(q);
+            if (c == ',' && comma < 0) comma = q;
+            if (c == ')') { close = q; break; }
+            if (c == '(') break;
         }
-        return comma > 0 && close > comma && parse_int(s, n, i + 1, comma, d) && parse_int(s, n, comma + 1, close, l) &&
+        return comma > 0 && close > comma && parse_int_v(v, i + 1, comma, d) && parse_int_v(v, comma + 1, close, l) &&
                *l >= 0;
     }
     int64_t e = i;
-    while (e < n && is_num(s[e])) e++;
-    return (e == n || s[e] == ',') && parse_int(s, n, i, e, d);
+    while (e < n && e < lim && is_num(v.at(e))) e++;
+    if (e == lim && e < n) return false;
+    return (e == n || v.at(e) == ',') && parse_int_v(v, i, e, d);
 }
 
-// the "inside an item" state at the first byte of each lane's 64 (wave-uniform tile t)
-__device__ __forceinline__ bool rl_lane_inside(const uint8_t* s, int64_t n, int64_t t0, int64_t a) {
+// the "inside an item" state at the first byte a of this lane's `per` bytes
+__device__ __forceinline__ bool rl_lane_inside(const RlView& v, int64_t a, int per) {
     const int lane = lane_id();
-    // this lane's last parenthesis (2 * position + open), -1: none
-    int64_t last = -1;
-    for (int64_t i = a; i < a + RL_LANE && i < n; i++)
-        if (s[i] == '(' || s[i] == ')') last = 2 * i + (s[i] == '(');
+    int64_t last = -1;   // this lane's last parenthesis (2 * position + open), -1: none
+    for (int64_t i = a; i < a + per && i < v.n; i++) {
+        const uint8_t c = v.at(i);
+        if (c == '(' || c == ')') last = 2 * i + (c == '(');
+    }
     int64_t ex = __shfl_up(last, 1, 64);
     if (lane == 0) ex = -1;
 #pragma unroll
@@ -150,15 +193,12 @@ __device__ __forceinline__ bool rl_lane_inside(const uint8_t* s, int64_t n, int6
         const int64_t o = __shfl_up(ex, d, 64);
         if (lane >= d && o > ex) ex = o;
     }
-    // before the tile: the last parenthesis among its 32 preceding bytes
-    const int64_t b = t0 - 32 + (lane & 31);
-    const bool par = lane < 32 && b >= 0 && b < n && (s[b] == '(' || s[b] == ')');
+    // before the tile: the last parenthesis among its RL_BEHIND preceding bytes
+    const int64_t b = v.t0 - RL_BEHIND + (lane & (RL_BEHIND - 1));
+    const bool par = lane < RL_BEHIND && b >= 0 && (v.at(b) == '(' || v.at(b) == ')');
     const unsigned long long pm = __ballot(par);
     bool tile_in = false;
-    if (pm) {
-        const int l = 63 - __clzll((long long)pm);
-        tile_in = s[t0 - 32 + l] == '(';
-    }
+    if (pm) tile_in = v.at(v.t0 - RL_BEHIND + (63 - __clzll((long long)pm))) == '(';
     return ex >= 0 ? (ex & 1) != 0 : tile_in;
 }
 
@@ -168,12 +208,12 @@ struct RlLane {
 
 // walk the lane's bytes: item starts (in order) to f(i, d, l); byte-class errors to err
 template <typename F>
-__device__ __forceinline__ RlLane rl_lane(const uint8_t* s, int64_t n, int64_t a, bool inside, int32_t* err, F&& f) {
+__device__ __forceinline__ RlLane rl_lane(const RlView& v, int64_t a, bool inside, int32_t* err, F&& f) {
     RlLane r{0, 0, 0, -1};
     bool bad = false;
-    uint8_t prev = a > 0 ? s[a - 1] : (uint8_t)',';
-    for (int64_t i = a; i < a + RL_LANE && i < n; i++) {
-        const uint8_t c = s[i];
+    uint8_t prev = a > 0 ? v.at(a - 1) : (uint8_t)',';
+    for (int64_t i = a; i < a + RL_LANE && i < v.n; i++) {
+        const uint8_t c = v.at(i);
         bool start = false;
         if (c == '(') { start = true; inside = true; }
         else if (c == ')') { inside = false; }
@@ -183,7 +223,7 @@ __device__ __forceinline__ RlLane rl_lane(const uint8_t* s, int64_t n, int64_t a
         }
         if (start) {
             int64_t d = 0, l = 1;
-            if (!rl_item(s, n, i, &d, &l)) bad = true;
+            if (!rl_item(v, i, &d, &l)) bad = true;
             f(i, d, l, r);
             r.cnt++;
             r.dsum += d;
@@ -192,32 +232,64 @@ __device__ __forceinline__ RlLane rl_lane(const uint8_t* s, int64_t n, int64_t a
         }
         prev = c;
     }
-    if (bad) atomicOr(err, 1);
+    if (bad && err) atomicOr(err, 1);
     return r;
 }
 
+// One launch set parses both run lines: tiles [0, j0.ntiles) are line 0's, the rest line 1's.
+struct RlJob {
+    const uint8_t* s;
+    int64_t n, ntiles;
+    int64_t* tsum;      // 4 per tile: pass-1 summaries, then their exclusive prefixes
+    int32_t* start;
+    int32_t* len;
+    int64_t* cum;
+    int64_t* d_count;   // [0] items, [1] total length
+};
+__device__ __forceinline__ const RlJob& rl_job(const RlJob& j0, const RlJob& j1, int64_t& t) {
+    if (t < j0.ntiles) return j0;
+    t -= j0.ntiles;
+    return j1;
+}
+
 // pass 1: per tile (count, delta sum, length sum, last length) -> tsum[4 * t]
-__global__ __launch_bounds__(256) void k_rl_tiles(const uint8_t* __restrict__ s, int64_t n, int64_t* __restrict__ tsum,
-                                                  int32_t* __restrict__ err) {
-    const int64_t t = (int64_t)blockIdx.x * 4 + wave_in_block();
-    const int64_t t0 = t * RL_TILE;
-    if (t0 >= n) return;
+__global__ __launch_bounds__(256) void k_rl_tiles(RlJob j0, RlJob j1, int32_t* __restrict__ err) {
+    __shared__ uint8_t stage[4][RL_STAGE];
+    int64_t t = (int64_t)blockIdx.x * 4 + wave_in_block();
+    if (t >= j0.ntiles + j1.ntiles) return;
+    const RlJob& J = rl_job(j0, j1, t);
+    const int64_t t0 = t * RL_TILE, n = J.n;
     const int lane = lane_id();
+    const RlView v = rl_stage<RL_TILE>(J.s, n, t0, stage[wave_in_block()]);
     const int64_t a = t0 + (int64_t)lane * RL_LANE;
-    const bool inside = rl_lane_inside(s, n, t0, a);
-    const RlLane r = rl_lane(s, n, a, inside, err, [](int64_t, int64_t, int64_t, const RlLane&) {});
+    const bool inside = rl_lane_inside(v, a, RL_LANE);
+    const RlLane r = rl_lane(v, a, inside, err, [](int64_t, int64_t, int64_t, const RlLane&) {});
     const int64_t c = wave_sum(r.cnt), d = wave_sum(r.dsum), l = wave_sum(r.lsum);
     const unsigned long long hm = __ballot(r.cnt > 0);
     const int64_t last = hm ? __shfl(r.lastlen, 63 - __clzll((long long)hm), 64) : -1;
+    int64_t* tsum = J.tsum;
     if (lane == 0) { tsum[4 * t] = c; tsum[4 * t + 1] = d; tsum[4 * t + 2] = l; tsum[4 * t + 3] = last; }
+    // the lane's own totals for the write pass (after the 4 * ntiles summaries)
+    int64_t* ld = tsum + 4 * J.ntiles + (t * 64 + lane) * 4;
+    ld[0] = r.cnt; ld[1] = r.dsum; ld[2] = r.lsum; ld[3] = r.lastlen;
 }
 
 // pass 2 (one block): exclusive prefix over tiles of (count, deltas, lengths) and the last item
 // length before each tile (-1: none); the totals -> d_count[0..1]
-__global__ __launch_bounds__(1024) void k_rl_scan(int64_t ntiles, int64_t* __restrict__ tsum, int64_t* __restrict__ d_count) {
-    __shared__ int64_t wc[16], wd[16], wl[16], wlast[16];
+constexpr int RL_SCAN_T = 256;   // (a 1024-thread block waits for a whole CU beside a running strip)
+__global__ __launch_bounds__(RL_SCAN_T) void k_rl_scan(RlJob j0, RlJob j1) {   // block b: line b
+    constexpr int NW = RL_SCAN_T / 64;
+    __shared__ int64_t wc[NW], wd[NW], wl[NW], wlast[NW];
+    const RlJob& J = blockIdx.x == 0 ? j0 : j1;
+    const int64_t ntiles = J.ntiles;
+    int64_t* tsum = J.tsum;
+    int64_t* d_count = J.d_count;
+    if (ntiles <= 0) {
+        if (threadIdx.x == 0 && d_count) { d_count[0] = 0; d_count[1] = 0; }
+        return;
+    }
     const int tid = (int)threadIdx.x, lane = lane_id(), w = wave_in_block();
-    const int64_t per = (ntiles + 1023) / 1024, b0 = tid * per;
+    const int64_t per = (ntiles + RL_SCAN_T - 1) / RL_SCAN_T, b0 = tid * per;
     int64_t c = 0, d = 0, l = 0, last = -1;
     for (int64_t t = b0; t < b0 + per && t < ntiles; t++) {
         c += tsum[4 * t]; d += tsum[4 * t + 1]; l += tsum[4 * t + 2];
@@ -243,35 +315,38 @@ __global__ __launch_bounds__(1024) void k_rl_scan(int64_t ntiles, int64_t* __res
         ec += tc; ed += td; el += tl;
         if (tlast >= 0) elast = tlast;
     }
-    if (tid == 1023) { d_count[0] = ec; d_count[1] = el; }
+    if (tid == RL_SCAN_T - 1 && d_count) { d_count[0] = ec; d_count[1] = el; }
 }
 
 // pass 3: every item's start (running sum of deltas), length and the exclusive prefix of lengths;
 // starts must be >= 0, ascending and disjoint, and end within int32 (k_run_finish's checks)
-__global__ __launch_bounds__(256) void k_rl_write(const uint8_t* __restrict__ s, int64_t n, const int64_t* __restrict__ tsum,
-                                                  int32_t* __restrict__ start, int32_t* __restrict__ len,
-                                                  int64_t* __restrict__ cum, int32_t* __restrict__ err) {
-    const int64_t t = (int64_t)blockIdx.x * 4 + wave_in_block();
-    const int64_t t0 = t * RL_TILE;
-    if (t0 >= n) return;
+__global__ __launch_bounds__(256) void k_rl_write(RlJob j0, RlJob j1, int32_t* __restrict__ err) {
+    __shared__ uint8_t stage[4][RL_STAGE];
+    int64_t t = (int64_t)blockIdx.x * 4 + wave_in_block();
+    if (t >= j0.ntiles + j1.ntiles) return;
+    const RlJob& J = rl_job(j0, j1, t);
+    const int64_t t0 = t * RL_TILE, n = J.n;
+    const int64_t* tsum = J.tsum;
+    int32_t* start = J.start;
+    int32_t* len = J.len;
+    int64_t* cum = J.cum;
     const int lane = lane_id();
+    const RlView v = rl_stage<RL_TILE>(J.s, n, t0, stage[wave_in_block()]);
     const int64_t a = t0 + (int64_t)lane * RL_LANE;
-    const bool inside = rl_lane_inside(s, n, t0, a);
-    // the lane's totals first (a dry pass), then its exclusive prefixes over the wave
-    int32_t dummy = 0;
-    const RlLane tot = rl_lane(s, n, a, inside, &dummy, [](int64_t, int64_t, int64_t, const RlLane&) {});
+    const bool inside = rl_lane_inside(v, a, RL_LANE);
+    // the lane's totals (pass 1 kept them), then its exclusive prefixes over the wave
+    const int64_t* ld = tsum + 4 * J.ntiles + (t * 64 + lane) * 4;
+    const RlLane tot{ld[0], ld[1], ld[2], ld[3]};
     const int64_t ic = wave_incl_add(tot.cnt), id = wave_incl_add(tot.dsum), il = wave_incl_add(tot.lsum);
     // the last item length before this lane (in earlier lanes, else before the tile)
     const unsigned long long hm = __ballot(tot.cnt > 0) & ((1ull << lane) - 1ull);
     const int64_t prevlen = hm ? __shfl(tot.lastlen, 63 - __clzll((long long)hm), 64) : tsum[4 * t + 3];
-    const int64_t hm2 = __shfl(tot.lastlen, hm ? 63 - __clzll((long long)hm) : 0, 64);
-    (void)hm2;
     const int64_t rank0 = tsum[4 * t] + ic - tot.cnt;
     int64_t run_start = tsum[4 * t + 1] + id - tot.dsum;   // start of the last item before this lane's first
     int64_t run_cum = tsum[4 * t + 2] + il - tot.lsum;
     int64_t prev_end = rank0 > 0 ? run_start + (prevlen >= 0 ? prevlen : 0) : INT64_MIN;
     bool bad = false;
-    rl_lane(s, n, a, inside, &dummy, [&](int64_t, int64_t d, int64_t l, const RlLane& r) {
+    rl_lane(v, a, inside, nullptr, [&](int64_t, int64_t d, int64_t l, const RlLane& r) {
         const int64_t rank = rank0 + r.cnt;
         const int64_t st = run_start + d;
         if (st < 0 || st + l > INT32_MAX || (rank > 0 && st < prev_end)) bad = true;
@@ -417,7 +492,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill(const uint8_t* __restri
 // ---------------------------------------------------------------------------------------------
 // record line, per 64-byte block (the usual path).  A token "(dp,l)" is at most 25 bytes, so the
 // "inside a token" state at a block's first byte follows from the last parenthesis before it (the
-// lanes before it in the 4 KiB tile, else the 32 bytes before the tile; rl_lane_inside).  Pass 1
+// lanes before it in the 1 KiB tile, else the 32 bytes before the tile; rl_lane_inside).  Pass 1
 // stores per block its state and its sums of output bytes (literal 1, token l) and token deltas;
 // two exclusive scans over the blocks give every block's output offset and running p; the fill
 // recomputes a block's bytes from those (decompression.cpp:210-236), with the range check of
@@ -429,27 +504,30 @@ constexpr int TK_B = 64;   // record bytes per block (one lane in pass 1, one wa
 __global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ s, int64_t n, int64_t* __restrict__ bin,
                                                     int64_t* __restrict__ bcontrib, int64_t* __restrict__ bdelta,
                                                     int32_t* __restrict__ err) {
+    // one wave per 1 KiB tile (16 bytes per lane, staged in LDS); 4 lanes make one 64-byte block
+    constexpr int TL = 16, TT = 64 * TL;
+    __shared__ uint8_t stage[4][RL_BEHIND + TT + RL_AHEAD];
     const int64_t t = (int64_t)blockIdx.x * 4 + wave_in_block();
-    const int64_t t0 = t * (64 * TK_B);
+    const int64_t t0 = t * TT;
     if (t0 >= n) return;
     const int lane = lane_id();
-    const int64_t a = t0 + (int64_t)lane * TK_B;
-    bool inside = rl_lane_inside(s, n, t0, a);
-    const int64_t b = a / TK_B;
-    if (a >= n) return;
+    const RlView v = rl_stage<TT>(s, n, t0, stage[wave_in_block()]);
+    const int64_t a = t0 + (int64_t)lane * TL;
+    bool inside = rl_lane_inside(v, a, TL);
     const bool in0 = inside;
     int64_t cs = 0, ds = 0;
     bool bad = false;
-    for (int64_t i = a; i < a + TK_B && i < n; i++) {
-        const uint8_t c = s[i];
+    for (int64_t i = a; i < a + TL && i < n; i++) {
+        const uint8_t c = v.at(i);
         if (c == '(') {
             int64_t comma = -1, close = -1, d = 0, l = 0;
             for (int64_t q = i + 1; q < n && q < i + 32; q++) {
-                if (s[q] == ',' && comma < 0) comma = q;
-                if (s[q] == ')') { close = q; break; }
-                if (s[q] == '(') break;
+                const uint8_t cq = v.at(q);
+                if (cq == ',' && comma < 0) comma = q;
+                if (cq == ')') { close = q; break; }
+                if (cq == '(') break;
             }
-            if (!(comma > 0 && close > comma && parse_int(s, n, i + 1, comma, &d) && parse_int(s, n, comma + 1, close, &l)) ||
+            if (!(comma > 0 && close > comma && parse_int_v(v, i + 1, comma, &d) && parse_int_v(v, comma + 1, close, &l)) ||
                 l < 0)
                 bad = true;
             cs += l;
@@ -463,9 +541,17 @@ __global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ 
         }
     }
     if (bad) atomicOr(err, 1);
-    bin[b] = in0;
-    bcontrib[b] = cs;
-    bdelta[b] = ds;
+    cs += __shfl_xor(cs, 1, 64);
+    cs += __shfl_xor(cs, 2, 64);
+    ds += __shfl_xor(ds, 1, 64);
+    ds += __shfl_xor(ds, 2, 64);
+    static_assert(4 * TL == TK_B, "four lanes per block");
+    const int64_t b = t * (TT / TK_B) + (lane >> 2);
+    if ((lane & 3) == 0 && b * TK_B < n) {
+        bin[b] = in0;
+        bcontrib[b] = cs;
+        bdelta[b] = ds;
+    }
 }
 
 // one wave per block: literals and token copies into dec at the block's offsets; tokens beyond
@@ -714,6 +800,145 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Output-centric formatter (the usual path).  A block owns OB = 4096 bytes of the OUTPUT, aligned
+// to 16 bytes in memory; every thread builds 16 output bytes in registers and stores them with one
+// 16-byte store (head and tail threads byte by byte).  Output byte o is the '\n' after a line when
+// o % 51 == 50, else position j = o - o / 51; its byte is 'N' inside an N run, else the decoded
+// byte at j minus the N positions before j, lowercased inside a lowercase run
+// (decompression.cpp:241-274).  The block's decoded bytes and the runs it touches are staged in
+// LDS (runs from the global lists when they are more than OFRUNS); a thread finds its first runs by
+// binary search in LDS and then walks them.  (The position-centric k_format_span wrote each
+// position's byte to LDS, 16 bytes apart per lane, and copied the line-broken range out again.)
+// ---------------------------------------------------------------------------------------------
+constexpr int OPT = 16, OB = 256 * OPT, OFRUNS = 384;
+
+// Block boundaries: output offset o_b = o_first + b * OB clamped to [0, total]; its position
+// j_b = o - o / 51; per boundary [decoded offset of j_b, first N run and first lowercase run ending
+// after j_b, j_b].  One thread per (boundary, run list).
+__global__ void k_out_index(int64_t nres, int64_t total, int64_t o_first, int64_t nblk, const int32_t* __restrict__ ns,
+                            const int32_t* __restrict__ nl, const int64_t* __restrict__ ncum, int64_t nn,
+                            const int32_t* __restrict__ ls, const int32_t* __restrict__ ll, int64_t nlr,
+                            int64_t* __restrict__ tab) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * (nblk + 1); i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = i >> 1;
+        int64_t o = o_first + b * OB;
+        o = o < 0 ? 0 : (o > total ? total : o);
+        const int64_t J = o - o / 51;
+        if (i & 1) {
+            tab[4 * b + 2] = first_run_ending_after(ls, ll, nlr, J);
+        } else {
+            const int64_t r = first_run_ending_after(ns, nl, nn, J);
+            tab[4 * b + 0] = J - n_before_at(ns, nl, ncum, nn, r, J);
+            tab[4 * b + 1] = r;
+            tab[4 * b + 3] = J;
+        }
+    }
+}
+
+template <typename V>
+__device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t nres, const uint8_t* sdec, int64_t dbase,
+                                             const V& N, int64_t cn, int64_t ntot, const V& L, int64_t cl, uint8_t* out) {
+    const int64_t oc = o0 < 0 ? 0 : o0;
+    if (oc >= total || o0 + OPT <= 0) return;
+    int64_t j = oc - oc / 51;
+    int col = (int)(oc % 51);
+    int64_t rn = first_end_after(N, 0, cn, j), rl = first_end_after(L, 0, cl, j);
+    int64_t n_s = INT64_MAX, n_e = INT64_MAX, n_b = ntot, l_s = INT64_MAX, l_e = INT64_MAX;
+    if (rn < cn) { n_s = N.st(rn); n_e = N.en(rn); n_b = N.nb(rn); }
+    if (rl < cl) { l_s = L.st(rl); l_e = L.en(rl); }
+    uint64_t lo = 0, hi = 0;
+    const int k0 = (int)(oc - o0), k1 = total - o0 < OPT ? (int)(total - o0) : OPT;
+    for (int k = k0; k < k1; k++) {
+        uint32_t c;
+        if (col == 50) {
+            c = '\n';
+            col = 0;
+        } else {
+            while (j >= n_e) {
+                rn++;
+                if (rn < cn) { n_s = N.st(rn); n_e = N.en(rn); n_b = N.nb(rn); }
+                else { n_s = n_e = INT64_MAX; n_b = ntot; }
+            }
+            while (j >= l_e) {
+                rl++;
+                if (rl < cl) { l_s = L.st(rl); l_e = L.en(rl); }
+                else l_s = l_e = INT64_MAX;
+            }
+            c = j >= n_s ? (uint32_t)'N' : (uint32_t)sdec[j - n_b - dbase];
+            if (j >= l_s) c = c_tolower((uint8_t)c);
+            j++;
+            col++;
+        }
+        if (k < 8) lo |= (uint64_t)c << (8 * k);
+        else hi |= (uint64_t)c << (8 * (k - 8));
+    }
+    (void)nres;
+    if (k0 == 0 && k1 == OPT) {
+        *reinterpret_cast<uint4*>(out + o0) = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+    } else {
+        for (int k = k0; k < k1; k++) out[o0 + k] = (uint8_t)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xff);
+    }
+}
+
+// runs of the global lists from index a on, as views starting at 0 (format_out16's fallback)
+struct GlobalRunsAt {
+    const int32_t* s;
+    const int32_t* l;
+    const int64_t* b;
+    int64_t a;
+    __device__ int64_t st(int64_t r) const { return s[a + r]; }
+    __device__ int64_t en(int64_t r) const { return (int64_t)s[a + r] + l[a + r]; }
+    __device__ int64_t nb(int64_t r) const { return b ? b[a + r] : 0; }
+};
+
+__global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ dec, int64_t nres, int64_t total, int64_t o_first,
+                                                    const int32_t* __restrict__ ns, const int32_t* __restrict__ nl,
+                                                    const int64_t* __restrict__ ncum, int64_t nn,
+                                                    const int32_t* __restrict__ ls, const int32_t* __restrict__ ll,
+                                                    int64_t nlr, const int64_t* __restrict__ tab, uint8_t* __restrict__ out) {
+    __shared__ uint32_t sdec_w[OB / 4 + 2];
+    __shared__ int32_t s_ns[OFRUNS], s_ne[OFRUNS], s_ls[OFRUNS], s_le[OFRUNS];
+    __shared__ int64_t s_nb[OFRUNS];
+    __shared__ int64_t st[8];
+    const int tid = threadIdx.x;
+    const int64_t b = blockIdx.x;   // (a grid-stride loop over blocks: 0.35-0.43 ms instead of 0.27)
+    if (tid < 8) st[tid] = tab[4 * b + tid];
+    __syncthreads();
+    const int64_t d0 = st[0], d1 = st[4];
+    const int64_t n_lo = st[1], n_hi = st[5] < nn ? st[5] + 1 : nn;
+    const int64_t l_lo = st[2], l_hi = st[6] < nlr ? st[6] + 1 : nlr;
+    const int64_t ntot = nn ? ncum[nn - 1] + nl[nn - 1] : 0;
+    const bool lds_runs = n_hi - n_lo <= OFRUNS && l_hi - l_lo <= OFRUNS;
+    const int64_t a0 = d0 & ~(int64_t)3;
+    const int64_t nw = (d1 - a0 + 3) >> 2;
+    const uint32_t* decw = reinterpret_cast<const uint32_t*>(dec + a0);
+    for (int64_t i = tid; i < nw; i += 256) sdec_w[i] = decw[i];
+    if (lds_runs) {
+        for (int64_t r = n_lo + tid; r < n_hi; r += 256) {
+            const int32_t x = ns[r];
+            s_ns[r - n_lo] = x;
+            s_ne[r - n_lo] = x + nl[r];
+            s_nb[r - n_lo] = ncum[r];
+        }
+        for (int64_t r = l_lo + tid; r < l_hi; r += 256) {
+            const int32_t x = ls[r];
+            s_ls[r - l_lo] = x;
+            s_le[r - l_lo] = x + ll[r];
+        }
+    }
+    __syncthreads();
+    const uint8_t* sdec = reinterpret_cast<const uint8_t*>(sdec_w);
+    const int64_t o0 = o_first + b * OB + (int64_t)tid * OPT;
+    if (lds_runs) {
+        const LdsRuns N{s_ns, s_ne, s_nb}, L{s_ls, s_le, nullptr};
+        format_out16(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
+    } else {
+        const GlobalRunsAt N{ns, nl, ncum, n_lo}, L{ls, ll, nullptr, l_lo};
+        format_out16(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
+    }
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -745,27 +970,21 @@ int dc_last_paren(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_parti
 
 int64_t dc_run_cap(int64_t n) { return n / 2 + 2; }
 
-int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
-                  int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s) {
+namespace {
+bool rl_tiled() {   // (SCCG_RL_SCAN=1, A/B runs: the scan-based parser)
+    static const bool v = getenv("SCCG_RL_SCAN") == nullptr;
+    return v;
+}
+bool rl_tiled_ok(int64_t n) { return rl_tiled() && (n + RL_TILE - 1) / RL_TILE <= 64 * 1024; }
+
+// the scan-based parser of one line (lines over 64 MiB, or SCCG_RL_SCAN)
+int parse_runs_scan(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
+                    int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s) {
     if (n <= 0) {
         SCCG_HIP(hipMemsetAsync(d_count, 0, 2 * sizeof(int64_t), s));
         return 0;
     }
     const int64_t cap = dc_run_cap(n);
-    const int64_t ntiles = (n + RL_TILE - 1) / RL_TILE;
-    // (SCCG_RL_TILED=1, A/B runs: the tiled parser; chr1 reconstruction 1.65 vs 1.08 ms with the
-    // scan-based one -- one wave per 4 KiB of run text walks 64 bytes per lane from HBM)
-    static const bool old_path = getenv("SCCG_RL_TILED") == nullptr;
-    if (!old_path && ntiles <= 64 * 1024 && 4 * ntiles <= 2 * (n + 4)) {
-        // tiled: d_flag holds the per-tile summaries (4 per tile), d_dlt is unused
-        const unsigned g = (unsigned)((ntiles + 3) / 4);
-        hipLaunchKernelGGL(k_rl_tiles, dim3(g), dim3(256), 0, s, d_s, n, d_flag, d_err);
-        hipLaunchKernelGGL(k_rl_scan, dim3(1), dim3(1024), 0, s, ntiles, d_flag, d_count);
-        hipLaunchKernelGGL(k_rl_write, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_flag, r->start, r->len, r->cum,
-                           d_err);
-        SCCG_HIP(hipGetLastError());
-        return 0;
-    }
     int rc = dc_last_paren(d_s, n, d_lp, d_partial, s);
     if (rc) return rc;
     SCCG_HIP(hipMemsetAsync(d_dlt, 0, (size_t)cap * sizeof(int64_t), s));   // deltas past the runs scan as 0
@@ -787,6 +1006,44 @@ int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64
     return dev_excl_sum(r->cum, r->cum, cap, d_count + 1, d_partial, s);
 }
 
+RlJob rl_job_of(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* tsum, int64_t* d_count) {
+    return RlJob{d_s, n > 0 ? n : 0, n > 0 ? (n + RL_TILE - 1) / RL_TILE : 0, tsum, r->start, r->len, r->cum, d_count};
+}
+
+int parse_runs_tiled(const RlJob& j0, const RlJob& j1, int32_t* d_err, hipStream_t s) {
+    const int64_t nt = j0.ntiles + j1.ntiles;
+    if (nt > 0) {
+        const unsigned g = (unsigned)((nt + 3) / 4);
+        hipLaunchKernelGGL(k_rl_tiles, dim3(g), dim3(256), 0, s, j0, j1, d_err);
+        hipLaunchKernelGGL(k_rl_scan, dim3(2), dim3(RL_SCAN_T), 0, s, j0, j1);
+        hipLaunchKernelGGL(k_rl_write, dim3(g), dim3(256), 0, s, j0, j1, d_err);
+    } else {
+        hipLaunchKernelGGL(k_rl_scan, dim3(2), dim3(RL_SCAN_T), 0, s, j0, j1);   // (zero counts)
+    }
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+}  // namespace
+
+int dc_parse_runs(const uint8_t* d_s, int64_t n, DcRuns* r, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt,
+                  int64_t* d_partial, int32_t* d_err, int64_t* d_count, hipStream_t s) {
+    if (n > 0 && rl_tiled_ok(n)) {   // tiled: d_flag holds the per-tile summaries (4 per tile)
+        DcRuns none{};
+        return parse_runs_tiled(rl_job_of(d_s, n, r, d_flag, d_count), rl_job_of(nullptr, 0, &none, nullptr, nullptr), d_err, s);
+    }
+    return parse_runs_scan(d_s, n, r, d_lp, d_flag, d_dlt, d_partial, d_err, d_count, s);
+}
+
+int dc_parse_runs2(const uint8_t* s0, int64_t n0, DcRuns* r0, int64_t* d_count0, const uint8_t* s1, int64_t n1, DcRuns* r1,
+                   int64_t* d_count1, int64_t* d_lp, int64_t* d_flag, int64_t* d_dlt, int64_t* d_partial, int32_t* d_err,
+                   hipStream_t s) {
+    if (rl_tiled_ok(n0) && rl_tiled_ok(n1))   // both lines in one launch set; summaries in d_flag / d_dlt
+        return parse_runs_tiled(rl_job_of(s0, n0, r0, d_flag, d_count0), rl_job_of(s1, n1, r1, d_dlt, d_count1), d_err, s);
+    int rc = dc_parse_runs(s0, n0, r0, d_lp, d_flag, d_dlt, d_partial, d_err, d_count0, s);
+    if (!rc) rc = dc_parse_runs(s1, n1, r1, d_lp, d_flag, d_dlt, d_partial, d_err, d_count1, s);
+    return rc;
+}
+
 int dc_n_check(const DcRuns& nr, const int64_t* d_ncnt, const int64_t* d_D, int32_t* d_err, hipStream_t s) {
     hipLaunchKernelGGL(k_n_check, dim3(1), dim3(64), 0, s, (const int32_t*)nr.start, (const int32_t*)nr.len, d_ncnt, d_D,
                        d_err);
@@ -804,7 +1061,7 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
     if (dc_tok_tiled()) {
         // per 64-byte block: state, output bytes, deltas; their exclusive prefixes -> d_off, d_dsum
         const int64_t nb = (n + TK_B - 1) / TK_B;
-        const unsigned g = (unsigned)((n + 4 * 64 * TK_B - 1) / (4 * 64 * TK_B));
+        const unsigned g = (unsigned)((n + 4 * 1024 - 1) / (4 * 1024));   // 4 waves of 1 KiB per block
         hipLaunchKernelGGL(k_tok_blocks, dim3(g), dim3(256), 0, s, d_s, n, d_lp, d_contrib, d_dlt, d_err);
         SCCG_HIP(hipGetLastError());
         int rc = dev_excl_sum(d_contrib, d_off, nb, d_total, d_partial, s);
@@ -831,8 +1088,8 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
 }
 
 bool dc_tok_tiled() {
-    // (SCCG_TOK_TILED=1, A/B runs: per-64-byte-block decoding; chr1 1.14 vs 1.08 ms scan-based)
-    static const bool v = getenv("SCCG_TOK_TILED") != nullptr;
+    // (SCCG_TOK_SCAN=1, A/B runs: the scan-based record-line path; chr1 1.04-1.05 ms vs 1.02-1.03 tiled)
+    static const bool v = getenv("SCCG_TOK_SCAN") == nullptr;
     return v;
 }
 
@@ -852,11 +1109,29 @@ int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int
     return 0;
 }
 
-int64_t dc_format_span_words(int64_t nres) { return 3 * ((nres + FSPAN - 1) / FSPAN + 2); }
+int64_t dc_format_span_words(int64_t nres) {   // (both formatters' tables; the output's misalignment adds a block)
+    const int64_t a = 3 * ((nres + FSPAN - 1) / FSPAN + 2), o = 4 * ((nres + nres / 50 + 16) / OB + 3);
+    return a > o ? a : o;
+}
 
 int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out,
               hipStream_t s) {
     if (nres <= 0) return 0;
+    static const bool span_path = getenv("SCCG_FMT_SPAN") != nullptr;   // (A/B runs: the position-centric writer)
+    if (!span_path) {
+        const int64_t total = nres + (nres - 1) / 50;   // the final '\n' is the caller's
+        const int64_t o_first = -(int64_t)((uintptr_t)d_out & 15);
+        const int64_t nblk = (total - o_first + OB - 1) / OB;
+        hipLaunchKernelGGL(k_out_index, dim3(grid_for(2 * (nblk + 1), 256)), dim3(256), 0, s, nres, total, o_first, nblk,
+                           (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
+                           (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, d_span);
+        SCCG_HIP(hipGetLastError());
+        PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_out, dim3((unsigned)nblk), dim3(256), 0, s, d_dec, nres, total, o_first,
+                    (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
+                    (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out);
+        SCCG_HIP(hipGetLastError());
+        return 0;
+    }
     const int64_t nspan = (nres + FSPAN - 1) / FSPAN;
     hipLaunchKernelGGL(k_span_index, dim3(grid_for(2 * (nspan + 1), 256)), dim3(256), 0, s, nres, nspan,
                        (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,

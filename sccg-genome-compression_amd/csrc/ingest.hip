@@ -555,6 +555,47 @@ __global__ void k_run_textwrite(const int32_t* __restrict__ rs, const int32_t* _
 
 }  // namespace
 
+// The target's header in one single-block launch: the first '>' at a line start, then the first
+// '\n' after it, 16 KiB per block step (a FASTA header sits at byte 0, so this is one or two steps;
+// a target without one is scanned to its end by this block, ~1 us per 16 KiB).  It replaces an
+// init launch and two 64-block ticket searches, which in multi-context runs waited ~50 us each for
+// CU slots behind the other context's grids.  d_sc[0] = header start (n: none), d_sc[1] = its '\n'
+// (n: none), d_sc[2..3] = 0.
+constexpr int FH_T = 256, FH_PER = 64;   // (a 1024-thread block would wait for a whole free CU)
+__global__ __launch_bounds__(FH_T) void k_find_header(const uint8_t* __restrict__ buf, int64_t n, int64_t* __restrict__ d_sc) {
+    __shared__ unsigned long long s_hit;
+    int64_t res[2] = {n, n};
+    for (int ph = 0; ph < 2; ph++) {
+        if (ph == 1 && res[0] >= n) break;
+        const int64_t from = ph == 0 ? 0 : res[0] + 1;
+        for (int64_t cs = from & ~(int64_t)63; cs < n; cs += (int64_t)FH_T * FH_PER) {
+            if (threadIdx.x == 0) s_hit = ~0ull;
+            __syncthreads();
+            const int64_t p0 = cs + (int64_t)threadIdx.x * FH_PER;
+            if (p0 < n) {
+                uint32_t w[FH_PER / 4];
+                load_words<FH_PER / 4>(buf, n, p0, w);
+                uint8_t prev = p0 > 0 ? buf[p0 - 1] : (uint8_t)'\n';
+                int64_t hit = -1;
+#pragma unroll
+                for (int i = 0; i < FH_PER; i++) {
+                    const uint8_t c = wb(w, i);
+                    const int64_t p = p0 + i;
+                    const bool ok = p >= from && p < n && (ph == 0 ? (c == '>' && prev == '\n') : c == '\n');
+                    if (ok && hit < 0) hit = p;
+                    prev = c;
+                }
+                if (hit >= 0) atomicMin(&s_hit, (unsigned long long)hit);
+            }
+            __syncthreads();
+            const unsigned long long h = s_hit;
+            __syncthreads();   // (s_hit is reset next step)
+            if (h != ~0ull) { res[ph] = (int64_t)h; break; }
+        }
+    }
+    if (threadIdx.x == 0) { d_sc[0] = res[0]; d_sc[1] = res[1]; d_sc[2] = 0; d_sc[3] = 0; }
+}
+
 // =============================================================================================
 int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, int mode, uint8_t c, int64_t* res,
                        int64_t* ticket_slot, hipStream_t s) {
@@ -572,12 +613,7 @@ int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, 
 int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t s) {
     // d_sc[0] = header start (first '>' at a line start), d_sc[1] = its '\n' (n if none);
     // d_sc[2], d_sc[3] are the chunk tickets (free for the caller afterwards); one init launch
-    int rc = dev_set_i64(d_sc, 4, {n, n, 0, 0}, s);
-    if (rc || n <= 0) return rc;
-    hipLaunchKernelGGL(k_first_match, dim3(64), dim3(SCCG_BLOCK), 0, s, buf, n, (const int64_t*)nullptr, 0, (uint8_t)'>',
-                       d_sc, reinterpret_cast<unsigned int*>(d_sc + 2));
-    hipLaunchKernelGGL(k_first_match, dim3(64), dim3(SCCG_BLOCK), 0, s, buf, n, (const int64_t*)d_sc, 1, (uint8_t)'\n',
-                       d_sc + 1, reinterpret_cast<unsigned int*>(d_sc + 3));
+    hipLaunchKernelGGL(k_find_header, dim3(1), dim3(FH_T), 0, s, buf, n, d_sc);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

@@ -945,8 +945,9 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     GET(int64_t, dsum, B_D_DSUM, nenc + 1);
     const int64_t nmax = nlower > nnl ? nlower : nnl;   // >= dc_run_cap of either line but for n <= 3
     GET(int64_t, lp, B_D_LP, nmax + 4);
-    GET(int64_t, flag, B_D_FLAG, nmax + 4);
-    GET(int64_t, dlt, B_D_DLT, nmax + 4);
+    // (the tiled run-line parser keeps 4 + 256 int64 per 1 KiB tile in flag / dlt: <= n / 4 + 260)
+    GET(int64_t, flag, B_D_FLAG, nmax + 4 + 264);
+    GET(int64_t, dlt, B_D_DLT, nmax + 4 + 264);
     GET(int64_t, part, B_PARTIAL, scan_partials_needed(nmax + 4) + 16);
     GET(int32_t, ls, B_D_LS, dc_run_cap(nlower));
     GET(int32_t, ll, B_D_LL, dc_run_cap(nlower));
@@ -961,19 +962,19 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
     DcRuns lr{}, nr{};
     lr.start = ls; lr.len = ll; lr.cum = lc;
-    TRY(dc_parse_runs(lower, nlower, &lr, lp, flag, dlt, part, d_err, sc + 14, s));
     nr.start = ns; nr.len = nlr; nr.cum = nc;
-    TRY(dc_parse_runs(nline, nnl, &nr, lp, flag, dlt, part, d_err, sc + 16, s));
+    TRY(dc_parse_runs2(lower, nlower, &lr, sc + 14, nline, nnl, &nr, sc + 16, lp, flag, dlt, part, d_err, s));
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
-    HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // n <= 0 skips the range check's wait
+    if (!dc_tok_tiled()) HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // (nenc <= 0 skips the range check's wait)
     TRY(dc_n_check(nr, sc + 16, sc + 12, d_err, s));
-    // one readback: decoded length, error bits, |R'|, both run lines' counts and totals
+    // one readback: decoded length, error bits, both run lines' counts and totals -- with the tiled
+    // record line (range check in the fill) it does not wait for the reference's strip, whose |R'|
+    // is read with the final error bits
     int64_t D = 0, nRp = 0, cnt[4] = {0, 0, 0, 0};
     int32_t err = 0;
     {
-        const RbItem it[4] = {{sc + 12, &D, (int)sizeof D}, {d_err, &err, (int)sizeof err}, {sc + 9, &nRp, (int)sizeof nRp},
-                              {sc + 14, cnt, (int)sizeof cnt}};
-        TRY(dev_readback(it, 4, s));
+        const RbItem it[3] = {{sc + 12, &D, (int)sizeof D}, {d_err, &err, (int)sizeof err}, {sc + 14, cnt, (int)sizeof cnt}};
+        TRY(dev_readback(it, 3, s));
     }
     lr.n = cnt[0]; lr.total = cnt[1];
     nr.n = cnt[2]; nr.total = cnt[3];
@@ -987,18 +988,17 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     if (size_only) return SCCG_OK;
     if (total > out_cap) return ctx->fail(SCCG_E_NOMEM, "output needs %lld bytes", (long long)total);
     GET(uint8_t, dec, B_D_DEC, D + 64);
+    HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // the fill copies from R'
     TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s, sc + 9, d_err));
     if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
     TRY(dev_put_bytes(out + hlen, "\n", 1, s));
     GET(int64_t, span, B_D_SPAN, dc_format_span_words(nres));
     TRY(dc_format(dec, nres, nr, lr, span, out + hlen + 1, s));
     TRY(dev_put_bytes(out + total - 1, "\n", 1, s));
-    if (dc_tok_tiled()) {   // the range check ran with the fill: read the error bits behind the output
-        const RbItem it{d_err, &err, (int)sizeof err};
-        TRY(dev_readback(&it, 1, s));
+    {   // (tiled record line: the range check ran with the fill) error bits and |R'| behind the output
+        const RbItem it[2] = {{d_err, &err, (int)sizeof err}, {sc + 9, &nRp, (int)sizeof nRp}};
+        TRY(dev_readback(it, 2, s));
         if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
-    } else {
-        HIPTRY(hipStreamSynchronize(s));
     }
     ctx->stats.target_bases = nres;
     ctx->stats.reference_bases = nRp;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-stream kernel timeline of the last compress in a rocprofv3 --kernel-trace CSV (diagnostics).
 
-    python trace_streams.py <kernel_trace.csv> [--start-kernel k_first_match] [--n 80]
+    python trace_streams.py <kernel_trace.csv> [--start-kernel k_find_header] [--n 80]
 
 One line per kernel of the last group (a group opens at the start kernel more than 1 ms after the
 previous group): start and end offset (us), stream, short name, grid size.
@@ -20,7 +20,7 @@ from pmc_summary import short  # noqa: E402
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
-    ap.add_argument("--start-kernel", default="k_first_match")
+    ap.add_argument("--start-kernel", default="k_find_header")
     ap.add_argument("--n", type=int, default=80)
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.csv)), key=lambda r: int(r["Start_Timestamp"]))
