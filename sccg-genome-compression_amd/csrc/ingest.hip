@@ -369,24 +369,54 @@ __device__ __forceinline__ TileSum block_scan_tiles(TileSum v, TileSum* wsum, Ti
     return ts_compose(wsum[w], ex);
 }
 
-__global__ __launch_bounds__(SCAN_B) void k_strip_scan_local(int64_t ntiles, int64_t* __restrict__ ta, int64_t* __restrict__ tb,
+// (SCCG_SCAN_T threads per block, SCAN_B / SCAN_T tiles per thread.  A 1024-thread block waits for
+// a whole free CU -- the target's scan sat ~140 us behind the reference strip's write pass on the
+// side stream in a chr1 trace -- but 256-thread builds measured within noise end to end.)
+#ifndef SCCG_SCAN_T
+#define SCCG_SCAN_T 1024
+#endif
+constexpr int SCAN_T = SCCG_SCAN_T, SCAN_PER = SCAN_B / SCAN_T;
+__global__ __launch_bounds__(SCAN_T) void k_strip_scan_local(int64_t ntiles, int64_t* __restrict__ ta, int64_t* __restrict__ tb,
                                                           int64_t* __restrict__ tfa, int64_t* __restrict__ tfb,
                                                           int32_t* __restrict__ tlast, TileSum* __restrict__ btot) {
     __shared__ TileSum wsum[17];
-    const int64_t t = (int64_t)blockIdx.x * SCAN_B + threadIdx.x;
-    const TileSum v = t < ntiles ? TileSum{ta[t], tb[t], tfa[t], tfb[t], tlast[t]} : TileSum{0, 0, 0, 0, -1};
+    const TileSum id{0, 0, 0, 0, -1};
+    const int64_t t0 = (int64_t)blockIdx.x * SCAN_B + (int64_t)threadIdx.x * SCAN_PER;
+    TileSum v[SCAN_PER], agg = id;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        const int64_t t = t0 + k;
+        v[k] = t < ntiles ? TileSum{ta[t], tb[t], tfa[t], tfb[t], tlast[t]} : id;
+        agg = ts_compose(agg, v[k]);
+    }
     TileSum tot;
-    const TileSum ex = block_scan_tiles(v, wsum, &tot);
-    if (t < ntiles) { ta[t] = ex.a; tb[t] = ex.b; tfa[t] = ex.fa; tfb[t] = ex.fb; tlast[t] = ex.last; }
+    TileSum run = block_scan_tiles(agg, wsum, &tot);
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        const int64_t t = t0 + k;
+        if (t < ntiles) { ta[t] = run.a; tb[t] = run.b; tfa[t] = run.fa; tfb[t] = run.fb; tlast[t] = run.last; }
+        run = ts_compose(run, v[k]);
+    }
     if (threadIdx.x == 0) btot[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(SCAN_B) void k_strip_scan_blocks(int64_t nblk, TileSum* __restrict__ btot) {
+__global__ __launch_bounds__(SCAN_T) void k_strip_scan_blocks(int64_t nblk, TileSum* __restrict__ btot) {
     __shared__ TileSum wsum[17];
-    const TileSum v = (int64_t)threadIdx.x < nblk ? btot[threadIdx.x] : TileSum{0, 0, 0, 0, -1};
+    const TileSum id{0, 0, 0, 0, -1};
+    const int64_t i0 = (int64_t)threadIdx.x * SCAN_PER;
+    TileSum v[SCAN_PER], agg = id;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        v[k] = i0 + k < nblk ? btot[i0 + k] : id;
+        agg = ts_compose(agg, v[k]);
+    }
     TileSum tot;
-    const TileSum ex = block_scan_tiles(v, wsum, &tot);
-    if ((int64_t)threadIdx.x < nblk) btot[threadIdx.x] = ex;
+    TileSum run = block_scan_tiles(agg, wsum, &tot);
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        if (i0 + k < nblk) btot[i0 + k] = run;
+        run = ts_compose(run, v[k]);
+    }
     if (threadIdx.x == 0) btot[SCAN_B] = tot;
 }
 
@@ -638,9 +668,9 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     const int64_t nblk = (ntiles + SCAN_B - 1) / SCAN_B;
     if (nblk > SCAN_B) return SCCG_E_UNSUPPORTED;   // > 4 GiB of FASTA
     TileSum* btot = reinterpret_cast<TileSum*>(sc.block_sums);
-    hipLaunchKernelGGL(k_strip_scan_local, dim3((unsigned)nblk), dim3(SCAN_B), 0, s, ntiles, sc.tile_a, sc.tile_b,
+    hipLaunchKernelGGL(k_strip_scan_local, dim3((unsigned)nblk), dim3(SCAN_T), 0, s, ntiles, sc.tile_a, sc.tile_b,
                        sc.tile_fa, sc.tile_fb, sc.tile_last, btot);
-    hipLaunchKernelGGL(k_strip_scan_blocks, dim3(1), dim3(SCAN_B), 0, s, nblk, btot);
+    hipLaunchKernelGGL(k_strip_scan_blocks, dim3(1), dim3(SCAN_T), 0, s, nblk, btot);
     hipLaunchKernelGGL(k_strip_scan_apply, dim3(grid_for(ntiles, 256)), dim3(256), 0, s, ntiles, sc.tile_a, sc.tile_b,
                        sc.tile_fa, sc.tile_fb, sc.tile_last, btot, sc.tile_off, sc.tile_off2, sc.tile_carry, d_len,
                        d_len2);

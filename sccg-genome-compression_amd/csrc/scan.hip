@@ -2,7 +2,7 @@
 //
 // Used for every compaction offset in the pipeline (FASTA strip, run lists, per-segment and
 // per-match text offsets).  Tile = 256 threads x 16 items; block partials are scanned by one
-// 1024-thread block.  HBM-bound: 8 B read twice + 8 B written per element.
+// 256-thread block.  HBM-bound: 8 B read twice + 8 B written per element.
 #include "internal.h"
 
 #include <cstring>
@@ -69,17 +69,32 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_reduce(const int64_t* __res
     if (threadIdx.x == 0) partial[blockIdx.x] = tot;
 }
 
+// Single-block scans: SCCG_SB_T threads (256-thread builds do not wait for a whole free CU beside
+// other grids; A/B on the genome bench within noise, so 1024 stays).
+#ifndef SCCG_SB_T
+#define SCCG_SB_T 1024
+#endif
+constexpr int SB_T = SCCG_SB_T, PART_PER = 4;
 template <class Op>
-__global__ __launch_bounds__(1024) void k_partials_scan(int64_t* __restrict__ partial, int64_t nb,
+__global__ __launch_bounds__(SB_T) void k_partials_scan(int64_t* __restrict__ partial, int64_t nb,
                                                         int64_t* __restrict__ total) {
     __shared__ int64_t tmp[17];
     int64_t carry = Op::id();
-    for (int64_t base = 0; base < nb; base += 1024) {
-        int64_t idx = base + threadIdx.x;
-        int64_t v = idx < nb ? partial[idx] : Op::id();
+    for (int64_t base = 0; base < nb; base += SB_T * PART_PER) {
+        const int64_t i0 = base + (int64_t)threadIdx.x * PART_PER;
+        int64_t v[PART_PER], acc = Op::id();
+#pragma unroll
+        for (int k = 0; k < PART_PER; k++) {
+            v[k] = i0 + k < nb ? partial[i0 + k] : Op::id();
+            acc = Op::f(acc, v[k]);
+        }
         int64_t tot;
-        int64_t ex = block_excl<Op>(v, tmp, &tot);
-        if (idx < nb) partial[idx] = Op::f(carry, ex);
+        int64_t run = Op::f(carry, block_excl<Op>(acc, tmp, &tot));
+#pragma unroll
+        for (int k = 0; k < PART_PER; k++) {
+            if (i0 + k < nb) partial[i0 + k] = run;
+            run = Op::f(run, v[k]);
+        }
         carry = Op::f(carry, tot);
     }
     if (threadIdx.x == 0 && total) *total = carry;
@@ -108,26 +123,34 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(const int64_t* __restr
     }
 }
 
-// small inputs (<= 16 Ki elements): one 1024-thread block, one launch; a thread's (<= 16) loads are
-// issued together
-constexpr int SMALL_PER = 16;
+// small inputs (<= 16 Ki elements): one 256-thread block, one launch; a thread owns up to 64
+// consecutive elements, reduced 16 at a time (the 16 loads issued together), then re-read
+// (L2-hot) for the prefixes
+constexpr int SMALL_PER = 16, SMALL_MAX = 16384;   // (<= 64 elements per thread at 256 threads)
 template <class Op>
-__global__ __launch_bounds__(1024) void k_small_scan(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ out,
+__global__ __launch_bounds__(SB_T) void k_small_scan(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ out,
                                                      int64_t* __restrict__ total) {
     __shared__ int64_t tmp[17];
-    const int64_t per = (n + 1023) / 1024, base = (int64_t)threadIdx.x * per;
-    int64_t v[SMALL_PER];
+    const int64_t per = (n + SB_T - 1) / SB_T, base = (int64_t)threadIdx.x * per;
     int64_t acc = Op::id();
+    for (int64_t g = 0; g < per; g += SMALL_PER) {
+        int64_t v[SMALL_PER];
 #pragma unroll
-    for (int i = 0; i < SMALL_PER; i++) v[i] = (i < per && base + i < n) ? in[base + i] : Op::id();
+        for (int i = 0; i < SMALL_PER; i++) v[i] = (g + i < per && base + g + i < n) ? in[base + g + i] : Op::id();
 #pragma unroll
-    for (int i = 0; i < SMALL_PER; i++) acc = Op::f(acc, v[i]);
+        for (int i = 0; i < SMALL_PER; i++) acc = Op::f(acc, v[i]);
+    }
     int64_t tot;
     int64_t run = block_excl<Op>(acc, tmp, &tot);
+    for (int64_t g = 0; g < per; g += SMALL_PER) {
+        int64_t v[SMALL_PER];
 #pragma unroll
-    for (int i = 0; i < SMALL_PER; i++) {
-        if (i < per && base + i < n) out[base + i] = run;
-        run = Op::f(run, v[i]);
+        for (int i = 0; i < SMALL_PER; i++) v[i] = (g + i < per && base + g + i < n) ? in[base + g + i] : Op::id();
+#pragma unroll
+        for (int i = 0; i < SMALL_PER; i++) {
+            if (g + i < per && base + g + i < n) out[base + g + i] = run;
+            run = Op::f(run, v[i]);
+        }
     }
     if (threadIdx.x == 0 && total) *total = tot;
 }
@@ -139,14 +162,14 @@ int scan_impl(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int6
         if (d_total) return dev_set_i64(d_total, 1, {0}, s);
         return 0;
     }
-    if (n <= 1024 * SMALL_PER) {
-        hipLaunchKernelGGL(k_small_scan<Op>, dim3(1), dim3(1024), 0, s, in, n, out, d_total);
+    if (n <= SMALL_MAX) {
+        hipLaunchKernelGGL(k_small_scan<Op>, dim3(1), dim3(SB_T), 0, s, in, n, out, d_total);
         SCCG_HIP(hipGetLastError());
         return 0;
     }
     const int64_t nb = (n + TILE - 1) / TILE;
     hipLaunchKernelGGL(k_tile_reduce<Op>, dim3((unsigned)nb), dim3(SCCG_BLOCK), 0, s, in, n, d_partial);
-    hipLaunchKernelGGL(k_partials_scan<Op>, dim3(1), dim3(1024), 0, s, d_partial, nb, d_total);
+    hipLaunchKernelGGL(k_partials_scan<Op>, dim3(1), dim3(SB_T), 0, s, d_partial, nb, d_total);
     hipLaunchKernelGGL(k_tile_scan<Op>, dim3((unsigned)nb), dim3(SCCG_BLOCK), 0, s, in, n,
                        (const int64_t*)d_partial, out);
     SCCG_HIP(hipGetLastError());

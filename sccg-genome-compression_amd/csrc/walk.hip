@@ -917,7 +917,13 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
 
 // The end of a round in one block: the frozen fills of a batch (wave 0), then the chunks whose
 // entry state (predecessor's exit) differs from the one their trajectory used -> plist, scal[0].
-__global__ __launch_bounds__(1024) void k_round_tail(WalkPtrs A, int fbase, int fcap) {
+// (SCCG_RT_T=256 builds: 256 threads with 16 chunks each in flight, so the block does not wait for
+// a whole free CU; A/B on the genome bench within noise, chr1 +3-6 %, so 1024 stays)
+#ifndef SCCG_RT_T
+#define SCCG_RT_T 1024
+#endif
+constexpr int RT_T = SCCG_RT_T;
+__global__ __launch_bounds__(RT_T) void k_round_tail(WalkPtrs A, int fbase, int fcap) {
     if (A.scal[9]) return;   // void pre-queued round
     __shared__ int32_t sj[FROZEN_MAX], sy[FROZEN_MAX];
     __shared__ int32_t trig[RESPEC_MAX_TRIGGERS];
@@ -928,7 +934,7 @@ __global__ __launch_bounds__(1024) void k_round_tail(WalkPtrs A, int fbase, int 
     const int32_t next = A.round + 1;
     // RT_U chunks per thread and step, their state loaded together (one memory round trip per step
     // instead of one per chunk: the loop is latency-bound)
-    constexpr int RT_U = 8;
+    constexpr int RT_U = RT_T >= 1024 ? 8 : 16;
     const int32_t nthr = (int32_t)blockDim.x;
     for (int32_t jb = (int32_t)threadIdx.x; jb < A.C; jb += nthr * RT_U) {
         int32_t ex[RT_U], ep[RT_U], ux[RT_U], up[RT_U], lr[RT_U];
@@ -2584,7 +2590,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
         if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fbase_cap), dim3(SCCG_BLOCK), 0, s, A, 0);
-        hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(1024), 0, s, A, 0, fbase_cap);
+        hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(RT_T), 0, s, A, 0, fbase_cap);
         SCCG_HIP(hipGetLastError());
         return 0;
     };
@@ -2759,7 +2765,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
             auto frozen_batch = [&](int fbase, int fcap, bool init_fy) -> int {   // no-op past the list
                 if (init_fy) SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.fy, INT32_MAX, fcap, s));
                 if (fcap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fcap), dim3(SCCG_BLOCK), 0, s, A, fbase);
-                hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(1024), 0, s, A, fbase, fcap);   // + pending
+                hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(RT_T), 0, s, A, fbase, fcap);   // + pending
                 SCCG_HIP(hipGetLastError());
                 return 0;
             };

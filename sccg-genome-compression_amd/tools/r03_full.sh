@@ -10,7 +10,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -n 1 $OUT/gpu_tests.out
 run() { local lib=$1; shift; [ "$lib" = "-" ] && lib=""; env SCCG_LIB_PATH=$lib timeout -k 10 180 python3 "$@" 2>/dev/null | tail -n 1; }
 for pass in 1 2; do
-  for v in head:- prev:variants/prev/libsccg.so; do
+  for v in head:- prev:variants/prev2/libsccg.so; do
     IFS=: read name lib <<< "$v"
     echo "[$(date +%T)] $pass $name"
     echo "$name genome $(run $lib bench.py --no-cpu-baseline --no-decomp --no-e2e --no-check --steps 10)" >> $OUT/res.txt || exit 1
