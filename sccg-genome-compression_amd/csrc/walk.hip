@@ -128,6 +128,7 @@ struct WalkPtrs {
     int32_t* guess;
     int32_t* plist;       // chunks walked in the current round
     int32_t* rlist;       // chunks resumed after an escalation
+    int32_t* clist;       // chunks a fix-up carries on into (k_walk<.., true>), count in scal[11]
     int32_t* newX;        // staged fix-up results (k_commit)
     int32_t* newP;
     int32_t* conv;
@@ -489,23 +490,32 @@ constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cand
 #define WALK_WAVES_PER_EU 5
 #endif
 // nlist_dev (optional): the list length from device memory (a round queued before the host knows it)
-template <bool DBG>
+// CARRY: the carry launch of a round (list = A.clist): each listed chunk is walked from its
+// predecessor's staged exit and committed here, and the walk carries on while the rule allows.
+template <bool DBG, bool CARRY>
 __global__ __launch_bounds__(64 * WWPB) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
 void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const int32_t* __restrict__ nlist_dev) {
     __shared__ WalkLds lds_all[WWPB];
     const int w = wave_in_block(), lane = lane_id();
     const int32_t li = (int32_t)blockIdx.x * WWPB + w;
     if (nlist_dev) nlist = *nlist_dev;
+    if (CARRY && nlist > A.C) nlist = A.C;
     if (li >= nlist || A.scal[9]) return;
     WalkLds& L = lds_all[w];
-    const int32_t j = uni(list[li]);
-    const int32_t kind = uni(A.kind[j]);
-    const int32_t lo_j = j * A.S;
-    const int32_t hi_j = (lo_j + A.S < A.nT) ? lo_j + A.S : A.nT;
+    int32_t j = uni(list[li]);   // (j, lo_j, hi_j ... change when the walk carries on, below)
+    const int32_t kind = CARRY ? KIND_FIX : uni(A.kind[j]);
+    int32_t lo_j = j * A.S;
+    int32_t hi_j = (lo_j + A.S < A.nT) ? lo_j + A.S : A.nT;
     const int32_t lastk = A.nT - A.k;
 
     int32_t x, P, n = 0, q = 0, ob, cb = -1, cc = 0;
-    if (kind == KIND_SPEC) {
+    if (CARRY) {   // entry: the predecessor's staged exit (k_commit has not run yet)
+        cb = uni(A.cur[j]);
+        ob = 1 - cb;
+        cc = uni(A.cnt[cb][j]);
+        x = uni(A.newX[j - 1]);
+        P = uni(A.newP[j - 1]);
+    } else if (kind == KIND_SPEC) {
         ob = uni(A.cur[j]);
         x = lo_j;
         if (A.round == 1) {   // first guess: the anchor vote at the chunk start (anchor_diag)
@@ -541,9 +551,11 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         n = uni(A.escN[j]);
         q = uni(A.escQ[j]);
     }
-    if (lane == 0) A.status[j] = ST_OK;
-    if (blockIdx.x == 0 && threadIdx.x == 0) A.scal[5] = 0;   // frozen list of this round's commit
-    const int32_t x_entry = x, P_entry = P;
+    if (!CARRY) {
+        if (lane == 0) A.status[j] = ST_OK;
+        if (blockIdx.x == 0 && threadIdx.x == 0) A.scal[5] = 0;   // frozen list of this round's commit
+    }
+    int32_t x_entry = x, P_entry = P;
     const uint64_t dbg_t0 = DBG ? wall_clock64() : 0;
     uint64_t dbg_c[13] = {};   // matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail,
                                // t_hash, t_wide, wide positions
@@ -557,12 +569,21 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         if (lane == 0) { A.cnt[ob][j] = 0; A.exitX[j] = INVALID; A.exitP[j] = INVALID; }
         return;
     }
-    int32_t* ot = A.bt[ob] + (size_t)j * A.cap;
-    int32_t* op = A.bp[ob] + (size_t)j * A.cap;
-    int32_t* ol = A.bl[ob] + (size_t)j * A.cap;
-    const int32_t* ct = cb >= 0 ? A.bt[cb] + (size_t)j * A.cap : nullptr;
-    const int32_t* cp = cb >= 0 ? A.bp[cb] + (size_t)j * A.cap : nullptr;
-    const int32_t* cl = cb >= 0 ? A.bl[cb] + (size_t)j * A.cap : nullptr;
+    // The trajectory buffers: the main walk keeps their addresses; the carry walk (whose chunk
+    // changes) forms them where they are used -- loop-carried, they cost it registers it spills.
+    const size_t cap = (size_t)A.cap;
+    int32_t* const ot0 = CARRY ? nullptr : A.bt[ob] + (size_t)j * cap;
+    int32_t* const op0 = CARRY ? nullptr : A.bp[ob] + (size_t)j * cap;
+    int32_t* const ol0 = CARRY ? nullptr : A.bl[ob] + (size_t)j * cap;
+    const int32_t* const ct0 = CARRY || cb < 0 ? nullptr : A.bt[cb] + (size_t)j * cap;
+    const int32_t* const cp0 = CARRY || cb < 0 ? nullptr : A.bp[cb] + (size_t)j * cap;
+    const int32_t* const cl0 = CARRY || cb < 0 ? nullptr : A.bl[cb] + (size_t)j * cap;
+#define W_OT (CARRY ? A.bt[ob] + (size_t)j * cap : ot0)
+#define W_OP (CARRY ? A.bp[ob] + (size_t)j * cap : op0)
+#define W_OL (CARRY ? A.bl[ob] + (size_t)j * cap : ol0)
+#define W_CT (CARRY ? A.bt[cb] + (size_t)j * cap : ct0)
+#define W_CP (CARRY ? A.bp[cb] + (size_t)j * cap : cp0)
+#define W_CL (CARRY ? A.bl[cb] + (size_t)j * cap : cl0)
 
     RegWin W;
     W.P = INVALID;
@@ -570,11 +591,11 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     BufPos B;                   // the LDS copy of R'/T' (see WalkLds)
     int32_t lme = x;   // target index after the last match of this walk (start of the open literal run)
     bool converged = false, escalated = false;
-    const int32_t scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
+    int32_t scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
     // stale entry (predecessor re-walked in this round): converge within the budget or give up
-    const bool stale = A.stale_budget > 0 && kind == KIND_FIX && j > 0 && A.lround[j - 1] == A.round;
-    const int32_t budget_end = stale && x + A.stale_budget < scan_end ? x + A.stale_budget : scan_end;
-    const int32_t old_seedq = cb >= 0 ? uni(A.seedq[j]) : 0;
+    const bool stale = !CARRY && A.stale_budget > 0 && kind == KIND_FIX && j > 0 && A.lround[j - 1] == A.round;
+    int32_t budget_end = stale && x + A.stale_budget < scan_end ? x + A.stale_budget : scan_end;
+    int32_t old_seedq = cb >= 0 ? uni(A.seedq[j]) : 0;
     int32_t seed_x = x, seedq = 0;
     bool truncated = false;
     // the previous trajectory (fix-ups), 64 entries at a time in registers: lane i holds entry cq0 + i
@@ -582,18 +603,24 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     auto load_prev = [&](int32_t from) {
         cq0 = from;
         const int32_t qi = from + lane;
-        ctv = qi < cc ? ct[qi] : INT32_MAX;
-        cpv = qi < cc ? cp[qi] : 0;
-        clv = qi < cc ? cl[qi] : 0;
+        ctv = qi < cc ? W_CT[qi] : INT32_MAX;
+        cpv = qi < cc ? W_CP[qi] : 0;
+        clv = qi < cc ? W_CL[qi] : 0;
     };
     if (cb >= 0) load_prev(q);   // issued now, waited for at the first match
     // records of the trajectory not stored yet: entries [rb_n0, n), entry rb_n0 + i in lane i (a store
     // per step would make every later load wait for it: vmcnt counts stores and loads in issue order)
     int32_t rb_n0 = n, rbt = 0, rbp = 0, rbl = 0;
     auto flush_recs = [&]() {
-        if (lane < n - rb_n0) { ot[rb_n0 + lane] = rbt; op[rb_n0 + lane] = rbp; ol[rb_n0 + lane] = rbl; }
+        if (lane < n - rb_n0) { W_OT[rb_n0 + lane] = rbt; W_OP[rb_n0 + lane] = rbp; W_OL[rb_n0 + lane] = rbl; }
         rb_n0 = n;
     };
+    // A fix-up whose entry is final (its predecessor is not walked in this round) and that ends at
+    // its chunk end without converging hands the next chunk to the round's carry launch, which
+    // walks it from that exit and carries on from chunk to chunk in one wave: a run of chunks whose
+    // speculation failed is then walked in one round, not one round per chunk.  (The loop below
+    // only iterates in the carry instantiation, so the main walk's registers stay as they were.)
+    for (int carried = CARRY ? 1 : 0;; carried++) {
     while (x < scan_end) {
         if (x >= budget_end) { truncated = true; break; }
         if (DBG) tick(9);
@@ -678,7 +705,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         const int32_t p = (int32_t)(uint32_t)pk;
         if (p == 0) {   // pn2 == 0: the reference falls back to the ungated (pn1, ln1) (:134-138)
             escalated = true;
-            if (lane == 0) {
+            if (lane == 0 && !CARRY) {   // (a carried chunk is left as it was: pending next round)
                 if (kind == KIND_SPEC) { A.cnt[ob][j] = 0; A.exitX[j] = INVALID; A.exitP[j] = INVALID; }
                 else {
                     A.status[j] = ST_ESC;
@@ -711,9 +738,9 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
                 flush_recs();
                 const int32_t rest = cc - q - 1;
                 for (int i = lane; i < rest; i += 64) {
-                    ot[n + i] = ct[q + 1 + i];
-                    op[n + i] = cp[q + 1 + i];
-                    ol[n + i] = cl[q + 1 + i];
+                    W_OT[n + i] = W_CT[q + 1 + i];
+                    W_OP[n + i] = W_CP[q + 1 + i];
+                    W_OL[n + i] = W_CL[q + 1 + i];
                 }
                 n += rest;
                 rb_n0 = n;   // the copied suffix is stored already
@@ -727,40 +754,105 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     }
     flush_recs();
     if (escalated) return;
-    if (DBG && lane == 0) {
-        tick(9);
-        uint64_t* d = A.dbg + (size_t)j * DBG_SLOTS;
-        d[0] = wall_clock64() - dbg_t0;
-        for (int i = 0; i < 13; i++) d[1 + i] = dbg_c[i];
-        d[14] = (uint64_t)A.round;
-        d[15] = dbg_t0;   // start (wall clock), for the launch's start spread
-    }
-    if (lane == 0 && truncated) {   // nothing to commit; the chunk stays pending
-        A.conv[j] = 0;
-        A.changed[j] = 0;
-        A.walked[j] = A.round;
-        A.frozen[j] = 0;
-        A.status[j] = ST_TRUNC;
-        return;
-    }
-    if (lane == 0) {
-        A.cnt[ob][j] = n;
-        if (cb < 0) {   // speculative: the trajectory is the chunk's first, take it as is
-            A.exitX[j] = x; A.exitP[j] = P;
-            A.seedq[j] = seedq;
-        } else {        // fix-up: staged; k_commit decides
-            const int32_t nx = converged ? A.exitX[j] : x, np = converged ? A.exitP[j] : P;
-            A.newX[j] = nx; A.newP[j] = np;
-            A.conv[j] = converged;
-            A.changed[j] = nx != A.exitX[j] || np != A.exitP[j];
-            A.walked[j] = A.round;
-            // ended in a long literal run with P frozen at the chunk end: k_frozen_scan territory
-            A.frozen[j] = !converged && x == hi_j && x - lme >= FROZEN_MIN;
-            A.trapped[j] = !converged && x - x_entry >= A.S / 2 && (P - P_entry < TRAP_P && P_entry - P < TRAP_P);
+    const int32_t nx = converged ? uni(A.exitX[j]) : x, np = converged ? uni(A.exitP[j]) : P;
+    const bool frozen_end = !converged && x == hi_j && x - lme >= FROZEN_MIN;
+    const bool trapped = !converged && x - x_entry >= A.S / 2 && (P - P_entry < TRAP_P && P_entry - P < TRAP_P);
+    const bool exit_changed = nx != uni(A.exitX[j]) || np != uni(A.exitP[j]);
+    if (!CARRY) {
+        if (DBG && lane == 0) {
+            tick(9);
+            uint64_t* d = A.dbg + (size_t)j * DBG_SLOTS;
+            d[0] = wall_clock64() - dbg_t0;
+            for (int i = 0; i < 13; i++) d[1 + i] = dbg_c[i];
+            d[14] = (uint64_t)A.round;
+            d[15] = dbg_t0;   // start (wall clock), for the launch's start spread
         }
-        A.status[j] = converged ? ST_CONV : ST_DONE;
+        if (lane == 0 && truncated) {   // nothing to commit; the chunk stays pending
+            A.conv[j] = 0;
+            A.changed[j] = 0;
+            A.walked[j] = A.round;
+            A.frozen[j] = 0;
+            A.status[j] = ST_TRUNC;
+            return;
+        }
+        if (lane == 0) {
+            A.cnt[ob][j] = n;
+            if (cb < 0) {   // speculative: the trajectory is the chunk's first, take it as is
+                A.exitX[j] = x; A.exitP[j] = P;
+                A.seedq[j] = seedq;
+            } else {        // fix-up: staged; k_commit decides
+                A.newX[j] = nx; A.newP[j] = np;
+                A.conv[j] = converged;
+                A.changed[j] = exit_changed;
+                A.walked[j] = A.round;
+                // ended in a long literal run with P frozen at the chunk end: k_frozen_scan territory
+                A.frozen[j] = frozen_end;
+                A.trapped[j] = trapped;
+            }
+            A.status[j] = converged ? ST_CONV : ST_DONE;
+        }
+        if (truncated) return;
+        // carry on only from a fix-up whose commit is certain (k_commit takes it: its predecessor is
+        // not listed, and -- by the rule below -- not carried into either), and not where the
+        // frozen scan (frozen end) or the trapped re-speculation (k_round_tail) resolves faster
+        if (kind != KIND_FIX || (j > 0 && uni(A.lround[j - 1]) == A.round)) return;
+        if (converged || !exit_changed || frozen_end || trapped) return;
+        const int32_t j1 = j + 1;
+        if (j1 >= A.C || uni(A.lround[j1]) == A.round || (j1 + 1 < A.C && uni(A.lround[j1 + 1]) == A.round)) return;
+        if (lane == 0) {
+            const int32_t at = atomicAdd(&A.scal[11], 1);
+            if (at < A.C) A.clist[at] = j1;
+        }
+        return;
+    } else {
+        // a carried chunk: not on the round's list, so k_commit never sees it -- committed here.
+        // A frozen end is left pending (next round's fix-up hands it to the frozen scan).
+        if (frozen_end) return;
+        if (lane == 0) {
+            A.cnt[ob][j] = n;
+            A.cur[j] = ob;
+            A.exitX[j] = nx; A.exitP[j] = np;
+            A.usedX[j] = x_entry; A.usedP[j] = P_entry;
+            A.seedq[j] = 0;
+            A.conv[j] = converged;
+            A.changed[j] = exit_changed;
+            A.walked[j] = A.round;
+            A.frozen[j] = 0;
+            A.trapped[j] = trapped;
+        }
+    }
+    // carry into chunk j + 1 when its entry changed and nobody else walks it or depends on it in
+    // this round: j + 1 is not listed, and neither is j + 2 (a listed chunk's predecessor must keep
+    // its state for the whole round, so that its own commit rule -- and carry -- stay exact)
+    if (converged || !exit_changed || frozen_end || trapped) return;
+    const int32_t j1 = j + 1;
+    if (j1 >= A.C || uni(A.lround[j1]) == A.round || (j1 + 1 < A.C && uni(A.lround[j1 + 1]) == A.round)) return;
+    j = j1;
+    lo_j = j * A.S;
+    hi_j = (lo_j + A.S < A.nT) ? lo_j + A.S : A.nT;
+    scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
+    budget_end = scan_end;
+    cb = uni(A.cur[j]);
+    ob = 1 - cb;
+    cc = uni(A.cnt[cb][j]);
+    old_seedq = uni(A.seedq[j]);
+    n = 0;
+    q = 0;
+    rb_n0 = 0;
+    seedq = 0;
+    converged = false;
+    x_entry = x;
+    P_entry = P;
+    load_prev(0);
     }
 }
+
+#undef W_OT
+#undef W_OP
+#undef W_OL
+#undef W_CT
+#undef W_CP
+#undef W_CL
 
 // Commit the fix-ups of a round.  A re-walk that converged is always taken.  One that did not is
 // taken only if its predecessor's exit did not change in this round: otherwise its entry was a
@@ -772,6 +864,7 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
     if (A.scal[9]) return;   // void pre-queued round
     if (nlist_dev) nlist = *nlist_dev;
     if (blockIdx.x == 0 && threadIdx.x < FROZEN_MAX) A.fy[threadIdx.x] = INT32_MAX;   // for k_frozen_scan
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.scal[11] = 0;   // the round's carry list was consumed
     for (int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); i < nlist; i += (int32_t)(gridDim.x * blockDim.x)) {
         const int32_t j = list[i];
         if (A.kind[j] == KIND_SPEC || A.status[j] == ST_ESC || A.status[j] == ST_TRUNC) continue;
@@ -910,6 +1003,7 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.scal[0] = 0; A.scal[1] = 0; A.scal[2] = startX; A.scal[3] = startP;
         A.scal[5] = 0;   // frozen count (k_walk resets it too, but a void round's k_walk returns first)
+        A.scal[11] = 0;  // carry list
         A.snapX[0] = startX;
         A.snapP[0] = startP;
     }
@@ -2212,6 +2306,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.guess = c.take<int32_t>(C);
     A.plist = c.take<int32_t>(C);
     A.rlist = c.take<int32_t>(C);
+    A.clist = c.take<int32_t>(C);
     A.newX = c.take<int32_t>(C); A.newP = c.take<int32_t>(C);
     A.conv = c.take<int32_t>(C); A.changed = c.take<int32_t>(C); A.walked = c.take<int32_t>(C);
     A.lround = c.take<int32_t>(C);
@@ -2251,7 +2346,16 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
 
 // SCCG_DEBUG runs take the instrumented walk
 using WalkKernel = void (*)(WalkPtrs, const int32_t*, int32_t, const int32_t*);
-WalkKernel walk_kernel(const WalkPtrs& A) { return A.dbg ? k_walk<true> : k_walk<false>; }
+WalkKernel walk_kernel(const WalkPtrs& A) { return A.dbg ? k_walk<true, false> : k_walk<false, false>; }
+// the round's carry launch (after its k_walk, before k_commit): up to CARRY_GRID * WWPB carry chains
+// (chunks past that stay pending for the next round, as without carrying)
+constexpr int CARRY_GRID = 256;
+int launch_carry(const WalkPtrs& A, hipStream_t s) {
+    PROF_LAUNCH(PROF_WALK_CHAIN, s, (A.dbg ? k_walk<true, true> : k_walk<false, true>), dim3(CARRY_GRID), dim3(64 * WWPB), 0, s, A,
+                (const int32_t*)A.clist, 0, (const int32_t*)(A.scal + 11));
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
 
 struct FullC {
     int64_t lmax;
@@ -2587,6 +2691,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         const int32_t* nd = dev_nlist ? A.scal : nullptr;
         PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(A.C, WWPB)), dim3(64 * WWPB), 0, s, A, (const int32_t*)A.plist,
                     A.C, nd);
+        RC(launch_carry(A, s));
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
         if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fbase_cap), dim3(SCCG_BLOCK), 0, s, A, 0);
@@ -2754,6 +2859,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                 PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WWPB)), dim3(64 * WWPB), 0, s, A,
                             (const int32_t*)A.plist, nlist, (const int32_t*)nullptr);
                 SCCG_HIP(hipGetLastError());
+                RC(launch_carry(A, s));
             }
             res->rounds = round;
             // Commit, fill the first frozen runs and find the next round's pending chunks without

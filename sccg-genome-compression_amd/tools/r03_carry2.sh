@@ -1,0 +1,20 @@
+#!/bin/bash
+# Carry launch, main-walk addresses restored: GPU suite subset, then head vs previous commit, 3 passes.
+set -o pipefail
+OUT=gpurun_out/r03carry2
+mkdir -p $OUT
+export TMPDIR=/tmp
+T=sccg-genome-compression_amd/tools
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.out 2>&1 || { tail -30 $OUT/gpu_tests.out; exit 1; }
+tail -n 1 $OUT/gpu_tests.out
+run() { local lib=$1 ee=$2; shift 2; [ "$lib" = "-" ] && lib=""; env SCCG_LIB_PATH=$lib $ee timeout -k 10 180 python3 "$@" 2>/dev/null | tail -n 1; }
+for pass in 1 2 3; do
+  for v in head:- prev:variants/prev3/libsccg.so; do
+    IFS=: read name lib <<< "$v"
+    echo "[$(date +%T)] $pass $name"
+    echo "$name chr1 $(run $lib X=1 $T/bench_pair.py hg 247249719 249250621 1 --steps 10 --prof)" >> $OUT/res.txt || exit 1
+    echo "$name genome $(run $lib X=1 bench.py --no-cpu-baseline --no-decomp --no-e2e --no-check --steps 10)" >> $OUT/res.txt || exit 1
+  done
+done
+echo "head chr1_shift2 $(run - SCCG_ANCHOR_SHIFT=-2 $T/bench_pair.py hg 247249719 249250621 1 --steps 2 --sha)" >> $OUT/res.txt
+echo done

@@ -9,6 +9,8 @@ the chr21 / T2T pairs also through the host API and the round trip (sccg_reconst
 import hashlib
 import json
 import os
+import subprocess
+import sys
 import threading
 
 import pytest
@@ -119,3 +121,29 @@ def test_compress_files_vs_reference(ctx, tmp_path):
     tp.write_bytes(tfa2)
     ctx.compress_files(str(rp), str(tp), str(op))
     assert op.read_bytes() == ctx.compress(rfa2, tfa2)
+
+
+def test_poor_speculation_rounds_bounded():
+    """With a quarter-size anchor table (SCCG_ANCHOR_SHIFT=-2) most chunks get wrong first guesses;
+    round 2 used to resolve one chunk per pending run per round (thousands of rounds on chr1-sized
+    pairs).  Fix-ups now carry on into the next chunk (walk.hip k_walk): the chr21 pair must still
+    give the reference's bytes, in fewer than 64 rounds.  (A child process: the knob is read once.)"""
+    e = {m["name"]: m for m in _manifest()}.get("chr21")
+    if e is None:
+        pytest.skip("chr21 not pinned")
+    code = (
+        "import hashlib, json, sys\n"
+        f"sys.path.insert(0, {HERE!r})\n"
+        "import synthlib\n"
+        "from pkg import sccg\n"
+        f"rfa, tfa = synthlib.synth_pair({e['profile']!r}, {e['ref_len']}, {e['tgt_len']}, {e['seed']})\n"
+        "c = sccg.Context(0)\n"
+        "rec = c.compress(rfa, tfa)\n"
+        "print(json.dumps({'sha': hashlib.sha256(rec).hexdigest(), 'rounds': c.stats()['walk_rounds']}))\n"
+    )
+    env = dict(os.environ, SCCG_ANCHOR_SHIFT="-2")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["sha"] == e["record_sha256"]
+    assert d["rounds"] < 64, d
