@@ -561,27 +561,36 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restr
                                                           const int64_t* __restrict__ bdsum, const int64_t* __restrict__ d_nref,
                                                           const uint8_t* __restrict__ R, uint8_t* __restrict__ dec,
                                                           int32_t* __restrict__ err) {
+    __shared__ uint8_t stg[WPB][2 * TK_B];
     const int64_t b = (int64_t)blockIdx.x * WPB + wave_in_block();
     const int64_t base = b * TK_B;
     if (base >= n) return;
     const int lane = lane_id();
     const int64_t i = base + lane;
+    // the block's 64 bytes and the 64 after them (a token starting in the block ends within 32) in
+    // LDS: the token parses below read LDS, not one dependent HBM byte after the other
+    uint8_t* st = stg[wave_in_block()];
     const uint8_t c = i < n ? s[i] : (uint8_t)',';
+    st[lane] = c;
+    st[TK_B + lane] = i + TK_B < n ? s[i + TK_B] : (uint8_t)0;
+    wave_sync();
+    const RlView v{st - RL_BEHIND, base, n, TK_B};   // v.at(q) = st[q - base]
     const bool par = i < n && (c == '(' || c == ')');
     // the last parenthesis strictly before this byte inside the block, else the block's state
     const unsigned long long pm = __ballot(par) & ((1ull << lane) - 1ull);
-    const bool inside = pm ? s[base + 63 - __clzll((long long)pm)] == '(' : bin[b] != 0;
+    const bool inside = pm ? st[63 - __clzll((long long)pm)] == '(' : bin[b] != 0;
     int64_t contrib = 0, d = 0;
     bool tok = false;
     if (i < n) {
         if (c == '(') {
             int64_t comma = -1, close = -1, l = 0;
             for (int64_t q = i + 1; q < n && q < i + 32; q++) {
-                if (s[q] == ',' && comma < 0) comma = q;
-                if (s[q] == ')') { close = q; break; }
-                if (s[q] == '(') break;
+                const uint8_t cq = v.at(q);
+                if (cq == ',' && comma < 0) comma = q;
+                if (cq == ')') { close = q; break; }
+                if (cq == '(') break;
             }
-            if (comma > 0 && close > comma && parse_int(s, n, i + 1, comma, &d) && parse_int(s, n, comma + 1, close, &l) && l >= 0) {
+            if (comma > 0 && close > comma && parse_int_v(v, i + 1, comma, &d) && parse_int_v(v, comma + 1, close, &l) && l >= 0) {
                 tok = true;
                 contrib = l;
             }
