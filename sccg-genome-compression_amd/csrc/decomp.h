@@ -10,6 +10,29 @@ struct DcRuns {
     int64_t total;    // sum of len
 };
 
+// Token table of the fused reconstruction (decomp.hip k_tok_emit): entry 0 a sentinel, entry 1 + j
+// token j of the record line (decoded offset, absolute reference position, length, record offset
+// after its ')').
+struct DcTokTab {
+    int64_t *o, *p, *l, *r;
+};
+struct DcTokBuf {
+    DcTokTab tab;      // capacity dc_tok_cap(n) entries each
+    int64_t* btok;     // >= n / 64 + 2: tokens per 64-byte block
+    int64_t* btoff;    // >= n / 64 + 2: their exclusive prefix
+    int64_t* d_ntok;   // tokens of the line (entries 1..*d_ntok)
+};
+int64_t dc_tok_cap(int64_t n);
+// what the fused formatter reads: the token table, the record line, R' and |R'| (device)
+struct DcFmtSrc {
+    DcTokTab tk;
+    const int64_t* d_ntok;
+    const uint8_t* rec;
+    int64_t nrec;
+    const uint8_t* R;
+    const int64_t* d_nref;
+};
+
 // every '\n' of the record text, unordered: d_buf[0] = their count, d_buf[1, 1 + DC_NL_CAP) the
 // first DC_NL_CAP found (one pass; the caller sorts them, or uses dc_find_lines when there are more)
 constexpr int DC_NL_CAP = 32;
@@ -38,7 +61,12 @@ int dc_n_check(const DcRuns& nr, const int64_t* d_ncnt, const int64_t* d_D, int3
 // when given); *d_total = decoded length
 int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,
                       int64_t* d_dsum, const int64_t* d_nref, hipEvent_t nref_ready, int64_t* d_partial, int32_t* d_err,
-                      int64_t* d_total, hipStream_t s);
+                      int64_t* d_total, hipStream_t s, const DcTokBuf* tk = nullptr);
+// fused path (tk given to dc_decode_prepare): d_err bit 2 for tokens beyond *d_nref
+int dc_tok_range(const DcTokBuf& tk, int64_t cap, const int64_t* d_nref, int32_t* d_err, hipStream_t s);
+// true: the reconstruction expands tokens inside the formatter (no decoded buffer); opt-in with
+// SCCG_DC_FUSED=1 (A/B runs), the fill + format path otherwise
+bool dc_fused();
 // (tiled path, dc_tok_tiled(): the range check against *d_nref happens here, d_err bit 2)
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
                    const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s,
@@ -48,5 +76,7 @@ bool dc_tok_tiled();
 // N insertion + lowercase + 50-column wrap of nres result bytes into d_out (no final '\n');
 // d_span: scratch of dc_format_span_words(nres) int64 (per-span run indices)
 int64_t dc_format_span_words(int64_t nres);
+// With fz (fused path) d_dec is unused: the decoded bytes come from fz's token table; the stream
+// waits for wait_before (the reference strip) between the block index and the formatter.
 int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out,
-              hipStream_t s);
+              hipStream_t s, const DcFmtSrc* fz = nullptr, hipEvent_t wait_before = nullptr);

@@ -503,7 +503,7 @@ constexpr int TK_B = 64;   // record bytes per block (one lane in pass 1, one wa
 
 __global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ s, int64_t n, int64_t* __restrict__ bin,
                                                     int64_t* __restrict__ bcontrib, int64_t* __restrict__ bdelta,
-                                                    int32_t* __restrict__ err) {
+                                                    int32_t* __restrict__ err, int64_t* __restrict__ btok) {
     // one wave per 1 KiB tile (16 bytes per lane, staged in LDS); 4 lanes make one 64-byte block
     constexpr int TL = 16, TT = 64 * TL;
     __shared__ uint8_t stage[4][RL_BEHIND + TT + RL_AHEAD];
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ 
     const int64_t a = t0 + (int64_t)lane * TL;
     bool inside = rl_lane_inside(v, a, TL);
     const bool in0 = inside;
-    int64_t cs = 0, ds = 0;
+    int64_t cs = 0, ds = 0, tk = 0;
     bool bad = false;
     for (int64_t i = a; i < a + TL && i < n; i++) {
         const uint8_t c = v.at(i);
@@ -530,6 +530,8 @@ __global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ 
             if (!(comma > 0 && close > comma && parse_int_v(v, i + 1, comma, &d) && parse_int_v(v, comma + 1, close, &l)) ||
                 l < 0)
                 bad = true;
+            else
+                tk++;
             cs += l;
             ds += d;
             inside = true;
@@ -545,12 +547,15 @@ __global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ 
     cs += __shfl_xor(cs, 2, 64);
     ds += __shfl_xor(ds, 1, 64);
     ds += __shfl_xor(ds, 2, 64);
+    tk += __shfl_xor(tk, 1, 64);
+    tk += __shfl_xor(tk, 2, 64);
     static_assert(4 * TL == TK_B, "four lanes per block");
     const int64_t b = t * (TT / TK_B) + (lane >> 2);
     if ((lane & 3) == 0 && b * TK_B < n) {
         bin[b] = in0;
         bcontrib[b] = cs;
         bdelta[b] = ds;
+        if (btok) btok[b] = tk;
     }
 }
 
@@ -615,6 +620,79 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restr
         const int64_t pj = __shfl(p, j), lj = __shfl(contrib, j), oj = __shfl(o, j);
         wave_copy(dec + oj, R + pj, lj, lane);
     }
+}
+
+// Token table of the fused reconstruction (the default): instead of copying bytes into a decoded
+// buffer that the formatter reads back (k_tok_fill2), one wave per 64-byte block writes each token's
+// decoded offset o, absolute reference position p, length l and the record offset r right after its
+// ')' (decompression.cpp:210-236).  Entry 0 is a sentinel (0, 0, 0, 0) for the literals before the
+// first token; token j of the line is entry 1 + j.  Decoded byte x then lies in entry t = the last
+// with o_t <= x: it is R'[p_t + x - o_t] when x < o_t + l_t, else the literal rec[r_t + x - o_t - l_t]
+// (between a token's ')' and the next '(' every byte is a literal, :231-236).  Needs no R', so it
+// runs beside the reference strip; the range check (:223-229) is k_tok_range, after the strip.
+__global__ __launch_bounds__(SCCG_BLOCK) void k_tok_emit(const uint8_t* __restrict__ s, int64_t n,
+                                                         const int64_t* __restrict__ bin, const int64_t* __restrict__ boff,
+                                                         const int64_t* __restrict__ bdsum, const int64_t* __restrict__ btoff,
+                                                         DcTokTab tk) {
+    __shared__ uint8_t stg[WPB][2 * TK_B];
+    const int64_t b = (int64_t)blockIdx.x * WPB + wave_in_block();
+    const int64_t base = b * TK_B;
+    if (base >= n) return;
+    const int lane = lane_id();
+    const int64_t i = base + lane;
+    uint8_t* st = stg[wave_in_block()];
+    const uint8_t c = i < n ? s[i] : (uint8_t)',';
+    st[lane] = c;
+    st[TK_B + lane] = i + TK_B < n ? s[i + TK_B] : (uint8_t)0;
+    wave_sync();
+    const RlView v{st - RL_BEHIND, base, n, TK_B};
+    const bool par = i < n && (c == '(' || c == ')');
+    const unsigned long long pm = __ballot(par) & ((1ull << lane) - 1ull);
+    const bool inside = pm ? st[63 - __clzll((long long)pm)] == '(' : bin[b] != 0;
+    int64_t contrib = 0, d = 0, close = -1;
+    bool tok = false;
+    if (i < n) {
+        if (c == '(') {
+            int64_t comma = -1, l = 0;
+            for (int64_t q = i + 1; q < n && q < i + 32; q++) {
+                const uint8_t cq = v.at(q);
+                if (cq == ',' && comma < 0) comma = q;
+                if (cq == ')') { close = q; break; }
+                if (cq == '(') break;
+            }
+            if (comma > 0 && close > comma && parse_int_v(v, i + 1, comma, &d) && parse_int_v(v, comma + 1, close, &l) && l >= 0) {
+                tok = true;
+                contrib = l;
+            }
+        } else if (c == ')') {
+            contrib = inside ? 0 : 1;
+        } else if (!inside) {
+            contrib = 1;
+        }
+    }
+    const int64_t o = boff[b] + wave_incl_add(contrib) - contrib;
+    const int64_t p = bdsum[b] + wave_incl_add(d);   // running p, this token included
+    const unsigned long long tm = __ballot(tok);
+    if (tok) {
+        const int64_t e = 1 + btoff[b] + __popcll(tm & ((1ull << lane) - 1ull));
+        tk.o[e] = o;
+        tk.p[e] = p;
+        tk.l[e] = contrib;
+        tk.r[e] = close + 1;
+    }
+    if (b == 0 && lane == 0) { tk.o[0] = 0; tk.p[0] = 0; tk.l[0] = 0; tk.r[0] = 0; }
+}
+
+// d_err bit 2 for a token beyond the reference (p < 0 or p + l > |R'|, decompression.cpp:223-229)
+__global__ void k_tok_range(DcTokTab tk, const int64_t* __restrict__ d_ntok, const int64_t* __restrict__ d_nref,
+                            int32_t* __restrict__ err) {
+    const int64_t nt = *d_ntok, nref = *d_nref;
+    bool bad = false;
+    for (int64_t t = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= nt; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = tk.p[t], l = tk.l[t];
+        if (p < 0 || p + l > nref) bad = true;
+    }
+    if (bad) atomicOr(err, 2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -821,26 +899,37 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
 // position's byte to LDS, 16 bytes apart per lane, and copied the line-broken range out again.)
 // ---------------------------------------------------------------------------------------------
 constexpr int OPT = 16, OB = 256 * OPT, OFRUNS = 384;
+constexpr int TW = 5;   // k_out_index entries per block boundary
 
 // Block boundaries: output offset o_b = o_first + b * OB clamped to [0, total]; its position
-// j_b = o - o / 51; per boundary [decoded offset of j_b, first N run and first lowercase run ending
-// after j_b, j_b].  One thread per (boundary, run list).
+// j_b = o - o / 51; per boundary [decoded offset d_b of j_b, first N run and first lowercase run
+// ending after j_b, j_b, and (fused path, tko given) the token-table entry holding d_b: the last
+// with o_t <= d_b].  One thread per (boundary, run list).
 __global__ void k_out_index(int64_t nres, int64_t total, int64_t o_first, int64_t nblk, const int32_t* __restrict__ ns,
                             const int32_t* __restrict__ nl, const int64_t* __restrict__ ncum, int64_t nn,
                             const int32_t* __restrict__ ls, const int32_t* __restrict__ ll, int64_t nlr,
-                            int64_t* __restrict__ tab) {
+                            const int64_t* __restrict__ tko, const int64_t* __restrict__ d_ntok, int64_t* __restrict__ tab) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * (nblk + 1); i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t b = i >> 1;
         int64_t o = o_first + b * OB;
         o = o < 0 ? 0 : (o > total ? total : o);
         const int64_t J = o - o / 51;
         if (i & 1) {
-            tab[4 * b + 2] = first_run_ending_after(ls, ll, nlr, J);
+            tab[TW * b + 2] = first_run_ending_after(ls, ll, nlr, J);
         } else {
             const int64_t r = first_run_ending_after(ns, nl, nn, J);
-            tab[4 * b + 0] = J - n_before_at(ns, nl, ncum, nn, r, J);
-            tab[4 * b + 1] = r;
-            tab[4 * b + 3] = J;
+            const int64_t d = J - n_before_at(ns, nl, ncum, nn, r, J);
+            tab[TW * b + 0] = d;
+            tab[TW * b + 1] = r;
+            tab[TW * b + 3] = J;
+            if (tko) {
+                int64_t lo = 0, hi = *d_ntok;   // entry 0 (o = 0) qualifies
+                while (lo < hi) {
+                    const int64_t m = (lo + hi + 1) >> 1;
+                    if (tko[m] <= d) lo = m; else hi = m - 1;
+                }
+                tab[TW * b + 4] = lo;
+            }
         }
     }
 }
@@ -909,14 +998,14 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
     __shared__ uint32_t sdec_w[OB / 4 + 2];
     __shared__ int32_t s_ns[OFRUNS], s_ne[OFRUNS], s_ls[OFRUNS], s_le[OFRUNS];
     __shared__ int64_t s_nb[OFRUNS];
-    __shared__ int64_t st[8];
+    __shared__ int64_t st[2 * TW];
     const int tid = threadIdx.x;
     const int64_t b = blockIdx.x;   // (a grid-stride loop over blocks: 0.35-0.43 ms instead of 0.27)
-    if (tid < 8) st[tid] = tab[4 * b + tid];
+    if (tid < 2 * TW) st[tid] = tab[TW * b + tid];
     __syncthreads();
-    const int64_t d0 = st[0], d1 = st[4];
-    const int64_t n_lo = st[1], n_hi = st[5] < nn ? st[5] + 1 : nn;
-    const int64_t l_lo = st[2], l_hi = st[6] < nlr ? st[6] + 1 : nlr;
+    const int64_t d0 = st[0], d1 = st[TW];
+    const int64_t n_lo = st[1], n_hi = st[TW + 1] < nn ? st[TW + 1] + 1 : nn;
+    const int64_t l_lo = st[2], l_hi = st[TW + 2] < nlr ? st[TW + 2] + 1 : nlr;
     const int64_t ntot = nn ? ncum[nn - 1] + nl[nn - 1] : 0;
     const bool lds_runs = n_hi - n_lo <= OFRUNS && l_hi - l_lo <= OFRUNS;
     const int64_t a0 = d0 & ~(int64_t)3;
@@ -935,6 +1024,157 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
             s_ls[r - l_lo] = x;
             s_le[r - l_lo] = x + ll[r];
         }
+    }
+    __syncthreads();
+    const uint8_t* sdec = reinterpret_cast<const uint8_t*>(sdec_w);
+    const int64_t o0 = o_first + b * OB + (int64_t)tid * OPT;
+    if (lds_runs) {
+        const LdsRuns N{s_ns, s_ne, s_nb}, L{s_ls, s_le, nullptr};
+        format_out16(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
+    } else {
+        const GlobalRunsAt N{ns, nl, ncum, n_lo}, L{ls, ll, nullptr, l_lo};
+        format_out16(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused reconstruction formatter (the default): k_format_out with the block's decoded bytes expanded
+// from the token table instead of read from a decoded buffer -- the tokens the block touches
+// (k_out_index entries t_b .. t_b+1) are staged in LDS beside its runs, then each thread gathers 16
+// decoded bytes (a token's R' bytes with five dword loads, else bytes from R' / the record's
+// literals) into the block's LDS copy, and formats as k_format_out.  The decoded buffer is never
+// written or re-read (the fill wrote ~|T| bytes and the formatter read them back), and the token
+// table is built beside the reference strip, so the strip is followed directly by this kernel.
+// ---------------------------------------------------------------------------------------------
+constexpr int OTOK = 128;
+
+struct TokLds {
+    const int64_t *o, *p, *l, *r;
+    int64_t base;
+    __device__ int64_t O(int64_t t) const { return o[t - base]; }
+    __device__ int64_t P(int64_t t) const { return p[t - base]; }
+    __device__ int64_t L(int64_t t) const { return l[t - base]; }
+    __device__ int64_t R(int64_t t) const { return r[t - base]; }
+};
+struct TokGlobal {
+    const int64_t *o, *p, *l, *r;
+    __device__ int64_t O(int64_t t) const { return o[t]; }
+    __device__ int64_t P(int64_t t) const { return p[t]; }
+    __device__ int64_t L(int64_t t) const { return l[t]; }
+    __device__ int64_t R(int64_t t) const { return r[t]; }
+};
+
+// decoded bytes [x, x + 16) into w[0..3] (bytes outside [d0, d1) are 0: no format position reads them)
+template <typename TV>
+__device__ __forceinline__ void expand16(int64_t x, int64_t d0, int64_t d1, int64_t t_lo, int64_t t_hi, const TV& T,
+                                         const uint8_t* __restrict__ R, int64_t nref, const uint8_t* __restrict__ rec,
+                                         int64_t nrec, uint32_t* w) {
+    const int64_t xs = x < d0 ? d0 : x;
+    int64_t lo = t_lo, hi = t_hi;   // last entry with o <= xs (o of t_lo <= d0 by construction)
+    while (lo < hi) {
+        const int64_t m = (lo + hi + 1) >> 1;
+        if (T.O(m) <= xs) lo = m; else hi = m - 1;
+    }
+    int64_t t = lo, o = T.O(t), l = T.L(t), p = T.P(t), r = T.R(t);
+    int64_t onext = t < t_hi ? T.O(t + 1) : INT64_MAX;
+    bool pv = p >= 0 && p + l <= nref;
+    if (x >= o && x + 16 <= o + l && pv) {   // all 16 from one token: dword loads (R' has >= 64 B of slack)
+        const uint8_t* s0 = R + p + (x - o);
+        const unsigned sh = (unsigned)((uintptr_t)s0 & 3);
+        const uint32_t* a = reinterpret_cast<const uint32_t*>((uintptr_t)s0 & ~(uintptr_t)3);
+        const uint32_t w0 = a[0], w1 = a[1], w2 = a[2], w3 = a[3], w4 = a[4];
+        w[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        w[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        w[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        w[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        return;
+    }
+    // every source first (a 32-bit code: R' offset, or the record offset | 1 << 31; ~0 = none; the
+    // host takes this path only when |R'| and the record line are below 2^31), then all 16 loads
+    uint32_t src[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int64_t y = x + k;
+        src[k] = ~0u;
+        if (y >= xs && y < d1) {
+            while (y >= onext) {
+                t++;
+                o = onext; l = T.L(t); p = T.P(t); r = T.R(t);
+                onext = t < t_hi ? T.O(t + 1) : INT64_MAX;
+                pv = p >= 0 && p + l <= nref;
+            }
+            if (y < o + l) {
+                if (pv) src[k] = (uint32_t)(p + (y - o));
+            } else {
+                const int64_t q = r + (y - o - l);
+                if (q >= 0 && q < nrec) src[k] = (uint32_t)q | 0x80000000u;
+            }
+        }
+    }
+    uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t c = src[k];
+        const uint32_t b = c == ~0u ? 0u : (c >> 31) ? rec[c & 0x7fffffffu] : R[c];
+        v[k >> 2] |= b << (8 * (k & 3));
+    }
+    w[0] = v[0]; w[1] = v[1]; w[2] = v[2]; w[3] = v[3];
+}
+
+#ifndef SCCG_FUSED_WAVES
+#define SCCG_FUSED_WAVES 1
+#endif
+__global__ __launch_bounds__(256, SCCG_FUSED_WAVES) void k_format_fused(DcFmtSrc F, int64_t nres, int64_t total, int64_t o_first,
+                                                      const int32_t* __restrict__ ns, const int32_t* __restrict__ nl,
+                                                      const int64_t* __restrict__ ncum, int64_t nn,
+                                                      const int32_t* __restrict__ ls, const int32_t* __restrict__ ll,
+                                                      int64_t nlr, const int64_t* __restrict__ tab, uint8_t* __restrict__ out) {
+    __shared__ uint32_t sdec_w[OB / 4 + 8];
+    __shared__ int32_t s_ns[OFRUNS], s_ne[OFRUNS], s_ls[OFRUNS], s_le[OFRUNS];
+    __shared__ int64_t s_nb[OFRUNS];
+    __shared__ int64_t s_to[OTOK], s_tp[OTOK], s_tl[OTOK], s_tr[OTOK];
+    __shared__ int64_t st[2 * TW + 1];
+    const int tid = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    if (tid < 2 * TW) st[tid] = tab[TW * b + tid];
+    if (tid == 2 * TW) st[2 * TW] = *F.d_nref;
+    __syncthreads();
+    const int64_t d0 = st[0], d1 = st[TW];
+    const int64_t n_lo = st[1], n_hi = st[TW + 1] < nn ? st[TW + 1] + 1 : nn;
+    const int64_t l_lo = st[2], l_hi = st[TW + 2] < nlr ? st[TW + 2] + 1 : nlr;
+    const int64_t t_lo = st[4], t_hi = st[TW + 4];
+    const int64_t nref = st[2 * TW];
+    const int64_t ntot = nn ? ncum[nn - 1] + nl[nn - 1] : 0;
+    const bool lds_runs = n_hi - n_lo <= OFRUNS && l_hi - l_lo <= OFRUNS;
+    const bool lds_tok = t_hi - t_lo < OTOK;
+    if (lds_tok) {
+        for (int64_t t = t_lo + tid; t <= t_hi; t += 256) {
+            s_to[t - t_lo] = F.tk.o[t];
+            s_tp[t - t_lo] = F.tk.p[t];
+            s_tl[t - t_lo] = F.tk.l[t];
+            s_tr[t - t_lo] = F.tk.r[t];
+        }
+    }
+    if (lds_runs) {
+        for (int64_t r = n_lo + tid; r < n_hi; r += 256) {
+            const int32_t x = ns[r];
+            s_ns[r - n_lo] = x;
+            s_ne[r - n_lo] = x + nl[r];
+            s_nb[r - n_lo] = ncum[r];
+        }
+        for (int64_t r = l_lo + tid; r < l_hi; r += 256) {
+            const int32_t x = ls[r];
+            s_ls[r - l_lo] = x;
+            s_le[r - l_lo] = x + ll[r];
+        }
+    }
+    __syncthreads();
+    const int64_t a0 = d0 & ~(int64_t)3;
+    const int64_t nch = (d1 - a0 + 15) >> 4;
+    for (int64_t c = tid; c < nch; c += 256) {
+        uint32_t* w = sdec_w + 4 * c;
+        if (lds_tok) expand16(a0 + 16 * c, d0, d1, t_lo, t_hi, TokLds{s_to, s_tp, s_tl, s_tr, t_lo}, F.R, nref, F.rec, F.nrec, w);
+        else expand16(a0 + 16 * c, d0, d1, t_lo, t_hi, TokGlobal{F.tk.o, F.tk.p, F.tk.l, F.tk.r}, F.R, nref, F.rec, F.nrec, w);
     }
     __syncthreads();
     const uint8_t* sdec = reinterpret_cast<const uint8_t*>(sdec_w);
@@ -1062,23 +1302,34 @@ int dc_n_check(const DcRuns& nr, const int64_t* d_ncnt, const int64_t* d_D, int3
 
 int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_contrib, int64_t* d_dlt, int64_t* d_off,
                       int64_t* d_dsum, const int64_t* d_nref, hipEvent_t nref_ready, int64_t* d_partial, int32_t* d_err,
-                      int64_t* d_total, hipStream_t s) {
+                      int64_t* d_total, hipStream_t s, const DcTokBuf* tk) {
     if (n <= 0) {
         SCCG_HIP(hipMemsetAsync(d_total, 0, sizeof(int64_t), s));
+        if (tk) {   // no tokens: the sentinel entry alone
+            SCCG_HIP(hipMemsetAsync(tk->d_ntok, 0, sizeof(int64_t), s));
+            for (int64_t* a : {tk->tab.o, tk->tab.p, tk->tab.l, tk->tab.r}) SCCG_HIP(hipMemsetAsync(a, 0, sizeof(int64_t), s));
+        }
         return 0;
     }
     if (dc_tok_tiled()) {
         // per 64-byte block: state, output bytes, deltas; their exclusive prefixes -> d_off, d_dsum
         const int64_t nb = (n + TK_B - 1) / TK_B;
         const unsigned g = (unsigned)((n + 4 * 1024 - 1) / (4 * 1024));   // 4 waves of 1 KiB per block
-        hipLaunchKernelGGL(k_tok_blocks, dim3(g), dim3(256), 0, s, d_s, n, d_lp, d_contrib, d_dlt, d_err);
+        hipLaunchKernelGGL(k_tok_blocks, dim3(g), dim3(256), 0, s, d_s, n, d_lp, d_contrib, d_dlt, d_err,
+                           tk ? tk->btok : nullptr);
         SCCG_HIP(hipGetLastError());
         int rc = dev_excl_sum(d_contrib, d_off, nb, d_total, d_partial, s);
         if (rc) return rc;
         rc = dev_excl_sum(d_dlt, d_dsum, nb, nullptr, d_partial, s);
+        if (rc || !tk) return rc;   // (unfused: the range check is in the fill, dc_decode_fill)
+        rc = dev_excl_sum(tk->btok, tk->btoff, nb, tk->d_ntok, d_partial, s);
+        if (rc) return rc;
+        PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_emit, dim3(grid_for(nb, WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n, (const int64_t*)d_lp,
+                    (const int64_t*)d_off, (const int64_t*)d_dsum, (const int64_t*)tk->btoff, tk->tab);
+        SCCG_HIP(hipGetLastError());
         (void)d_nref;
         (void)nref_ready;
-        return rc;   // (the range check is in the fill, dc_decode_fill)
+        return 0;   // (the range check: dc_tok_range, after the reference strip)
     }
     int rc = dc_last_paren(d_s, n, d_lp, d_partial, s);
     if (rc) return rc;
@@ -1092,6 +1343,20 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
     if (nref_ready) SCCG_HIP(hipStreamWaitEvent(s, nref_ready, 0));
     hipLaunchKernelGGL(k_tok_check, dim3(g), dim3(256), 0, s, d_s, n, (const int64_t*)d_dsum, (const int64_t*)d_dlt,
                        (const int64_t*)d_contrib, d_nref, d_err);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int64_t dc_tok_cap(int64_t n) { return n / 5 + 2; }   // a token "(d,l)" takes >= 5 bytes; tokens are disjoint
+
+bool dc_fused() {   // (opt-in, SCCG_DC_FUSED=1: measured slower so far)
+    static const bool v = dc_tok_tiled() && getenv("SCCG_DC_FUSED") != nullptr;
+    return v;
+}
+
+int dc_tok_range(const DcTokBuf& tk, int64_t cap, const int64_t* d_nref, int32_t* d_err, hipStream_t s) {
+    const unsigned g = grid_for(cap, 256) > 1024 ? 1024 : grid_for(cap, 256);
+    hipLaunchKernelGGL(k_tok_range, dim3(g), dim3(256), 0, s, tk.tab, (const int64_t*)tk.d_ntok, d_nref, d_err);
     SCCG_HIP(hipGetLastError());
     return 0;
 }
@@ -1119,28 +1384,41 @@ int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int
 }
 
 int64_t dc_format_span_words(int64_t nres) {   // (both formatters' tables; the output's misalignment adds a block)
-    const int64_t a = 3 * ((nres + FSPAN - 1) / FSPAN + 2), o = 4 * ((nres + nres / 50 + 16) / OB + 3);
+    const int64_t a = 3 * ((nres + FSPAN - 1) / FSPAN + 2), o = TW * ((nres + nres / 50 + 16) / OB + 3);
     return a > o ? a : o;
 }
 
 int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out,
-              hipStream_t s) {
-    if (nres <= 0) return 0;
+              hipStream_t s, const DcFmtSrc* fz, hipEvent_t wait_before) {
+    if (nres <= 0) {
+        if (wait_before) SCCG_HIP(hipStreamWaitEvent(s, wait_before, 0));
+        return 0;
+    }
     static const bool span_path = getenv("SCCG_FMT_SPAN") != nullptr;   // (A/B runs: the position-centric writer)
-    if (!span_path) {
+    if (fz || !span_path) {
         const int64_t total = nres + (nres - 1) / 50;   // the final '\n' is the caller's
         const int64_t o_first = -(int64_t)((uintptr_t)d_out & 15);
         const int64_t nblk = (total - o_first + OB - 1) / OB;
         hipLaunchKernelGGL(k_out_index, dim3(grid_for(2 * (nblk + 1), 256)), dim3(256), 0, s, nres, total, o_first, nblk,
                            (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
-                           (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, d_span);
+                           (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, fz ? (const int64_t*)fz->tk.o : nullptr,
+                           fz ? fz->d_ntok : nullptr, d_span);
         SCCG_HIP(hipGetLastError());
+        if (wait_before) SCCG_HIP(hipStreamWaitEvent(s, wait_before, 0));
+        if (fz) {
+            PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_fused, dim3((unsigned)nblk), dim3(256), 0, s, *fz, nres, total, o_first,
+                        (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
+                        (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out);
+            SCCG_HIP(hipGetLastError());
+            return 0;
+        }
         PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_out, dim3((unsigned)nblk), dim3(256), 0, s, d_dec, nres, total, o_first,
                     (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
                     (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out);
         SCCG_HIP(hipGetLastError());
         return 0;
     }
+    if (wait_before) SCCG_HIP(hipStreamWaitEvent(s, wait_before, 0));
     const int64_t nspan = (nres + FSPAN - 1) / FSPAN;
     hipLaunchKernelGGL(k_span_index, dim3(grid_for(2 * (nspan + 1), 256)), dim3(256), 0, s, nres, nspan,
                        (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,

@@ -54,6 +54,8 @@ enum Slot {
     B_DX, B_DELTA,
     // a second FASTA-strip scratch set (the reference strips beside the target, on the side stream)
     B_TILE2_A, B_TILE2_B, B_TILE2_FA, B_TILE2_FB, B_TILE2_LAST, B_TILE2_OFF, B_TILE2_OFF2, B_TILE2_CARRY, B_TILE2_BSUM,
+    // fused reconstruction: token table, tokens per record block and their prefix
+    B_D_TOK, B_D_BTOK,
     B_COUNT
 };
 
@@ -955,10 +957,23 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     GET(int32_t, ns, B_D_NS, dc_run_cap(nnl));
     GET(int32_t, nlr, B_D_NL, dc_run_cap(nnl));
     GET(int64_t, nc, B_D_NC, dc_run_cap(nnl));
+    // fused path: the record line becomes a token table (no R' needed) that the formatter expands
+    const bool fused = dc_fused() && rn < ((int64_t)1 << 31) && nenc < ((int64_t)1 << 31);   // (32-bit sources)
+    DcTokBuf tk{};
+    const int64_t tcap = dc_tok_cap(nenc > 0 ? nenc : 0);
+    if (fused) {
+        GET(int64_t, tkb, B_D_TOK, 4 * tcap);
+        tk.tab = DcTokTab{tkb, tkb + tcap, tkb + 2 * tcap, tkb + 3 * tcap};
+        const int64_t nbk = (nenc > 0 ? nenc : 0) / 64 + 2;
+        GET(int64_t, btk, B_D_BTOK, 2 * nbk);
+        tk.btok = btk;
+        tk.btoff = btk + nbk;
+        tk.d_ntok = sc + 24;
+    }
     HIPTRY(hipEventRecord(ctx->ev_fork2, s));
     HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
     TRY(dc_decode_prepare(enc, nenc, lp2, contrib, dlt2, doff, dsum, sc + 9, ctx->ev_rstrip, part2, d_err, sc + 12,
-                          ctx->side2));
+                          ctx->side2, fused ? &tk : nullptr));
     HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
     DcRuns lr{}, nr{};
     lr.start = ls; lr.len = ll; lr.cum = lc;
@@ -987,6 +1002,25 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     *out_len = total;
     if (size_only) return SCCG_OK;
     if (total > out_cap) return ctx->fail(SCCG_E_NOMEM, "output needs %lld bytes", (long long)total);
+    if (fused) {
+        // range check after the strip on side2; the formatter expands the tokens straight from R'
+        HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_rstrip, 0));
+        TRY(dc_tok_range(tk, tcap, sc + 9, d_err, ctx->side2));
+        HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
+        if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
+        TRY(dev_put_bytes(out + hlen, "\n", 1, s));
+        GET(int64_t, span, B_D_SPAN, dc_format_span_words(nres));
+        const DcFmtSrc fz{tk.tab, tk.d_ntok, enc, nenc > 0 ? nenc : 0, Rp, sc + 9};
+        TRY(dc_format(nullptr, nres, nr, lr, span, out + hlen + 1, s, &fz, ctx->ev_rstrip));
+        TRY(dev_put_bytes(out + total - 1, "\n", 1, s));
+        HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
+        const RbItem it[2] = {{d_err, &err, (int)sizeof err}, {sc + 9, &nRp, (int)sizeof nRp}};
+        TRY(dev_readback(it, 2, s));
+        if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
+        ctx->stats.target_bases = nres;
+        ctx->stats.reference_bases = nRp;
+        return SCCG_OK;
+    }
     GET(uint8_t, dec, B_D_DEC, D + 64);
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // the fill copies from R'
     TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s, sc + 9, d_err));

@@ -90,6 +90,13 @@ constexpr int CH_GRID = 512;           // scan blocks (1024 threads, 16 position
 constexpr int CH_HCAP = 4096;          // band hits kept per block and generation
 constexpr int32_t CHAIN_MCAP = 1 << 22;   // matches a chain may take
 constexpr int CH_GENS_PER_SYNC = 4;    // generations queued per host check
+#ifndef SCCG_CH_FF_SPAN
+#define SCCG_CH_FF_SPAN (32 * 1024)
+#endif
+// find-first generations scan at most CH_GRID * CH_FF_SPAN target positions (then the next one goes
+// on from there): a scan over the whole rest of the target kept every block before the hit busy
+// for its whole span (T2T-like 100 Mb pair: ~73 us per generation, 40 generations)
+constexpr int64_t CH_FF_SPAN = SCCG_CH_FF_SPAN;
 constexpr int CH_MAX_GENS = 4096;      // generations per chain
 constexpr int64_t CH_DENSE_HITS = 32768;  // band hits of one generation that switch the chain to find-first generations
 constexpr int CH_DENSE_N = 32;         // hand back to the chunk rounds when CH_DENSE_N matches
@@ -1168,11 +1175,13 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
         }
     };
     const int32_t lastk1 = A.nT - k + 1;
-    const int64_t total = (int64_t)lastk1 - x;
+    int64_t total = (int64_t)lastk1 - x;
+    if (first_only && total > CH_FF_SPAN * CH_GRID) total = CH_FF_SPAN * CH_GRID;
+    const int64_t end = (int64_t)x + (total > 0 ? total : 0);   // < lastk1: the next generation goes on from end
     int64_t span = total > 0 ? (total + CH_GRID - 1) / CH_GRID : 0;
     span = (span + 15) & ~(int64_t)15;
     const int64_t b0 = (int64_t)x + (int64_t)blockIdx.x * span;
-    const int64_t b1 = b0 + span < lastk1 ? b0 + span : lastk1;
+    const int64_t b1 = b0 + span < end ? b0 + span : end;
     int32_t* oy = A.chh_y + (size_t)blockIdx.x * CH_HCAP;
     uint32_t* ok = A.chh_k + (size_t)blockIdx.x * CH_HCAP;
     int32_t cnt = 0;
@@ -1241,7 +1250,10 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
     }
     if (tid == 0) {
         A.chh_n[blockIdx.x] = cnt < CH_HCAP ? cnt : CH_HCAP;
-        A.chh_tr[blockIdx.x] = covered < b1 ? (int32_t)covered : INT32_MAX;
+        // (a window that stops before the target's end: the block holding its end reports it as
+        // not covered, so the step ends the generation there)
+        const bool cut = covered >= b1 && b0 < b1 && b1 == end && end < lastk1;
+        A.chh_tr[blockIdx.x] = covered < b1 ? (int32_t)covered : cut ? (int32_t)end : INT32_MAX;
     }
 }
 
@@ -1291,7 +1303,17 @@ __global__ __launch_bounds__(64) void k_chain_step(WalkPtrs A) {
     bool gen_end = false;
     int64_t hits = 0;         // band hits of this generation
     int64_t visited = 0;      // of which the step visited
-    for (int b = 0; b < CH_GRID && !gen_end && !reason; b++) {
+    // skip the leading blocks without hits and without a cut (their hit counts read at once, 8 per
+    // lane, instead of one dependent pair of loads per block)
+    int bstart = CH_GRID;
+    static_assert(CH_GRID % 64 == 0, "blocks per lane");
+    for (int i = 0; i < CH_GRID / 64; i++) {
+        const int b = lane * (CH_GRID / 64) + i;
+        if ((A.chh_n[b] > 0 || A.chh_tr[b] != INT32_MAX) && b < bstart) bstart = b;
+    }
+    bstart = wave_min(bstart);
+    if (bstart > 0 && lane == 0) A.chs[11] = 0;   // (what block 0, without hits or a cut, does below)
+    for (int b = bstart; b < CH_GRID && !gen_end && !reason; b++) {
         const int32_t nh = A.chh_n[b], tr = A.chh_tr[b];
         hits += nh;
         const int32_t* hy = A.chh_y + (size_t)b * CH_HCAP;

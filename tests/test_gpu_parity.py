@@ -271,6 +271,32 @@ def test_token_copy_alignments(ctx, seed):
     assert ctx.reconstruct(rec, rfa) == oraclelib.decompress(rec, rfa)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_token_dense_blocks(ctx, seed):
+    """Record lines whose 4 KiB output blocks hold hundreds of tokens of length 0..3 (the fused
+    formatter stages up to 128 tokens per block in LDS and searches the global table beyond that),
+    mixed with N / lowercase runs and literals, against the oracle (decompression.cpp:210-274)."""
+    rng = random.Random(900 + seed)
+    ref = "".join(rng.choice("ACGT") for _ in range(5_000))
+    rfa = fuzzgen.to_fasta(ref)
+    toks, prev, dec_len = [], 0, 0
+    for _ in range(20_000):
+        if rng.random() < 0.1:
+            lit = rng.choice("ACGT") * rng.randint(1, 3)
+            toks.append(lit)
+            dec_len += len(lit)
+        else:
+            ln = rng.randint(0, 3)
+            p = rng.randint(0, len(ref) - ln)
+            toks.append(f"({p - prev},{ln})")
+            prev = p
+            dec_len += ln
+    lower = f"(100,{dec_len // 3})" if seed else ""
+    nline = "(50,7)" if seed == 2 else ""
+    rec = (f"{lower}\n{nline}\n" + "".join(toks)).encode()
+    assert ctx.reconstruct(rec, rfa) == oraclelib.decompress(rec, rfa)
+
+
 _RUN_LINE_CASES = {
     "empty_lines": b"\n\n(0,10)", "one_n": b"\n(5,3)\n(0,10)", "lower_and_n": b"(2,4)\n(5,3)\n(0,10)AC",
     "n_tail": b"\n(10,2)\n(0,10)", "n_past": b"\n(20,5)\n(0,3)", "lower_singleton": b"7\n\n(0,10)",
