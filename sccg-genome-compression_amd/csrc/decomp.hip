@@ -622,7 +622,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restr
     }
 }
 
-// Token table of the fused reconstruction (the default): instead of copying bytes into a decoded
+// Token table of the fused reconstruction (opt-in, SCCG_DC_FUSED=1): instead of copying bytes into a decoded
 // buffer that the formatter reads back (k_tok_fill2), one wave per 64-byte block writes each token's
 // decoded offset o, absolute reference position p, length l and the record offset r right after its
 // ')' (decompression.cpp:210-236).  Entry 0 is a sentinel (0, 0, 0, 0) for the literals before the
@@ -1038,7 +1038,124 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fused reconstruction formatter (the default): k_format_out with the block's decoded bytes expanded
+// Pipelined formatter (opt-in, SCCG_FMT_PIPE=1): a resident grid (8 blocks per CU) walks the output tiles of
+// k_format_out, block b taking tiles b, b + G, b + 2G, ...; while it formats one tile from LDS the
+// loads of the next (its decoded words and runs, into registers) and the k_out_index row of the one
+// after are in flight, so a tile costs max(format, memory) instead of two dependent HBM round trips
+// plus the format (k_format_out: 62 k blocks in ~30 generations, ~9 us each for chr1).  Two LDS
+// buffers alternate; tiles touching more than PRUNS runs of a kind read that run list from global.
+// ---------------------------------------------------------------------------------------------
+constexpr int PRUNS = 128;
+
+struct PipeRegs {
+    uint32_t w[5];
+    int32_t ns, ne, ls, le;
+    int64_t nb;
+};
+
+struct PipeTile {
+    int64_t d0, d1, a0, nw, n_lo, n_hi, l_lo, l_hi;
+    bool lds;
+    __device__ PipeTile(const int64_t* r, int64_t nn, int64_t nlr) {
+        d0 = r[0];
+        d1 = r[TW];
+        a0 = d0 & ~(int64_t)3;
+        nw = (d1 - a0 + 3) >> 2;
+        n_lo = r[1];
+        n_hi = r[TW + 1] < nn ? r[TW + 1] + 1 : nn;
+        l_lo = r[2];
+        l_hi = r[TW + 2] < nlr ? r[TW + 2] + 1 : nlr;
+        lds = n_hi - n_lo <= PRUNS && l_hi - l_lo <= PRUNS;
+    }
+};
+
+__device__ __forceinline__ void pipe_load(const PipeTile& T, const uint8_t* __restrict__ dec, const int32_t* __restrict__ ns,
+                                          const int32_t* __restrict__ nl, const int64_t* __restrict__ ncum,
+                                          const int32_t* __restrict__ ls, const int32_t* __restrict__ ll, int tid, PipeRegs& R) {
+    const uint32_t* decw = reinterpret_cast<const uint32_t*>(dec + T.a0);
+#pragma unroll
+    for (int q = 0; q < 5; q++) R.w[q] = tid + 256 * q < T.nw ? decw[tid + 256 * q] : 0u;
+    if (T.lds) {
+        const int64_t rn = T.n_lo + tid, rl = T.l_lo + tid;
+        if (rn < T.n_hi) { R.ns = ns[rn]; R.ne = R.ns + nl[rn]; R.nb = ncum[rn]; }
+        if (rl < T.l_hi) { R.ls = ls[rl]; R.le = R.ls + ll[rl]; }
+    }
+}
+
+__device__ __forceinline__ void pipe_store(const PipeTile& T, const PipeRegs& R, int tid, uint32_t* sdec, int32_t* sns,
+                                           int32_t* sne, int64_t* snb, int32_t* sls, int32_t* sle) {
+#pragma unroll
+    for (int q = 0; q < 5; q++)
+        if (tid + 256 * q < T.nw) sdec[tid + 256 * q] = R.w[q];
+    if (T.lds) {
+        if (T.n_lo + tid < T.n_hi) { sns[tid] = R.ns; sne[tid] = R.ne; snb[tid] = R.nb; }
+        if (T.l_lo + tid < T.l_hi) { sls[tid] = R.ls; sle[tid] = R.le; }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_format_pipe(const uint8_t* __restrict__ dec, int64_t nres, int64_t total, int64_t o_first,
+                                                     int64_t nblk, const int32_t* __restrict__ ns, const int32_t* __restrict__ nl,
+                                                     const int64_t* __restrict__ ncum, int64_t nn,
+                                                     const int32_t* __restrict__ ls, const int32_t* __restrict__ ll,
+                                                     int64_t nlr, const int64_t* __restrict__ tab, uint8_t* __restrict__ out) {
+    static_assert(5 * 256 >= OB / 4 + 2, "five words per thread cover a tile's decoded bytes");
+    __shared__ uint32_t sdec[2][OB / 4 + 4];
+    __shared__ int32_t s_ns[2][PRUNS], s_ne[2][PRUNS], s_ls[2][PRUNS], s_le[2][PRUNS];
+    __shared__ int64_t s_nb[2][PRUNS];
+    __shared__ int64_t st[3][2 * TW];
+    const int tid = threadIdx.x;
+    const int64_t G = gridDim.x, b0 = blockIdx.x;
+    if (b0 >= nblk) return;
+    const int64_t ntot = nn ? ncum[nn - 1] + nl[nn - 1] : 0;
+    if (tid < 2 * TW) {
+        st[0][tid] = tab[TW * b0 + tid];
+        if (b0 + G < nblk) st[1][tid] = tab[TW * (b0 + G) + tid];
+    }
+    __syncthreads();
+    PipeRegs R{};
+    {
+        const PipeTile T(st[0], nn, nlr);
+        pipe_load(T, dec, ns, nl, ncum, ls, ll, tid, R);
+        pipe_store(T, R, tid, sdec[0], s_ns[0], s_ne[0], s_nb[0], s_ls[0], s_le[0]);
+    }
+    __syncthreads();
+    for (int64_t i = 0;; i++) {
+        const int64_t bc = b0 + i * G;
+        if (bc >= nblk) break;
+        const int cur = (int)(i & 1), nxt = cur ^ 1;
+        const bool has_next = bc + G < nblk;
+        // the next tile's loads and the row after it, in flight while this tile is formatted
+        int64_t tv = 0;
+        if (has_next) {
+            const PipeTile Tn(st[(i + 1) % 3], nn, nlr);   // (rebuilt from LDS after the format: fewer live registers)
+            pipe_load(Tn, dec, ns, nl, ncum, ls, ll, tid, R);
+            if (tid < 2 * TW && bc + 2 * G < nblk) tv = tab[TW * (bc + 2 * G) + tid];
+        }
+        {
+            const PipeTile T(st[i % 3], nn, nlr);
+            const uint8_t* sd = reinterpret_cast<const uint8_t*>(sdec[cur]);
+            const int64_t o0 = o_first + bc * OB + (int64_t)tid * OPT;
+            if (T.lds) {
+                const LdsRuns N{s_ns[cur], s_ne[cur], s_nb[cur]}, L{s_ls[cur], s_le[cur], nullptr};
+                format_out16(o0, total, nres, sd, T.a0, N, T.n_hi - T.n_lo, ntot, L, T.l_hi - T.l_lo, out);
+            } else {
+                const GlobalRunsAt N{ns, nl, ncum, T.n_lo}, L{ls, ll, nullptr, T.l_lo};
+                format_out16(o0, total, nres, sd, T.a0, N, T.n_hi - T.n_lo, ntot, L, T.l_hi - T.l_lo, out);
+            }
+        }
+        if (!has_next) break;
+        __syncthreads();   // buffer nxt (tile i - 1's) and row (i + 2) % 3 (= (i - 1) % 3) are free
+        {
+            const PipeTile Tn(st[(i + 1) % 3], nn, nlr);
+            pipe_store(Tn, R, tid, sdec[nxt], s_ns[nxt], s_ne[nxt], s_nb[nxt], s_ls[nxt], s_le[nxt]);
+        }
+        if (tid < 2 * TW) st[(i + 2) % 3][tid] = tv;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused reconstruction formatter (opt-in, SCCG_DC_FUSED=1): k_format_out with the block's decoded bytes expanded
 // from the token table instead of read from a decoded buffer -- the tokens the block touches
 // (k_out_index entries t_b .. t_b+1) are staged in LDS beside its runs, then each thread gathers 16
 // decoded bytes (a token's R' bytes with five dword loads, else bytes from R' / the record's
@@ -1407,6 +1524,31 @@ int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns
         if (wait_before) SCCG_HIP(hipStreamWaitEvent(s, wait_before, 0));
         if (fz) {
             PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_fused, dim3((unsigned)nblk), dim3(256), 0, s, *fz, nres, total, o_first,
+                        (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
+                        (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out);
+            SCCG_HIP(hipGetLastError());
+            return 0;
+        }
+        // (SCCG_FMT_PIPE=1, A/B runs: the resident pipelined grid; measured slower)
+        static const bool pipe = getenv("SCCG_FMT_PIPE") != nullptr;
+        if (pipe) {
+            static const int cus = [] {
+                int dev = 0, n = 0;
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+                return n > 0 ? n : 256;
+            }();
+            // resident blocks only (every block walks the same number of tiles: a second generation
+            // of blocks would double the time)
+            static const int per_cu = [] {
+                const char* e = getenv("SCCG_FMT_PIPE_BPC");
+                if (e && atoi(e) > 0) return atoi(e);
+                int n = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_format_pipe, 256, 0) != hipSuccess || n <= 0) n = 4;
+                return n;
+            }();
+            const int64_t g = (int64_t)cus * per_cu < nblk ? (int64_t)cus * per_cu : nblk;
+            PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_pipe, dim3((unsigned)g), dim3(256), 0, s, d_dec, nres, total, o_first, nblk,
                         (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
                         (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out);
             SCCG_HIP(hipGetLastError());

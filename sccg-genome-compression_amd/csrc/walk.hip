@@ -86,10 +86,16 @@ constexpr int32_t CAND_CAP = 65536;  // early sweep: first-k-mer occurrences kep
 #endif
 constexpr int CH_BAND = SCCG_CH_BAND;   // band half-width (reference positions around P)
 constexpr int CH_TBITS = CH_BAND <= 2048 ? 13 : 14;   // band key table: 8192 / 16384 LDS slots (load <= 1/2)
-constexpr int CH_GRID = 512;           // scan blocks (1024 threads, 16 positions each per step)
+#ifndef SCCG_CH_GRID
+#define SCCG_CH_GRID 512
+#endif
+constexpr int CH_GRID = SCCG_CH_GRID;  // scan blocks (1024 threads, 16 positions each per step)
 constexpr int CH_HCAP = 4096;          // band hits kept per block and generation
 constexpr int32_t CHAIN_MCAP = 1 << 22;   // matches a chain may take
-constexpr int CH_GENS_PER_SYNC = 4;    // generations queued per host check
+#ifndef SCCG_CH_GENS_PER_SYNC
+#define SCCG_CH_GENS_PER_SYNC 4
+#endif
+constexpr int CH_GENS_PER_SYNC = SCCG_CH_GENS_PER_SYNC;    // generations queued per host check
 #ifndef SCCG_CH_FF_SPAN
 #define SCCG_CH_FF_SPAN (32 * 1024)
 #endif
@@ -627,7 +633,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     // walks it from that exit and carries on from chunk to chunk in one wave: a run of chunks whose
     // speculation failed is then walked in one round, not one round per chunk.  (The loop below
     // only iterates in the carry instantiation, so the main walk's registers stay as they were.)
-    for (int carried = CARRY ? 1 : 0;; carried++) {
+    for (;;) {
     while (x < scan_end) {
         if (x >= budget_end) { truncated = true; break; }
         if (DBG) tick(9);
