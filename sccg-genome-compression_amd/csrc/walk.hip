@@ -36,6 +36,7 @@ constexpr int WPB = 4;                 // chunks (waves) per block
 constexpr int WWPB = SCCG_WALK_WPB;
 constexpr int WCAP = 256;              // window positions held in LDS (2m+1 <= WCAP)
 constexpr int32_t INVALID = INT32_MIN;
+constexpr int32_t NEVER = INT32_MIN + 1;   // usedX of a chunk never walked: differs from every state
 constexpr int ANCHOR_K = 32;
 // Walk keys are exact 2-bit codes of at most KEY_K bases (common.h).  For k > KEY_K (a non-parity
 // parameter override; the reference hard-codes k = 14, compression.cpp:373) every key is the code of
@@ -96,6 +97,7 @@ constexpr int32_t CHAIN_MCAP = 1 << 22;   // matches a chain may take
 #define SCCG_CH_GENS_PER_SYNC 4
 #endif
 constexpr int CH_GENS_PER_SYNC = SCCG_CH_GENS_PER_SYNC;    // generations queued per host check
+constexpr int FF_MIN_CHUNKS = 8;       // frozen-first start: chunk 0's walk stuck for at least this many chunks
 #ifndef SCCG_CH_FF_SPAN
 #define SCCG_CH_FF_SPAN (32 * 1024)
 #endif
@@ -522,6 +524,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     const int32_t lastk = A.nT - A.k;
 
     int32_t x, P, n = 0, q = 0, ob, cb = -1, cc = 0;
+    bool first_spec = false;
     if (CARRY) {   // entry: the predecessor's staged exit (k_commit has not run yet)
         cb = uni(A.cur[j]);
         ob = 1 - cb;
@@ -531,7 +534,10 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     } else if (kind == KIND_SPEC) {
         ob = uni(A.cur[j]);
         x = lo_j;
-        if (A.round == 1) {   // first guess: the anchor vote at the chunk start (anchor_diag)
+        // a chunk's first speculation (round 1, or the round after a frozen-first round 1 that
+        // walked chunk 0 alone): guess from the anchors, re-seed a stuck guess
+        first_spec = uni(A.usedX[j]) == NEVER;
+        if (first_spec) {   // first guess: the anchor vote at the chunk start (anchor_diag)
             int32_t d = anchor_diag(A, lo_j);
             // no vote there (an indel, N run or diverged copy under the 128 probes): vote further
             // into the chunk.  A chunk left without a guess costs a whole serial re-walk next round
@@ -659,7 +665,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
             x = (x + 64 < scan_end) ? x + 64 : scan_end;
             if (x < scan_end) {
                 int32_t wend = budget_end;
-                if (kind == KIND_SPEC && A.round == 1) {   // re-seed a stuck first guess (see RESEED_GAP)
+                if (first_spec) {   // re-seed a stuck first guess (see RESEED_GAP)
                     if (x - (lme > seed_x ? lme : seed_x) >= RESEED_GAP) {
                         seed_x = x;
                         const int32_t d = anchor_diag(A, x);
@@ -979,7 +985,6 @@ __device__ void frozen_apply_wave(const WalkPtrs& A, int fbase, int fcap, int32_
 // Chunk state before round 1: no trajectory, no exit, never walked; round 1 takes every chunk,
 // chunk 0 exact (a fix-up from the first match's end, with an empty trajectory), the others
 // speculative.
-constexpr int32_t NEVER = INT32_MIN + 1;   // "no entry used yet": differs from every state
 // DEV: the start state comes from the first-step statistics in fc (the usual case: the target's
 // first k-mer has candidates, compression.cpp:64-161 with pme == -1); when they say otherwise,
 // chunk 0 gets no entry (its walk is a no-op) and the host redoes the first step and the init.
@@ -1019,6 +1024,20 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
         A.scal[11] = 0;  // carry list
         A.snapX[0] = startX;
         A.snapP[0] = startP;
+    }
+}
+
+// Frozen-first start (host first step, chunk 0 literal-only for >= FF_MIN_CHUNKS chunks): round 1
+// walked chunk 0 alone and the frozen chain settled the stuck stretch after it; every chunk still
+// never walked (and not already listed) now gets its first speculation in round 2 -- the chunks of
+// the stuck stretch are never speculated onto the true alignment that the stuck walk never takes.
+__global__ void k_spec_rest(WalkPtrs A) {
+    const int32_t next = A.round + 1;
+    for (int32_t q = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); q < A.C; q += (int32_t)(gridDim.x * blockDim.x)) {
+        if (A.usedX[q] != NEVER || A.lround[q] == next) continue;
+        A.kind[q] = KIND_SPEC;
+        A.lround[q] = next;
+        A.plist[atomicAdd(&A.scal[0], 1)] = q;
     }
 }
 
@@ -2871,10 +2890,36 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         hipLaunchKernelGGL(k_walk_init<false>, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s,
                            A, startX, startP);
     SCCG_HIP(hipGetLastError());
+    // Frozen-first (host first step only): when the walk from the first match finds no window hit
+    // for FF_MIN_CHUNKS chunks (a stuck walk: T2T-like pairs), round 1 walks chunk 0 alone, the frozen
+    // chain takes the stuck stretch, and the other chunks are speculated in round 2 (k_spec_rest) --
+    // instead of speculating every chunk of the stuck stretch onto an alignment the walk never takes.
+    // The probe is k_frozen_scan on a stand-in entry (chunk 0's exit = the start state), reset after.
+    static const bool ff_env = getenv("SCCG_NO_FROZEN_FIRST") == nullptr;
+    bool frozen_first = false;
+    if (ff_env && !pre_round && startP != INVALID && lastk >= 0 && A.C >= 2 * FF_MIN_CHUNKS) {
+        RC(dev_set_i32(A.flist, 1, {0}, s));
+        RC(dev_set_i32(A.exitX, 1, {startX}, s));
+        RC(dev_set_i32(A.exitP, 1, {startP}, s));
+        RC(dev_set_i32(A.scal + 5, 1, {1}, s));
+        RC(dev_set_i32(A.fy, 1, {INT32_MAX}, s));
+        hipLaunchKernelGGL(k_frozen_scan, dim3(256, 1), dim3(SCCG_BLOCK), 0, s, A, 0);
+        SCCG_HIP(hipGetLastError());
+        int32_t y0 = INT32_MAX;
+        {
+            const RbItem it{A.fy, &y0, (int)sizeof y0};
+            RC(dev_readback(&it, 1, s));
+        }
+        RC(dev_set_i32(A.exitX, 1, {INVALID}, s));
+        RC(dev_set_i32(A.exitP, 1, {INVALID}, s));
+        RC(dev_set_i32(A.scal + 5, 1, {0}, s));
+        frozen_first = (int64_t)y0 >= (int64_t)FF_MIN_CHUNKS * A.S;
+        if (dbgp) fprintf(stderr, "[walk] frozen-first probe: first window hit %d -> %s\n", y0, frozen_first ? "on" : "off");
+    }
 
     if (startP != INVALID && lastk >= 0) {
         mark("anchors");
-        int32_t nlist = A.C;
+        int32_t nlist = frozen_first ? 1 : A.C;   // (k_walk_init listed chunk j at plist[j])
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
         static const bool chains_env = getenv("SCCG_NO_CHAINS") == nullptr;   // (A/B and tests)
         bool chains_on = chains_env;   // off for the rest of the call after a trapped chain
@@ -3092,6 +3137,12 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                     SCCG_HIP(hipStreamSynchronize(s));
                     for (int q = 0; q < nshow; q++) fprintf(stderr, "      m%d (%d,%d,%d)\n", q, tt[q], pp[q], ll[q]);
                 }
+            }
+            if (frozen_first && round == 1) {   // first speculation of every chunk still never walked
+                hipLaunchKernelGGL(k_spec_rest, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A);
+                SCCG_HIP(hipGetLastError());
+                const RbItem it{A.scal, &nlist, (int)sizeof nlist};
+                RC(dev_readback(&it, 1, s));
             }
             if (round == 2 && spec_text && nlist == 0) text_done = true;
             if (!nlist) break;
