@@ -190,6 +190,9 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--contexts", type=int, default=2, help="library contexts (host threads) per GPU")
+    ap.add_argument("--queue", choices=["lpt", "twoend"], default="lpt",
+                    help="pair order over the contexts: largest first onto the first free context (lpt), or "
+                         "even contexts from the largest end and odd ones from the smallest (twoend)")
     ap.add_argument("--hw-queues", type=int, default=HW_QUEUES_DEFAULT,
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--workload", choices=["genome", "chr1"], default="genome",
@@ -270,8 +273,9 @@ def main() -> None:
 
     # persistent lane threads: a step releases them through one barrier and joins them at another
     # (no thread start per step)
-    nxt = [0]
+    nxt = [0, len(order) - 1]   # next from the largest end, next from the smallest end
     qlock = threading.Lock()
+    lane_idx = {id(ln): i for i, ln in enumerate(lanes)}
     go = threading.Barrier(n_lanes + 1)
     done = threading.Barrier(n_lanes + 1)
     stop = [False]
@@ -283,12 +287,17 @@ def main() -> None:
             if stop[0]:
                 return
             try:
+                small_end = args.queue == "twoend" and lane_idx[id(lane)] % 2 == 1
                 while True:
                     with qlock:
-                        if nxt[0] >= len(order):
+                        if nxt[0] > nxt[1]:
                             break
-                        name = order[nxt[0]]
-                        nxt[0] += 1
+                        if small_end:
+                            name = order[nxt[1]]
+                            nxt[1] -= 1
+                        else:
+                            name = order[nxt[0]]
+                            nxt[0] += 1
                     dr, rn, dt_, tn = pairs[name]
                     n = lane.ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, lane.out.data_ptr(), lane.cap,
                                                  lane.stream.cuda_stream)
@@ -308,7 +317,7 @@ def main() -> None:
         t.start()
 
     def run_shard() -> None:
-        nxt[0] = 0
+        nxt[0], nxt[1] = 0, len(order) - 1
         go.wait()
         done.wait()
         if errors:
@@ -482,7 +491,7 @@ def main() -> None:
             "config": {"workload": wl, "chromosomes": len(jobs), "pairs_rank0": len(order),
                        "target_bases": job["target_bases"], "reference_bases": job["reference_bases"],
                        "k": 14, "m": 100, "params": "reference constants (compression.cpp:373-379), local controller on",
-                       "contexts_per_gpu": n_lanes, "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                       "contexts_per_gpu": n_lanes, "pair_queue": args.queue, "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "parallelism": f"LPT chromosome shard x{world}, RCCL gather of record streams to rank 0",
                        "record_bytes": job["record_bytes"]},
             "roofline": roof,
