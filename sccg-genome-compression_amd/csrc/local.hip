@@ -663,9 +663,11 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
         // Fewer resident blocks per CU than fit (4) leave room for the global walk's preparation and
         // round 1, which otherwise wait for the whole pass (it fills every CU's VGPRs and LDS).
         // Measured (blocks/CU 4 / 3 / 2): whole genome on 1 GPU 28.5 / 27.3 / 27.2 ms, chr1 pair
-        // 1.57 / 1.55 / 1.54 ms, local-mode pair 2.84 / 2.90 / 2.97 ms.  SCCG_LOCAL_BPC overrides.
+        // 1.57 / 1.55 / 1.54 ms, local-mode pair 2.84 / 2.90 / 2.97 ms.  Round 3, genome with two
+        // contexts (3 / 2, interleaved, 8 pairs of runs, profiles/r03/local_bpc_ab*): 2 faster in 6 of
+        // 8, medians 22.5-24.1 vs 22.3-22.4 ms -- 2 is the default.  SCCG_LOCAL_BPC overrides.
         const char* e = getenv("SCCG_LOCAL_BPC");
-        const int bpc = e ? atoi(e) : 3;
+        const int bpc = e ? atoi(e) : 2;
         if (bpc >= 1 && bpc < per) per = bpc;
         return (unsigned)(cus * per);
     }();
