@@ -6,6 +6,7 @@ gets them instead.  `make -C oracle sanitize` builds oracle/_san/sccg_oracle wit
 reference) runs through it -- compression and decompression -- and must give the reference's bytes
 and exit code with no sanitizer report.
 """
+import fcntl
 import os
 import subprocess
 
@@ -19,7 +20,11 @@ SAN = os.path.join(REPO, "oracle", "_san", "sccg_oracle")
 
 @pytest.fixture(scope="module")
 def san_bin():
-    r = subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "sanitize"], capture_output=True, text=True)
+    # pytest-xdist workers each build the fixture: serialise the make so none runs the binary while
+    # another relinks it
+    with open(os.path.join(REPO, "oracle", ".san.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "sanitize"], capture_output=True, text=True)
     if r.returncode != 0 or not os.path.exists(SAN):
         pytest.skip("sanitizer build unavailable: " + r.stderr[-300:])
     return SAN
