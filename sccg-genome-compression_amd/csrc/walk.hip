@@ -98,6 +98,13 @@ constexpr int32_t CHAIN_MCAP = 1 << 22;   // matches a chain may take
 #endif
 constexpr int CH_GENS_PER_SYNC = SCCG_CH_GENS_PER_SYNC;    // generations queued per host check
 constexpr int FF_MIN_CHUNKS = 8;       // frozen-first start: chunk 0's walk stuck for at least this many chunks
+// A frozen-first (stuck, literal-heavy: T2T-like) target is walked in chunks of FF_CHUNK bases: its
+// divergent stretches hold ~400 short matches per 16 Ki chunk, each a latency-bound walk step, so
+// the round's slowest chunks set the walk.  Measured on the 100 Mb T2T-like pair (chunk 4 / 6 / 8 /
+// 12 / 16 Ki: 15.7 / 8.8 / 8.1 / 9.3 / 10.5 ms, sha unchanged); hg-like pairs keep the size rule
+// (the whole genome at 8 Ki took 160 ms: their well-speculated chunks gain nothing from splitting
+// and poorly-speculated ones multiply).
+constexpr int FF_CHUNK = 8192;
 #ifndef SCCG_CH_FF_SPAN
 #define SCCG_CH_FF_SPAN (32 * 1024)
 #endif
@@ -2532,6 +2539,11 @@ int resolve_escalations(WalkPtrs& A, hipStream_t s, std::vector<int32_t>* resume
 size_t walk_workspace_bytes(int64_t nR, int64_t nT, int k, int chunk) {
     size_t used = 0;
     carve(nullptr, 0, nullptr, nR, nullptr, nT, k, 100, chunk, &used);
+    if (chunk > FF_CHUNK) {   // room for a frozen-first walk re-chunked to FF_CHUNK
+        size_t used2 = 0;
+        carve(nullptr, 0, nullptr, nR, nullptr, nT, k, 100, FF_CHUNK, &used2);
+        if (used2 > used) used = used2;
+    }
     return used + 4096;
 }
 
@@ -2695,9 +2707,23 @@ int global_prepare(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
     return 0;
 }
 
-int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
-                          void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
-                          bool abs_p, const EmitTarget* late_out, bool keep_flat) {
+namespace {
+// A frozen-first walk found at a chunk size above FF_CHUNK is restarted at FF_CHUNK (a fresh call on
+// the same workspace: the carve, the preparation and every chunk's state are laid out again).  The
+// restart keeps what the first attempt learned or handed out: the exact first step, the caller's
+// resolved text position (EmitTarget::resolve is called once per compress) and round1_queued.
+constexpr int WALK_RECHUNK = -2;
+struct Rechunk {
+    bool on = false;                        // this is the restart
+    bool resolved = false;                  // late_out->resolve was called: its output pointer
+    uint8_t* out = nullptr;
+    bool r1 = false;                        // late_out->round1_queued was called
+    int32_t first_y = 0, first_p = 0, first_l = 0;
+};
+
+int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
+                        void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
+                        bool abs_p, const EmitTarget* late_out, bool keep_flat, Rechunk* rt) {
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
     const Prepared g = g_prep;   // queued by global_prepare (the caller ordered s after it)
     g_prep = Prepared{};
@@ -2756,12 +2782,15 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     const bool dbg_rounds = getenv("SCCG_DEBUG") != nullptr;
     bool pre_round = false, spec_queued = false;
     int32_t rs_pre[6] = {};
-    if (walkable && dev_first && A.C > 0) {
+    if (walkable && dev_first && !rt->on && A.C > 0) {
         hipLaunchKernelGGL(k_walk_init<true>, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s,
                            A, 0, 0);
         A.round = 1;
         RC(queue_round(FROZEN_FIRST, false));
-        if (late_out && late_out->round1_queued) RC(late_out->round1_queued(late_out->user, s));
+        if (late_out && late_out->round1_queued && !rt->r1) {
+            rt->r1 = true;
+            RC(late_out->round1_queued(late_out->user, s));
+        }
         A.round = 2;
         RC(queue_round(FROZEN_FIRST, true));
         pre_round = true;
@@ -2772,7 +2801,15 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     bool resolved = false, spec_text = false, text_done = false;
     int64_t spec_r[2] = {0, 0};   // total chunk matches, text bytes
     auto resolve_out = [&]() -> int {
-        if (!resolved && late_out) RC(late_out->resolve(late_out->user, &out));
+        if (!resolved && late_out) {
+            if (rt->resolved) {
+                out = rt->out;
+            } else {
+                RC(late_out->resolve(late_out->user, &out));
+                rt->resolved = true;
+                rt->out = out;
+            }
+        }
         resolved = true;
         return 0;
     };
@@ -2799,7 +2836,11 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     };
 
     // ---- the exact first (ungated) step: first target position with any candidate
-    if (walkable) {
+    if (walkable && rt->on) {   // (a re-chunked restart: found by the first attempt)
+        first_y = rt->first_y;
+        first_p = rt->first_p;
+        first_l = rt->first_l;
+    } else if (walkable) {
         int32_t x0 = 0;
         unsigned long long r[9];   // fc[4..11]: first hit, first exotic, statistics of the batch's x0; fc[12]
         if (pre_round) {
@@ -2897,7 +2938,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     // The probe is k_frozen_scan on a stand-in entry (chunk 0's exit = the start state), reset after.
     static const bool ff_env = getenv("SCCG_NO_FROZEN_FIRST") == nullptr;
     bool frozen_first = false;
-    if (ff_env && !pre_round && startP != INVALID && lastk >= 0 && A.C >= 2 * FF_MIN_CHUNKS) {
+    if (ff_env && !pre_round && !rt->on && startP != INVALID && lastk >= 0 && A.C >= 2 * FF_MIN_CHUNKS) {
         RC(dev_set_i32(A.flist, 1, {0}, s));
         RC(dev_set_i32(A.exitX, 1, {startX}, s));
         RC(dev_set_i32(A.exitP, 1, {startP}, s));
@@ -2915,7 +2956,15 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
         RC(dev_set_i32(A.scal + 5, 1, {0}, s));
         frozen_first = (int64_t)y0 >= (int64_t)FF_MIN_CHUNKS * A.S;
         if (dbgp) fprintf(stderr, "[walk] frozen-first probe: first window hit %d -> %s\n", y0, frozen_first ? "on" : "off");
+        static const bool rechunk_env = getenv("SCCG_NO_RECHUNK") == nullptr;   // (A/B)
+        if (frozen_first && rechunk_env && A.S > FF_CHUNK) {
+            rt->first_y = first_y;
+            rt->first_p = first_p;
+            rt->first_l = first_l;
+            return WALK_RECHUNK;
+        }
     }
+    if (rt->on) frozen_first = true;   // (the first attempt's probe)
 
     if (startP != INVALID && lastk >= 0) {
         mark("anchors");
@@ -3197,7 +3246,7 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     g_last_n = nm;
 
     // ---- record text: literal gap + "(dp,l)" per match, then the tail literal
-    if (late_out) RC(late_out->resolve(late_out->user, &out));   // the caller's text position is known now
+    RC(resolve_out());   // the caller's text position is known now
     int64_t text = 0;
     int32_t tail_from = 0;
     if (nm > 0) {
@@ -3223,4 +3272,19 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     *out_len = text + (tail > 0 ? tail : 0);
     mark("emit");
     return 0;
+}
+
+}  // namespace
+
+int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
+                          void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
+                          bool abs_p, const EmitTarget* late_out, bool keep_flat) {
+    Rechunk rt;
+    const int rc = match_and_emit_impl(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, out, out_len, res, s, abs_p, late_out,
+                                       keep_flat, &rt);
+    if (rc != WALK_RECHUNK) return rc;
+    if (walk_workspace_bytes(nRp, nTp, k, FF_CHUNK) > ws_bytes) return SCCG_E_INTERNAL;
+    rt.on = true;
+    return match_and_emit_impl(Rp, nRp, Tp, nTp, k, m, FF_CHUNK, ws, ws_bytes, out, out_len, res, s, abs_p, late_out,
+                               keep_flat, &rt);
 }
