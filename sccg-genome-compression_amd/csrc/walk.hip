@@ -98,12 +98,13 @@ constexpr int32_t CHAIN_MCAP = 1 << 22;   // matches a chain may take
 #endif
 constexpr int CH_GENS_PER_SYNC = SCCG_CH_GENS_PER_SYNC;    // generations queued per host check
 constexpr int FF_MIN_CHUNKS = 8;       // frozen-first start: chunk 0's walk stuck for at least this many chunks
-// A frozen-first (stuck, literal-heavy: T2T-like) target is walked in chunks of FF_CHUNK bases: its
-// divergent stretches hold ~400 short matches per 16 Ki chunk, each a latency-bound walk step, so
-// the round's slowest chunks set the walk.  Measured on the 100 Mb T2T-like pair (chunk 4 / 6 / 8 /
-// 12 / 16 Ki: 15.7 / 8.8 / 8.1 / 9.3 / 10.5 ms, sha unchanged); hg-like pairs keep the size rule
-// (the whole genome at 8 Ki took 160 ms: their well-speculated chunks gain nothing from splitting
-// and poorly-speculated ones multiply).
+// SCCG_RECHUNK=1 (opt-in): a frozen-first (stuck, literal-heavy: T2T-like) target is walked again
+// in chunks of FF_CHUNK bases.  Its divergent stretches hold ~400 short matches per 16 Ki chunk,
+// each a latency-bound walk step, so the round's slowest chunks set the walk: the 100 Mb T2T-like
+// pair 10.4 -> 8.3 ms and 20 Mb pairs -20..-30 %.  But on the T2T-like whole genome (24 pairs at
+// UCSC lengths) the smaller chunks multiply the poorly-speculated ones that the rounds resolve one
+// by one: chr3 44 -> 231 ms (72 -> 323 rounds), chr6 33 -> 186 ms, genome 0.50 -> 0.86 s
+// (profiles/r03/rechunk_ab/) -- so the default keeps the size rule.
 constexpr int FF_CHUNK = 8192;
 #ifndef SCCG_CH_FF_SPAN
 #define SCCG_CH_FF_SPAN (32 * 1024)
@@ -2956,7 +2957,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         RC(dev_set_i32(A.scal + 5, 1, {0}, s));
         frozen_first = (int64_t)y0 >= (int64_t)FF_MIN_CHUNKS * A.S;
         if (dbgp) fprintf(stderr, "[walk] frozen-first probe: first window hit %d -> %s\n", y0, frozen_first ? "on" : "off");
-        static const bool rechunk_env = getenv("SCCG_NO_RECHUNK") == nullptr;   // (A/B)
+        static const bool rechunk_env = getenv("SCCG_RECHUNK") != nullptr;   // opt-in (see FF_CHUNK)
         if (frozen_first && rechunk_env && A.S > FF_CHUNK) {
             rt->first_y = first_y;
             rt->first_p = first_p;

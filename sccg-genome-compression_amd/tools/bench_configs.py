@@ -30,6 +30,10 @@ def main() -> None:
     ap.add_argument("--only", default="")
     ap.add_argument("--contexts", type=int, default=1,
                     help="genome: contexts (host threads) per GPU compressing chromosomes concurrently")
+    ap.add_argument("--genome-profile", default="hg", choices=["hg", "t2t"],
+                    help="genome: synthetic profile of the 24 pairs (t2t = BASELINE configs[4]'s shape at UCSC lengths)")
+    ap.add_argument("--roundtrip", action="store_true",
+                    help="genome: reconstruct every pair on the GPU and compare it with its target FASTA")
     args = ap.parse_args()
     import torch
     import sccg
@@ -102,8 +106,9 @@ def genome(ctx, dev, stream, args, to_dev) -> None:
     t0 = time.perf_counter()
     pairs = []
     for i, (rl, tl) in enumerate(zip(multigpu.HG18, multigpu.HG19)):
-        rfa, tfa = synth.synth_pair("hg", int(rl * args.scale), int(tl * args.scale), i + 1)
+        rfa, tfa = synth.synth_pair(args.genome_profile, int(rl * args.scale), int(tl * args.scale), i + 1)
         pairs.append((to_dev(rfa), len(rfa), to_dev(tfa), len(tfa)))
+        print(f"[genome] pair {i + 1}/24 generated ({time.perf_counter() - t0:.1f} s)", file=sys.stderr, flush=True)
         del rfa, tfa
     gen_s = time.perf_counter() - t0
     cap = max(ctx.compress_bound(r, t) for _, r, _, t in pairs)
@@ -163,9 +168,17 @@ def genome(ctx, dev, stream, args, to_dev) -> None:
         st = ctx.stats()
         per_s.append({"ms": round((time.perf_counter() - t1) * 1e3, 2), "rounds": st["walk_rounds"],
                       "switch": st["switch_segment"], "matches": st["n_matches"]})
+        if args.roundtrip:   # record -> FASTA on the GPU, compared with the target on the device
+            n_rec = ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, d_rec.data_ptr(), cap, stream)
+            need = ctx.reconstruct_device(dr.data_ptr(), rn, d_rec.data_ptr(), n_rec, 0, 0, stream)
+            d_fa = torch.empty(need + 64, dtype=torch.uint8, device=dev)
+            n_fa = ctx.reconstruct_device(dr.data_ptr(), rn, d_rec.data_ptr(), n_rec, d_fa.data_ptr(), need + 64, stream)
+            per_s[-1]["roundtrip_exact"] = bool(n_fa == tn and torch.equal(d_fa[:n_fa], dt_))
+            del d_fa
     for c in ctxs[1:]:
         c.close()
-    print(json.dumps({"workload": "hg19_vs_hg18_genome_1gpu", "contexts": len(ctxs), "chromosomes": len(pairs), "target_bases": bases,
+    wl = "hg19_vs_hg18_genome_1gpu" if args.genome_profile == "hg" else "t2t_like_genome_1gpu"
+    print(json.dumps({"workload": wl, "roundtrip_all_exact": all(p.get("roundtrip_exact", False) for p in per_s) if args.roundtrip else None, "contexts": len(ctxs), "chromosomes": len(pairs), "target_bases": bases,
                       "record_bytes": rec_bytes, "seconds": best, "bases_per_s": bases / best,
                       "lpt_max_over_mean_8gpu": multigpu.max_over_mean(per, 8), "generate_seconds": gen_s,
                       "per_chromosome": dict(zip(multigpu.CHROMS, per_s))}),
