@@ -147,3 +147,26 @@ def test_poor_speculation_rounds_bounded():
     d = json.loads(out.stdout.strip().splitlines()[-1])
     assert d["sha"] == e["record_sha256"]
     assert d["rounds"] < 64, d
+
+
+def test_t2t_like_genome_roundtrip():
+    """BASELINE configs[4]'s shape: the 24 chromosome pairs with the T2T-like profile (the stuck,
+    literal-heavy path of compression.cpp:83-101), here at 1/8 of the UCSC lengths.  No reference
+    pins exist at this scale (the reference's stuck walk runs at ~2.5 Mbase/s), so the check is the
+    size-independent round trip: record -> FASTA on the GPU gives back every target byte for byte.
+    (The full-length genome is measured by tools/bench_configs.py --genome-profile t2t --roundtrip.)"""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "sccg-genome-compression_amd"))
+    import multigpu
+    c = sccg.Context(0)
+    try:
+        bad, rounds = [], {}
+        for i, (rl, tl) in enumerate(zip(multigpu.HG18, multigpu.HG19)):
+            rfa, tfa = synthlib.synth_pair("t2t", rl // 8, tl // 8, i + 1)
+            rec = _device_compress(c, rfa, tfa)
+            rounds[multigpu.CHROMS[i]] = c.stats()["walk_rounds"]
+            if c.reconstruct(rec, rfa) != tfa:
+                bad.append(multigpu.CHROMS[i])
+        assert not bad, (bad, rounds)
+        assert max(rounds.values()) < 1000, rounds
+    finally:
+        c.close()
