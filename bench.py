@@ -20,10 +20,15 @@ own host thread, so one pair's host round trips overlap another pair's kernels.
 
 Printed (rank 0): one JSON line.  value = the genome's target bases / max-over-ranks step time
 (strong scaling: the job is fixed, N GPUs share it); roofline of the dominant kernel (HIP events
-on the launching streams, SURVEY §8(d) algorithmic bytes) and of the whole job; the reference
-compression.cpp timed on this host on BASELINE configs[0] (the chr21 pair); the chr1 record
-stream reconstructed on the GPU (configs[3]); per-chromosome sha256 checked against the
-reference's, pinned in tests/golden/genome_manifest.json.
+on the launching streams, SURVEY §8(d) algorithmic bytes) and of the whole job (DESIGN.md §4's
+design model beside SURVEY §8(d)'s); the reference compression.cpp timed on this host on
+BASELINE configs[0] (the chr21 pair); the chr1 record stream reconstructed on the GPU
+(configs[3]); the T2T-like genome (configs[4]'s shape, 24 pairs at UCSC lengths); the whole
+genome from FASTA files to record files (with and without the 7z step); per-chromosome sha256
+checked against the reference's, pinned in tests/golden/genome_manifest.json.
+
+The distributed pieces (timed_region, gather_streams, job_totals, check_pins) take the process
+group from torch.distributed and are exercised with gloo on CPU by tests/test_bench_cpu.py.
 """
 from __future__ import annotations
 
@@ -45,6 +50,7 @@ sys.path.insert(0, PKG_DIR)
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "target bases compressed/sec at 1/2/4/8 GPUs; bit-exact record stream vs CPU ref"
 MANIFEST = os.path.join(REPO, "tests", "golden", "genome_manifest.json")
+CPU_BASELINE_N1 = os.path.join(REPO, "profiles", "cpu_baseline.json")   # the N = 1 line's measurement
 # GPU_MAX_HW_QUEUES for the run: 0 keeps the environment's (HIP's default, 4).  Measured on the
 # genome bench (profiles/r03_ab.txt): 2 contexts with 4 queues 24.1-24.5 ms per step, with 8 queues
 # 28.0-28.3 ms, 3 contexts with 8-12 queues 26.0-31.3 ms, 1 context 29.8-29.9 ms.
@@ -55,15 +61,36 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# ------------------------------------------------------------------------------------------------
+# algorithmic byte models
+# ------------------------------------------------------------------------------------------------
 def walk_alg_bytes(nT: int) -> float:
     """the walk's share of B_global, 0.5 B per target base (packed target + packed
     reference along the matches)."""
     return 0.5 * nT
 
 
-def job_alg_bytes(nT: int, nR: int, nRp: int, out: int) -> float:
-    """SURVEY §8(d) B_global = 1.25(|T|+|R|) + 0.25|R| + 4|R'| + 0.5|T| + |out|."""
+def survey_alg_bytes(nT: int, nR: int, nRp: int, out: int) -> float:
+    """SURVEY §8(d) B_global = 1.25(|T|+|R|) + 0.25|R| + 4|R'| + 0.5|T| + |out|.  Its 4|R'| term is
+    a CSR k-mer position index, which this design never builds."""
     return 1.25 * (nT + nR) + 0.25 * nR + 4.0 * nRp + 0.5 * nT + out
+
+
+def design_alg_bytes(tfa: int, rfa: int, nT: int, nR: int, nRp: int, out: int, mode_global: bool) -> float:
+    """What this design must move at least, per pair: both FASTA texts read once
+    and their stripped + N-erased copies written (ingest, compression.cpp:181-220, :523-557), T read
+    once for the run lines (:341-368, :527-555), R' read once by the first-step sweep (the exact
+    ungated first step, :64-161 with pme == -1), the walk's 0.5 B per target base,
+    and the record text written.  The local pass (compression.cpp:372-481) is counted only for the
+    segments of a pair that stays local (both segment strings once)."""
+    ingest = tfa + rfa + 2.0 * (nT + nR)
+    runs = float(nT)
+    b = ingest + runs + out
+    if mode_global:
+        b += nRp + walk_alg_bytes(nT)
+    else:
+        b += 2.0 * min(nT, nR)
+    return b
 
 
 def kernel_alg_bytes(kernel: str, tot: dict) -> float | None:
@@ -75,7 +102,7 @@ def kernel_alg_bytes(kernel: str, tot: dict) -> float | None:
     if kernel == "run_extract":          # T once
         return float(tot["target_bases"])
     if kernel == "first_sweep_anchors":  # R' once + one 8-byte anchor slot per 32 reference bases
-        return tot["reference_bases"] * (1.0 + 8.0 / 32.0)
+        return tot["walk_reference_bases"] * (1.0 + 8.0 / 32.0)
     if kernel == "local_segments":       # both segment strings (up to the switch, bounded by all of them)
         return 2.0 * min(tot["target_bases"], tot["reference_bases"])
     return None
@@ -86,6 +113,105 @@ def load_manifest() -> dict:
         return {e["name"]: e for e in json.load(open(MANIFEST))}
     except Exception:
         return {}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# ------------------------------------------------------------------------------------------------
+# distributed pieces (RCCL on the GPU box, gloo in tests/test_bench_cpu.py)
+# ------------------------------------------------------------------------------------------------
+def timed_region(step, steps: int, warmup: int, world: int, sync=lambda: None, device=None) -> float:
+    """W untimed steps, then exactly K steps between a barrier + device sync on both sides; the
+    MAX over ranks of the elapsed time (the job ends with its slowest rank)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def gather_streams(results: dict, order: list, world: int, device) -> dict | None:
+    """Every rank's per-chromosome record streams on rank 0 (multigpu.gather_records: one size
+    all-gather + one gather to rank 0); None on the other ranks."""
+    import multigpu
+    if world <= 1:
+        return {n: results[n][0].cpu().numpy().tobytes() for n in order}
+    return multigpu.gather_records({n: results[n][0] for n in order}, device=device)
+
+
+def job_totals(tot: dict, world: int) -> tuple[dict, list]:
+    """Per-rank totals summed over the ranks (all_gather_object), and the per-rank list."""
+    import torch.distributed as dist
+    totals = [tot]
+    if world > 1:
+        got = [None] * world
+        dist.all_gather_object(got, tot)
+        totals = got
+    return {k: sum(t[k] for t in totals) for k in tot}, totals
+
+
+def check_pins(streams: dict | None, pins: dict) -> dict | None:
+    """sha256 of each gathered record stream against the reference's pinned one (rank 0)."""
+    if streams is None:
+        return None
+    checked = [n for n in streams if n in pins]
+    bad = [n for n in checked if hashlib.sha256(streams[n]).hexdigest() != pins[n]["record_sha256"]]
+    return {"chromosomes": len(streams), "pinned_checked": len(checked), "pinned_mismatch": bad,
+            "reference": "oracle/_ref (compression.cpp compiled unchanged), tests/golden/genome_manifest.json"}
+
+
+def cpu_baseline_pointer() -> dict | None:
+    """N > 1 lines: the CPU baseline is measured by the N = 1 run only (rank 0, bounded sample);
+    repeat its committed value with a pointer to it."""
+    try:
+        doc = json.load(open(CPU_BASELINE_N1))
+    except Exception:
+        return None
+    out = dict(doc)
+    out["measured_in"] = os.path.relpath(CPU_BASELINE_N1, REPO) + " (the N = 1 bench line; not re-run at N > 1)"
+    return out
+
+
+def cpu_genome_estimate(cores: int | None = None) -> dict | None:
+    """The whole hg19-vs-hg18 genome on host cores, from the 24 reference walls in the manifest
+    (measured by tests/golden/pin_genome.py in the build container, concurrently under a RAM
+    budget): total CPU-seconds, single-core rate, and the LPT makespan over P cores."""
+    import multigpu
+    pins = load_manifest()
+    walls = [pins[n]["reference_wall_s"] for n in multigpu.CHROMS if n in pins and "reference_wall_s" in pins[n]]
+    if len(walls) < len(multigpu.CHROMS):
+        return None
+    nT = sum(multigpu.HG19)
+    P = cores or 8
+    loads = [sum(walls[i] for i in part) for part in multigpu.lpt_shard(walls, P)]
+    return {"cpu_seconds": round(sum(walls), 1), "target_bases": nT, "bases_per_s_one_core": nT / sum(walls),
+            "cores": P, "lpt_makespan_s": round(max(loads), 1), "bases_per_s_on_P_cores": nT / max(loads),
+            "note": "compiled reference (oracle/_ref, g++ -O2, stub 7z) walls from tests/golden/genome_manifest.json, "
+                    "measured in the build container (8x 'Intel(R) Xeon(R) Processor', 62 GB; pairs run concurrently "
+                    "under a 46 GB RAM budget); makespan = LPT of those walls over P cores, RAM permitting "
+                    "(chr1 alone needs 17.4 GB)"}
 
 
 def cpu_baseline(timeout_s: int) -> dict | None:
@@ -131,17 +257,9 @@ def cpu_baseline(timeout_s: int) -> dict | None:
     finally:
         shutil.rmtree(d, ignore_errors=True)
     pin = load_manifest().get("chr21", {}).get("record_sha256")
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
     return {"value": tl / dt, "unit": "target bases/s", "cores": 1, "kind": kind,
             "sample": f"BASELINE configs[0]: hg19-vs-hg18 chr21-sized synthetic pair |R|={rl:,} |T|={tl:,} (seed 21), "
-                      f"wall {dt:.1f} s, single-threaded ({cpu}), stub 7z, stdout to /dev/null",
+                      f"wall {dt:.1f} s, single-threaded ({cpu_model()}), stub 7z, stdout to /dev/null",
             "record_matches_pinned": (sha == pin) if pin else None}
 
 
@@ -184,15 +302,226 @@ class Lane:
         self.cap = cap
 
 
+class LanePool:
+    """Persistent lane threads: run(job) hands every lane the same pair queue (largest first onto
+    the first free lane) through one barrier and joins them at another (no thread start per step).
+    job(lane, name) does one pair on that lane."""
+
+    def __init__(self, lanes: list, dev):
+        import torch
+        self.lanes, self.dev = lanes, dev
+        self.go = threading.Barrier(len(lanes) + 1)
+        self.done = threading.Barrier(len(lanes) + 1)
+        self.lock = threading.Lock()
+        self.queue: list = []
+        self.job = None
+        self.errors: list = []
+        self.stop = False
+
+        def worker(lane):
+            torch.cuda.set_device(dev)
+            while True:
+                self.go.wait()
+                if self.stop:
+                    return
+                try:
+                    while True:
+                        with self.lock:
+                            if not self.queue:
+                                break
+                            name = self.queue.pop(0)
+                        self.job(lane, name)
+                except Exception as e:   # noqa: BLE001 -- reported after the step
+                    self.errors.append(e)
+                self.done.wait()
+
+        self.threads = [threading.Thread(target=worker, args=(ln,), daemon=True) for ln in lanes]
+        for t in self.threads:
+            t.start()
+
+    def run(self, order: list, job) -> None:
+        self.queue = list(order)
+        self.job = job
+        self.go.wait()
+        self.done.wait()
+        if self.errors:
+            raise self.errors[0]
+
+    def sync(self) -> None:
+        for ln in self.lanes:
+            ln.stream.synchronize()
+
+    def close(self) -> None:
+        self.stop = True
+        self.go.wait()
+        for t in self.threads:
+            t.join()
+
+
+def gen_pairs(jobs: list, profile: str, dev, keep_host: set) -> tuple[dict, dict, int, int]:
+    """Synthetic pairs (threads: the C generator releases the GIL), uploaded to HBM.  Returns
+    {name: (d_ref, |ref FASTA|, d_tgt, |tgt FASTA|)}, the host FASTA of the names in keep_host, and
+    the FASTA byte totals."""
+    import torch
+    import synth
+    host, lock = {}, threading.Lock()
+
+    def gen(job):
+        name, rl, tl, seed = job
+        rfa, tfa = synth.synth_pair(profile, rl, tl, seed)
+        with lock:
+            host[name] = (rfa, tfa)
+
+    ths = [threading.Thread(target=gen, args=(j,)) for j in jobs]
+    for b in range(0, len(ths), 8):
+        for t in ths[b:b + 8]:
+            t.start()
+        for t in ths[b:b + 8]:
+            t.join()
+    pairs = {}
+    for name, _, _, _ in jobs:
+        rfa, tfa = host[name]
+        pairs[name] = (torch.frombuffer(bytearray(rfa), dtype=torch.uint8).to(dev), len(rfa),
+                       torch.frombuffer(bytearray(tfa), dtype=torch.uint8).to(dev), len(tfa))
+    rb = sum(len(v[0]) for v in host.values())
+    tb = sum(len(v[1]) for v in host.values())
+    kept = {n: host[n] for n in keep_host if n in host}
+    host.clear()
+    return pairs, kept, rb, tb
+
+
+def device_job(pairs: dict, results: dict, dev):
+    """The pair job of a step: compress the HBM-resident pair on the lane and keep its record text."""
+    import torch
+
+    def job(lane, name):
+        dr, rn, dt_, tn = pairs[name]
+        n = lane.ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, lane.out.data_ptr(), lane.cap,
+                                     lane.stream.cuda_stream)
+        st = lane.ctx.stats()
+        prev = results.get(name)
+        with torch.cuda.stream(lane.stream):
+            buf = prev[0] if prev is not None and prev[0].numel() == n else torch.empty(n, dtype=torch.uint8, device=dev)
+            buf.copy_(lane.out[:n])   # the pair's record stream, kept for the gather (the step syncs)
+        results[name] = (buf, st)
+    return job
+
+
+def t2t_genome(pool: LanePool, jobs: list, world: int, rank: int, dev, steps: int) -> dict:
+    """BASELINE configs[4]'s shape: the same 24 UCSC length pairs with the T2T-like profile (the
+    stuck, literal-heavy walk of compression.cpp:83-101), each rank its LPT shard; one warm pass,
+    then `steps` timed passes (max over ranks); record sha256 against the reference's pins
+    (t2t_<chrom> in tests/golden/genome_manifest.json, tests/golden/pin_genome.py)."""
+    import torch
+    import multigpu
+    import torch.distributed as dist
+    t0 = time.perf_counter()
+    tj = [(f"t2t_{n}", rl, tl, seed) for n, rl, tl, seed in jobs]
+    pairs, _, _, _ = gen_pairs(tj, "t2t", dev, set())
+    gen_s = time.perf_counter() - t0
+    order = sorted(pairs, key=lambda n: -pairs[n][3])
+    results: dict = {}
+    job = device_job(pairs, results, dev)
+    def step():
+        pool.run(order, job)
+        pool.sync()
+
+    dt = timed_region(step, steps, 1, world, torch.cuda.synchronize, dev)
+    shas = {n: hashlib.sha256(results[n][0].cpu().numpy().tobytes()).hexdigest() for n in order}
+    per = {n: {"rounds": results[n][1]["walk_rounds"], "chains": results[n][1]["walk_chains"],
+               "matches": results[n][1]["n_matches"], "mode": "global" if results[n][1]["mode_global"] else "local"}
+           for n in order}
+    nT = sum(results[n][1]["target_bases"] for n in order)
+    if world > 1:
+        got = [None] * world
+        dist.all_gather_object(got, (shas, per, nT))
+        shas, per, nT = {}, {}, 0
+        for s_, p_, n_ in got:
+            shas.update(s_)
+            per.update(p_)
+            nT += n_
+    del pairs, results
+    torch.cuda.empty_cache()
+    pins = load_manifest()
+    checked = [n for n in shas if n in pins]
+    bad = [n for n in checked if shas[n] != pins[n]["record_sha256"]]
+    ms = dt / steps * 1e3
+    worst = max(per, key=lambda n: per[n]["rounds"]) if per else None
+    return {"workload": "BASELINE configs[4] shape: T2T-like profile (tandem arrays, 1e-2 SNPs, >100-bp deletions "
+                        "every ~100 kb) on the 24 hg18/hg19 UCSC length pairs, seed = chromosome index",
+            "target_bases": nT, "ms": ms, "bases_per_s": nT / (ms * 1e-3), "steps": steps,
+            "pinned_checked": len(checked), "pinned_mismatch": bad,
+            "max_rounds": per[worst]["rounds"] if worst else None, "max_rounds_chrom": worst,
+            "generate_s": round(gen_s, 1), "per_chromosome": per,
+            "lpt_max_over_mean_8gpu": multigpu.max_over_mean([j[2] for j in jobs], 8)}
+
+
+def end_to_end_genome(pool: LanePool, host_fa: dict, order: list, pins: dict, reps: int = 2) -> dict:
+    """The whole genome from FASTA files to record files (compression.cpp:181-331 per pair, 7z
+    excluded), every pair through sccg_compress_files on the lanes (two contexts: one pair's file
+    reads and PCIe copies overlap another's kernels), files in the page cache; then once more with
+    the reference's `7z a -mx=9` per pair started as soon as that pair's file is closed (genome.py's
+    Emitter overlap, compression.cpp:306-318), if 7z is installed on this host."""
+    import genome
+    d = tempfile.mkdtemp(prefix="sccg_e2eg_")
+    try:
+        fa_bytes = 0
+        for n in order:
+            rfa, tfa = host_fa[n]
+            os.makedirs(os.path.join(d, "ref"), exist_ok=True)
+            os.makedirs(os.path.join(d, "tgt"), exist_ok=True)
+            open(os.path.join(d, "ref", n + ".fa"), "wb").write(rfa)
+            open(os.path.join(d, "tgt", n + ".fa"), "wb").write(tfa)
+            fa_bytes += len(rfa) + len(tfa)
+        out = os.path.join(d, "out")
+        stats: dict = {}
+
+        def job_with(em):
+            def job(lane, name):
+                st = genome.compress_pair_files(lane.ctx, os.path.join(d, "ref", name + ".fa"),
+                                                os.path.join(d, "tgt", name + ".fa"), out, name, em)
+                stats[name] = st
+            return job
+
+        pool.run(order, job_with(None))   # warm (staging buffers)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            pool.run(order, job_with(None))
+            ts.append(time.perf_counter() - t0)
+        bad = [n for n in order if n in pins and hashlib.sha256(
+            open(os.path.join(out, n, "compressed_genome.txt"), "rb").read()).hexdigest() != pins[n]["record_sha256"]]
+        nT = sum(stats[n]["target_bases"] for n in order)
+        res = {"workload": "24 hg19-vs-hg18 pairs: FASTA files (page cache) -> <out>/<chrom>/compressed_genome.txt "
+                           "closed, 7z excluded (sccg_compress_files, 2 contexts)",
+               "target_bases": nT, "fasta_bytes": fa_bytes, "ms": min(ts) * 1e3, "ms_all": [round(t * 1e3, 1) for t in ts],
+               "bases_per_s": nT / min(ts), "host_to_file_GBps": fa_bytes / min(ts) / 1e9,
+               "pinned_checked": len([n for n in order if n in pins]), "pinned_mismatch": bad}
+        sz = shutil.which("7z")
+        if sz:
+            em = genome.Emitter(out, True, sz)
+            t0 = time.perf_counter()
+            pool.run(order, job_with(em))
+            t_gpu = time.perf_counter() - t0
+            rc = em.wait()
+            t_all = time.perf_counter() - t0
+            res["with_7z"] = {"ms": t_all * 1e3, "gpu_part_ms": t_gpu * 1e3, "bases_per_s": nT / t_all, "rc": rc,
+                              "7z": sz, "archive_bytes": sum(os.path.getsize(os.path.join(out, n, "compressed_genome.txt.7z"))
+                                                            for n in order if os.path.exists(os.path.join(out, n, "compressed_genome.txt.7z")))}
+        else:
+            res["with_7z"] = "7z is not installed on this host (no package index: it cannot be added); the 7z step "\
+                             "is the reference's `7z a -mx=9` and runs unchanged where 7z exists (genome.py Emitter)"
+        return res
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--contexts", type=int, default=2, help="library contexts (host threads) per GPU")
-    ap.add_argument("--queue", choices=["lpt", "twoend"], default="lpt",
-                    help="pair order over the contexts: largest first onto the first free context (lpt), or "
-                         "even contexts from the largest end and odd ones from the smallest (twoend)")
     ap.add_argument("--hw-queues", type=int, default=HW_QUEUES_DEFAULT,
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--workload", choices=["genome", "chr1"], default="genome",
@@ -202,7 +531,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the pinned sha256 checks")
     ap.add_argument("--no-decomp", action="store_true", help="skip the configs[3] reconstruction")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (files) measurement")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (files) measurements")
+    ap.add_argument("--no-t2t", action="store_true", help="skip the T2T-like genome (configs[4] shape)")
+    ap.add_argument("--t2t-steps", type=int, default=2)
     ap.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events in the timed region")
     args = ap.parse_args()
     if args.hw_queues > 0:
@@ -212,7 +543,6 @@ def main() -> None:
     import torch.distributed as dist
     import multigpu
     import sccg
-    import synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -233,33 +563,12 @@ def main() -> None:
         jobs = [(f"chr1_r{r}", multigpu.HG18[0], multigpu.HG19[0], 1 + r) for r in range(world)]
         mine = [jobs[rank]]
 
-    # ---- inputs: generated on the host (threads: the C generator releases the GIL), then resident
+    # ---- inputs: generated on the host, then resident in HBM
     t0 = time.perf_counter()
-    pairs: dict = {}
-    host_fa: dict = {}
-    lock = threading.Lock()
-
-    def gen(job):
-        name, rl, tl, seed = job
-        rfa, tfa = synth.synth_pair("hg", rl, tl, seed)
-        with lock:
-            host_fa[name] = (rfa, tfa)
-
-    ths = [threading.Thread(target=gen, args=(j,)) for j in mine]
-    nthr = 8
-    for b in range(0, len(ths), nthr):
-        for t in ths[b:b + nthr]:
-            t.start()
-        for t in ths[b:b + nthr]:
-            t.join()
-    for name, rl, tl, seed in mine:
-        rfa, tfa = host_fa[name]
-        pairs[name] = (torch.frombuffer(bytearray(rfa), dtype=torch.uint8).to(dev), len(rfa),
-                       torch.frombuffer(bytearray(tfa), dtype=torch.uint8).to(dev), len(tfa))
+    want_e2e_genome = args.workload == "genome" and not args.no_e2e
+    keep = {n for n, _, _, _ in mine} if want_e2e_genome else {"chr1", f"chr1_r{rank}"}
+    pairs, host_fa, ref_fa_bytes, tgt_fa_bytes = gen_pairs(mine, "hg", dev, keep)
     keep_chr1 = host_fa.get("chr1") or host_fa.get(f"chr1_r{rank}")
-    tgt_fa_bytes = sum(len(v[1]) for v in host_fa.values())
-    ref_fa_bytes = sum(len(v[0]) for v in host_fa.values())
-    host_fa.clear()
     torch.cuda.synchronize()
     log(f"[rank {rank}] {len(mine)} pairs generated and resident in {time.perf_counter() - t0:.1f} s "
         f"({ref_fa_bytes + tgt_fa_bytes:,} FASTA bytes)")
@@ -267,68 +576,15 @@ def main() -> None:
     n_lanes = max(1, min(args.contexts, len(mine)))
     cap = max(sccg.Context.compress_bound_static(p[1], p[3]) for p in pairs.values())
     lanes = [Lane(sccg, torch, dev, cap, local) for _ in range(n_lanes)]
+    pool = LanePool(lanes, dev)
     order = sorted(pairs, key=lambda n: -pairs[n][3])   # largest first onto the first free lane
     results: dict = {}      # name -> (device tensor of its record text, stats)
-    errors: list = []
-
-    # persistent lane threads: a step releases them through one barrier and joins them at another
-    # (no thread start per step)
-    nxt = [0, len(order) - 1]   # next from the largest end, next from the smallest end
-    qlock = threading.Lock()
-    lane_idx = {id(ln): i for i, ln in enumerate(lanes)}
-    go = threading.Barrier(n_lanes + 1)
-    done = threading.Barrier(n_lanes + 1)
-    stop = [False]
-
-    def worker(lane: Lane) -> None:
-        torch.cuda.set_device(dev)
-        while True:
-            go.wait()
-            if stop[0]:
-                return
-            try:
-                small_end = args.queue == "twoend" and lane_idx[id(lane)] % 2 == 1
-                while True:
-                    with qlock:
-                        if nxt[0] > nxt[1]:
-                            break
-                        if small_end:
-                            name = order[nxt[1]]
-                            nxt[1] -= 1
-                        else:
-                            name = order[nxt[0]]
-                            nxt[0] += 1
-                    dr, rn, dt_, tn = pairs[name]
-                    n = lane.ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, lane.out.data_ptr(), lane.cap,
-                                                 lane.stream.cuda_stream)
-                    st = lane.ctx.stats()
-                    prev = results.get(name)
-                    with torch.cuda.stream(lane.stream):
-                        buf = prev[0] if prev is not None and prev[0].numel() == n else \
-                            torch.empty(n, dtype=torch.uint8, device=dev)
-                        buf.copy_(lane.out[:n])   # the pair's record stream, kept for the gather
-                    results[name] = (buf, st)
-            except Exception as e:   # noqa: BLE001 -- reported after the step
-                errors.append(e)
-            done.wait()
-
-    lane_threads = [threading.Thread(target=worker, args=(ln,), daemon=True) for ln in lanes]
-    for t in lane_threads:
-        t.start()
-
-    def run_shard() -> None:
-        nxt[0], nxt[1] = 0, len(order) - 1
-        go.wait()
-        done.wait()
-        if errors:
-            raise errors[0]
-
+    job = device_job(pairs, results, dev)
     gathered: list = [None]
 
     def step() -> None:
-        run_shard()
-        for ln in lanes:
-            ln.stream.synchronize()
+        pool.run(order, job)
+        pool.sync()
         if world > 1:
             # per-chromosome record streams -> rank 0 over RCCL (multigpu.gather_records): one size
             # all-gather, then one gather of each rank's packed streams; only rank 0 receives
@@ -337,54 +593,36 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     lanes[0].ctx.profile(not args.no_prof)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    dt = timed_region(step, args.steps, 0, world, torch.cuda.synchronize, dev)
     prof = lanes[0].ctx.profile_get()
     lanes[0].ctx.profile(False)
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
 
     # ---- per-rank totals (all ranks' target bases make up the whole job)
     tot = {"target_bases": sum(results[n][1]["target_bases"] for n in order),
            "reference_bases": sum(results[n][1]["reference_bases"] for n in order),
+           "walk_reference_bases": sum(results[n][1]["walk_reference_bases"] for n in order),
            "record_bytes": sum(int(results[n][0].numel()) for n in order),
-           "tgt_fa": tgt_fa_bytes, "ref_fa": ref_fa_bytes}
-    totals = [tot]
-    if world > 1:
-        got = [None] * world
-        dist.all_gather_object(got, tot)
-        totals = got
-    job = {k: sum(t[k] for t in totals) for k in tot}
+           "tgt_fa": tgt_fa_bytes, "ref_fa": ref_fa_bytes,
+           "design_bytes": sum(design_alg_bytes(pairs[n][3], pairs[n][1], results[n][1]["target_bases"],
+                                                results[n][1]["reference_bases"], results[n][1]["walk_reference_bases"],
+                                                int(results[n][0].numel()), bool(results[n][1]["mode_global"]))
+                               for n in order),
+           "survey_bytes": sum(survey_alg_bytes(results[n][1]["target_bases"], results[n][1]["reference_bases"],
+                                                results[n][1]["walk_reference_bases"], int(results[n][0].numel()))
+                               for n in order)}
+    job_tot, _ = job_totals(tot, world)
 
     # ---- parity: every chromosome's record stream against the reference's pinned sha256
     parity = None
     if not args.no_check:
-        streams = {}
-        if world > 1:
-            if rank == 0:
-                streams = gathered[0]
-        else:
-            streams = {n: results[n][0].cpu().numpy().tobytes() for n in order}
+        streams = gathered[0] if world > 1 else gather_streams(results, order, 1, dev)
         if rank == 0:
-            pins = load_manifest()
-            checked = [n for n in streams if n in pins and args.workload == "genome"]
-            bad = [n for n in checked if hashlib.sha256(streams[n]).hexdigest() != pins[n]["record_sha256"]]
-            parity = {"chromosomes": len(streams), "pinned_checked": len(checked), "pinned_mismatch": bad,
-                      "reference": "oracle/_ref (compression.cpp compiled unchanged), tests/golden/genome_manifest.json"}
+            pins = load_manifest() if args.workload == "genome" else {}
+            parity = check_pins(streams, pins)
             if args.workload == "chr1":
                 parity["record_sha256"] = hashlib.sha256(next(iter(streams.values()))).hexdigest()
-            if bad:
-                raise SystemExit(f"bench: record streams differ from the reference for {bad}")
+            if parity["pinned_mismatch"]:
+                raise SystemExit(f"bench: record streams differ from the reference for {parity['pinned_mismatch']}")
 
     # ---- configs[3]: the chr1 record stream back to FASTA on this GPU (rank 0, outside the step)
     decomp = None
@@ -423,8 +661,10 @@ def main() -> None:
         decomp = {"workload": "BASELINE configs[3]: chr1 record stream -> FASTA on 1 GPU", "target_bases": nTd,
                   "ms": ddt * 1e3, "bases_per_s": nTd / ddt, "roundtrip_exact": exact,
                   "roofline_job": {"bound": "hbm", "alg_bytes": b_dec, "achieved": b_dec / ddt / 1e9,
-                                   "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": b_dec / ddt / 1e9 / HBM_PEAK_GBS},
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": b_dec / ddt / 1e9 / HBM_PEAK_GBS,
+                                   "model": "SURVEY §8(d) B_decomp = |rec| + |R| + |T_fa| + |T_matched|"},
                   "kernels": {k: {"ms_per_call": v[0] / ks, "launches_per_call": v[1] / ks} for k, v in dprof.items()}}
+        del d_fa
         if not exact:
             raise SystemExit("bench: chr1 reconstruction differs from the target FASTA")
 
@@ -432,9 +672,23 @@ def main() -> None:
     if rank == 0 and not args.no_e2e and keep_chr1 is not None:
         pin = load_manifest().get("chr1", {}).get("record_sha256") if args.workload == "genome" else None
         e2e = end_to_end(lanes[0].ctx, keep_chr1[0], keep_chr1[1], pin)
+    e2e_genome = None
+    if want_e2e_genome and world == 1 and not args.names:
+        e2e_genome = end_to_end_genome(pool, host_fa, order, load_manifest() if not args.no_check else {})
+    host_fa.clear()
+
+    t2t = None
+    if args.workload == "genome" and not args.no_t2t and not args.names:
+        # the hg pairs' HBM is not needed any more
+        for n in list(pairs):
+            del pairs[n]
+        torch.cuda.empty_cache()
+        t2t = t2t_genome(pool, jobs, world, rank, dev, max(1, args.t2t_steps))
+        if rank == 0 and t2t["pinned_mismatch"]:
+            raise SystemExit(f"bench: T2T-like record streams differ from the reference for {t2t['pinned_mismatch']}")
 
     if rank == 0:
-        value = job["target_bases"] * args.steps / dt
+        value = job_tot["target_bases"] * args.steps / dt
         ms_step = dt * 1e3 / args.steps
         kernels = {k: {"ms_per_step": v[0] / args.steps, "launches_per_step": v[1] / args.steps,
                        "avg_launch_ms": v[0] / v[1]} for k, v in prof.items()}
@@ -457,19 +711,35 @@ def main() -> None:
                     roof["traffic"] = pmc["hbm_bytes_per_launch"]
                     roof["traffic_over_alg"] = round(pmc["hbm_bytes_per_launch"] / alg, 3)
                     roof["traffic_source"] = pmc["source"]
-        nRp = sum(results[n][1]["reference_bases"] for n in order)   # |R'| <= |R| (N erased); bound
-        b_job = sum(job_alg_bytes(results[n][1]["target_bases"], results[n][1]["reference_bases"],
-                                  results[n][1]["reference_bases"], int(results[n][0].numel())) for n in order)
-        if world > 1:
-            b_job = b_job * job["target_bases"] / max(1, tot["target_bases"])   # other ranks: same model per base
-        roof_job = {"bound": "hbm", "alg_bytes_per_step": b_job, "achieved": b_job / (ms_step * 1e-3) / 1e9,
-                    "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
-                    "frac": b_job / (ms_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
-                    "model": "SURVEY §8(d) B_global = 1.25(|T|+|R|) + 0.25|R| + 4|R'| + 0.5|T| + |out| (|R'| taken as |R|)"}
-        del nRp
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        # other kernels' achieved rates against the same models (HIP events) and their PMC bytes
+        kroof = {}
+        for k in ("fasta_strip", "first_sweep_anchors", "run_extract"):
+            if k in prof and prof[k][1]:
+                ab = kernel_alg_bytes(k, tot) / (prof[k][1] / args.steps)
+                am = prof[k][0] / prof[k][1]
+                e = {"alg_bytes_per_launch": ab, "avg_launch_ms": am, "achieved_GBps": ab / (am * 1e-3) / 1e9,
+                     "frac": ab / (am * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                pmc = load_pmc({"first_sweep_anchors": "k_sweep_early"}.get(k, k))
+                if pmc:
+                    e["traffic_per_launch"] = pmc["hbm_bytes_per_launch"]
+                kroof[k] = e
+        per_s = ms_step * 1e-3
+        roof_job = {"bound": "hbm", "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                    "alg_bytes_per_step": job_tot["design_bytes"],
+                    "achieved": job_tot["design_bytes"] / per_s / 1e9,
+                    "frac": job_tot["design_bytes"] / per_s / 1e9 / (HBM_PEAK_GBS * world),
+                    "model": "design (DESIGN.md §4, bench.design_alg_bytes): per pair both FASTA read + T, R, T', R' "
+                             "written once (ingest) + T once (run lines) + R' once (first-step sweep) + 0.5 B per "
+                             "target base (walk, SURVEY §8(d)) + the record text; a pair that stays local: its segments "
+                             "once instead of the sweep and walk.  |R'| measured per pair.",
+                    "survey_model": {"alg_bytes_per_step": job_tot["survey_bytes"],
+                                     "frac": job_tot["survey_bytes"] / per_s / 1e9 / (HBM_PEAK_GBS * world),
+                                     "model": "SURVEY §8(d) B_global = 1.25(|T|+|R|) + 0.25|R| + 4|R'| + 0.5|T| + |out| "
+                                              "with measured |R'|; its 4|R'| CSR index is not built by this design"}}
+        if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_timeout)
+        else:
+            cpu = cpu_baseline_pointer()
         per = {n: {"mode": "global" if results[n][1]["mode_global"] else "local",
                    "rounds": results[n][1]["walk_rounds"], "matches": results[n][1]["n_matches"],
                    "record_bytes": int(results[n][0].numel())} for n in order}
@@ -489,25 +759,26 @@ def main() -> None:
             "dtype": "u8",
             "data": "synthetic (tools/synth.c hg profile, seed = chromosome index); real hg18/hg19 unavailable offline",
             "config": {"workload": wl, "chromosomes": len(jobs), "pairs_rank0": len(order),
-                       "target_bases": job["target_bases"], "reference_bases": job["reference_bases"],
+                       "target_bases": job_tot["target_bases"], "reference_bases": job_tot["reference_bases"],
                        "k": 14, "m": 100, "params": "reference constants (compression.cpp:373-379), local controller on",
-                       "contexts_per_gpu": n_lanes, "pair_queue": args.queue, "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                       "contexts_per_gpu": n_lanes, "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "parallelism": f"LPT chromosome shard x{world}, RCCL gather of record streams to rank 0",
-                       "record_bytes": job["record_bytes"]},
+                       "record_bytes": job_tot["record_bytes"]},
             "roofline": roof,
+            "roofline_kernels": kroof,
             "roofline_job": roof_job,
             "cpu_baseline": cpu,
+            "cpu_genome_estimate": cpu_genome_estimate(),
             "parity": parity,
             "decompress": decomp,
             "end_to_end": e2e,
+            "end_to_end_genome": e2e_genome,
+            "t2t_genome": t2t,
             "kernels": kernels,
             "per_chromosome_rank0": per,
         }
         print(json.dumps(line), flush=True)
-    stop[0] = True
-    go.wait()
-    for t in lane_threads:
-        t.join()
+    pool.close()
     for ln in lanes:
         ln.ctx.close()
     if world > 1:

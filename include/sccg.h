@@ -78,6 +78,7 @@ typedef struct {
     int64_t walk_chunks;      /* global walk: chunks */
     int64_t record_bytes;     /* length of the whole compressed_genome.txt */
     int64_t walk_chains;      /* global walk: frozen chains resolved by the chain kernels */
+    int64_t walk_reference_bases; /* |R'|: the reference with every 'N' erased (compression.cpp:556) */
 } sccg_stats;
 
 int sccg_ctx_create(int device, sccg_ctx** out);

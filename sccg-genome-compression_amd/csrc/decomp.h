@@ -68,6 +68,9 @@ int dc_tok_range(const DcTokBuf& tk, int64_t cap, const int64_t* d_nref, int32_t
 // SCCG_DC_FUSED=1 (A/B runs), the fill + format path otherwise
 bool dc_fused();
 // (tiled path, dc_tok_tiled(): the range check against *d_nref happens here, d_err bit 2)
+// the tiled path's range check alone (k_tok_fill2 without writing): d_err bit 2
+int dc_tok_range_tiled(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
+                       const int64_t* d_nref, int32_t* d_err, hipStream_t s);
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
                    const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s,
                    const int64_t* d_nref, int32_t* d_err);

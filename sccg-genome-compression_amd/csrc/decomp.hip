@@ -560,7 +560,10 @@ __global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ 
 }
 
 // one wave per block: literals and token copies into dec at the block's offsets; tokens beyond
-// the reference (p < 0 or p + l > |R'|, decompression.cpp:223-229) set d_err bit 2 and copy nothing
+// the reference (p < 0 or p + l > |R'|, decompression.cpp:223-229) set d_err bit 2 and copy nothing.
+// WRITE = false: the range check alone (no dec; a size query or an early error must report
+// SCCG_E_RANGE exactly as the full decode would)
+template <bool WRITE>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restrict__ s, int64_t n,
                                                           const int64_t* __restrict__ bin, const int64_t* __restrict__ boff,
                                                           const int64_t* __restrict__ bdsum, const int64_t* __restrict__ d_nref,
@@ -612,6 +615,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restr
         atomicOr(err, 2);
         tok = false;
     }
+    if (!WRITE) return;
     if (!tok && contrib == 1 && c != '(') dec[o] = c;   // literals, a stray ')' included
     unsigned long long tm = __ballot(tok);
     while (tm) {
@@ -1489,13 +1493,22 @@ int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int
                    const int64_t* d_nref, int32_t* d_err) {
     if (n <= 0) return 0;
     if (dc_tok_tiled()) {
-        PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_fill2, dim3(grid_for((n + TK_B - 1) / TK_B, WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n,
+        PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_fill2<true>, dim3(grid_for((n + TK_B - 1) / TK_B, WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n,
                     d_lp, d_off, d_dsum, d_nref, d_R, d_dec, d_err);
         SCCG_HIP(hipGetLastError());
         return 0;
     }
     PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_fill, dim3(grid_for(n, 64 * WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n, d_lp, d_off, d_dsum, d_dlt,
                        d_contrib, d_R, d_dec);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int dc_tok_range_tiled(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
+                       const int64_t* d_nref, int32_t* d_err, hipStream_t s) {
+    if (n <= 0 || !dc_tok_tiled()) return 0;   // (the scan path checked the range in dc_decode_prepare)
+    hipLaunchKernelGGL(k_tok_fill2<false>, dim3(grid_for((n + TK_B - 1) / TK_B, WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n, d_lp,
+                       d_off, d_dsum, d_nref, (const uint8_t*)nullptr, (uint8_t*)nullptr, d_err);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

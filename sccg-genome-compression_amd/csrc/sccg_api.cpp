@@ -542,6 +542,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     bool stoi_fail = false;
     st.target_bases = nT;
     st.reference_bases = nR;
+    st.walk_reference_bases = lr[1];
     mark("ingest");
     const bool has_hdr = hdr[0] < tn;
     const int64_t hlen = has_hdr ? hdr[1] - hdr[0] : 0;
@@ -707,16 +708,36 @@ constexpr size_t STAGE_PIECE = (size_t)16 << 20;
 static_assert(STAGE_THREADS * STAGE_SLOTS <= 16, "sccg_ctx::stage");
 
 int staging_init(sccg_ctx* ctx) {
-    if (ctx->copy_ref) return 0;
+    // idempotent piece by piece: a call after a partial failure completes what is missing instead of
+    // allocating (and leaking) the slots and events again
     for (int i = 0; i < STAGE_THREADS * STAGE_SLOTS; i++) {
-        HIPTRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->stage[i]), STAGE_PIECE, hipHostMallocDefault));
-        HIPTRY(hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming));
+        if (!ctx->stage[i]) HIPTRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->stage[i]), STAGE_PIECE, hipHostMallocDefault));
+        if (!ctx->stage_ev[i]) HIPTRY(hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming));
     }
-    HIPTRY(hipEventCreateWithFlags(&ctx->ev_ref_in, hipEventDisableTiming));
-    HIPTRY(hipEventCreateWithFlags(&ctx->ev_tgt_in, hipEventDisableTiming));
-    HIPTRY(hipStreamCreateWithFlags(&ctx->copy_tgt, hipStreamNonBlocking));
-    HIPTRY(hipStreamCreateWithFlags(&ctx->copy_ref, hipStreamNonBlocking));
+    if (!ctx->ev_ref_in) HIPTRY(hipEventCreateWithFlags(&ctx->ev_ref_in, hipEventDisableTiming));
+    if (!ctx->ev_tgt_in) HIPTRY(hipEventCreateWithFlags(&ctx->ev_tgt_in, hipEventDisableTiming));
+    if (!ctx->copy_tgt) HIPTRY(hipStreamCreateWithFlags(&ctx->copy_tgt, hipStreamNonBlocking));
+    if (!ctx->copy_ref) HIPTRY(hipStreamCreateWithFlags(&ctx->copy_ref, hipStreamNonBlocking));
     return 0;
+}
+
+// whole contents of an open descriptor that is not a regular file (a FIFO, /dev/stdin, a process
+// substitution): read to EOF, as the reference's ifstream + getline loop does (compression.cpp:186-218)
+bool slurp_fd(int fd, std::vector<uint8_t>* v) {
+    v->clear();
+    size_t n = 0;
+    for (;;) {
+        if (v->size() - n < ((size_t)1 << 20)) v->resize(n + ((size_t)4 << 20));
+        const ssize_t r = read(fd, v->data() + n, v->size() - n);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        if (r == 0) break;
+        n += (size_t)r;
+    }
+    v->resize(n);
+    return true;
 }
 
 struct FileLoad {
@@ -816,8 +837,28 @@ int compress_files_impl(sccg_ctx* ctx, const sccg_params& P, const char* ref_pat
     ft.v = open(tgt_path, O_RDONLY);
     if (ft.v < 0) return ctx->fail(SCCG_E_OPEN_TGT, "Error opening target file: %s", tgt_path);
     struct stat sr{}, stt{};
-    if (fstat(fr.v, &sr) || !S_ISREG(sr.st_mode)) return ctx->fail(SCCG_E_OPEN_REF, "reference is not a regular file: %s", ref_path);
-    if (fstat(ft.v, &stt) || !S_ISREG(stt.st_mode)) return ctx->fail(SCCG_E_OPEN_TGT, "target is not a regular file: %s", tgt_path);
+    const bool reg_r = !fstat(fr.v, &sr) && S_ISREG(sr.st_mode);
+    const bool reg_t = !fstat(ft.v, &stt) && S_ISREG(stt.st_mode);
+    if (!reg_r || !reg_t) {
+        // a FIFO / pipe / character device has no size to stage by: read both to EOF into host
+        // memory (reference first, as the reference does) and take the host path
+        std::vector<uint8_t> hr, ht;
+        if (!slurp_fd(fr.v, &hr)) return ctx->fail(SCCG_E_OPEN_REF, "Error reading reference file: %s", ref_path);
+        if (!slurp_fd(ft.v, &ht)) return ctx->fail(SCCG_E_OPEN_TGT, "Error reading target file: %s", tgt_path);
+        sccg_buf b{nullptr, 0};
+        const int rc = sccg_compress_ex(ctx, &P, (const char*)hr.data(), hr.size(), (const char*)ht.data(), ht.size(), &b);
+        if (rc && rc != SCCG_E_DELTA_STOI) { sccg_buf_free(&b); return rc; }
+        Fd fo;
+        fo.v = open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        const bool ok = fo.v >= 0 && !write_all(fo.v, (const uint8_t*)b.data, b.len);
+        const int64_t n = (int64_t)b.len;
+        sccg_buf_free(&b);
+        if (!ok) return ctx->fail(SCCG_E_WRITE, "cannot write %s", out_path);
+        if (close(fo.v)) { fo.v = -1; return ctx->fail(SCCG_E_WRITE, "closing %s failed", out_path); }
+        fo.v = -1;
+        *out_len = n;
+        return rc;
+    }
     TRY(staging_init(ctx));
     const int64_t rn = (int64_t)sr.st_size, tn = (int64_t)stt.st_size;
     uint8_t* drf = reinterpret_cast<uint8_t*>(ctx->get(B_RFA, (size_t)rn + 16));
@@ -835,13 +876,15 @@ int compress_files_impl(sccg_ctx* ctx, const sccg_params& P, const char* ref_pat
     L.npiece[1] = (tn + (int64_t)STAGE_PIECE - 1) / (int64_t)STAGE_PIECE;
     std::vector<std::thread> th;
     for (int t = 0; t < STAGE_THREADS; t++) th.emplace_back([&L, t] { L.reader(t); });
-    struct Join {
-        std::vector<std::thread>& th;
-        FileLoad& L;
+    struct Join {   // every exit path: the readers joined, then their queued copies drained (a later
+        std::vector<std::thread>& th;   // ctx->get() may reallocate the buffers they write into)
+        sccg_ctx* ctx;
         ~Join() {
             for (auto& x : th) if (x.joinable()) x.join();
+            (void)hipStreamSynchronize(ctx->copy_ref);
+            (void)hipStreamSynchronize(ctx->copy_tgt);
         }
-    } join{th, L};
+    } join{th, ctx};
     const InputReady rdy{&FileLoad::ref_ready, &FileLoad::tgt_ready, &L};
     int64_t len = 0;
     int rc = compress_device_impl(ctx, P, drf, rn, dtf, tn, dout, (int64_t)cap, &len, &rdy);
@@ -996,9 +1039,19 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     if (err & 1) return ctx->fail(SCCG_E_PARSE, "record text outside the run/token grammar");
     if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
     const int64_t nres = D + nr.total;
-    if (err & 4) return ctx->fail(SCCG_E_PARSE, "N positions beyond the sequence");
     const int64_t hlen = has_hdr ? end[0] : 0;
     const int64_t total = hlen + 1 + nres + (nres > 0 ? (nres - 1) / 50 : 0) + 1;
+    if (!fused && dc_tok_tiled() && (size_only || (err & 4) || total > out_cap)) {
+        // the tiled record line checks the token range in its fill: a size query or an early error
+        // runs that check alone first, so it reports SCCG_E_RANGE as the full decode (and the
+        // reference, which exits at :223-229 before it places N) would
+        HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
+        TRY(dc_tok_range_tiled(enc, nenc, lp2, doff, dsum, sc + 9, d_err, s));
+        const RbItem it{d_err, &err, (int)sizeof err};
+        TRY(dev_readback(&it, 1, s));
+        if (err & 2) return ctx->fail(SCCG_E_RANGE, "token exceeds the reference (decompression.cpp:223-229)");
+    }
+    if (err & 4) return ctx->fail(SCCG_E_PARSE, "N positions beyond the sequence");
     *out_len = total;
     if (size_only) return SCCG_OK;
     if (total > out_cap) return ctx->fail(SCCG_E_NOMEM, "output needs %lld bytes", (long long)total);

@@ -60,6 +60,12 @@ class Emitter:
         path = os.path.join(d, "compressed_genome.txt")
         with open(path, "wb") as f:
             f.write(rec)
+        self.written(name, path, rc_n)
+
+    def written(self, name: str, path: str, rc_n: int) -> None:
+        """The record file of `name` is closed at `path` (by emit, or by sccg_compress_files
+        itself): start its 7z now, unless its delta_encode failed (stoi: text kept, no 7z)."""
+        self.done.add(name)
         if rc_n:
             print(f"Error: {name}: stoi", file=sys.stderr)
             self.rc = 1
@@ -77,6 +83,28 @@ class Emitter:
                 self.rc = 1
         self.procs = []
         return self.rc
+
+
+def compress_pair_files(ctx, ref_path: str, tgt_path: str, out_dir: str, name: str, em: Emitter | None) -> dict:
+    """One pair from FASTA files straight to <out_dir>/<name>/compressed_genome.txt through
+    sccg_compress_files (pinned staging, compression.cpp:181-331 without 7z), then its 7z through
+    the Emitter.  Returns the pair's stats with its rc (the CLI's failure points as error codes)."""
+    import sccg
+    d = os.path.join(out_dir, name)
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, "compressed_genome.txt")
+    rc_n, st = 0, {}
+    try:
+        ctx.compress_files(ref_path, tgt_path, path)
+        st = ctx.stats()
+    except sccg.SccgError as e:
+        rc_n = e.rc
+    if em is not None:
+        if rc_n and rc_n != sccg.SCCG_E_DELTA_STOI:
+            em.emit(name, b"", rc_n)
+        else:
+            em.written(name, path, rc_n)
+    return dict(st, rc=rc_n)
 
 
 def compress_shard(mine: list[str], ref_dir: str, tgt_dir: str, make_ctx, em: Emitter | None,
@@ -127,6 +155,60 @@ def compress_shard(mine: list[str], ref_dir: str, tgt_dir: str, make_ctx, em: Em
     return parts, stats
 
 
+def compress_shard_files(mine: list[str], ref_dir: str, tgt_dir: str, make_ctx, em: Emitter, err_hip: int,
+                         contexts: int = 2) -> dict:
+    """Rank 0's own pairs: FASTA files -> record files through sccg_compress_files, `contexts`
+    library contexts each driven by its own host thread (one pair's file reads and copies overlap
+    another's kernels), 7z started per pair as its file closes.  Never raises (see compress_shard)."""
+    import threading
+    stats: dict[str, dict] = {}
+    todo = sorted(mine, key=lambda n: -os.path.getsize(os.path.join(tgt_dir, n + ".fa"))
+                  if os.path.exists(os.path.join(tgt_dir, n + ".fa")) else 0)
+    lock = threading.Lock()
+
+    def worker():
+        ctx = None
+        try:
+            ctx = make_ctx()
+        except Exception as e:   # noqa: BLE001
+            print(f"Error: no context: {e}", file=sys.stderr)
+        while True:
+            with lock:
+                if not todo:
+                    break
+                n = todo.pop(0)
+            if ctx is None:
+                with lock:
+                    stats[n] = {"rc": err_hip}
+                    em.emit(n, b"", err_hip)
+                continue
+            st = compress_pair_files(ctx, os.path.join(ref_dir, n + ".fa"), os.path.join(tgt_dir, n + ".fa"),
+                                     em.out_dir, n, None)
+            with lock:
+                stats[n] = st
+                if st["rc"] and st["rc"] != sccg_delta_stoi():
+                    em.emit(n, b"", st["rc"])
+                else:
+                    em.written(n, os.path.join(em.out_dir, n, "compressed_genome.txt"), st["rc"])
+        if ctx is not None:
+            try:
+                ctx.close()
+            except Exception:   # noqa: BLE001
+                pass
+
+    ths = [threading.Thread(target=worker) for _ in range(max(1, contexts))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return stats
+
+
+def sccg_delta_stoi() -> int:
+    import sccg
+    return sccg.SCCG_E_DELTA_STOI
+
+
 def collect(names: list[str], parts: dict, stats: dict, em: Emitter | None, dev, world: int) -> dict:
     """The job's exchange: every rank's record texts and stats to rank 0 (multigpu.gather_records
     + gather_to_root); rank 0 emits the chromosomes it did not compress itself (a pair no rank
@@ -160,6 +242,7 @@ def main(argv=None) -> int:
     ap.add_argument("--out", required=True)
     ap.add_argument("--names", default="", help="comma-separated subset (default: all common *.fa)")
     ap.add_argument("--no-7z", action="store_true")
+    ap.add_argument("--contexts", type=int, default=2, help="rank 0: library contexts (host threads) on its GPU")
     args = ap.parse_args(argv)
 
     import torch
@@ -185,8 +268,12 @@ def main(argv=None) -> int:
     em = Emitter(args.out, not args.no_7z) if rank == 0 else None
 
     t0 = time.perf_counter()
-    parts, stats = compress_shard(mine, args.ref_dir, args.tgt_dir, lambda: sccg.Context(local), em,
-                                  sccg.ERR_CODES["SCCG_E_HIP"])
+    if em is not None:   # rank 0: files straight to record files (sccg_compress_files)
+        parts, stats = {}, compress_shard_files(mine, args.ref_dir, args.tgt_dir, lambda: sccg.Context(local), em,
+                                                sccg.ERR_CODES["SCCG_E_HIP"], args.contexts)
+    else:
+        parts, stats = compress_shard(mine, args.ref_dir, args.tgt_dir, lambda: sccg.Context(local), em,
+                                      sccg.ERR_CODES["SCCG_E_HIP"])
     t_comp = time.perf_counter() - t0
     all_stats = collect(names, parts, stats, em, dev, world)
     rc = 0

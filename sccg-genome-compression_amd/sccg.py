@@ -45,7 +45,8 @@ class Stats(ctypes.Structure):
                 ("target_bases", ctypes.c_int64), ("reference_bases", ctypes.c_int64),
                 ("n_matches", ctypes.c_int64), ("literal_bases", ctypes.c_int64),
                 ("walk_rounds", ctypes.c_int64), ("walk_chunks", ctypes.c_int64),
-                ("record_bytes", ctypes.c_int64), ("walk_chains", ctypes.c_int64)]
+                ("record_bytes", ctypes.c_int64), ("walk_chains", ctypes.c_int64),
+                ("walk_reference_bases", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -6,10 +6,14 @@ Runs oracle/_ref/compression + decompression (compiled from /root/reference, stu
   * the 24 synthetic hg18/hg19 chromosome pairs at their UCSC lengths (hg profile, seed = chromosome
     index 1..24, X = 23, Y = 24 -- exactly the pairs bench.py and tools/bench_configs.py compress),
   * the 100 Mb T2T-like pair (t2t profile, seed 7; the stuck / literal-heavy path),
+  * BASELINE configs[4]'s shape at full size: the same 24 UCSC length pairs with the T2T-like
+    profile (seed = chromosome index, names t2t_chr1 .. t2t_chrY -- exactly the pairs
+    `bench.py`'s t2t_genome leg and `tools/bench_configs.py --genome-profile t2t` compress),
 
 and writes their record / FASTA sha256 to genome_manifest.json.  Build container only: the
 reference needs ~70 B of RAM per reference base (17.4 GB for chr1), so pairs run concurrently
-under a RAM budget, largest first (about 20 min on 8 cores / 62 GB).
+under a RAM budget, largest first (about 20 min on 8 cores / 62 GB for the hg pairs; the
+T2T-like pairs' stuck walk runs ~3 s per Mb, about an hour more).
 
     python tests/golden/pin_genome.py [--budget-gb 46] [--only chr21,t2t100]
 """
@@ -36,6 +40,8 @@ def jobs() -> list[dict]:
     for i, (name, rl, tl) in enumerate(zip(multigpu.CHROMS, multigpu.HG18, multigpu.HG19)):
         out.append({"name": name, "profile": "hg", "ref_len": rl, "tgt_len": tl, "seed": i + 1})
     out.append({"name": "t2t100", "profile": "t2t", "ref_len": 100_000_000, "tgt_len": 100_000_000, "seed": 7})
+    for i, (name, rl, tl) in enumerate(zip(multigpu.CHROMS, multigpu.HG18, multigpu.HG19)):
+        out.append({"name": "t2t_" + name, "profile": "t2t", "ref_len": rl, "tgt_len": tl, "seed": i + 1})
     return out
 
 

@@ -68,3 +68,53 @@ def test_genome_driver_single_rank(tmp_path):
     for name, (rfa, tfa) in pairs.items():
         assert (od / name / "compressed_genome.txt").read_bytes() == oraclelib.compress(rfa, tfa)
         assert (od / name / "compressed_genome.txt.7z").exists()
+
+
+def test_cli_fifo_inputs(tmp_path):
+    """Inputs that are not regular files (FIFOs: process substitution, /dev/stdin) are read to EOF,
+    as the reference's ifstream does (compression.cpp:186-218), not rejected."""
+    import threading
+    rfa, tfa = synthlib.synth_pair("hg", 300_000, 301_000, 33)
+    rp, tp = tmp_path / "r.fifo", tmp_path / "t.fifo"
+    os.mkfifo(rp)
+    os.mkfifo(tp)
+
+    def feed(path, data):
+        with open(path, "wb") as f:
+            f.write(data)
+
+    ths = [threading.Thread(target=feed, args=(rp, rfa)), threading.Thread(target=feed, args=(tp, tfa))]
+    for t in ths:
+        t.start()
+    out = tmp_path / "out"
+    p = subprocess.run([os.path.join(BIN, "compression"), str(rp), str(tp), str(out)], env=ENV, capture_output=True,
+                       timeout=120)
+    for t in ths:
+        t.join(timeout=30)
+    assert p.returncode == 0, p.stderr
+    assert (out / "compressed_genome.txt").read_bytes() == oraclelib.compress(rfa, tfa)
+
+
+def test_size_query_reports_range_like_full_decode():
+    """A record whose token lies beyond the reference (decompression.cpp:223-229): the size-only
+    query (d_out NULL) and the full decode both return SCCG_E_RANGE."""
+    import torch
+    from pkg import sccg
+    ctx = sccg.Context(0)
+    try:
+        rfa = b">r\n" + b"ACGT" * 50 + b"\n"
+        for rec in (b"\n,\n(0,20)(500,30)", b">h\n\n(3,2)\n(0,20)(500,30)", b"\n,\nAC(190,20)"):
+            dev = torch.device("cuda", 0)
+            d_r = torch.frombuffer(bytearray(rfa), dtype=torch.uint8).to(dev)
+            d_c = torch.frombuffer(bytearray(rec), dtype=torch.uint8).to(dev)
+            d_o = torch.empty(1 << 16, dtype=torch.uint8, device=dev)
+            rcs = []
+            for ptr, cap in ((0, 0), (d_o.data_ptr(), 1 << 16), (d_o.data_ptr(), 4)):
+                try:
+                    ctx.reconstruct_device(d_r.data_ptr(), len(rfa), d_c.data_ptr(), len(rec), ptr, cap)
+                    rcs.append(0)
+                except sccg.SccgError as e:
+                    rcs.append(e.rc)
+            assert rcs == [sccg.ERR_CODES["SCCG_E_RANGE"]] * 3, (rec, rcs)
+    finally:
+        ctx.close()
