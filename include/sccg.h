@@ -16,6 +16,8 @@
  *                                     :341-368/:495-555, local loop :372-481, global pass
  *                                     :484-574, delta_encode :222-304)
  * sccg_match                          match_sequences                    compression.cpp:36-179
+ * sccg_walk_range / _device           its global walk from a state        compression.cpp:64-161
+ *                                     (one chromosome split across GPUs)
  * sccg_reconstruct / _device          decompress_genome after 7z +       decompression.cpp:43-114,
  *                                     reconstruct_genome + file body     :117-279, :316-323
  *
@@ -140,6 +142,21 @@ int sccg_compress_files(sccg_ctx* ctx, const sccg_params* params, const char* re
 int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, size_t nt, int k,
                int m, int global, int64_t offset, sccg_records* out);
 void sccg_records_free(sccg_records* r);
+
+/* The global walk of match_sequences(Sr, St, k, m, true) (compression.cpp:64-161) entered at state
+ * (index = x0, prev_match_end = P0) and run until the first state with index >= x_end (or until
+ * index > |St| - k): its match records (kind 1, pos = p, len = l, t = target index; the literals are
+ * the gaps) and that exit state, exit_state[0] = index, exit_state[1] = prev_match_end.  This is the
+ * engine of one chromosome's walk split across GPUs (multigpu.split_walk):
+ * two walks that reach the same state coincide afterwards.  Sr, St: N-erased, uppercased sequences
+ * (R', T' of compression.cpp:556-557).  P0 == -1 (the ungated first step) only with x0 == 0;
+ * 0 <= m <= 127, 1 <= k <= 32.  The _device form takes device pointers (stream: hipStream_t or
+ * NULL); both return host records (sccg_records_free). */
+int sccg_walk_range(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, size_t nt, int k, int m,
+                    int64_t x0, int64_t P0, int64_t x_end, sccg_records* out, int64_t* exit_state);
+int sccg_walk_range_device(sccg_ctx* ctx, const void* d_ref, size_t nr, const void* d_tgt, size_t nt, int k,
+                           int m, int64_t x0, int64_t P0, int64_t x_end, sccg_records* out, int64_t* exit_state,
+                           void* stream);
 
 /* Decompression after 7z: record text (contents of the extracted compressed_genome.txt) +
  * reference FASTA -> exact bytes of <out>/reconstructed_genome.fa. */

@@ -21,6 +21,7 @@ enum ProfId {
     PROF_WALK_CHAIN,     // k_chain_fill (end of a frozen chain)
     PROF_DC_DECODE,      // k_tok_fill
     PROF_DC_FORMAT,      // k_format
+    PROF_WALK_CARRY,     // k_walk<., true>: a round's carry launch
     PROF_COUNT
 };
 void prof_begin(hipStream_t s, int id);
@@ -173,6 +174,12 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
                           int chunk, void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len,
                           WalkResult* res, hipStream_t s, bool abs_p = false, const EmitTarget* late_out = nullptr,
                           bool keep_flat = true);
+// The global walk from state (x0, P0) until the first index >= x_end (sccg_walk_range; the
+// reference's walk compression.cpp:64-161 entered mid-way): its matches stay in ws (global_matches),
+// the exit state comes back.  P0 == -1 only with x0 == 0 (the ungated first step).
+int global_walk_range(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
+                      size_t ws_bytes, int64_t x0, int64_t P0, int64_t x_end, int64_t* exit_x, int64_t* exit_P,
+                      WalkResult* res, hipStream_t s);
 // the raw match list of the last global_match_and_emit (device pointers inside ws)
 int global_matches(void* ws, const int32_t** t, const int32_t** p, const int32_t** l, int64_t* n);
 

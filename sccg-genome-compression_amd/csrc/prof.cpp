@@ -61,7 +61,7 @@ Registry& reg() {
 const char* const NAMES[PROF_COUNT] = {
     "fasta_strip", "run_extract", "run_text", "local_segments", "local_pass_k10", "local_emit", "n_filter",
     "first_sweep_anchors", "walk", "presence_scan", "fullc_scan", "match_emit", "walk_chain",
-    "dc_decode", "dc_format",
+    "dc_decode", "dc_format", "walk_carry",
 };
 
 // each host thread brackets its own launches (several contexts may launch the same family at once)

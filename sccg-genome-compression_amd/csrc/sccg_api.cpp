@@ -1210,6 +1210,74 @@ int sccg_reconstruct(sccg_ctx* ctx, const char* ref_fa, size_t ref_len, const ch
 }
 
 // match_sequences seam (compression.cpp:36): local segments or the windowed global walk
+// the walk from a state over device-resident R', T' (one chromosome's walk split
+// across ranks, multigpu.split_walk): matches as kind-1 records with their target index
+int walk_range_dev(sccg_ctx* ctx, const uint8_t* R, int64_t nr, const uint8_t* T, int64_t nt, int k, int m, int64_t x0,
+                   int64_t P0, int64_t x_end, sccg_records* out, int64_t* exit_state, hipStream_t s) {
+    if (m < 0 || 2 * m + 1 > 256 || k < 1 || k > 32 || nr >= (int64_t)INT32_MAX - 8 || nt >= (int64_t)INT32_MAX - 8)
+        return ctx->fail(SCCG_E_UNSUPPORTED, "sccg_walk_range takes 0 <= m <= 127, 1 <= k <= 32");
+    if (x0 < 0 || x0 > nt || P0 < -1 || P0 >= (nr > 0 ? nr : 1) || (P0 == -1 && x0 != 0))
+        return ctx->fail(SCCG_E_UNSUPPORTED, "sccg_walk_range: state (x0, P0) outside the walk's states");
+    const size_t wsb = walk_workspace_bytes(nr, nt, k, walk_chunk(nt));
+    void* ws = ctx->get(B_WALK, wsb);
+    if (!ws) return ctx->fail(SCCG_E_NOMEM, "walk workspace");
+    WalkResult wr{};
+    int64_t ex = 0, ep = -1;
+    TRY(global_walk_range(R, nr, T, nt, k, m, walk_chunk(nt), ws, wsb, x0, P0, x_end, &ex, &ep, &wr, s));
+    const int32_t *dt, *dp, *dl;
+    int64_t nm;
+    global_matches(ws, &dt, &dp, &dl, &nm);
+    const size_t n = (size_t)nm;
+    out->n = nm;
+    out->kind = (uint8_t*)malloc(n ? n : 1);
+    out->pos = (int32_t*)malloc((n ? n : 1) * 4);
+    out->len = (int32_t*)malloc((n ? n : 1) * 4);
+    out->t = (int64_t*)malloc((n ? n : 1) * 8);
+    std::vector<int32_t> ht(n ? n : 1);
+    if (!out->kind || !out->pos || !out->len || !out->t) return ctx->fail(SCCG_E_NOMEM, "host allocation");
+    if (n) {
+        HIPTRY(hipMemcpyAsync(ht.data(), dt, n * 4, hipMemcpyDeviceToHost, s));
+        HIPTRY(hipMemcpyAsync(out->pos, dp, n * 4, hipMemcpyDeviceToHost, s));
+        HIPTRY(hipMemcpyAsync(out->len, dl, n * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIPTRY(hipStreamSynchronize(s));
+    for (size_t i = 0; i < n; i++) { out->kind[i] = 1; out->t[i] = ht[i]; }
+    exit_state[0] = ex;
+    exit_state[1] = ep;
+    ctx->stats = sccg_stats{};
+    ctx->stats.mode_global = 1;
+    ctx->stats.n_matches = nm;
+    ctx->stats.walk_rounds = wr.rounds;
+    ctx->stats.walk_chunks = wr.chunks;
+    ctx->stats.target_bases = nt;
+    ctx->stats.walk_reference_bases = nr;
+    return SCCG_OK;
+}
+
+int sccg_walk_range_device(sccg_ctx* ctx, const void* d_ref, size_t nr, const void* d_tgt, size_t nt, int k, int m,
+                           int64_t x0, int64_t P0, int64_t x_end, sccg_records* out, int64_t* exit_state, void* stream) {
+    if (!ctx || !out || !exit_state || (!d_ref && nr) || (!d_tgt && nt)) return SCCG_E_INVALID;
+    memset(out, 0, sizeof *out);
+    HIPTRY(hipSetDevice(ctx->device));
+    global_prepare_reset();   // buffers shared with compress: never reuse its preparation
+    return walk_range_dev(ctx, (const uint8_t*)d_ref, (int64_t)nr, (const uint8_t*)d_tgt, (int64_t)nt, k, m, x0, P0, x_end,
+                          out, exit_state, stream ? (hipStream_t)stream : ctx->stream);
+}
+
+int sccg_walk_range(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, size_t nt, int k, int m, int64_t x0,
+                    int64_t P0, int64_t x_end, sccg_records* out, int64_t* exit_state) {
+    if (!ctx || !out || !exit_state || (!sr && nr) || (!st && nt)) return SCCG_E_INVALID;
+    memset(out, 0, sizeof *out);
+    HIPTRY(hipSetDevice(ctx->device));
+    global_prepare_reset();
+    hipStream_t s = ctx->stream;
+    GET(uint8_t, R, B_RP, nr + 64);
+    GET(uint8_t, T, B_TP, nt + 64);
+    if (nr) HIPTRY(hipMemcpyAsync(R, sr, nr, hipMemcpyHostToDevice, s));
+    if (nt) HIPTRY(hipMemcpyAsync(T, st, nt, hipMemcpyHostToDevice, s));
+    return walk_range_dev(ctx, R, (int64_t)nr, T, (int64_t)nt, k, m, x0, P0, x_end, out, exit_state, s);
+}
+
 int sccg_match(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, size_t nt, int k, int m, int global,
                int64_t offset, sccg_records* out) {
     if (!ctx || !out || (!sr && nr) || (!st && nt)) return SCCG_E_INVALID;

@@ -97,6 +97,8 @@ constexpr int32_t CHAIN_MCAP = 1 << 22;   // matches a chain may take
 #define SCCG_CH_GENS_PER_SYNC 4
 #endif
 constexpr int CH_GENS_PER_SYNC = SCCG_CH_GENS_PER_SYNC;    // generations queued per host check
+constexpr int ROUND_BATCH_DEFAULT = 1;   // rounds queued per host readback from ROUND_BATCH_FROM on (1: off; A/B pending)
+constexpr int ROUND_BATCH_FROM = 4;
 constexpr int FF_MIN_CHUNKS = 8;       // frozen-first start: chunk 0's walk stuck for at least this many chunks
 // SCCG_RECHUNK=1 (opt-in): a frozen-first (stuck, literal-heavy: T2T-like) target is walked again
 // in chunks of FF_CHUNK bases.  Its divergent stretches hold ~400 short matches per 16 Ki chunk,
@@ -131,6 +133,9 @@ struct WalkPtrs {
     const uint8_t* T;
     int32_t nR, nT, k, m, S, C, cap;
     int32_t kp;               // key length: min(k, KEY_K); k > KEY_K confirms the rest by extension (KEY_K)
+    // the target range the chunks cover: [xlo, xhi) (the whole T' = [0, nT) except for a range walk,
+    // sccg_walk_range: the walk from a given state stops at the first index >= xhi)
+    int32_t xlo, xhi;
     int32_t* bt[2];
     int32_t* bp[2];
     int32_t* bl[2];
@@ -165,7 +170,9 @@ struct WalkPtrs {
     int32_t* flist;       // committed frozen chunks of the round
     int32_t* fy;          // per listed frozen chunk: first window hit after its exit (k_frozen_scan)
     int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round,
-                          // [5] frozen count, [6] frozen-scan first hit
+                          // [5] frozen count, [6] frozen-scan first hit, [9] void round, [11] carry count,
+                          // [12] trapped triggers of the round end
+    int32_t* trig;        // the round end's trapped triggers (RESPEC_MAX_TRIGGERS)
     uint64_t* atab;
     uint32_t agen;            // anchor tag generation (one per call)
     int32_t round;            // walk round of the launch (kernel argument copy)
@@ -205,6 +212,13 @@ struct WalkPtrs {
     uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
     int32_t dbg_phases;       // SCCG_DEBUG_PHASES: also per-phase clocks
 };
+
+// chunk j's target range [lo, hi)
+__device__ __forceinline__ int32_t chunk_lo(const WalkPtrs& A, int32_t j) { return A.xlo + j * A.S; }
+__device__ __forceinline__ int32_t chunk_hi(const WalkPtrs& A, int32_t j) {
+    const int32_t lo = A.xlo + j * A.S;
+    return lo + A.S < A.xhi ? lo + A.S : A.xhi;
+}
 
 // Per-wave LDS: the window's Bloom filter (wide literal scans) and a copy of the last 2 KiB the
 // extension loaded from R' and from T'.  A match step reads its next window (R' around the new P),
@@ -523,12 +537,14 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     const int32_t li = (int32_t)blockIdx.x * WWPB + w;
     if (nlist_dev) nlist = *nlist_dev;
     if (CARRY && nlist > A.C) nlist = A.C;
+    // the round's frozen list starts empty (also when nothing is listed: a round queued blind)
+    if (!CARRY && blockIdx.x == 0 && threadIdx.x == 0 && !A.scal[9]) A.scal[5] = 0;
     if (li >= nlist || A.scal[9]) return;
     WalkLds& L = lds_all[w];
     int32_t j = uni(list[li]);   // (j, lo_j, hi_j ... change when the walk carries on, below)
     const int32_t kind = CARRY ? KIND_FIX : uni(A.kind[j]);
-    int32_t lo_j = j * A.S;
-    int32_t hi_j = (lo_j + A.S < A.nT) ? lo_j + A.S : A.nT;
+    int32_t lo_j = chunk_lo(A, j);
+    int32_t hi_j = chunk_hi(A, j);
     const int32_t lastk = A.nT - A.k;
 
     int32_t x, P, n = 0, q = 0, ob, cb = -1, cc = 0;
@@ -560,7 +576,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
             P = uni(P);
             if (lane == 0) A.guess[j] = P;
         } else {
-            P = uni(A.guess[j]);   // re-speculation (k_round_tail)
+            P = uni(A.guess[j]);   // re-speculation (k_round_respec)
         }
         if (lane == 0) { A.usedX[j] = lo_j; A.usedP[j] = P; }
     } else if (kind == KIND_FIX) {   // result is committed (or discarded) by k_commit
@@ -580,7 +596,6 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     }
     if (!CARRY) {
         if (lane == 0) A.status[j] = ST_OK;
-        if (blockIdx.x == 0 && threadIdx.x == 0) A.scal[5] = 0;   // frozen list of this round's commit
     }
     int32_t x_entry = x, P_entry = P;
     const uint64_t dbg_t0 = DBG ? wall_clock64() : 0;
@@ -821,7 +836,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         if (truncated) return;
         // carry on only from a fix-up whose commit is certain (k_commit takes it: its predecessor is
         // not listed, and -- by the rule below -- not carried into either), and not where the
-        // frozen scan (frozen end) or the trapped re-speculation (k_round_tail) resolves faster
+        // frozen scan (frozen end) or the trapped re-speculation (k_round_respec) resolves faster
         if (kind != KIND_FIX || (j > 0 && uni(A.lround[j - 1]) == A.round)) return;
         if (converged || !exit_changed || frozen_end || trapped) return;
         const int32_t j1 = j + 1;
@@ -855,8 +870,8 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     const int32_t j1 = j + 1;
     if (j1 >= A.C || uni(A.lround[j1]) == A.round || (j1 + 1 < A.C && uni(A.lround[j1 + 1]) == A.round)) return;
     j = j1;
-    lo_j = j * A.S;
-    hi_j = (lo_j + A.S < A.nT) ? lo_j + A.S : A.nT;
+    lo_j = chunk_lo(A, j);
+    hi_j = chunk_hi(A, j);
     scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
     budget_end = scan_end;
     cb = uni(A.cur[j]);
@@ -924,7 +939,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int fbas
     reg_window(A, P, W);
     if (W.n <= 0) return;
     bloom_window(W, L);
-    const int32_t end = A.nT - A.k + 1;
+    const int32_t end = A.nT - A.k + 1 < A.xhi ? A.nT - A.k + 1 : A.xhi;   // (a range walk stops at xhi)
     const int64_t gw = (int64_t)blockIdx.x * WPB + wave_in_block(), G = (int64_t)gridDim.x * WPB;
     for (int64_t base = x0 + gw * 64 * WIDE; base < end; base += G * 64 * WIDE) {
         if (base >= (int64_t)__hip_atomic_load(&A.fy[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
@@ -967,7 +982,7 @@ __device__ void frozen_apply_wave(const WalkPtrs& A, int fbase, int fcap, int32_
             const int32_t q = q0 + lane;
             bool fill = false;
             if (q < A.C) {
-                const int32_t lo = q * A.S, hi = lo + A.S < A.nT ? lo + A.S : A.nT;
+                const int32_t lo = chunk_lo(A, q), hi = chunk_hi(A, q);
                 const int32_t ex = hi < lastk1 ? hi : lastk1;
                 fill = ex <= y;
                 if (fill) {
@@ -1049,66 +1064,55 @@ __global__ void k_spec_rest(WalkPtrs A) {
     }
 }
 
-// The end of a round in one block: the frozen fills of a batch (wave 0), then the chunks whose
-// entry state (predecessor's exit) differs from the one their trajectory used -> plist, scal[0].
-// (SCCG_RT_T=256 builds: 256 threads with 16 chunks each in flight, so the block does not wait for
-// a whole free CU; A/B on the genome bench within noise, chr1 +3-6 %, so 1024 stays)
-#ifndef SCCG_RT_T
-#define SCCG_RT_T 1024
-#endif
-constexpr int RT_T = SCCG_RT_T;
-__global__ __launch_bounds__(RT_T) void k_round_tail(WalkPtrs A, int fbase, int fcap) {
+// The end of a round, three launches (one block over all chunks was a latency-bound loop of
+// ~70 us per round, the fixed cost the stuck T2T-like pairs pay ~100 times):
+//   k_round_fill     one wave: the frozen fills of a batch; resets the pending list and triggers;
+//   k_round_pending  grid, one thread per chunk: the chunks whose entry state (predecessor's exit)
+//                    differs from the one their trajectory used -> plist, scal[0] (list order is
+//                    free: the walk takes the listed chunks in any order);
+//   k_round_respec   one block: re-speculation after the trapped triggers the scan found.
+constexpr int RESPEC_T = 1024;
+__global__ __launch_bounds__(64) void k_round_fill(WalkPtrs A, int fbase, int fcap) {
     if (A.scal[9]) return;   // void pre-queued round
     __shared__ int32_t sj[FROZEN_MAX], sy[FROZEN_MAX];
-    __shared__ int32_t trig[RESPEC_MAX_TRIGGERS];
-    __shared__ int32_t ntrig;
-    if (threadIdx.x < 64 && fcap > 0) frozen_apply_wave(A, fbase, fcap, sj, sy);
-    if (threadIdx.x == 0) { A.scal[0] = 0; ntrig = 0; }
-    __syncthreads();
+    if (fcap > 0) frozen_apply_wave(A, fbase, fcap, sj, sy);
+    if (threadIdx.x == 0) { A.scal[0] = 0; A.scal[12] = 0; }
+}
+
+__global__ __launch_bounds__(256) void k_round_pending(WalkPtrs A) {
+    if (A.scal[9]) return;
     const int32_t next = A.round + 1;
-    // RT_U chunks per thread and step, their state loaded together (one memory round trip per step
-    // instead of one per chunk: the loop is latency-bound)
-    constexpr int RT_U = RT_T >= 1024 ? 8 : 16;
-    const int32_t nthr = (int32_t)blockDim.x;
-    for (int32_t jb = (int32_t)threadIdx.x; jb < A.C; jb += nthr * RT_U) {
-        int32_t ex[RT_U], ep[RT_U], ux[RT_U], up[RT_U], lr[RT_U];
-#pragma unroll
-        for (int u = 0; u < RT_U; u++) {
-            const int32_t j = jb + u * nthr;
-            if (j < A.C) {
-                ex[u] = j ? A.exitX[j - 1] : A.scal[2];
-                ep[u] = j ? A.exitP[j - 1] : A.scal[3];
-                ux[u] = A.usedX[j];
-                up[u] = A.usedP[j];
-                lr[u] = A.lround[j];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < RT_U; u++) {
-            const int32_t j = jb + u * nthr;
-            if (j >= A.C) break;
-            const bool pend = ex[u] != INVALID && !(ex[u] == ux[u] && ep[u] == up[u]);
-            if (!pend) {
-                if (lr[u] == next) A.lround[j] = A.round;   // listed by an earlier batch of this round
-                continue;
-            }
-            A.snapX[j] = ex[u];
-            A.snapP[j] = ep[u];
-            A.kind[j] = KIND_FIX;
-            A.lround[j] = next;
-            A.plist[atomicAdd(&A.scal[0], 1)] = j;
-            if (j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round) {
-                const int t = atomicAdd(&ntrig, 1);
-                if (t < RESPEC_MAX_TRIGGERS) trig[t] = j;
-            }
-        }
+    const int32_t j = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (j >= A.C) return;
+    const int32_t ex = j ? A.exitX[j - 1] : A.scal[2];
+    const int32_t ep = j ? A.exitP[j - 1] : A.scal[3];
+    const int32_t ux = A.usedX[j], up = A.usedP[j], lr = A.lround[j];
+    const bool pend = ex != INVALID && !(ex == ux && ep == up);
+    if (!pend) {
+        if (lr == next) A.lround[j] = A.round;   // listed by an earlier batch of this round
+        return;
     }
-    __syncthreads();
-    // re-speculate the still-speculative chunks after each trapped trigger (see TRAP_P)
+    A.snapX[j] = ex;
+    A.snapP[j] = ep;
+    A.kind[j] = KIND_FIX;
+    A.lround[j] = next;
+    A.plist[atomicAdd(&A.scal[0], 1)] = j;
+    if (j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round) {
+        const int t = atomicAdd(&A.scal[12], 1);
+        if (t < RESPEC_MAX_TRIGGERS) A.trig[t] = j;
+    }
+}
+
+// re-speculate the still-speculative chunks after each trapped trigger (see TRAP_P)
+__global__ __launch_bounds__(RESPEC_T) void k_round_respec(WalkPtrs A) {
+    if (A.scal[9]) return;
+    const int ntrig = A.scal[12];
+    if (!ntrig) return;
+    const int32_t next = A.round + 1;
     const int nt = ntrig < RESPEC_MAX_TRIGGERS ? ntrig : RESPEC_MAX_TRIGGERS;
     const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6), lane = lane_id();
     for (int t = w; t < nt; t += nw) {
-        const int32_t j = trig[t], P = A.snapP[j];
+        const int32_t j = A.trig[t], P = A.snapP[j];
         for (int32_t q0 = j + 1; q0 <= j + RESPEC_AHEAD && q0 < A.C; q0 += 64) {
             const int32_t q = q0 + lane;
             // every chunk after a pending one is unconfirmed, so replacing its trajectory by another
@@ -1125,6 +1129,15 @@ __global__ __launch_bounds__(RT_T) void k_round_tail(WalkPtrs A, int fbase, int 
             if (run != ~0ull) break;
         }
     }
+}
+
+// the three round-end launches (fcap = 0: the pending scan alone)
+int launch_round_end(const WalkPtrs& A, int fbase, int fcap, hipStream_t s) {
+    hipLaunchKernelGGL(k_round_fill, dim3(1), dim3(64), 0, s, A, fbase, fcap);
+    hipLaunchKernelGGL(k_round_pending, dim3(grid_for(A.C, 256)), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_round_respec, dim3(1), dim3(RESPEC_T), 0, s, A);
+    SCCG_HIP(hipGetLastError());
+    return 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1475,7 +1488,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_chain_fill(WalkPtrs A) {
     const int lane = lane_id(), k = A.k;
     const int32_t lastk1 = A.nT - k + 1;
     const int32_t xe = A.chs[1], nm = A.chs[3], x0 = A.chs[9], P0 = A.chs[10];
-    const int32_t lo = q * A.S, hi = lo + A.S < A.nT ? lo + A.S : A.nT;
+    const int32_t lo = chunk_lo(A, q), hi = chunk_hi(A, q);
     const int32_t lo_c = lo < lastk1 ? lo : lastk1, hi_c = hi < lastk1 ? hi : lastk1;
     if (reason == 2 && hi_c > xe) return;   // the chain handed back before this chunk's end
     // walk state at a boundary v: after the last chain match starting before v (or the start)
@@ -2332,6 +2345,8 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.kp = k < KEY_K ? k : KEY_K;
     A.C = (int32_t)((nT + S - 1) / S);
     if (A.C < 1) A.C = 1;
+    A.xlo = 0;
+    A.xhi = (int32_t)nT;
     A.cap = S / k + 4;
     const size_t C = (size_t)A.C, cap = (size_t)A.cap;
     // front: what depends on R' alone (the early sweep fills it before |T'| is known)
@@ -2370,6 +2385,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.frozen = c.take<int32_t>(C); A.flist = c.take<int32_t>(C);
     A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);
+    A.trig = c.take<int32_t>(RESPEC_MAX_TRIGGERS);
     A.flat_off = c.take<int64_t>(C + 1);
     const size_t maxm = (size_t)(nT / k + 2);
     A.ft = c.take<int32_t>(maxm); A.fp = c.take<int32_t>(maxm); A.fl = c.take<int32_t>(maxm);
@@ -2406,7 +2422,7 @@ WalkKernel walk_kernel(const WalkPtrs& A) { return A.dbg ? k_walk<true, false> :
 // (chunks past that stay pending for the next round, as without carrying)
 constexpr int CARRY_GRID = 256;
 int launch_carry(const WalkPtrs& A, hipStream_t s) {
-    PROF_LAUNCH(PROF_WALK_CHAIN, s, (A.dbg ? k_walk<true, true> : k_walk<false, true>), dim3(CARRY_GRID), dim3(64 * WWPB), 0, s, A,
+    PROF_LAUNCH(PROF_WALK_CARRY, s, (A.dbg ? k_walk<true, true> : k_walk<false, true>), dim3(CARRY_GRID), dim3(64 * WWPB), 0, s, A,
                 (const int32_t*)A.clist, 0, (const int32_t*)(A.scal + 11));
     SCCG_HIP(hipGetLastError());
     return 0;
@@ -2714,6 +2730,15 @@ namespace {
 // restart keeps what the first attempt learned or handed out: the exact first step, the caller's
 // resolved text position (EmitTarget::resolve is called once per compress) and round1_queued.
 constexpr int WALK_RECHUNK = -2;
+// A range walk (sccg_walk_range): the global walk from state (x0, P0) until the first index >= x_end
+// (orc_walk_range's contract, compression.cpp:64-161 entered mid-way), on chunks covering
+// [x0, min(x_end, |T'|)).  P0 == -1 (ungated) only at x0 == 0: the usual exact first step.  Chains,
+// the frozen-first probe and the pre-queued device first step are off (accelerations whose
+// bookkeeping assumes the whole target); the frozen scans stop at x_end.
+struct RangeWalk {
+    int64_t x0 = 0, P0 = -1, x_end = 0;
+    int64_t exit_x = 0, exit_P = -1;        // out
+};
 struct Rechunk {
     bool on = false;                        // this is the restart
     bool resolved = false;                  // late_out->resolve was called: its output pointer
@@ -2724,8 +2749,11 @@ struct Rechunk {
 
 int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
                         void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,
-                        bool abs_p, const EmitTarget* late_out, bool keep_flat, Rechunk* rt) {
+                        bool abs_p, const EmitTarget* late_out, bool keep_flat, Rechunk* rt, RangeWalk* rw = nullptr) {
     if (m < 0 || 2 * m + 1 > WCAP || k > KMAX || k < 1) return SCCG_E_UNSUPPORTED;
+    const bool range = rw != nullptr;
+    if (range && (rw->x0 < 0 || rw->P0 < -1 || (rw->P0 == -1 && rw->x0 != 0) || rw->x0 > nTp || rw->P0 >= nRp))
+        return SCCG_E_UNSUPPORTED;
     const Prepared g = g_prep;   // queued by global_prepare (the caller ordered s after it)
     g_prep = Prepared{};
     const bool prepared = g.ws == ws && g.R == Rp && g.T == Tp && g.nR == nRp && g.nT == nTp && g.k == k && g.m == m &&
@@ -2735,9 +2763,27 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
     if (used > ws_bytes) return SCCG_E_INTERNAL;
     res->rounds = 0;
     res->chains = 0;
-    res->chunks = A.C;
     res->n_matches = 0;
     const int32_t lastk = (int32_t)nTp - k;
+    // a range walk's exit when it takes no match: literal steps up to min(x_end, |T'| - k + 1)
+    auto literal_exit = [&](int64_t from) -> int64_t {
+        const int64_t lim = rw->x_end < (int64_t)lastk + 1 ? rw->x_end : (int64_t)lastk + 1;
+        return from < lim ? lim : from;
+    };
+    if (range) {
+        const int64_t xe = rw->x_end < nTp ? rw->x_end : nTp;
+        A.xlo = (int32_t)rw->x0;
+        A.xhi = (int32_t)(xe > rw->x0 ? xe : rw->x0);
+        A.C = (int32_t)(((int64_t)A.xhi - A.xlo + chunk - 1) / chunk);
+        if (A.C < 1) A.C = 1;
+        g_last_n = 0;
+        if (nRp < k || lastk < 0) {   // no k-mer to probe: every step is a literal
+            rw->exit_x = literal_exit(rw->x0);
+            rw->exit_P = rw->P0;
+            return 0;
+        }
+    }
+    res->chunks = A.C;
 
     // ---- anchors -> speculative guesses for chunks 1..C-1 (queued first: they do not depend on
     //      the first step, so the GPU builds them while the host waits for it)
@@ -2769,8 +2815,8 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
         if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fbase_cap), dim3(SCCG_BLOCK), 0, s, A, 0);
-        hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(RT_T), 0, s, A, 0, fbase_cap);
         SCCG_HIP(hipGetLastError());
+        RC(launch_round_end(A, 0, fbase_cap, s));
         return 0;
     };
     static const bool dev_first = getenv("SCCG_HOST_FIRST_STEP") == nullptr;
@@ -2783,7 +2829,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
     const bool dbg_rounds = getenv("SCCG_DEBUG") != nullptr;
     bool pre_round = false, spec_queued = false;
     int32_t rs_pre[6] = {};
-    if (walkable && dev_first && !rt->on && A.C > 0) {
+    if (walkable && dev_first && !rt->on && !range && A.C > 0) {
         hipLaunchKernelGGL(k_walk_init<true>, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s,
                            A, 0, 0);
         A.round = 1;
@@ -2837,7 +2883,8 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
     };
 
     // ---- the exact first (ungated) step: first target position with any candidate
-    if (walkable && rt->on) {   // (a re-chunked restart: found by the first attempt)
+    if (walkable && range && rw->P0 >= 0) {   // (a range walk from a gated state: no first step)
+    } else if (walkable && rt->on) {   // (a re-chunked restart: found by the first attempt)
         first_y = rt->first_y;
         first_p = rt->first_p;
         first_l = rt->first_l;
@@ -2923,7 +2970,12 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
     }
     mark("first_step");
     int32_t startX, startP;
-    if (first_y != INVALID) { startX = first_y + first_l; startP = first_p + first_l - 1; }
+    if (range && rw->P0 >= 0) { startX = (int32_t)rw->x0; startP = (int32_t)rw->P0; }
+    else if (range && (first_y == INVALID || first_y >= rw->x_end)) {   // no match before x_end
+        rw->exit_x = literal_exit(0);
+        rw->exit_P = -1;
+        return 0;
+    } else if (first_y != INVALID) { startX = first_y + first_l; startP = first_p + first_l - 1; }
     else { startX = lastk + 1 > 0 ? lastk + 1 : 0; startP = INVALID; }
 
     // ---- init chunk state
@@ -2939,7 +2991,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
     // The probe is k_frozen_scan on a stand-in entry (chunk 0's exit = the start state), reset after.
     static const bool ff_env = getenv("SCCG_NO_FROZEN_FIRST") == nullptr;
     bool frozen_first = false;
-    if (ff_env && !pre_round && !rt->on && startP != INVALID && lastk >= 0 && A.C >= 2 * FF_MIN_CHUNKS) {
+    if (ff_env && !pre_round && !rt->on && !range && startP != INVALID && lastk >= 0 && A.C >= 2 * FF_MIN_CHUNKS) {
         RC(dev_set_i32(A.flist, 1, {0}, s));
         RC(dev_set_i32(A.exitX, 1, {startX}, s));
         RC(dev_set_i32(A.exitP, 1, {startP}, s));
@@ -2972,30 +3024,51 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         int32_t nlist = frozen_first ? 1 : A.C;   // (k_walk_init listed chunk j at plist[j])
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
         static const bool chains_env = getenv("SCCG_NO_CHAINS") == nullptr;   // (A/B and tests)
-        bool chains_on = chains_env;   // off for the rest of the call after a trapped chain
+        bool chains_on = chains_env && !range;   // off for the rest of the call after a trapped chain
         // with the device first step, rounds 1 and 2 went out before the first readback
         const int64_t round0 = pre_round ? 2 : 1;
+        // Rounds queued blind (SCCG_ROUND_BATCH, from round ROUND_BATCH_FROM on): once the first rounds
+        // settled the bulk, the stuck / trapped targets go on for tens of rounds with few pending
+        // chunks each, and a host readback per round costs as much as the round's kernels.  A
+        // batch queues `batch` whole rounds back to back -- every kernel takes the pending count
+        // from device memory (scal[0], written by the previous round's end; a round with nothing
+        // pending is a handful of empty launches) -- and the host reads the status once, behind the
+        // last.  Frozen chunks beyond the blind batch's FROZEN_FIRST, escalations and chains are
+        // handled after that readback exactly as after a single round: a blind round only leaves
+        // such chunks pending, so the loop's exactness argument is unchanged.
+        static const int round_batch = [] { const char* e = getenv("SCCG_ROUND_BATCH"); const int v = e ? atoi(e) : ROUND_BATCH_DEFAULT; return v >= 1 && v <= 64 ? v : ROUND_BATCH_DEFAULT; }();
+        int batch = 1;
         for (int64_t round = round0;; round++) {
             A.round = (int32_t)round;   // every kernel of the round gets it by value
             const bool queued = pre_round && round == round0;
             if (!queued) {
-                PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(nlist, WWPB)), dim3(64 * WWPB), 0, s, A,
-                            (const int32_t*)A.plist, nlist, (const int32_t*)nullptr);
-                SCCG_HIP(hipGetLastError());
-                RC(launch_carry(A, s));
+                for (int b = 0; b < batch; b++) {
+                    A.round = (int32_t)(round + b);
+                    const bool dev = b > 0;   // the batch's later rounds: list length on the device
+                    const int32_t gl = dev ? A.C : nlist;
+                    PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(gl, WWPB)), dim3(64 * WWPB), 0, s, A,
+                                (const int32_t*)A.plist, gl, dev ? (const int32_t*)A.scal : (const int32_t*)nullptr);
+                    SCCG_HIP(hipGetLastError());
+                    RC(launch_carry(A, s));
+                    // Commit, fill the first frozen runs and find the next round's pending chunks
+                    // without waiting for the host; more frozen chunks and the rare escalated
+                    // (pn2 == 0) ones are handled after the batch's one sync.
+                    hipLaunchKernelGGL(k_commit, dim3(grid_for(gl, 256) > 4096 ? 4096 : grid_for(gl, 256)), dim3(256), 0, s, A,
+                                       (const int32_t*)A.plist, gl, dev ? (const int32_t*)A.scal : (const int32_t*)nullptr);
+                    if (b + 1 < batch) {   // a whole round; the last one's end is queued below
+                        hipLaunchKernelGGL(k_frozen_scan, dim3(256, FROZEN_FIRST), dim3(SCCG_BLOCK), 0, s, A, 0);
+                        RC(launch_round_end(A, 0, FROZEN_FIRST, s));
+                    }
+                }
+                round += batch - 1;
+                A.round = (int32_t)round;
             }
             res->rounds = round;
-            // Commit, fill the first frozen runs and find the next round's pending chunks without
-            // waiting for the host; more frozen chunks and the rare escalated (pn2 == 0) ones are
-            // handled after the round's one sync.
-            if (!queued)
-                hipLaunchKernelGGL(k_commit, dim3(grid_for(nlist, 256) > 4096 ? 4096 : grid_for(nlist, 256)), dim3(256), 0, s, A,
-                                   (const int32_t*)A.plist, nlist, (const int32_t*)nullptr);
             auto frozen_batch = [&](int fbase, int fcap, bool init_fy) -> int {   // no-op past the list
                 if (init_fy) SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.fy, INT32_MAX, fcap, s));
                 if (fcap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fcap), dim3(SCCG_BLOCK), 0, s, A, fbase);
-                hipLaunchKernelGGL(k_round_tail, dim3(1), dim3(RT_T), 0, s, A, fbase, fcap);   // + pending
                 SCCG_HIP(hipGetLastError());
+                RC(launch_round_end(A, fbase, fcap, s));   // fills + pending
                 return 0;
             };
             int32_t rs[6];
@@ -3196,6 +3269,9 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
             }
             if (round == 2 && spec_text && nlist == 0) text_done = true;
             if (!nlist) break;
+            // the next iteration's batch: blind rounds once past the first ones, unless this round
+            // left work only the host resolves (escalations, a chain about to start)
+            batch = (round + 1 >= ROUND_BATCH_FROM && !rs[1]) ? round_batch : 1;
             if (round > 4 * (int64_t)A.C + 16) return SCCG_E_INTERNAL;
             if (late_out && late_out->abandon && late_out->abandon(late_out->user)) return WALK_ABANDONED;
         }
@@ -3245,6 +3321,14 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
     res->n_matches = nm;
     g_last = A;
     g_last_n = nm;
+    if (range) {   // the exit state: the last chunk's (its walk ends at the first index >= x_end)
+        int32_t ex[2];
+        const RbItem it[2] = {{A.exitX + (A.C - 1), &ex[0], 4}, {A.exitP + (A.C - 1), &ex[1], 4}};
+        RC(dev_readback(it, 2, s));
+        rw->exit_x = ex[0];
+        rw->exit_P = ex[1];
+        return 0;
+    }
 
     // ---- record text: literal gap + "(dp,l)" per match, then the tail literal
     RC(resolve_out());   // the caller's text position is known now
@@ -3276,6 +3360,22 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
 }
 
 }  // namespace
+
+int global_walk_range(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk, void* ws,
+                      size_t ws_bytes, int64_t x0, int64_t P0, int64_t x_end, int64_t* exit_x, int64_t* exit_P,
+                      WalkResult* res, hipStream_t s) {
+    global_prepare_reset();
+    Rechunk rt;
+    RangeWalk rw;
+    rw.x0 = x0; rw.P0 = P0; rw.x_end = x_end;
+    int64_t tl = 0;
+    const int rc = match_and_emit_impl(Rp, nRp, Tp, nTp, k, m, chunk, ws, ws_bytes, nullptr, &tl, res, s, false, nullptr,
+                                       true, &rt, &rw);
+    if (rc) return rc;
+    *exit_x = rw.exit_x;
+    *exit_P = rw.exit_P;
+    return 0;
+}
 
 int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nTp, int k, int m, int chunk,
                           void* ws, size_t ws_bytes, uint8_t* out, int64_t* out_len, WalkResult* res, hipStream_t s,

@@ -89,6 +89,11 @@ def load_library():
     lib.sccg_match.argtypes = [vp, c, sz, c, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64,
                                ctypes.POINTER(Records)]
     lib.sccg_records_free.argtypes = [ctypes.POINTER(Records)]
+    if hasattr(lib, "sccg_walk_range"):
+        lib.sccg_walk_range.argtypes = [vp, c, sz, c, sz, ctypes.c_int, ctypes.c_int, i64, i64, i64,
+                                        ctypes.POINTER(Records), ctypes.POINTER(i64)]
+        lib.sccg_walk_range_device.argtypes = [vp, vp, sz, vp, sz, ctypes.c_int, ctypes.c_int, i64, i64, i64,
+                                               ctypes.POINTER(Records), ctypes.POINTER(i64), vp]
     lib.sccg_reconstruct.argtypes = [vp, c, sz, c, sz, ctypes.POINTER(Buf)]
     lib.sccg_reconstruct_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
     lib.sccg_buf_free.argtypes = [ctypes.POINTER(Buf)]
@@ -238,6 +243,28 @@ class Context:
     def compress_bound_static(ref_len: int, tgt_len: int) -> int:
         """sccg_compress_bound without a context (it needs no device)."""
         return load_library().sccg_compress_bound(ref_len, tgt_len)
+
+    def _walk_out(self, rc: int, recs: Records, ex) -> tuple[list, tuple[int, int]]:
+        if rc:
+            self._err(rc)
+        out = [(recs.t[i], recs.pos[i], recs.len[i]) for i in range(recs.n)]
+        self.lib.sccg_records_free(ctypes.byref(recs))
+        return out, (ex[0], ex[1])
+
+    def walk_range(self, sr: bytes, st: bytes, k: int, m: int, x0: int, p0: int, x_end: int):
+        """The global walk (compression.cpp:64-161) from state (x0, P0) until index >= x_end on the
+        N-erased uppercase R', T' (sccg_walk_range): ([(t, p, l)], (exit index, exit P))."""
+        recs, ex = Records(), (ctypes.c_int64 * 2)()
+        rc = self.lib.sccg_walk_range(self.ptr, sr, len(sr), st, len(st), k, m, x0, p0, x_end, ctypes.byref(recs), ex)
+        return self._walk_out(rc, recs, ex)
+
+    def walk_range_device(self, d_r: int, nr: int, d_t: int, nt: int, k: int, m: int, x0: int, p0: int, x_end: int,
+                          stream: int = 0):
+        """walk_range on device-resident R', T' (sccg_walk_range_device)."""
+        recs, ex = Records(), (ctypes.c_int64 * 2)()
+        rc = self.lib.sccg_walk_range_device(self.ptr, d_r, nr, d_t, nt, k, m, x0, p0, x_end, ctypes.byref(recs), ex,
+                                             stream or None)
+        return self._walk_out(rc, recs, ex)
 
     def match(self, sr: bytes, st: bytes, k: int, m: int, glob: bool, offset: int = 0):
         """match_sequences (compression.cpp:36) -> [(kind, p, l, t)] like the oracle's records."""
