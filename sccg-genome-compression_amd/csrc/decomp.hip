@@ -951,6 +951,54 @@ __device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t 
     if (rl < cl) { l_s = L.st(rl); l_e = L.en(rl); }
     uint64_t lo = 0, hi = 0;
     const int k0 = (int)(oc - o0), k1 = total - o0 < OPT ? (int)(total - o0) : OPT;
+    if (k0 == 0 && k1 == OPT) {
+        // Fast path: the thread's 16 output bytes are at most one '\n' (at knl) and 15-16 sequence
+        // bytes j .. jl-1; when no N-run or lowercase-run boundary falls inside them (runs are
+        // tens to thousands of bases long), they are one unaligned 16-byte LDS read (or all 'N'),
+        // a SWAR tolower and a byte shift -- instead of a per-byte loop with run bookkeeping.
+        const int knl = 50 - col;   // col in [0, 50]: the line's '\n' is output byte knl (if < 16)
+        const int nseq = knl < OPT ? OPT - 1 : OPT;
+        const int64_t jl = j + nseq;
+        const bool allN = n_s <= j && n_e >= jl, noN = n_s >= jl;
+        const bool allL = l_s <= j && l_e >= jl, noL = l_s >= jl;
+        if ((allN || noN) && (allL || noL)) {
+            uint32_t w[4];
+            if (allN) {
+                w[0] = w[1] = w[2] = w[3] = 0x4E4E4E4Eu;   // 'N'
+            } else {
+                const int64_t at = j - n_b - dbase;
+                const uint32_t* sw = reinterpret_cast<const uint32_t*>(sdec) + (at >> 2);
+                const uint32_t sh = (uint32_t)(at & 3);
+                uint32_t v[5];
+#pragma unroll
+                for (int q = 0; q < 5; q++) v[q] = sw[q];
+#pragma unroll
+                for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbyte(v[q + 1], v[q], sh);
+            }
+            if (allL) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {   // tolower of 'A'..'Z' only (bit 7 of a byte set where upper)
+                    const uint32_t x = w[q];
+                    const uint32_t ge_a = ((x | 0x80808080u) - 0x41414141u) & 0x80808080u;   // byte >= 'A' (7-bit)
+                    const uint32_t gt_z = ((x | 0x80808080u) - 0x5B5B5B5Bu) & 0x80808080u;   // byte >= 'Z' + 1
+                    const uint32_t up = ge_a & ~gt_z & ~x;   // (bytes >= 0x80 are no letters)
+                    w[q] = x + (up >> 2);
+                }
+            }
+            uint64_t slo = (uint64_t)w[0] | ((uint64_t)w[1] << 32), shi = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+            if (knl < OPT) {   // bytes from knl on move up by one; '\n' at knl
+                const uint64_t ulo = slo << 8, uhi = (shi << 8) | (slo >> 56);
+                const uint64_t mlo = knl >= 8 ? ~0ull : (knl ? (1ull << (8 * knl)) - 1ull : 0ull);
+                const uint64_t mhi = knl <= 8 ? 0ull : (1ull << (8 * (knl - 8))) - 1ull;
+                slo = (slo & mlo) | (ulo & ~mlo);
+                shi = (shi & mhi) | (uhi & ~mhi);
+                if (knl < 8) slo = (slo & ~(0xffull << (8 * knl))) | ((uint64_t)'\n' << (8 * knl));
+                else shi = (shi & ~(0xffull << (8 * (knl - 8)))) | ((uint64_t)'\n' << (8 * (knl - 8)));
+            }
+            *reinterpret_cast<uint4*>(out + o0) = make_uint4((uint32_t)slo, (uint32_t)(slo >> 32), (uint32_t)shi, (uint32_t)(shi >> 32));
+            return;
+        }
+    }
     for (int k = k0; k < k1; k++) {
         uint32_t c;
         if (col == 50) {
@@ -999,10 +1047,13 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
                                                     const int64_t* __restrict__ ncum, int64_t nn,
                                                     const int32_t* __restrict__ ls, const int32_t* __restrict__ ll,
                                                     int64_t nlr, const int64_t* __restrict__ tab, uint8_t* __restrict__ out) {
-    __shared__ uint32_t sdec_w[OB / 4 + 2];
+    // the tile's decoded bytes from a 16-byte-aligned base, 16 bytes per thread and load, with
+    // 16 bytes of slack for format_out16's unaligned 16-byte reads (dec holds >= 64 bytes of slack)
+    __shared__ uint4 sdec4[(OB + 64) / 16];
     __shared__ int32_t s_ns[OFRUNS], s_ne[OFRUNS], s_ls[OFRUNS], s_le[OFRUNS];
     __shared__ int64_t s_nb[OFRUNS];
     __shared__ int64_t st[2 * TW];
+    uint32_t* sdec_w = reinterpret_cast<uint32_t*>(sdec4);
     const int tid = threadIdx.x;
     const int64_t b = blockIdx.x;   // (a grid-stride loop over blocks: 0.35-0.43 ms instead of 0.27)
     if (tid < 2 * TW) st[tid] = tab[TW * b + tid];
@@ -1012,10 +1063,10 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
     const int64_t l_lo = st[2], l_hi = st[TW + 2] < nlr ? st[TW + 2] + 1 : nlr;
     const int64_t ntot = nn ? ncum[nn - 1] + nl[nn - 1] : 0;
     const bool lds_runs = n_hi - n_lo <= OFRUNS && l_hi - l_lo <= OFRUNS;
-    const int64_t a0 = d0 & ~(int64_t)3;
-    const int64_t nw = (d1 - a0 + 3) >> 2;
-    const uint32_t* decw = reinterpret_cast<const uint32_t*>(dec + a0);
-    for (int64_t i = tid; i < nw; i += 256) sdec_w[i] = decw[i];
+    const int64_t a0 = d0 & ~(int64_t)15;
+    const int64_t n16 = (d1 - a0 + 16 + 15) >> 4;   // <= (OB + 46) / 16
+    const uint4* dec4 = reinterpret_cast<const uint4*>(dec + a0);
+    for (int64_t i = tid; i < n16; i += 256) sdec4[i] = dec4[i];
     if (lds_runs) {
         for (int64_t r = n_lo + tid; r < n_hi; r += 256) {
             const int32_t x = ns[r];

@@ -258,14 +258,45 @@ __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t 
     return r;
 }
 
+// A lane's 64 bytes of a wave tile.  Loaded coalesced (SCCG_STRIP_COALESCED, default): load q of the
+// wave reads the tile's q-th KiB, 16 bytes per lane in lane order (8 cache lines per instruction,
+// against 32 when every lane reads its own 64 contiguous bytes), through the wave's 4 KiB of LDS,
+// from which every lane reads back its 64 contiguous bytes.
+#ifndef SCCG_STRIP_COALESCED
+#define SCCG_STRIP_COALESCED 1
+#endif
+__device__ __forceinline__ void load_lane64(const uint8_t* __restrict__ buf, int64_t n, int64_t off, uint4* __restrict__ tin,
+                                            uint32_t (&w)[SNW]) {
+    const int lane = lane_id();
+    const int64_t t0 = off - (int64_t)lane * SL;   // the wave tile's first byte
+    if (SCCG_STRIP_COALESCED && tin && t0 + STRIP_WTILE <= n && (((uintptr_t)(buf + t0)) & 15) == 0) {
+        const uint4* p = reinterpret_cast<const uint4*>(buf + t0);
+        uint4 v[SNW / 4];
+#pragma unroll
+        for (int q = 0; q < SNW / 4; q++) v[q] = p[64 * q + lane];
+        wave_sync();   // (the previous user of tin is done)
+#pragma unroll
+        for (int q = 0; q < SNW / 4; q++) tin[64 * q + lane] = v[q];
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < SNW / 4; q++) {
+            const uint4 x = tin[4 * lane + q];
+            w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
+        }
+        wave_sync();   // tin is free again (k_strip_write stages its output there)
+    } else {
+        load_words<SNW>(buf, n, off, w);
+    }
+}
+
 // A wave's tile: its words, the byte before it (lane 0's 'prev'), the masks, and each lane's prior
 // line status inside the wave (-1: no line start in the lanes before it).
 template <IngestMode MODE>
 __device__ __forceinline__ StripMasks strip_tile(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n, int64_t h,
                                                  int64_t he, int64_t off, uint32_t (&w)[SNW], int32_t& prior,
-                                                 uint64_t& lsm) {
+                                                 uint64_t& lsm, uint4* tin) {
     const int lane = lane_id();
-    load_words<SNW>(buf, n, off, w);
+    load_lane64(buf, n, off, tin, w);
     uint8_t prev = '\n';
     if (MODE == INGEST_REF) {
         const uint32_t up = (uint32_t)__shfl_up((int)w[SNW - 1], 1, 64) >> 24;
@@ -289,6 +320,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(FilterMode fm, con
                                                               const int64_t* __restrict__ hdr, int64_t* __restrict__ ta,
                                                               int64_t* __restrict__ tb, int64_t* __restrict__ tfa,
                                                               int64_t* __restrict__ tfb, int32_t* __restrict__ tlast) {
+    __shared__ uint4 tin_all[WPB][STRIP_WTILE / 16];
     const int64_t tile = (int64_t)blockIdx.x * WPB + wave_in_block();
     if (tile * STRIP_WTILE >= n) return;
     const int lane = lane_id();
@@ -297,7 +329,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(FilterMode fm, con
     uint32_t w[SNW];
     int32_t prior;
     uint64_t lsm;
-    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm);
+    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm, tin_all[wave_in_block()]);
     // a-bytes of a lane with a prior line start in the wave are resolved now
     const uint64_t ra = (uint64_t)__popcll(r.unknown), rb = (uint64_t)__popcll(r.known);
     const uint64_t rfa = (uint64_t)__popcll(r.unknown & r.fk), rfb = (uint64_t)__popcll(r.known & r.fk);
@@ -447,30 +479,32 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
                                                             const int32_t* __restrict__ tcarry,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
                                                             int32_t* __restrict__ flags) {
-    __shared__ uint32_t stage_all[WPB][STAGE_WORDS];
+    __shared__ uint4 stage_all4[WPB][(STAGE_WORDS + 3) / 4];   // (also the coalesced load's transpose)
     __shared__ uint32_t tab[16];
     if (threadIdx.x < 16) tab[threadIdx.x] = compact_sel(threadIdx.x);
     __syncthreads();
     const int64_t tile = (int64_t)blockIdx.x * WPB + wave_in_block();
     if (tile * STRIP_WTILE >= n) return;
     const int lane = lane_id();
-    uint32_t* st4 = stage_all[wave_in_block()];
+    uint32_t* st4 = reinterpret_cast<uint32_t*>(stage_all4[wave_in_block()]);
     uint8_t* s1 = reinterpret_cast<uint8_t*>(st4);
     const int64_t off = tile * STRIP_WTILE + (int64_t)lane * SL;
     const int64_t h = MODE == INGEST_TGT ? hdr[0] : 0, he = MODE == INGEST_TGT ? hdr[1] : 0;
     uint32_t w[SNW];
     int32_t prior;
     uint64_t lsm;
-    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm);
+    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm, stage_all4[wave_in_block()]);
     if (MODE == INGEST_REF && prior < 0) prior = tcarry[tile];
     const uint64_t keep = r.known | (prior == 1 ? r.unknown : 0ull), fkeep = keep & r.fk;
     const uint32_t c = (uint32_t)__popcll(keep) | ((uint32_t)__popcll(fkeep) << 16);
     const uint32_t incl = wave_incl_add<uint32_t>(c), tot = lane_val(incl, 63);
     const uint32_t ex = incl - c;
     if (flags && __ballot((keep & r.par) != 0) && lane == 0) atomicOr(flags, 1);
-    stage_lane<false>(s1, tab, w, keep, (int)(ex & 0xffff));
-    wave_sync();
-    stage_out(st4, (int)(tot & 0xffff), out, toff[tile]);
+    if (out) {   // (null: only the filtered copy is wanted -- the reconstruction needs R' alone)
+        stage_lane<false>(s1, tab, w, keep, (int)(ex & 0xffff));
+        wave_sync();
+        stage_out(st4, (int)(tot & 0xffff), out, toff[tile]);
+    }
     if (out2) {
         wave_sync();
         stage_lane<true>(s1, tab, w, fkeep, (int)(ex >> 16));

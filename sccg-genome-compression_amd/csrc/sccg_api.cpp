@@ -962,8 +962,7 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     const int64_t nenc = end[li + 2] - start[li + 2];
 
     // ---- reference (decompression.cpp:47-58, 105-110)
-    GET(uint8_t, R, B_R, rn + 64);
-    GET(uint8_t, Rp, B_RP, rn + 64);
+    GET(uint8_t, Rp, B_RP, rn + 64);   // (only R' is read: the strip writes no R here)
     bool n_is_comma = false;
     if (nnl == 1) {
         uint8_t c = 0;
@@ -975,7 +974,7 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     // length |R'| stays on the device, sc[9], until the range check and the parse's readback)
     HIPTRY(hipEventRecord(ctx->ev_fork, s));
     HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 8, nullptr, nullptr,
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, nullptr, sc + 8, nullptr, nullptr,
               n_is_comma ? FILTER_UPPER : FILTER_DROP_UPPERN_ONLY, Rp, 1, ctx->side));
     HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
 

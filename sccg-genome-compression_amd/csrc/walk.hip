@@ -77,6 +77,7 @@ constexpr int32_t RESEED_GAP = 1024;
 constexpr int32_t TRAP_P = 4096;
 constexpr int RESPEC_AHEAD = 256;
 constexpr int RESPEC_MAX_TRIGGERS = 64;
+constexpr int32_t UNGUESSED_LOOKBACK = 64;   // chunks back k_round_pending looks for a diagonal
 constexpr int32_t LONG_GAP = 4096;   // literal gaps of the record text copied grid-wide
 constexpr int32_t CAND_CAP = 65536;  // early sweep: first-k-mer occurrences kept (more: full sweep later)
 // Frozen chains (k_chain_*): a committed frozen chunk's exit state is walked on over the rest of the
@@ -171,8 +172,11 @@ struct WalkPtrs {
     int32_t* fy;          // per listed frozen chunk: first window hit after its exit (k_frozen_scan)
     int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round,
                           // [5] frozen count, [6] frozen-scan first hit, [9] void round, [11] carry count,
-                          // [12] trapped triggers of the round end
+                          // [12] trapped triggers of the round end, [13] frozen fills of the round end
     int32_t* trig;        // the round end's trapped triggers (RESPEC_MAX_TRIGGERS)
+    int32_t* fa_j;        // the round end's frozen fills: chunks fa_j+1 .. fa_l literal with P fa_p (scal[13])
+    int32_t* fa_l;
+    int32_t* fa_p;
     uint64_t* atab;
     uint32_t agen;            // anchor tag generation (one per call)
     int32_t round;            // walk round of the launch (kernel argument copy)
@@ -896,6 +900,16 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
 #undef W_CP
 #undef W_CL
 
+// Invariant shared by k_commit and the carry launch (k_walk<., true>), which commits the chunks it
+// carries into itself: within one round, (1) no chunk is both listed and carried; (2) a carry
+// never enters chunk j + 1 when j + 2 is listed (the carried chunk would change a listed chunk's
+// predecessor in mid-round); (3) a listed chunk's predecessor is neither listed-and-changed unless
+// k_commit sees it (pred_changed below) nor carried (by (2)).  So every commit decision reads a
+// predecessor state that is final for the round, and "take a non-converged fix-up only if the
+// predecessor did not change" stays exact.  tests/test_gpu_walk_range.py forces long carry chains
+// (SCCG_ANCHOR_SHIFT=-2: most speculative guesses wrong) beside frozen and trapped chunks and
+// checks every trajectory against the oracle's sequential walk (orc_walk_range).
+//
 // Commit the fix-ups of a round.  A re-walk that converged is always taken.  One that did not is
 // taken only if its predecessor's exit did not change in this round: otherwise its entry was a
 // stale (possibly garbage) state and adopting it would push that garbage one chunk further every
@@ -926,85 +940,110 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
 // Frozen chunks (committed fix-ups that ended in a long literal run with P unchanged up to their
 // chunk end; k_commit lists them): for each of the first FROZEN_MAX, the first position after its
 // exit whose k-mer key occurs in its window of P, over the whole rest of the target (grid.y picks
-// the frozen chunk; every wave builds its own copy of the window and scans a strided share).
-__global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int fbase) {
-    __shared__ WalkLds lds_all[WPB];
+// the frozen chunk).  A block holds the window's keys (<= 2m+1) and a one-hash 2^17-bit LDS
+// prefilter of them; every thread tests 64 consecutive target positions per step (five aligned
+// 16-byte loads, 2-bit codes, one prefilter bit per position; the rare prefilter hits are checked
+// against the keys), the grid striding over the target so the scan front moves evenly and stops
+// one step after the first hit.  (Round 3: a wave per 1024 positions with a 3-hash Bloom test and
+// 4 waves per CU -- 0.8 ms to scan a 243 Mb target to its end.)  For k > KEY_K a key hit is a
+// superset of a window hit (the first KEY_K bases), which only makes the fills conservative.
+constexpr int FZ_BITS = 17;
+constexpr int FZ_T = 256;
+constexpr unsigned FZ_GRID = 512;
+__global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
+    __shared__ uint32_t fbits[1 << (FZ_BITS - 5)];
+    __shared__ uint32_t wkeys[WCAP];
     if (A.scal[9]) return;   // void pre-queued round
     const int fi = (int)blockIdx.y, f = fbase + fi;
     if (f >= A.scal[5]) return;
+    const int tid = (int)threadIdx.x, kp = A.kp;
     const int32_t j = A.flist[f];
     const int32_t x0 = A.exitX[j], P = A.exitP[j];
-    WalkLds& L = lds_all[wave_in_block()];
-    RegWin W;
-    reg_window(A, P, W);
-    if (W.n <= 0) return;
-    bloom_window(W, L);
+    const int32_t wlo = P - A.m < 0 ? 0 : P - A.m;
+    const int32_t whi = (P + A.m < A.nR - A.k) ? P + A.m : A.nR - A.k;
+    const int nwin = whi - wlo + 1;
+    if (nwin <= 0) return;
+    {
+        uint4* b4 = reinterpret_cast<uint4*>(fbits);
+        for (int i = tid; i < (1 << (FZ_BITS - 5)) / 4; i += FZ_T) b4[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    for (int c = tid; c < nwin; c += FZ_T) {
+        const uint32_t key = walk_key(A.R + wlo + c, kp);
+        wkeys[c] = key;
+        const uint32_t h = slot_hash(key, FZ_BITS);
+        atomicOr(&fbits[h >> 5], 1u << (h & 31));
+    }
+    __syncthreads();
     const int32_t end = A.nT - A.k + 1 < A.xhi ? A.nT - A.k + 1 : A.xhi;   // (a range walk stops at xhi)
-    const int64_t gw = (int64_t)blockIdx.x * WPB + wave_in_block(), G = (int64_t)gridDim.x * WPB;
-    for (int64_t base = x0 + gw * 64 * WIDE; base < end; base += G * 64 * WIDE) {
-        if (base >= (int64_t)__hip_atomic_load(&A.fy[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-        const int32_t seg_end = base + 64 * WIDE < end ? (int32_t)(base + 64 * WIDE) : end;
-        const int32_t y = wide_scan(A, L, W, (int32_t)base, seg_end);
-        if (y < seg_end) {
-            if (lane_id() == 0) atomicMin(&A.fy[fi], y);
+    const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
+    const int64_t g0 = (int64_t)(x0 & ~63);
+    const int64_t gid = (int64_t)blockIdx.x * FZ_T + tid, G = (int64_t)gridDim.x * FZ_T;
+    for (int64_t base = g0 + 64 * gid; base < end; base += 64 * G) {
+        if (base > (int64_t)__hip_atomic_load(&A.fy[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        uint32_t cw[20], acc = 0, dw[20];
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(A.T + base);   // 4 KiB readable slack after T'
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                const uint4 v = src[i];
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int q = 0; q < 4; q++) { cw[4 * i + q] = swar_codes(wv[q], dw[4 * i + q]); acc |= dw[4 * i + q]; }
+            }
+        }
+        int32_t hit = -1;
+#pragma unroll
+        for (int g = 0; g < 4 && hit < 0; g++) {
+            uint64_t code = 0;
+            uint32_t bad = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                code |= (uint64_t)cw[4 * g + i] << (8 * i);
+                if (acc) bad |= nz_bytes(dw[4 * g + i]) << (4 * i);
+            }
+            uint32_t cand = 0;
+#pragma unroll
+            for (int st = 0; st < 16; st++) {
+                const uint32_t key = (uint32_t)(code >> (2 * st)) & MASK;
+                const uint32_t h = slot_hash(key, FZ_BITS);
+                // a k-mer with a non-ACGT byte always goes to the exact check (its key needs the bytes)
+                if (((bad >> st) & KM) || ((fbits[h >> 5] >> (h & 31)) & 1u)) cand |= 1u << st;
+            }
+            while (cand) {
+                const int st = __ffs((int)cand) - 1;
+                cand &= cand - 1;
+                const int64_t y = base + 16 * g + st;
+                if (y < x0 || y >= end) continue;
+                const uint32_t key = ((bad >> st) & KM) ? walk_key(A.T + y, kp) : (uint32_t)(code >> (2 * st)) & MASK;
+                bool in = false;
+                for (int c = 0; c < nwin && !in; c++) in = wkeys[c] == key;
+                if (in) { hit = (int32_t)y; break; }
+            }
+        }
+        if (hit >= 0) {
+            atomicMin(&A.fy[fi], hit);
             return;
         }
     }
 }
 
-// One wave: in chunk order, every frozen chunk of the batch not already covered settles the chunks
-// wholly before its first window hit y as literal-only: entry (min(lo, lastk+1), P), empty
-// trajectory, exit (min(hi, lastk+1), P) -- instead of one chunk per round.  Each fill is
+// The frozen fills of a batch: in chunk order, every frozen chunk of the batch not already covered
+// settles the chunks wholly before its first window hit y as literal-only: entry (min(lo, lastk+1),
+// P), empty trajectory, exit (min(hi, lastk+1), P) -- instead of one chunk per round.  Each fill is
 // consistent on its own (no hit before y), so batches may come in any order; the pending check
 // accepts a filled chunk only when it matches its predecessor's exit.
-__device__ void frozen_apply_wave(const WalkPtrs& A, int fbase, int fcap, int32_t* sj, int32_t* sy) {
-    const int lane = lane_id();
-    int nf = A.scal[5] - fbase;
-    if (nf > fcap) nf = fcap;
-    if (nf <= 0) return;
-    if (lane == 0) {   // insertion sort by chunk
-        for (int f = 0; f < nf; f++) {
-            const int32_t j = A.flist[fbase + f], y = A.fy[f];
-            int i = f;
-            while (i > 0 && sj[i - 1] > j) { sj[i] = sj[i - 1]; sy[i] = sy[i - 1]; i--; }
-            sj[i] = j; sy[i] = y;
-        }
-    }
-    wave_sync();
+// The chunks a frozen chunk j fills are j+1 .. last: exits are nondecreasing in the chunk index, so
+// last is the largest q with min(hi_q, lastk+1) <= y, in closed form.  (Round 3 did the fills
+// chunk by chunk in one wave: 1-1.8 ms per round on the T2T-like chromosomes.)
+__device__ __forceinline__ int32_t fill_last(const WalkPtrs& A, int32_t j, int32_t y) {
     const int32_t lastk1 = A.nT - A.k + 1;
-    int32_t filled_to = -1;
-    for (int f = 0; f < nf; f++) {
-        const int32_t j = sj[f], y = sy[f];
-        if (j <= filled_to || j + 1 >= A.C) continue;
-        const int32_t P = A.exitP[j];
-        int32_t last = j;
-        for (int32_t q0 = j + 1; q0 < A.C; q0 += 64) {
-            const int32_t q = q0 + lane;
-            bool fill = false;
-            if (q < A.C) {
-                const int32_t lo = chunk_lo(A, q), hi = chunk_hi(A, q);
-                const int32_t ex = hi < lastk1 ? hi : lastk1;
-                fill = ex <= y;
-                if (fill) {
-                    A.cnt[A.cur[q]][q] = 0;
-                    A.usedX[q] = lo < lastk1 ? lo : lastk1;
-                    A.usedP[q] = P;
-                    A.exitX[q] = ex;
-                    A.exitP[q] = P;
-                    A.changed[q] = 0;
-                    A.seedq[q] = 0;
-                    A.trapped[q] = 0;
-                }
-            }
-            const unsigned long long fm = __ballot(fill);   // chunks are ordered: a prefix fills
-            if (fm) last = q0 + 63 - __clzll((long long)fm);
-            if (fm != ~0ull) break;
-        }
-        filled_to = last;
-        wave_sync();
-    }
+    const int32_t cap = A.xhi < lastk1 ? A.xhi : lastk1;   // the last chunk's exit
+    if (y >= cap) return A.C - 1;
+    if (y < A.xlo) return j;
+    const int32_t q = (y - A.xlo) / A.S - 1;   // xlo + (q + 1) S <= y (every earlier chunk ends before cap)
+    return q < j ? j : (q > A.C - 1 ? A.C - 1 : q);
 }
-
 // Chunk state before round 1: no trajectory, no exit, never walked; round 1 takes every chunk,
 // chunk 0 exact (a fix-up from the first match's end, with an empty trajectory), the others
 // speculative.
@@ -1072,11 +1111,68 @@ __global__ void k_spec_rest(WalkPtrs A) {
 //                    free: the walk takes the listed chunks in any order);
 //   k_round_respec   one block: re-speculation after the trapped triggers the scan found.
 constexpr int RESPEC_T = 1024;
-__global__ __launch_bounds__(64) void k_round_fill(WalkPtrs A, int fbase, int fcap) {
+// (1) one block: the batch's frozen chunks sorted by chunk (rank sort), and the fills of the ones no
+//     earlier fill covers -> fa_j / fa_l / fa_p, count scal[13]; also resets the pending list
+__global__ __launch_bounds__(FROZEN_MAX) void k_round_fill(WalkPtrs A, int fbase, int fcap) {
     if (A.scal[9]) return;   // void pre-queued round
-    __shared__ int32_t sj[FROZEN_MAX], sy[FROZEN_MAX];
-    if (fcap > 0) frozen_apply_wave(A, fbase, fcap, sj, sy);
-    if (threadIdx.x == 0) { A.scal[0] = 0; A.scal[12] = 0; }
+    __shared__ int32_t rj[FROZEN_MAX], ry[FROZEN_MAX], sj[FROZEN_MAX], sy[FROZEN_MAX];
+    const int t = (int)threadIdx.x;
+    int nf = fcap > 0 ? A.scal[5] - fbase : 0;
+    if (nf > fcap) nf = fcap;
+    if (nf < 0) nf = 0;
+    int32_t j = 0, y = 0;
+    if (t < nf) { j = A.flist[fbase + t]; y = A.fy[t]; rj[t] = j; ry[t] = y; }
+    __syncthreads();
+    if (t < nf) {
+        int r = 0;
+        for (int f = 0; f < nf; f++) r += rj[f] < j || (rj[f] == j && f < t);
+        sj[r] = j;
+        sy[r] = y;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int na = 0;
+        int32_t filled_to = -1;
+        for (int r = 0; r < nf; r++) {
+            const int32_t jr = sj[r];
+            if (jr <= filled_to || jr + 1 >= A.C) continue;
+            const int32_t last = fill_last(A, jr, sy[r]);
+            if (last > jr) { A.fa_j[na] = jr; A.fa_l[na] = last; A.fa_p[na] = A.exitP[jr]; na++; }
+            filled_to = last;
+        }
+        A.scal[13] = na;
+        A.scal[0] = 0;
+        A.scal[12] = 0;
+    }
+}
+
+// (1b) grid, one thread per chunk: apply the fills (ranges disjoint and in chunk order)
+__global__ __launch_bounds__(256) void k_round_fillg(WalkPtrs A) {
+    if (A.scal[9]) return;
+    __shared__ int32_t fj[FROZEN_MAX], fl[FROZEN_MAX], fp[FROZEN_MAX];
+    const int na = A.scal[13];
+    if (!na) return;
+    for (int i = (int)threadIdx.x; i < na; i += 256) { fj[i] = A.fa_j[i]; fl[i] = A.fa_l[i]; fp[i] = A.fa_p[i]; }
+    __syncthreads();
+    const int32_t q = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= A.C) return;
+    int lo = 0, hi = na;   // entries with fj < q
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (fj[mid] < q) lo = mid + 1; else hi = mid;
+    }
+    if (lo == 0 || q > fl[lo - 1]) return;
+    const int32_t P = fp[lo - 1];
+    const int32_t lastk1 = A.nT - A.k + 1;
+    const int32_t lo_q = chunk_lo(A, q), hi_q = chunk_hi(A, q);
+    A.cnt[A.cur[q]][q] = 0;
+    A.usedX[q] = lo_q < lastk1 ? lo_q : lastk1;
+    A.usedP[q] = P;
+    A.exitX[q] = hi_q < lastk1 ? hi_q : lastk1;
+    A.exitP[q] = P;
+    A.changed[q] = 0;
+    A.seedq[q] = 0;
+    A.trapped[q] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_round_pending(WalkPtrs A) {
@@ -1090,6 +1186,27 @@ __global__ __launch_bounds__(256) void k_round_pending(WalkPtrs A) {
     const bool pend = ex != INVALID && !(ex == ux && ep == up);
     if (!pend) {
         if (lr == next) A.lround[j] = A.round;   // listed by an earlier batch of this round
+        // A chunk without a trajectory after its first speculation (no anchor vote anywhere in it:
+        // a tandem array, whose 32-mers all repeat, or an escalated speculation) waits until its
+        // predecessor settles, and a run of them is then resolved one chunk after another.
+        // Speculate it instead from the diagonal of the nearest earlier chunk that has an exit
+        // (<= UNGUESSED_LOOKBACK back): inside an array the walk keeps to one diagonal, and the
+        // window (+-m) around the guess snaps onto it at the first match.  (Exactness is the
+        // loop's: speculation only decides what the next rounds re-walk.)
+        if (j > 0 && ux != NEVER && A.exitX[j] == INVALID) {
+            int32_t r = -1;
+            for (int32_t q = j - 1; q >= 0 && q >= j - UNGUESSED_LOOKBACK; q--)
+                if (A.exitX[q] != INVALID) { r = q; break; }
+            if (r >= 0) {
+                const int64_t d = (int64_t)A.exitP[r] - A.exitX[r] + 1;
+                int64_t gp = (int64_t)chunk_lo(A, j) - 1 + d;
+                gp = gp < 0 ? 0 : (gp > A.nR - 1 ? A.nR - 1 : gp);
+                A.kind[j] = KIND_SPEC;
+                A.guess[j] = (int32_t)gp;
+                A.lround[j] = next;
+                A.plist[atomicAdd(&A.scal[0], 1)] = j;
+            }
+        }
         return;
     }
     A.snapX[j] = ex;
@@ -1133,7 +1250,8 @@ __global__ __launch_bounds__(RESPEC_T) void k_round_respec(WalkPtrs A) {
 
 // the three round-end launches (fcap = 0: the pending scan alone)
 int launch_round_end(const WalkPtrs& A, int fbase, int fcap, hipStream_t s) {
-    hipLaunchKernelGGL(k_round_fill, dim3(1), dim3(64), 0, s, A, fbase, fcap);
+    hipLaunchKernelGGL(k_round_fill, dim3(1), dim3(FROZEN_MAX), 0, s, A, fbase, fcap);
+    if (fcap > 0) hipLaunchKernelGGL(k_round_fillg, dim3(grid_for(A.C, 256)), dim3(256), 0, s, A);
     hipLaunchKernelGGL(k_round_pending, dim3(grid_for(A.C, 256)), dim3(256), 0, s, A);
     hipLaunchKernelGGL(k_round_respec, dim3(1), dim3(RESPEC_T), 0, s, A);
     SCCG_HIP(hipGetLastError());
@@ -1222,7 +1340,11 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
     };
     const int32_t lastk1 = A.nT - k + 1;
     int64_t total = (int64_t)lastk1 - x;
-    if (first_only && total > CH_FF_SPAN * CH_GRID) total = CH_FF_SPAN * CH_GRID;
+    // both modes scan at most CH_GRID * CH_FF_SPAN positions per generation (the next one goes on
+    // from the first position not covered): a band-mode generation ends as soon as P leaves the
+    // band -- after a few chance hits on a stuck stretch -- so scanning the whole rest of the
+    // target (round 3) spent ~0.8 ms per generation on a 243 Mb T2T-like target for hits it never used
+    if (total > CH_FF_SPAN * CH_GRID) total = CH_FF_SPAN * CH_GRID;
     const int64_t end = (int64_t)x + (total > 0 ? total : 0);   // < lastk1: the next generation goes on from end
     int64_t span = total > 0 ? (total + CH_GRID - 1) / CH_GRID : 0;
     span = (span + 15) & ~(int64_t)15;
@@ -2386,6 +2508,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);
     A.trig = c.take<int32_t>(RESPEC_MAX_TRIGGERS);
+    A.fa_j = c.take<int32_t>(FROZEN_MAX); A.fa_l = c.take<int32_t>(FROZEN_MAX); A.fa_p = c.take<int32_t>(FROZEN_MAX);
     A.flat_off = c.take<int64_t>(C + 1);
     const size_t maxm = (size_t)(nT / k + 2);
     A.ft = c.take<int32_t>(maxm); A.fp = c.take<int32_t>(maxm); A.fl = c.take<int32_t>(maxm);
@@ -2814,7 +2937,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         RC(launch_carry(A, s));
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
-        if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fbase_cap), dim3(SCCG_BLOCK), 0, s, A, 0);
+        if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, fbase_cap), dim3(FZ_T), 0, s, A, 0);
         SCCG_HIP(hipGetLastError());
         RC(launch_round_end(A, 0, fbase_cap, s));
         return 0;
@@ -2997,7 +3120,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         RC(dev_set_i32(A.exitP, 1, {startP}, s));
         RC(dev_set_i32(A.scal + 5, 1, {1}, s));
         RC(dev_set_i32(A.fy, 1, {INT32_MAX}, s));
-        hipLaunchKernelGGL(k_frozen_scan, dim3(256, 1), dim3(SCCG_BLOCK), 0, s, A, 0);
+        hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, 1), dim3(FZ_T), 0, s, A, 0);
         SCCG_HIP(hipGetLastError());
         int32_t y0 = INT32_MAX;
         {
@@ -3056,7 +3179,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(gl, 256) > 4096 ? 4096 : grid_for(gl, 256)), dim3(256), 0, s, A,
                                        (const int32_t*)A.plist, gl, dev ? (const int32_t*)A.scal : (const int32_t*)nullptr);
                     if (b + 1 < batch) {   // a whole round; the last one's end is queued below
-                        hipLaunchKernelGGL(k_frozen_scan, dim3(256, FROZEN_FIRST), dim3(SCCG_BLOCK), 0, s, A, 0);
+                        hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, FROZEN_FIRST), dim3(FZ_T), 0, s, A, 0);
                         RC(launch_round_end(A, 0, FROZEN_FIRST, s));
                     }
                 }
@@ -3066,7 +3189,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
             res->rounds = round;
             auto frozen_batch = [&](int fbase, int fcap, bool init_fy) -> int {   // no-op past the list
                 if (init_fy) SCCG_HIP(hipMemsetD32Async((hipDeviceptr_t)A.fy, INT32_MAX, fcap, s));
-                if (fcap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(256, fcap), dim3(SCCG_BLOCK), 0, s, A, fbase);
+                if (fcap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, fcap), dim3(FZ_T), 0, s, A, fbase);
                 SCCG_HIP(hipGetLastError());
                 RC(launch_round_end(A, fbase, fcap, s));   // fills + pending
                 return 0;

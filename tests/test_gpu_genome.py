@@ -1,5 +1,6 @@
-"""GPU parity at full size: BASELINE configs[2] (the whole hg19-vs-hg18 genome, 24 pairs) and the
-100 Mb T2T-like pair (configs[4]'s stuck / literal-heavy path), each record stream against the
+"""GPU parity at full size: BASELINE configs[2] (the whole hg19-vs-hg18 genome, 24 pairs), the
+100 Mb T2T-like pair and configs[4]'s shape at full length (the 24 T2T-like pairs at UCSC lengths:
+the stuck / literal-heavy path), each record stream against the
 sha256 of the REAL reference's output (oracle/_ref = compression.cpp compiled unchanged, run in the
 build container by tests/golden/pin_genome.py -> tests/golden/genome_manifest.json).
 
@@ -147,6 +148,34 @@ def test_poor_speculation_rounds_bounded():
     d = json.loads(out.stdout.strip().splitlines()[-1])
     assert d["sha"] == e["record_sha256"]
     assert d["rounds"] < 64, d
+
+
+def test_t2t_genome_24_pairs_vs_reference(ctx):
+    """BASELINE configs[4]'s shape at FULL size: the 24 T2T-like pairs at UCSC lengths (the stuck,
+    literal-heavy walk of compression.cpp:83-101 and the single global call at :561), each record
+    stream against the sha256 of the compiled reference's output (tests/golden/pin_genome.py,
+    names t2t_chr1 .. t2t_chrY), through the device-resident C ABI as bench.py's t2t_genome leg."""
+    pins = [e for e in _manifest() if e["name"].startswith("t2t_chr")]
+    if len(pins) < 24:
+        pytest.skip(f"T2T genome manifest incomplete ({len(pins)} of 24 pinned)")
+    bad, done = [], {}
+
+    def gen(e):
+        done[e["name"]] = synthlib.synth_pair("t2t", e["ref_len"], e["tgt_len"], e["seed"])
+
+    for b in range(0, len(pins), 6):
+        ths = [threading.Thread(target=gen, args=(e,)) for e in pins[b:b + 6]]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        for e in pins[b:b + 6]:
+            rfa, tfa = done.pop(e["name"])
+            assert hashlib.sha256(tfa).hexdigest() == e["tgt_fa_sha256"], e["name"]
+            rec = _device_compress(ctx, rfa, tfa)
+            if len(rec) != e["record_len"] or hashlib.sha256(rec).hexdigest() != e["record_sha256"]:
+                bad.append(e["name"])
+    assert not bad, bad
 
 
 def test_t2t_like_genome_roundtrip():

@@ -135,3 +135,40 @@ def test_split_walk_gpu_world2(name):
     assert hashlib.sha256(whole).hexdigest() == e["record_sha256"]
     # rank 1 walked its half at least once (and again if its guessed entry was not rank 0's exit)
     assert len(res[1][1]) >= 1
+
+
+def test_carry_chains_under_poor_speculation_vs_oracle():
+    """SCCG_ANCHOR_SHIFT=-2 (a quarter-size anchor table: most chunks' first guesses are wrong)
+    makes the rounds lean on carry chains (k_walk<., true> commits the chunks it carries into)
+    next to frozen (T2T-like) and trapped chunks; the whole walk and walks from mid-states must
+    still be the oracle's sequential walk (orc_walk_range).  A child process: the knob is read
+    once per process."""
+    import subprocess
+    import sys
+    code = (
+        "import json, sys\n"
+        f"sys.path.insert(0, {HERE!r})\n"
+        "import synthlib, oraclelib\n"
+        "from pkg import sccg\n"
+        "c = sccg.Context(0)\n"
+        "out = []\n"
+        "for prof, n, seed in (('hg', 3_000_000, 81), ('t2t', 3_000_000, 82), ('t2t', 6_000_000, 83)):\n"
+        "    rfa, tfa = synthlib.synth_pair(prof, n, n, seed)\n"
+        "    R, T = oraclelib.global_sequences(rfa, tfa)\n"
+        "    full = oraclelib.walk_range(R, T, 14, 100, 0, -1, len(T))\n"
+        "    got = c.walk_range(R, T, 14, 100, 0, -1, len(T))\n"
+        "    rounds = c.stats()['walk_rounds']\n"
+        "    ok = got == full\n"
+        "    m = full[0]\n"
+        "    if m:\n"
+        "        t, p, l = m[len(m) // 2]\n"
+        "        ok = ok and c.walk_range(R, T, 14, 100, t + l, p + l - 1, len(T)) == "
+        "oraclelib.walk_range(R, T, 14, 100, t + l, p + l - 1, len(T))\n"
+        "    out.append((prof, seed, ok, rounds, len(m)))\n"
+        "print(json.dumps(out))\n"
+    )
+    env = dict(os.environ, SCCG_ANCHOR_SHIFT="-2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(ok for _, _, ok, _, _ in res), res
