@@ -4,12 +4,19 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cerrno>
 #include <cstdlib>
 #include <filesystem>
 #include <fstream>
 #include <iostream>
 #include <sstream>
 #include <string>
+#include <vector>
+
+#include <spawn.h>
+#include <sys/wait.h>
+
+extern char** environ;
 
 inline bool slurp(const std::string& path, std::string& out) {
     std::ifstream f(path, std::ios::binary);
@@ -32,4 +39,23 @@ inline int cli_device() {
     const char* e = std::getenv("SCCG_DEVICE");
     if (!e) e = std::getenv("LOCAL_RANK");
     return e ? std::atoi(e) : 0;
+}
+
+// The reference runs 7z through std::system with the paths pasted into a shell string
+// (compression.cpp:308, decompression.cpp:34).  Same command, same stdout/stderr, same status
+// word (the wait status, as std::system returns it; 127 << 8 when 7z cannot be started, as the
+// shell reports it), but as an argv list: a path holding '"', '$(' or '`' is passed as a path,
+// never interpreted by a shell.
+inline int run_argv(const std::vector<std::string>& args) {
+    std::vector<char*> av;
+    for (const std::string& a : args) av.push_back(const_cast<char*>(a.c_str()));
+    av.push_back(nullptr);
+    std::cout.flush();
+    pid_t pid = 0;
+    if (posix_spawnp(&pid, av[0], nullptr, nullptr, av.data(), environ) != 0) return 127 << 8;
+    int status = 0;
+    while (waitpid(pid, &status, 0) < 0) {
+        if (errno != EINTR) return -1;
+    }
+    return status;
 }

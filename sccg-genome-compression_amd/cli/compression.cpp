@@ -82,8 +82,7 @@ int main(int argc, char* argv[]) {
     }
     std::cout << "mode=" << (st.mode_global ? "global" : "local") << " switch=" << st.switch_segment
               << " matches=" << st.n_matches << " bytes=" << st.record_bytes << "\n";
-    const std::string cmd = "7z a -mx=9 \"" + txt + ".7z\" \"" + txt + "\"";
-    const int r = std::system(cmd.c_str());
+    const int r = run_argv({"7z", "a", "-mx=9", txt + ".7z", txt});   // compression.cpp:308
     if (r != 0) {
         std::cerr << "Greska prilikom komprimiranja datoteke 7-zipom: " << r << " !\n";
         return 1;

@@ -17,8 +17,7 @@ int main(int argc, char* argv[]) {
         std::cerr << "Error: " << ex.what() << "\n";
         return 1;
     }
-    const std::string cmd = "7z e \"" + arc + "\" -o\"" + out_dir + "\" -y";
-    if (std::system(cmd.c_str()) != 0) {
+    if (run_argv({"7z", "e", arc, "-o" + out_dir, "-y"}) != 0) {   // decompression.cpp:34
         std::cerr << "Greska pri dekompresiji: " << arc << "\n";
         return 1;
     }

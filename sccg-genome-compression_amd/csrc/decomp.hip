@@ -904,18 +904,20 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
 // ---------------------------------------------------------------------------------------------
 constexpr int OPT = 16, OB = 256 * OPT, OFRUNS = 384;
 constexpr int TW = 5;   // k_out_index entries per block boundary
+constexpr int FMT_U_DEFAULT = 1;
+constexpr bool FMT_NT_DEFAULT = false;
 
 // Block boundaries: output offset o_b = o_first + b * OB clamped to [0, total]; its position
 // j_b = o - o / 51; per boundary [decoded offset d_b of j_b, first N run and first lowercase run
 // ending after j_b, j_b, and (fused path, tko given) the token-table entry holding d_b: the last
 // with o_t <= d_b].  One thread per (boundary, run list).
-__global__ void k_out_index(int64_t nres, int64_t total, int64_t o_first, int64_t nblk, const int32_t* __restrict__ ns,
+__global__ void k_out_index(int64_t nres, int64_t total, int64_t o_first, int64_t nblk, int64_t ob, const int32_t* __restrict__ ns,
                             const int32_t* __restrict__ nl, const int64_t* __restrict__ ncum, int64_t nn,
                             const int32_t* __restrict__ ls, const int32_t* __restrict__ ll, int64_t nlr,
                             const int64_t* __restrict__ tko, const int64_t* __restrict__ d_ntok, int64_t* __restrict__ tab) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * (nblk + 1); i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t b = i >> 1;
-        int64_t o = o_first + b * OB;
+        int64_t o = o_first + b * ob;
         o = o < 0 ? 0 : (o > total ? total : o);
         const int64_t J = o - o / 51;
         if (i & 1) {
@@ -938,7 +940,17 @@ __global__ void k_out_index(int64_t nres, int64_t total, int64_t o_first, int64_
     }
 }
 
-template <typename V>
+template <bool NT>
+__device__ __forceinline__ void store16(uint8_t* p, uint64_t lo, uint64_t hi) {
+    if (NT) {   // streaming store: the output is not read again by this kernel
+        __builtin_nontemporal_store(lo, reinterpret_cast<uint64_t*>(p));
+        __builtin_nontemporal_store(hi, reinterpret_cast<uint64_t*>(p) + 1);
+    } else {
+        *reinterpret_cast<uint4*>(p) = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+    }
+}
+
+template <typename V, bool NT = false>
 __device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t nres, const uint8_t* sdec, int64_t dbase,
                                              const V& N, int64_t cn, int64_t ntot, const V& L, int64_t cl, uint8_t* out) {
     const int64_t oc = o0 < 0 ? 0 : o0;
@@ -995,7 +1007,7 @@ __device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t 
                 if (knl < 8) slo = (slo & ~(0xffull << (8 * knl))) | ((uint64_t)'\n' << (8 * knl));
                 else shi = (shi & ~(0xffull << (8 * (knl - 8)))) | ((uint64_t)'\n' << (8 * (knl - 8)));
             }
-            *reinterpret_cast<uint4*>(out + o0) = make_uint4((uint32_t)slo, (uint32_t)(slo >> 32), (uint32_t)shi, (uint32_t)(shi >> 32));
+            store16<NT>(out + o0, slo, shi);
             return;
         }
     }
@@ -1025,7 +1037,7 @@ __device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t 
     }
     (void)nres;
     if (k0 == 0 && k1 == OPT) {
-        *reinterpret_cast<uint4*>(out + o0) = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+        store16<NT>(out + o0, lo, hi);
     } else {
         for (int k = k0; k < k1; k++) out[o0 + k] = (uint8_t)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xff);
     }
@@ -1042,6 +1054,9 @@ struct GlobalRunsAt {
     __device__ int64_t nb(int64_t r) const { return b ? b[a + r] : 0; }
 };
 
+// U: 16-byte outputs per thread (a block owns U * OB output bytes: fewer, larger dependent load
+// phases per byte); NT: streaming stores for the output.
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ dec, int64_t nres, int64_t total, int64_t o_first,
                                                     const int32_t* __restrict__ ns, const int32_t* __restrict__ nl,
                                                     const int64_t* __restrict__ ncum, int64_t nn,
@@ -1049,7 +1064,7 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
                                                     int64_t nlr, const int64_t* __restrict__ tab, uint8_t* __restrict__ out) {
     // the tile's decoded bytes from a 16-byte-aligned base, 16 bytes per thread and load, with
     // 16 bytes of slack for format_out16's unaligned 16-byte reads (dec holds >= 64 bytes of slack)
-    __shared__ uint4 sdec4[(OB + 64) / 16];
+    __shared__ uint4 sdec4[(U * OB + 64) / 16];
     __shared__ int32_t s_ns[OFRUNS], s_ne[OFRUNS], s_ls[OFRUNS], s_le[OFRUNS];
     __shared__ int64_t s_nb[OFRUNS];
     __shared__ int64_t st[2 * TW];
@@ -1064,9 +1079,14 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
     const int64_t ntot = nn ? ncum[nn - 1] + nl[nn - 1] : 0;
     const bool lds_runs = n_hi - n_lo <= OFRUNS && l_hi - l_lo <= OFRUNS;
     const int64_t a0 = d0 & ~(int64_t)15;
-    const int64_t n16 = (d1 - a0 + 16 + 15) >> 4;   // <= (OB + 46) / 16
+    const int64_t n16 = (d1 - a0 + 16 + 15) >> 4;   // <= (U * OB + 46) / 16
     const uint4* dec4 = reinterpret_cast<const uint4*>(dec + a0);
-    for (int64_t i = tid; i < n16; i += 256) sdec4[i] = dec4[i];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int64_t i = tid + 256 * u;
+        if (i < n16) sdec4[i] = dec4[i];
+    }
+    if (U * 256 + tid < n16) sdec4[U * 256 + tid] = dec4[U * 256 + tid];
     if (lds_runs) {
         for (int64_t r = n_lo + tid; r < n_hi; r += 256) {
             const int32_t x = ns[r];
@@ -1082,13 +1102,16 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
     }
     __syncthreads();
     const uint8_t* sdec = reinterpret_cast<const uint8_t*>(sdec_w);
-    const int64_t o0 = o_first + b * OB + (int64_t)tid * OPT;
-    if (lds_runs) {
-        const LdsRuns N{s_ns, s_ne, s_nb}, L{s_ls, s_le, nullptr};
-        format_out16(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
-    } else {
-        const GlobalRunsAt N{ns, nl, ncum, n_lo}, L{ls, ll, nullptr, l_lo};
-        format_out16(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int64_t o0 = o_first + b * (U * OB) + (int64_t)(u * 256 + tid) * OPT;
+        if (lds_runs) {
+            const LdsRuns N{s_ns, s_ne, s_nb}, L{s_ls, s_le, nullptr};
+            format_out16<LdsRuns, NT>(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
+        } else {
+            const GlobalRunsAt N{ns, nl, ncum, n_lo}, L{ls, ll, nullptr, l_lo};
+            format_out16<GlobalRunsAt, NT>(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
+        }
     }
 }
 
@@ -1579,8 +1602,20 @@ int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns
     if (fz || !span_path) {
         const int64_t total = nres + (nres - 1) / 50;   // the final '\n' is the caller's
         const int64_t o_first = -(int64_t)((uintptr_t)d_out & 15);
-        const int64_t nblk = (total - o_first + OB - 1) / OB;
-        hipLaunchKernelGGL(k_out_index, dim3(grid_for(2 * (nblk + 1), 256)), dim3(256), 0, s, nres, total, o_first, nblk,
+        // output bytes per k_format_out block (U * OB; the fused and pipelined formatters use OB)
+        static const int fmt_u = [] {
+            const char* e = getenv("SCCG_FMT_U");
+            const int u = e ? atoi(e) : FMT_U_DEFAULT;
+            return u == 1 || u == 2 || u == 4 ? u : FMT_U_DEFAULT;
+        }();
+        static const bool fmt_nt = [] {
+            const char* e = getenv("SCCG_FMT_NT");
+            return e ? atoi(e) != 0 : FMT_NT_DEFAULT;
+        }();
+        const bool pipe = getenv("SCCG_FMT_PIPE") != nullptr;
+        const int64_t ob = (fz || pipe) ? OB : (int64_t)fmt_u * OB;
+        const int64_t nblk = (total - o_first + ob - 1) / ob;
+        hipLaunchKernelGGL(k_out_index, dim3(grid_for(2 * (nblk + 1), 256)), dim3(256), 0, s, nres, total, o_first, nblk, ob,
                            (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
                            (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, fz ? (const int64_t*)fz->tk.o : nullptr,
                            fz ? fz->d_ntok : nullptr, d_span);
@@ -1594,7 +1629,6 @@ int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns
             return 0;
         }
         // (SCCG_FMT_PIPE=1, A/B runs: the resident pipelined grid; measured slower)
-        static const bool pipe = getenv("SCCG_FMT_PIPE") != nullptr;
         if (pipe) {
             static const int cus = [] {
                 int dev = 0, n = 0;
@@ -1618,9 +1652,14 @@ int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns
             SCCG_HIP(hipGetLastError());
             return 0;
         }
-        PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_out, dim3((unsigned)nblk), dim3(256), 0, s, d_dec, nres, total, o_first,
-                    (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
-                    (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out);
+#define SCCG_FMT_LAUNCH(U, NT)                                                                                       \
+    PROF_LAUNCH(PROF_DC_FORMAT, s, (k_format_out<U, NT>), dim3((unsigned)nblk), dim3(256), 0, s, d_dec, nres, total, o_first, \
+                (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,                          \
+                (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out)
+        if (fmt_u == 1) { if (fmt_nt) SCCG_FMT_LAUNCH(1, true); else SCCG_FMT_LAUNCH(1, false); }
+        else if (fmt_u == 2) { if (fmt_nt) SCCG_FMT_LAUNCH(2, true); else SCCG_FMT_LAUNCH(2, false); }
+        else { if (fmt_nt) SCCG_FMT_LAUNCH(4, true); else SCCG_FMT_LAUNCH(4, false); }
+#undef SCCG_FMT_LAUNCH
         SCCG_HIP(hipGetLastError());
         return 0;
     }

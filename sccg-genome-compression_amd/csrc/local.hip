@@ -430,6 +430,8 @@ __device__ __forceinline__ int32_t seg_count(int64_t nR, int64_t nT) {
     return n >= INT32_MAX / 2 ? 0 : (int32_t)n;   // beyond int positions: the host reports it
 }
 
+constexpr int LOCAL_STAGE1_DEFAULT = 64;   // segments of launch_local_all's first stage
+
 #ifndef LOCAL_WAVES_PER_EU
 #define LOCAL_WAVES_PER_EU 4   // the LDS allows 4 waves/SIMD (4 blocks of SegLds x 4); VGPRs must fit 128
 #endif
@@ -437,15 +439,17 @@ template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_all(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
                                                           const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
                                                           uint32_t* __restrict__ recs, SegStat* __restrict__ stat,
-                                                          int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl) {
+                                                          int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl,
+                                                          int32_t seg_lo, int32_t seg_hi) {
     __shared__ SegLds lds_all[WPB];
     const int64_t nR = *dnR, nT = *dnT;
-    const int32_t nseg = seg_count(nR, nT);
+    const int32_t nseg_all = seg_count(nR, nT);
+    const int32_t nseg = nseg_all < seg_hi ? nseg_all : seg_hi;
     const int w = wave_in_block(), lane = lane_id();
     SegLds& L = lds_all[w];
     const int32_t G = (int32_t)gridDim.x * WPB;
     SegWords cur, nxt;
-    int32_t seg = (int32_t)blockIdx.x * WPB + w;
+    int32_t seg = seg_lo + (int32_t)blockIdx.x * WPB + w;
     if (seg < nseg) seg_words_load(cur, seg, R, nR, T, nT);
     for (; seg < nseg; seg += G) {
         if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
@@ -461,7 +465,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
         // classes of seg-4 .. seg+4 (lane i holds seg-4+i; -1 = not published in this call)
         const int32_t idx = seg - 4 + lane;
         int v = -1;
-        if (lane < 9 && lane != 4 && idx >= 0 && idx < nseg) {
+        if (lane < 9 && lane != 4 && idx >= 0 && idx < nseg_all) {
             const int32_t t = __hip_atomic_load(&cls[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             v = (t >> 2) == gen ? (t & 3) : -1;
         }
@@ -671,14 +675,28 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
         if (bpc >= 1 && bpc < per) per = bpc;
         return (unsigned)(cus * per);
     }();
-    unsigned g = grid_for(nseg_max, WPB);
+    // Two stages: segments [0, s1) first, one per wave, then the rest behind them on the stream.  A
+    // switch among the first segments (every hg-like pair: the counter can switch at segment 4 at
+    // the earliest, and does) lowers ctl[1] before the second stage starts, so its waves exit at
+    // once -- instead of ~2 segments for every resident wave (~4,000 segment passes per pair, all
+    // discarded) before segment 4's window completes.  SCCG_LOCAL_STAGE1 = 0: one launch.
+    static const int32_t s1 = [] {
+        const char* e = getenv("SCCG_LOCAL_STAGE1");
+        const int v = e ? atoi(e) : LOCAL_STAGE1_DEFAULT;
+        return v > 0 ? (int32_t)((v + WPB - 1) / WPB * WPB) : 0;
+    }();
+    const int32_t st1 = s1 > 0 && nseg_max > s1 ? s1 : 0;
+    unsigned g = grid_for(nseg_max - st1, WPB);
     if (g > cap) g = cap;
     static const bool dbg = getenv("SCCG_DEBUG") != nullptr;
+    if (st1)
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3((unsigned)(st1 / WPB)), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT,
+                    recs, stat, cls, gen, ctl, 0, st1);
     if (dbg) {
         const unsigned long long z[16] = {};
         SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl);
+                    gen, ctl, st1, INT32_MAX);
         unsigned long long d[16];
         SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
         SCCG_HIP(hipStreamSynchronize(s));
@@ -689,7 +707,7 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
                 d[8] / 100.0, d[9] / 100.0, d[10] / 100.0, d[11] / 100.0, d[12] / 100.0);
     } else {
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl);
+                    gen, ctl, st1, INT32_MAX);
     }
     if (nseg_max > 4) {
         const unsigned gs = grid_for(nseg_max - 4, 256) > 2048 ? 2048 : grid_for(nseg_max - 4, 256);

@@ -417,7 +417,11 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     // header search and both strips run back to back; one sync reads every length (sc[0..9])
     // the reference strips on the side stream beside the target's header search + strip
     global_prepare_reset();
-    HIPTRY(hipEventRecord(ctx->ev_fork, s));
+    // The target's header search (one block) goes first when both inputs are resident: queued
+    // behind the reference strip's grid it waited ~85 us for issue slots on the chr1 pair, and the
+    // target strip -- on the walk's critical path -- waits for it.
+    HIPTRY(hipEventRecord(ctx->ev_fork, s));   // (the side stream forks before the search: no wait on it)
+    if (!rdy) TRY(launch_find_header(tfa, tn, sc, s));
     HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     if (rdy) {
         hipEvent_t e = nullptr;
@@ -430,8 +434,8 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         hipEvent_t e = nullptr;
         if (const int rc = rdy->tgt(rdy->user, &e)) return rc;
         HIPTRY(hipStreamWaitEvent(s, e, 0));
+        TRY(launch_find_header(tfa, tn, sc, s));
     }
-    TRY(launch_find_header(tfa, tn, sc, s));
     HIPTRY(hipEventRecord(ctx->ev_hdr, s));
     TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
     // ---- header + lowercase line (compression.cpp:337-368) and the N line: side2, driven by the

@@ -174,6 +174,7 @@ struct WalkPtrs {
                           // [5] frozen count, [6] frozen-scan first hit, [9] void round, [11] carry count,
                           // [12] trapped triggers of the round end, [13] frozen fills of the round end
     int32_t* trig;        // the round end's trapped triggers (RESPEC_MAX_TRIGGERS)
+    int32_t unguessed_spec;   // SCCG_UNGUESSED_SPEC: k_round_pending speculates chunks left without a trajectory
     int32_t* fa_j;        // the round end's frozen fills: chunks fa_j+1 .. fa_l literal with P fa_p (scal[13])
     int32_t* fa_l;
     int32_t* fa_p;
@@ -949,7 +950,7 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
 // superset of a window hit (the first KEY_K bases), which only makes the fills conservative.
 constexpr int FZ_BITS = 17;
 constexpr int FZ_T = 256;
-constexpr unsigned FZ_GRID = 512;
+constexpr unsigned FZ_GRID = 256;
 __global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
     __shared__ uint32_t fbits[1 << (FZ_BITS - 5)];
     __shared__ uint32_t wkeys[WCAP];
@@ -959,6 +960,7 @@ __global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
     const int tid = (int)threadIdx.x, kp = A.kp;
     const int32_t j = A.flist[f];
     const int32_t x0 = A.exitX[j], P = A.exitP[j];
+    const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
     const int32_t wlo = P - A.m < 0 ? 0 : P - A.m;
     const int32_t whi = (P + A.m < A.nR - A.k) ? P + A.m : A.nR - A.k;
     const int nwin = whi - wlo + 1;
@@ -969,14 +971,17 @@ __global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
     }
     __syncthreads();
     for (int c = tid; c < nwin; c += FZ_T) {
-        const uint32_t key = walk_key(A.R + wlo + c, kp);
+        uint32_t wv[4], bad;
+        uint64_t code;
+        loadw<4>(A.R + wlo + c, wv);   // (R' has 4 KiB of readable slack)
+        pack_codes<4>(wv, code, bad);
+        const uint32_t key = (bad & KM) ? exotic_key(A.R + wlo + c, kp) : (uint32_t)code & MASK;
         wkeys[c] = key;
         const uint32_t h = slot_hash(key, FZ_BITS);
         atomicOr(&fbits[h >> 5], 1u << (h & 31));
     }
     __syncthreads();
     const int32_t end = A.nT - A.k + 1 < A.xhi ? A.nT - A.k + 1 : A.xhi;   // (a range walk stops at xhi)
-    const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
     const int64_t g0 = (int64_t)(x0 & ~63);
     const int64_t gid = (int64_t)blockIdx.x * FZ_T + tid, G = (int64_t)gridDim.x * FZ_T;
     for (int64_t base = g0 + 64 * gid; base < end; base += 64 * G) {
@@ -1192,8 +1197,12 @@ __global__ __launch_bounds__(256) void k_round_pending(WalkPtrs A) {
         // Speculate it instead from the diagonal of the nearest earlier chunk that has an exit
         // (<= UNGUESSED_LOOKBACK back): inside an array the walk keeps to one diagonal, and the
         // window (+-m) around the guess snaps onto it at the first match.  (Exactness is the
-        // loop's: speculation only decides what the next rounds re-walk.)
-        if (j > 0 && ux != NEVER && A.exitX[j] == INVALID) {
+        // loop's: speculation only decides what the next rounds re-walk.)  Opt-in
+        // (SCCG_UNGUESSED_SPEC=1): on the T2T-like genome a wrong-diagonal speculation feeds the
+        // next fix-up a garbage entry whose frozen scan runs to the target's end (chr2 68 ms ->
+        // 0.7 s), and the synthetic tandem-array walk (walk_micro.py dense) kept its 55 rounds --
+        // its chunks do get votes, onto the wrong copies of the 171-bp unit.
+        if (A.unguessed_spec && j > 0 && ux != NEVER && A.exitX[j] == INVALID) {
             int32_t r = -1;
             for (int32_t q = j - 1; q >= 0 && q >= j - UNGUESSED_LOOKBACK; q--)
                 if (A.exitX[q] != INVALID) { r = q; break; }
@@ -2782,6 +2791,8 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
         return e ? atoi(e) : STALE_BUDGET_DEFAULT;
     }();
     A.stale_budget = sb;
+    static const int32_t ug = getenv("SCCG_UNGUESSED_SPEC") != nullptr;
+    A.unguessed_spec = ug;
     return A;
 }
 

@@ -40,6 +40,25 @@ def test_cli_roundtrip(tmp_path):
     assert (dec / "reconstructed_genome.fa").read_bytes() == tfa
 
 
+def test_cli_paths_with_shell_characters(tmp_path):
+    """7z runs from an argv list: an output folder named with '"', '$(' and '`' is used as a path,
+    and nothing in it is executed (the reference pastes it into a shell string)."""
+    rfa, tfa = synthlib.synth_pair("hg", 200_000, 200_500, 32)
+    (tmp_path / "r.fa").write_bytes(rfa)
+    (tmp_path / "t.fa").write_bytes(tfa)
+    out = tmp_path / 'o"$(touch pwned1)`touch pwned2`'
+    p = subprocess.run([os.path.join(BIN, "compression"), str(tmp_path / "r.fa"), str(tmp_path / "t.fa"), str(out)],
+                       env=ENV, capture_output=True, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr
+    assert (out / "compressed_genome.txt.7z").exists()
+    dec = tmp_path / "d$(touch pwned3)"
+    p = subprocess.run([os.path.join(BIN, "decompression"), str(out / "compressed_genome.txt.7z"), str(tmp_path / "r.fa"),
+                        str(dec)], env=ENV, capture_output=True, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr
+    assert (dec / "reconstructed_genome.fa").read_bytes() == tfa
+    assert not any((tmp_path / f"pwned{i}").exists() for i in (1, 2, 3))
+
+
 def test_cli_errors(tmp_path):
     p = subprocess.run([os.path.join(BIN, "compression"), str(tmp_path / "missing.fa"), str(tmp_path / "x.fa"),
                         str(tmp_path / "o")], env=ENV, capture_output=True)
