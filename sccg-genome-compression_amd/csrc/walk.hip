@@ -178,6 +178,9 @@ struct WalkPtrs {
     int32_t* fa_j;        // the round end's frozen fills: chunks fa_j+1 .. fa_l literal with P fa_p (scal[13])
     int32_t* fa_l;
     int32_t* fa_p;
+    int32_t* hintY;       // per chunk: a frozen scan's first window hit of P = hintP in this chunk (-1: none);
+    int32_t* hintP;       // a walk at (x <= hintY, hintP) in the chunk may jump to hintY (all literal steps)
+    int32_t skip_hints;   // SCCG_SKIP_HINTS (default on)
     uint64_t* atab;
     uint32_t agen;            // anchor tag generation (one per call)
     int32_t round;            // walk round of the launch (kernel argument copy)
@@ -232,15 +235,26 @@ __device__ __forceinline__ int32_t chunk_hi(const WalkPtrs& A, int32_t j) {
 // So most steps make no dependent HBM round trip at all; only an extension that runs past the copy
 // loads (and refreshes it).
 constexpr int WFBITS = 14;             // window pre-filter: 16384-bit Bloom filter, 3 hashes
-constexpr int LBV = 2048;              // bytes of R' and of T' kept per wave
+#ifndef WALK_LBV
+#define WALK_LBV 2048
+#endif
+constexpr int LBV = WALK_LBV;          // bytes of R' and of T' kept per wave (one HBM step loads them)
+constexpr int LBW = LBV / 256;         // dwords of each per lane and HBM step
+static_assert(LBW % 8 == 0, "whole 32-byte stretches per lane");
 constexpr int LEAD = 128;              // of which before the extension's start (the next window reaches back m)
+static_assert(LEAD % (4 * LBW) == 0, "the lead is whole lanes' stretches");
 __device__ __forceinline__ uint32_t wf_h1(uint32_t key) { return slot_hash(key, WFBITS); }
 __device__ __forceinline__ uint32_t wf_h2(uint32_t key) { return (key * 0x85EBCA77u) >> (32 - WFBITS); }
 __device__ __forceinline__ uint32_t wf_h3(uint32_t key) { return (key * 0xC2B2AE3Du + 0x27D4EB2Fu) >> (32 - WFBITS); }
+#ifndef WALK_GLDS
+#define WALK_GLDS 0
+#endif
+typedef __attribute__((address_space(1))) void GVoid;
+typedef __attribute__((address_space(3))) void LVoid;
 struct WalkLds {
     uint32_t wbits[1 << (WFBITS - 5)];
-    uint8_t rbuf[LBV + 64];   // R'[rb0, rb0 + LBV)  (+ slack read by the unaligned word loads)
-    uint8_t tbuf[LBV + 64];   // T'[tb0, tb0 + LBV)
+    __attribute__((aligned(16))) uint8_t rbuf[LBV + 64];   // R'[rb0, rb0 + LBV)  (+ slack read by the unaligned word loads)
+    __attribute__((aligned(16))) uint8_t tbuf[LBV + 64];   // T'[tb0, tb0 + LBV)
 };
 // the copy's bases (wave-uniform); NO_BUF: nothing copied yet
 constexpr int32_t NO_BUF = INT32_MIN / 2;
@@ -286,21 +300,23 @@ __device__ __forceinline__ void loadw_sel(bool in_lds, const uint8_t* lds, int32
     }
 }
 
-// first differing byte of two 32-byte stretches (32: none)
-__device__ __forceinline__ int first_diff32(const uint32_t (&r)[8], const uint32_t (&t)[8]) {
-    int pos = 32;
+// first differing byte of two 4*N-byte stretches (4*N: none)
+template <int N>
+__device__ __forceinline__ int first_diff(const uint32_t (&r)[N], const uint32_t (&t)[N]) {
+    int pos = 4 * N;
 #pragma unroll
-    for (int i = 7; i >= 0; i--) {
+    for (int i = N - 1; i >= 0; i--) {
         const uint32_t x = r[i] ^ t[i];
         if (x) pos = 4 * i + (__builtin_ctz(x) >> 3);
     }
     return pos;
 }
+__device__ __forceinline__ int first_diff32(const uint32_t (&r)[8], const uint32_t (&t)[8]) { return first_diff<8>(r, t); }
 
 // longest common extension of R[a..] and T[b..], at most maxlen bytes (extend_alignment,
-// compression.cpp:27-34); whole wave.  First from the LDS copy when both starts lie in it; then
-// from HBM, 2 KiB per round trip (lanes 0-3 load the LEAD bytes before the stretch compared), every
-// HBM step leaving its bytes in the copy.
+// compression.cpp:27-34); whole wave.  First from the LDS copy when both starts lie in it (2 KiB
+// per pass); then from HBM, LBV bytes per round trip (lanes 0-3 load the LEAD bytes before the
+// stretch compared), every HBM step leaving its bytes in the copy.
 __device__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a, int32_t b, int32_t maxlen) {
     const int lane = lane_id();
     if (maxlen <= 0) return 0;
@@ -308,47 +324,91 @@ __device__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a,
     if (a >= B.rb0 && b >= B.tb0 && a < B.rb0 + LBV && b < B.tb0 + LBV) {
         int32_t avail = B.rb0 + LBV - a < B.tb0 + LBV - b ? B.rb0 + LBV - a : B.tb0 + LBV - b;
         if (avail > maxlen) avail = maxlen;
-        const int32_t my = 32 * lane;
-        int32_t e = INT32_MAX;
-        if (my < avail) {
-            uint32_t r[8], t[8];
-            loadw_lds<8>(L.rbuf, a - B.rb0 + my, r);
-            loadw_lds<8>(L.tbuf, b - B.tb0 + my, t);
-            int pos = first_diff32(r, t);
-            if (avail - my < 32 && pos >= avail - my) pos = avail - my == maxlen - my ? avail - my : 32;
-            if (pos < 32) e = my + pos;
-        }
-        const unsigned long long sm = __ballot(e != INT32_MAX);
-        if (sm) {
-            const int32_t m = lane_val(e, first_lane(sm));
-            return m < maxlen ? m : maxlen;
+        for (int32_t base = 0; base < avail; base += 2048) {
+            const int32_t my = base + 32 * lane;
+            int32_t e = INT32_MAX;
+            if (my < avail) {
+                uint32_t r[8], t[8];
+                loadw_lds<8>(L.rbuf, a - B.rb0 + my, r);
+                loadw_lds<8>(L.tbuf, b - B.tb0 + my, t);
+                int pos = first_diff32(r, t);
+                if (avail - my < 32 && pos >= avail - my) pos = avail - my == maxlen - my ? avail - my : 32;
+                if (pos < 32) e = my + pos;
+            }
+            const unsigned long long sm = __ballot(e != INT32_MAX);
+            if (sm) {
+                const int32_t m = lane_val(e, first_lane(sm));
+                return m < maxlen ? m : maxlen;
+            }
         }
         if (avail >= maxlen) return maxlen;
         off = avail;
     }
     while (off < maxlen) {
         const int32_t lead = (a + off >= LEAD && b + off >= LEAD) ? LEAD : 0;
+#if WALK_GLDS
+        // LDS-DMA: the copy's bytes go straight to LDS (no staging registers), from 16-byte aligned
+        // bases at most 15 bytes before the lead; then compared from LDS like the copy above
+        {
+            const int32_t sa = (a + off - lead) & ~15, sb = (b + off - lead) & ~15;
+            wave_sync();   // the copy's previous readers are done
+#pragma unroll
+            for (int i = 0; i < LBV / 1024; i++) {
+                __builtin_amdgcn_global_load_lds((GVoid*)(A.R + sa + 1024 * i + 16 * lane), (LVoid*)(L.rbuf + 1024 * i), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((GVoid*)(A.T + sb + 1024 * i + 16 * lane), (LVoid*)(L.tbuf + 1024 * i), 16, 0, 0);
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the copy has landed
+            wave_sync();
+            B.rb0 = sa;
+            B.tb0 = sb;
+            const int32_t ra = a + off - sa, tb = b + off - sb;
+            int32_t avail = LBV - (ra > tb ? ra : tb);
+            if (avail > maxlen - off) avail = maxlen - off;
+            for (int32_t base = 0; base < avail; base += 2048) {
+                const int32_t my = base + 32 * lane;
+                int32_t e = INT32_MAX;
+                if (my < avail) {
+                    uint32_t r[8], t[8];
+                    loadw_lds<8>(L.rbuf, ra + my, r);
+                    loadw_lds<8>(L.tbuf, tb + my, t);
+                    int pos = first_diff32(r, t);
+                    if (avail - my < 32 && pos > avail - my) pos = avail - my;
+                    if (pos < 32 && my + pos < avail) e = off + my + pos;
+                }
+                const unsigned long long sm = __ballot(e != INT32_MAX);
+                if (sm) {
+                    const int32_t m = lane_val(e, first_lane(sm));
+                    return m < maxlen ? m : maxlen;
+                }
+            }
+            off += avail;
+            continue;
+        }
+#endif
         const int32_t sa = a + off - lead, sb = b + off - lead;
-        uint32_t r[8], t[8];
-        loadw<8>(A.R + sa + 32 * lane, r);
-        loadw<8>(A.T + sb + 32 * lane, t);
+        uint32_t r[LBW], t[LBW];
+        loadw<LBW>(A.R + sa + 4 * LBW * lane, r);
+        loadw<LBW>(A.T + sb + 4 * LBW * lane, t);
         wave_sync();   // the copy's previous readers are done
         {
-            uint4* dr = reinterpret_cast<uint4*>(L.rbuf) + 2 * lane;
-            uint4* dt = reinterpret_cast<uint4*>(L.tbuf) + 2 * lane;
-            dr[0] = make_uint4(r[0], r[1], r[2], r[3]); dr[1] = make_uint4(r[4], r[5], r[6], r[7]);
-            dt[0] = make_uint4(t[0], t[1], t[2], t[3]); dt[1] = make_uint4(t[4], t[5], t[6], t[7]);
+            uint4* dr = reinterpret_cast<uint4*>(L.rbuf) + (LBW / 4) * lane;
+            uint4* dt = reinterpret_cast<uint4*>(L.tbuf) + (LBW / 4) * lane;
+#pragma unroll
+            for (int i = 0; i < LBW / 4; i++) {
+                dr[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+                dt[i] = make_uint4(t[4 * i], t[4 * i + 1], t[4 * i + 2], t[4 * i + 3]);
+            }
         }
         wave_sync();
         B.rb0 = sa;
         B.tb0 = sb;
-        const int32_t rel = 32 * lane - lead;   // this lane's bytes, from a + off
+        const int32_t rel = 4 * LBW * lane - lead;   // this lane's bytes, from a + off
         int32_t e = INT32_MAX;
-        if (rel >= 0 && rel < maxlen - off) {
-            int pos = first_diff32(r, t);
+        if (rel >= 0 && rel < maxlen - off) {   // (LEAD is whole lanes' stretches: no lane straddles a + off)
+            int pos = first_diff<LBW>(r, t);
             const int32_t lim = maxlen - off - rel;
-            if (lim < 32 && pos > lim) pos = lim;
-            if (pos < 32) e = off + rel + pos;
+            if (lim < 4 * LBW && pos > lim) pos = lim;
+            if (pos < 4 * LBW) e = off + rel + pos;
         }
         const unsigned long long sm = __ballot(e != INT32_MAX);
         if (sm) {
@@ -479,47 +539,132 @@ __device__ void bloom_window(const RegWin& W, WalkLds& L) {
 // positions per wave step: 16 consecutive per lane, keys by shifting one packed code word; the
 // Bloom filter passes a superset, confirmed exactly against the register window in position order).
 constexpr int WIDE = 16;   // positions per lane per step (1024 per wave step)
-__device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, const RegWin& W, int32_t x, int32_t end) {
+#ifndef WIDE_DEPTH
+#define WIDE_DEPTH 1       // steps whose words are in flight ahead of the one tested
+#endif
+// one step's 1024 positions from base: first hit (exact), or -1
+__device__ __forceinline__ int32_t wide_step(const WalkPtrs& A, const WalkLds& L, const RegWin& W, int32_t base, int32_t end,
+                                             const uint32_t (&w)[8]) {
     const int lane = lane_id(), k = A.kp;
     const uint32_t MASK = (1u << (2 * k)) - 1u, KM = (1u << k) - 1u;
-    uint32_t w[8];   // 32 bytes >= WIDE + k - 1; the next step's words are loaded one step ahead
-    loadw<8>(A.T + x + WIDE * lane, w);
-    for (int32_t base = x; base < end; base += 64 * WIDE) {
-        const int32_t p0 = base + WIDE * lane;
-        uint64_t code;
-        uint32_t bad;
-        pack_codes<8>(w, code, bad);
-        if (base + 64 * WIDE < end) loadw<8>(A.T + p0 + 64 * WIDE, w);
-        // Bloom test for all 16 positions (independent LDS reads)
-        uint32_t cand = 0;
+    const int32_t p0 = base + WIDE * lane;
+    uint64_t code;
+    uint32_t bad;
+    pack_codes<8>(w, code, bad);
+    // Bloom test for all 16 positions (independent LDS reads)
+    uint32_t cand = 0;
 #pragma unroll
-        for (int st = 0; st < WIDE; st++) {
-            const uint32_t key = (bad >> st) & KM ? KEY_EXOTIC : (uint32_t)(code >> (2 * st)) & MASK;
-            const uint32_t f1 = wf_h1(key), f2 = wf_h2(key), f3 = wf_h3(key);
-            // exotic k-mers always go to the exact check (their key needs the bytes)
-            if (key == KEY_EXOTIC ||
-                ((L.wbits[f1 >> 5] >> (f1 & 31)) & (L.wbits[f2 >> 5] >> (f2 & 31)) & (L.wbits[f3 >> 5] >> (f3 & 31)) & 1u))
-                cand |= 1u << st;
+    for (int st = 0; st < WIDE; st++) {
+        const uint32_t key = (bad >> st) & KM ? KEY_EXOTIC : (uint32_t)(code >> (2 * st)) & MASK;
+        const uint32_t f1 = wf_h1(key), f2 = wf_h2(key), f3 = wf_h3(key);
+        // exotic k-mers always go to the exact check (their key needs the bytes)
+        if (key == KEY_EXOTIC ||
+            ((L.wbits[f1 >> 5] >> (f1 & 31)) & (L.wbits[f2 >> 5] >> (f2 & 31)) & (L.wbits[f3 >> 5] >> (f3 & 31)) & 1u))
+            cand |= 1u << st;
+    }
+    const int32_t lim = end - p0;
+    if (lim < WIDE) cand &= lim > 0 ? (1u << lim) - 1u : 0u;
+    // exact check of the candidates, lanes in position order
+    for (unsigned long long hm = __ballot(cand != 0); hm; hm &= hm - 1) {
+        const int l = __ffsll((long long)hm) - 1;
+        uint32_t c = lane_val(cand, l);
+        const uint32_t clo = lane_val((uint32_t)code, l), chi = lane_val((uint32_t)(code >> 32), l);
+        const uint32_t cbad = lane_val(bad, l);
+        const uint64_t lc = ((uint64_t)chi << 32) | clo;
+        while (c) {
+            const int st = __ffs((int)c) - 1;
+            c &= c - 1;
+            const int32_t y = base + WIDE * l + st;
+            const uint32_t key = (cbad >> st) & KM ? exotic_key(A.T + y, k) : (uint32_t)(lc >> (2 * st)) & MASK;
+            if (__ballot(win_match(A, W, key, y) != 0)) return y;
         }
-        const int32_t lim = end - p0;
-        if (lim < WIDE) cand &= lim > 0 ? (1u << lim) - 1u : 0u;
-        // exact check of the candidates, lanes in position order
-        for (unsigned long long hm = __ballot(cand != 0); hm; hm &= hm - 1) {
-            const int l = __ffsll((long long)hm) - 1;
-            uint32_t c = lane_val(cand, l);
-            const uint32_t clo = lane_val((uint32_t)code, l), chi = lane_val((uint32_t)(code >> 32), l);
-            const uint32_t cbad = lane_val(bad, l);
-            const uint64_t lc = ((uint64_t)chi << 32) | clo;
-            while (c) {
-                const int st = __ffs((int)c) - 1;
-                c &= c - 1;
-                const int32_t y = base + WIDE * l + st;
-                const uint32_t key = (cbad >> st) & KM ? exotic_key(A.T + y, k) : (uint32_t)(lc >> (2 * st)) & MASK;
-                if (__ballot(win_match(A, W, key, y) != 0)) return y;
-            }
+    }
+    return -1;
+}
+
+// Wide literal scan: first position in [x, end) whose k-mer occurs in the window W, or `end` (1024
+// positions per wave step: 16 consecutive per lane, keys by shifting one packed code word; the
+// Bloom filter passes a superset, confirmed exactly against the register window in position order).
+// The words of the next WIDE_DEPTH steps are in flight while a step is tested.
+__device__ __forceinline__ int32_t wide_scan(const WalkPtrs& A, const WalkLds& L, const RegWin& W, int32_t x, int32_t end) {
+    const int lane = lane_id();
+    uint32_t w[WIDE_DEPTH][8];   // 32 bytes >= WIDE + k - 1 per step
+#pragma unroll
+    for (int d = 0; d < WIDE_DEPTH; d++)
+        if (x + 64 * WIDE * d < end) loadw<8>(A.T + x + 64 * WIDE * d + WIDE * lane, w[d]);
+    for (int32_t base = x; base < end;) {
+#pragma unroll
+        for (int d = 0; d < WIDE_DEPTH; d++) {
+            uint32_t cur[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) cur[i] = w[d][i];
+            const int32_t nb = base + 64 * WIDE * WIDE_DEPTH;
+            if (nb < end) loadw<8>(A.T + nb + WIDE * lane, w[d]);
+            const int32_t y = wide_step(A, L, W, base, end, cur);
+            if (y >= 0) return y;
+            base += 64 * WIDE;
+            if (base >= end) return end;
         }
     }
     return end;
+}
+
+// Long literal scans (WIDE_RING): the words of the next 3 steps stream into LDS by LDS-DMA while a
+// step is tested -- a lone wave scanning a stuck stretch otherwise waits a whole HBM round trip
+// per 1024 positions (the register prefetch is one step deep: deeper costs the walk registers it
+// spills).  The four 1040-byte ring slots reuse the wave's R'/T' copy (invalidated: after a long
+// literal stretch it holds nothing the next step needs).  A slot is read with an inline-asm
+// ds_read after a counted vmcnt wait (a plain LDS read behind LDS-DMA gets a vmcnt(0) from the
+// compiler, which would drain the prefetch every step).  Every exit drains the DMA first.
+#ifndef WIDE_RING
+#define WIDE_RING 0
+#endif
+constexpr int RING_SLOT = 1040;          // 1024 positions + the k - 1 <= 15 bytes after them (16)
+constexpr int32_t RING_MIN = 8192;       // scans at least this long take the ring
+__device__ __forceinline__ uint8_t* ring_slot(WalkLds& L, int i) {
+    return ((i & 2) ? L.tbuf : L.rbuf) + (i & 1) * RING_SLOT;
+}
+__device__ __forceinline__ void ring_issue(const WalkPtrs& A, WalkLds& L, int i, int32_t base) {
+    const int lane = lane_id();
+    uint8_t* slot = ring_slot(L, i);
+    __builtin_amdgcn_global_load_lds((GVoid*)(A.T + base + 16 * lane), (LVoid*)slot, 16, 0, 0);
+    if (lane == 0) __builtin_amdgcn_global_load_lds((GVoid*)(A.T + base + 1024), (LVoid*)(slot + 1024), 16, 0, 0);
+}
+// wait until at most 2 * ahead LDS-DMA instructions are outstanding (each step issues two)
+__device__ __forceinline__ void ring_wait(int ahead) {
+    if (ahead >= 3) __builtin_amdgcn_s_waitcnt(0x0F76);
+    else if (ahead == 2) __builtin_amdgcn_s_waitcnt(0x0F74);
+    else if (ahead == 1) __builtin_amdgcn_s_waitcnt(0x0F72);
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
+}
+__device__ __forceinline__ void ring_read(WalkLds& L, int i, uint32_t (&w)[8]) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint32_t addr = (uint32_t)(size_t)(ring_slot(L, i) + 16 * lane_id());
+    v4u a, b;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)" : "=v"(a), "=v"(b) : "v"(addr) : "memory");
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+__device__ int32_t wide_scan_ring(const WalkPtrs& A, WalkLds& L, BufPos& B, const RegWin& W, int32_t x, int32_t end) {
+    B.rb0 = NO_BUF;   // the copy's space becomes the ring
+    B.tb0 = NO_BUF;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (this wave's earlier LDS accesses are done)
+    wave_sync();
+    const int32_t nsteps = (end - x + 1023) >> 10;
+    for (int d = 0; d < 3 && d < nsteps; d++) ring_issue(A, L, d, x + 1024 * d);
+    int32_t res = end;
+    for (int32_t st = 0; st < nsteps; st++) {
+        if (st + 3 < nsteps) ring_issue(A, L, (st + 3) & 3, x + 1024 * (st + 3));
+        const int32_t left = nsteps - 1 - st;
+        ring_wait(left < 3 ? left : 3);
+        uint32_t w[8];
+        ring_read(L, st & 3, w);
+        const int32_t y = wide_step(A, L, W, x + 1024 * st, end, w);
+        if (y >= 0) { res = y; break; }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // no DMA may land in the copy's space later
+    wave_sync();
+    return res;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -639,6 +784,13 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     int32_t lme = x;   // target index after the last match of this walk (start of the open literal run)
     bool converged = false, escalated = false;
     int32_t scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
+    // a frozen scan found the first window hit of this P in the chunk: the steps before it are
+    // literal (the scan covered every position from the frozen chunk's exit on), so the walk
+    // starts there -- the trajectory and exit are those of the walk from x
+    if (!CARRY && kind == KIND_FIX && A.skip_hints) {
+        const int32_t hy = uni(A.hintY[j]);
+        if (hy > x && hy < scan_end && uni(A.hintP[j]) == P) x = hy;
+    }
     // stale entry (predecessor re-walked in this round): converge within the budget or give up
     const bool stale = !CARRY && A.stale_budget > 0 && kind == KIND_FIX && j > 0 && A.lround[j - 1] == A.round;
     int32_t budget_end = stale && x + A.stale_budget < scan_end ? x + A.stale_budget : scan_end;
@@ -710,7 +862,8 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
                 if (bloomP != P) { bloom_window(W, L); bloomP = P; }
                 if (DBG) tick(10);
                 const int32_t x0 = x;
-                x = wide_scan(A, L, W, x, wend);   // exact: x is a hit (or wend)
+                if (WIDE_RING && wend - x >= RING_MIN) x = wide_scan_ring(A, L, B, W, x, wend);
+                else x = wide_scan(A, L, W, x, wend);   // exact: x is a hit (or wend)
                 if (DBG) { dbg_c[2]++; dbg_c[12] += x - x0; tick(11); }
             }
             continue;
@@ -1084,6 +1237,7 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
         A.lround[j] = 1;
         A.seedq[j] = 0;
         A.trapped[j] = 0;
+        A.hintY[j] = -1;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.scal[0] = 0; A.scal[1] = 0; A.scal[2] = startX; A.scal[3] = startP;
@@ -1143,6 +1297,8 @@ __global__ __launch_bounds__(FROZEN_MAX) void k_round_fill(WalkPtrs A, int fbase
             if (jr <= filled_to || jr + 1 >= A.C) continue;
             const int32_t last = fill_last(A, jr, sy[r]);
             if (last > jr) { A.fa_j[na] = jr; A.fa_l[na] = last; A.fa_p[na] = A.exitP[jr]; na++; }
+            // the chunk holding the hit: a walk in it with this P has only literal steps before sy[r]
+            if (last + 1 < A.C && sy[r] != INT32_MAX) { A.hintY[last + 1] = sy[r]; A.hintP[last + 1] = A.exitP[jr]; }
             filled_to = last;
         }
         A.scal[13] = na;
@@ -2518,6 +2674,8 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.scal = c.take<int32_t>(16);
     A.trig = c.take<int32_t>(RESPEC_MAX_TRIGGERS);
     A.fa_j = c.take<int32_t>(FROZEN_MAX); A.fa_l = c.take<int32_t>(FROZEN_MAX); A.fa_p = c.take<int32_t>(FROZEN_MAX);
+    A.hintY = c.take<int32_t>(C); A.hintP = c.take<int32_t>(C);
+    A.skip_hints = env_int("SCCG_SKIP_HINTS", 1);
     A.flat_off = c.take<int64_t>(C + 1);
     const size_t maxm = (size_t)(nT / k + 2);
     A.ft = c.take<int32_t>(maxm); A.fp = c.take<int32_t>(maxm); A.fl = c.take<int32_t>(maxm);
@@ -3268,7 +3426,8 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                         std::chrono::duration<double, std::milli>(tnow - tprev).count());
                 tprev = tnow;
             }
-            if (dbg && round <= 2) {   // per-chunk cost profile of the rounds' walked chunks
+            static const bool dbg_all = getenv("SCCG_DEBUG_ALLROUNDS") != nullptr;
+            if (dbg && (round <= 2 || dbg_all)) {   // per-chunk cost profile of the rounds' walked chunks
                 constexpr size_t DS = DBG_SLOTS;
                 std::vector<uint64_t> d(C * DS);
                 SCCG_HIP(hipMemcpyAsync(d.data(), A.dbg, C * DS * 8, hipMemcpyDeviceToHost, s));
