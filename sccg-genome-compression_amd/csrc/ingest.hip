@@ -263,7 +263,7 @@ __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t 
 // against 32 when every lane reads its own 64 contiguous bytes), through the wave's 4 KiB of LDS,
 // from which every lane reads back its 64 contiguous bytes.
 #ifndef SCCG_STRIP_COALESCED
-#define SCCG_STRIP_COALESCED 1
+#define SCCG_STRIP_COALESCED 0
 #endif
 __device__ __forceinline__ void load_lane64(const uint8_t* __restrict__ buf, int64_t n, int64_t off, uint4* __restrict__ tin,
                                             uint32_t (&w)[SNW]) {

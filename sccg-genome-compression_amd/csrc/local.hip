@@ -430,7 +430,7 @@ __device__ __forceinline__ int32_t seg_count(int64_t nR, int64_t nT) {
     return n >= INT32_MAX / 2 ? 0 : (int32_t)n;   // beyond int positions: the host reports it
 }
 
-constexpr int LOCAL_STAGE1_DEFAULT = 64;   // segments of launch_local_all's first stage
+constexpr int LOCAL_STAGE1_DEFAULT = 0;    // segments of launch_local_all's first stage
 
 #ifndef LOCAL_WAVES_PER_EU
 #define LOCAL_WAVES_PER_EU 4   // the LDS allows 4 waves/SIMD (4 blocks of SegLds x 4); VGPRs must fit 128

@@ -927,6 +927,21 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
                      int64_t out_cap, int64_t* out_len, bool size_only) {
     hipStream_t s = ctx->stream;
     GET(int64_t, sc, B_SCAL, 64);
+    // ---- reference (decompression.cpp:47-58, 105-110), first, on the side stream beside everything
+    //      that follows: its filter depends on the N line only when that line is exactly "," (then it
+    //      keeps the N's, FILTER_UPPER), so the usual filter starts now and that rare case redoes it
+    //      once the lines are known.  (Its length |R'| stays on the device, sc[9], until the range
+    //      check and the parse's readback.)
+    GET(uint8_t, Rp, B_RP, rn + 64);   // (only R' is read: the strip writes no R here)
+    HIPTRY(hipEventRecord(ctx->ev_fork, s));
+    HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, nullptr, sc + 8, nullptr, nullptr, FILTER_DROP_UPPERN_ONLY, Rp, 1, ctx->side));
+    HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
+    struct JoinSide {   // every exit path: the main stream waits for the strip (a later call reuses Rp)
+        sccg_ctx* c;
+        hipStream_t st;
+        ~JoinSide() { (void)hipStreamWaitEvent(st, c->ev_rstrip, 0); }
+    } join_side{ctx, s};
     // the line ends: one pass collects every '\n' (a record file holds 2-3); more than DC_NL_CAP
     // of them -> four ordered first-match searches
     int64_t nl[4];
@@ -965,8 +980,6 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     const uint8_t* enc = rec + start[li + 2];
     const int64_t nenc = end[li + 2] - start[li + 2];
 
-    // ---- reference (decompression.cpp:47-58, 105-110)
-    GET(uint8_t, Rp, B_RP, rn + 64);   // (only R' is read: the strip writes no R here)
     bool n_is_comma = false;
     if (nnl == 1) {
         uint8_t c = 0;
@@ -974,13 +987,12 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
         TRY(dev_readback(&it, 1, s));
         n_is_comma = c == ',';
     }
-    // the reference strips on the side stream beside the run-line and record-line parses (its
-    // length |R'| stays on the device, sc[9], until the range check and the parse's readback)
-    HIPTRY(hipEventRecord(ctx->ev_fork, s));
-    HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, nullptr, sc + 8, nullptr, nullptr,
-              n_is_comma ? FILTER_UPPER : FILTER_DROP_UPPERN_ONLY, Rp, 1, ctx->side));
-    HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
+    if (n_is_comma) {   // the N line is ",": the reference keeps its N's (redo the strip behind the first)
+        HIPTRY(hipEventRecord(ctx->ev_fork, s));
+        HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+        TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, nullptr, sc + 8, nullptr, nullptr, FILTER_UPPER, Rp, 1, ctx->side));
+        HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
+    }
 
     // ---- record line on side2 (own scratch) beside the run-line parses, which read counts back
     int32_t* d_err = reinterpret_cast<int32_t*>(sc + 40);

@@ -1096,17 +1096,26 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
 // exit whose k-mer key occurs in its window of P, over the whole rest of the target (grid.y picks
 // the frozen chunk).  A block holds the window's keys (<= 2m+1) and a one-hash 2^17-bit LDS
 // prefilter of them; every thread tests 64 consecutive target positions per step (five aligned
-// 16-byte loads, 2-bit codes, one prefilter bit per position; the rare prefilter hits are checked
-// against the keys), the grid striding over the target so the scan front moves evenly and stops
+// 16-byte loads, 2-bit codes, one prefilter bit per position; the prefilter hits -- 0.15 % of the
+// positions, ~6 per wave step -- are checked in a 512-slot LDS hash table of the keys, one or two
+// probes: a linear pass over the 201 keys per prefilter hit serialised every wave step and made
+// the scan 70x slower), the grid striding over the target so the scan front moves evenly and stops
 // one step after the first hit.  (Round 3: a wave per 1024 positions with a 3-hash Bloom test and
 // 4 waves per CU -- 0.8 ms to scan a 243 Mb target to its end.)  For k > KEY_K a key hit is a
 // superset of a window hit (the first KEY_K bases), which only makes the fills conservative.
 constexpr int FZ_BITS = 17;
+constexpr int FZ_TAB_BITS = 9;                 // exact check: the <= WCAP window keys in 512 slots
+constexpr int FZ_TAB = 1 << FZ_TAB_BITS;
+static_assert(FZ_TAB >= 2 * WCAP, "load factor <= 1/2");
+constexpr uint32_t FZ_EMPTY = 0xffffffffu;
+// (an exotic hash key equal to FZ_EMPTY shares a slot value with 0xfffffffe: a key match is then a
+// superset of a window hit, which only makes the scan's first hit conservative)
+__device__ __forceinline__ uint32_t fz_key(uint32_t key) { return key == FZ_EMPTY ? FZ_EMPTY - 1 : key; }
 constexpr int FZ_T = 256;
 constexpr unsigned FZ_GRID = 256;
 __global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
     __shared__ uint32_t fbits[1 << (FZ_BITS - 5)];
-    __shared__ uint32_t wkeys[WCAP];
+    __shared__ uint32_t wtab[FZ_TAB];   // the window's keys, open addressing (FZ_EMPTY: free)
     if (A.scal[9]) return;   // void pre-queued round
     const int fi = (int)blockIdx.y, f = fbase + fi;
     if (f >= A.scal[5]) return;
@@ -1121,6 +1130,7 @@ __global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
     {
         uint4* b4 = reinterpret_cast<uint4*>(fbits);
         for (int i = tid; i < (1 << (FZ_BITS - 5)) / 4; i += FZ_T) b4[i] = make_uint4(0, 0, 0, 0);
+        for (int i = tid; i < FZ_TAB; i += FZ_T) wtab[i] = FZ_EMPTY;
     }
     __syncthreads();
     for (int c = tid; c < nwin; c += FZ_T) {
@@ -1128,10 +1138,13 @@ __global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
         uint64_t code;
         loadw<4>(A.R + wlo + c, wv);   // (R' has 4 KiB of readable slack)
         pack_codes<4>(wv, code, bad);
-        const uint32_t key = (bad & KM) ? exotic_key(A.R + wlo + c, kp) : (uint32_t)code & MASK;
-        wkeys[c] = key;
+        const uint32_t key = fz_key((bad & KM) ? exotic_key(A.R + wlo + c, kp) : (uint32_t)code & MASK);
         const uint32_t h = slot_hash(key, FZ_BITS);
         atomicOr(&fbits[h >> 5], 1u << (h & 31));
+        for (uint32_t t = slot_hash(key, FZ_TAB_BITS);; t = (t + 1) & (FZ_TAB - 1)) {
+            const uint32_t old = atomicCAS(&wtab[t], FZ_EMPTY, key);
+            if (old == FZ_EMPTY || old == key) break;
+        }
     }
     __syncthreads();
     const int32_t end = A.nT - A.k + 1 < A.xhi ? A.nT - A.k + 1 : A.xhi;   // (a range walk stops at xhi)
@@ -1173,9 +1186,13 @@ __global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
                 cand &= cand - 1;
                 const int64_t y = base + 16 * g + st;
                 if (y < x0 || y >= end) continue;
-                const uint32_t key = ((bad >> st) & KM) ? walk_key(A.T + y, kp) : (uint32_t)(code >> (2 * st)) & MASK;
+                const uint32_t key = fz_key(((bad >> st) & KM) ? walk_key(A.T + y, kp) : (uint32_t)(code >> (2 * st)) & MASK);
                 bool in = false;
-                for (int c = 0; c < nwin && !in; c++) in = wkeys[c] == key;
+                for (uint32_t t = slot_hash(key, FZ_TAB_BITS);; t = (t + 1) & (FZ_TAB - 1)) {
+                    const uint32_t v = wtab[t];
+                    if (v == key) { in = true; break; }
+                    if (v == FZ_EMPTY) break;
+                }
                 if (in) { hit = (int32_t)y; break; }
             }
         }

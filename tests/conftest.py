@@ -16,3 +16,19 @@ def pytest_configure(config):
 def golden_cases():
     import goldens
     return goldens.load_cases()
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _torch_hip_first(request):
+    """GPU sessions: torch's HIP runtime is initialised before any library context.  torch ships its
+    own HIP runtime beside the system one that libsccg links; when a library context opens the
+    device first, torch can report "No HIP GPUs are available" later in the same process (seen
+    when a test that uses torch ran after library-only tests)."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.zeros(1, device="cuda:0")
+        except Exception:
+            pass
+    yield

@@ -119,11 +119,12 @@ def test_size_query_reports_range_like_full_decode():
     query (d_out NULL) and the full decode both return SCCG_E_RANGE."""
     import torch
     from pkg import sccg
+    dev = torch.device("cuda", 0)
+    torch.zeros(1, device=dev)   # torch's HIP runtime first (a library context created before it can leave torch without GPUs)
     ctx = sccg.Context(0)
     try:
         rfa = b">r\n" + b"ACGT" * 50 + b"\n"
         for rec in (b"\n,\n(0,20)(500,30)", b">h\n\n(3,2)\n(0,20)(500,30)", b"\n,\nAC(190,20)"):
-            dev = torch.device("cuda", 0)
             d_r = torch.frombuffer(bytearray(rfa), dtype=torch.uint8).to(dev)
             d_c = torch.frombuffer(bytearray(rec), dtype=torch.uint8).to(dev)
             d_o = torch.empty(1 << 16, dtype=torch.uint8, device=dev)
