@@ -128,10 +128,72 @@ __device__ __forceinline__ void seg_words_load(SegWords& W, int64_t seg, const u
     }
 }
 
+// Fast class-0 proof (switch detection only).  A full segment pair whose target is, on one diagonal
+// d of the reference segment, equal but for `mism` bytes: every target position whose k-mer lies
+// inside the overlap and holds none of those bytes has a candidate (the diagonal's own copy), so
+// the walk's literal steps are among the <= K * mism blocked positions, the |d| positions off the
+// overlap and the K - 1 positions at each end of it -- at most B = K * mism + |d| + 2 (K - 1).  When
+// 2 B <= nt the k = 14 pass matches (literals < nt) with a literal ratio <= T1 = 0.5: class 0
+// (compression.cpp:402-416), whatever the records are.  The diagonal comes from three probe k-mers
+// of the target searched in the reference segment's keys (the first k-mer of the hash build,
+// computed anyway).  Only the switch state machine needs the class; a pair that stays local gets
+// these segments' records from a second pass (k_local_pass, pass 3) before its record text.
+constexpr int FAST_NREC = -1;   // SegStat.nrec of a segment classified by the proof (records not written)
+template <int K>
+__device__ __forceinline__ bool fast_class0(const SegLds& L, int nr, int nt, uint64_t code, uint32_t bad) {
+    constexpr uint32_t MASK = (1u << (2 * K)) - 1u, KM = (1u << K) - 1u;
+    const int lane = lane_id();
+    const int p0 = lane * 16, lastr = nr - K;
+    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
+    const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
+    constexpr int PROBES[3] = {40, 480, 920};
+#pragma unroll
+    for (int pi = 0; pi < 3; pi++) {
+        const int sp = PROBES[pi];
+        if (sp + K > nt) continue;
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = t4[(sp >> 2) + i];
+        uint64_t pc;
+        uint32_t pb;
+        pack_codes<4>(w, pc, pb);
+        if (pb & KM) continue;   // (an exotic probe: its key needs the bytes)
+        const uint32_t pkey = (uint32_t)pc & MASK;
+        uint32_t hit = 0;
+#pragma unroll
+        for (int st = 0; st < 16; st++)
+            if (p0 + st <= lastr && !((bad >> st) & KM) && ((uint32_t)(code >> (2 * st)) & MASK) == pkey) hit |= 1u << st;
+        const unsigned long long hm = __ballot(hit != 0);
+        if (!hm) continue;
+        const int fl = first_lane(hm);
+        const int c = fl * 16 + (__builtin_ctz(lane_val(hit, fl)));
+        const int d = c - sp;   // T[j] against R[j + d]
+        const int j0 = d < 0 ? -d : 0, j1 = nt < nr - d ? nt : nr - d;
+        int cnt = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int j = j0 + 16 * lane + 4 * q;
+            if (j >= j1) continue;
+            const int a = j + d;
+            const uint32_t tv = __builtin_amdgcn_alignbyte(t4[(j >> 2) + 1], t4[j >> 2], (uint32_t)(j & 3));
+            const uint32_t rv = __builtin_amdgcn_alignbyte(r4[(a >> 2) + 1], r4[a >> 2], (uint32_t)(a & 3));
+            uint32_t x = tv ^ rv;
+            if (j1 - j < 4) x &= (1u << (8 * (j1 - j))) - 1u;
+            const uint32_t nz = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu | x) & 0x80808080u;   // bytes != 0
+            cnt += __builtin_popcount(nz);
+        }
+        const int mism = wave_sum(cnt);
+        const int bound = K * mism + (d < 0 ? -d : d) + 2 * (K - 1);
+        if (2 * bound <= nt) return true;
+    }
+    return false;
+}
+
 template <int K, bool DBG>
 __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pass, int non_n_prev, int upper,
                                                  const uint8_t* __restrict__ R, int64_t nR, const uint8_t* __restrict__ T,
-                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr) {
+                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr,
+                                                 bool fast = false) {
     const int lane = lane_id();
     const int64_t base = seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
@@ -172,14 +234,26 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     // ---- H: every k-mer of the reference segment (compression.cpp:41-47), counting-sorted by
     //      bucket; lane l owns starts 16l..16l+15
     const int lastr = nr - K;
+    uint64_t code = 0;
+    uint32_t bad = 0;
+    if (lane * 16 <= lastr) keys16<K>(&L.r[lane * 16], code, bad);   // lanes past lastr own no k-mer
+    if (K == 14 && fast && pass == 1 && nr == SEG_L && nt == SEG_L && fast_class0<K>(L, nr, nt, code, bad)) {
+        SegStat s;
+        s.nrec = FAST_NREC;
+        s.nmatch = 0;
+        s.lit = 0;
+        s.pass = 1;
+        s.non_n = (int)non_n;
+        s.first_p = -1;
+        s.last_p = -1;
+        s.pad = nt;
+        return s;
+    }
     uint32_t* cnt = L.skey;   // bucket counters live where the keys go later
     for (int i = lane; i < NB; i += 64) cnt[i] = 0;
     wave_sync();
     {
         const int p0 = lane * 16;
-        uint64_t code = 0;
-        uint32_t bad = 0;
-        if (p0 <= lastr) keys16<K>(&L.r[p0], code, bad);   // lanes past lastr own no k-mer
         uint32_t key[16], rank[16];
 #pragma unroll
         for (int st = 0; st < 16; st++) {
@@ -395,7 +469,9 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
     const int64_t G = (int64_t)gridDim.x * WPB;
     for (int64_t seg = seg0 + (int64_t)blockIdx.x * WPB + w; seg < seg_end; seg += G) {
         if (pass == 2 && stat[seg].pass != 0) continue;
-        const SegStat st = local_segment<K, DBG>(lds_all[w], seg, pass, pass == 2 ? stat[seg].non_n : 0, upper, R, nR, T,
+        if (pass == 3 && stat[seg].nrec != FAST_NREC) continue;   // (3: the records of fast-classified segments)
+        const int ps = pass == 3 ? 1 : pass;
+        const SegStat st = local_segment<K, DBG>(lds_all[w], seg, ps, ps == 2 ? stat[seg].non_n : 0, upper, R, nR, T,
                                                  nT, recs);
         if (lane_id() == 0) stat[seg] = st;
         wave_sync();   // the next segment reuses this wave's LDS
@@ -440,7 +516,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
                                                           const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
                                                           uint32_t* __restrict__ recs, SegStat* __restrict__ stat,
                                                           int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl,
-                                                          int32_t seg_lo, int32_t seg_hi) {
+                                                          int32_t seg_lo, int32_t seg_hi, int32_t fast) {
     __shared__ SegLds lds_all[WPB];
     const int64_t nR = *dnR, nT = *dnT;
     const int32_t nseg_all = seg_count(nR, nT);
@@ -454,7 +530,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
     for (; seg < nseg; seg += G) {
         if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
         if (seg + G < nseg) seg_words_load(nxt, seg + G, R, nR, T, nT);   // in flight during this segment
-        SegStat st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, &cur);
+        SegStat st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, &cur, fast != 0);
         if (!st.pass) {
             wave_sync();
             st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs);
@@ -686,17 +762,19 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
         return v > 0 ? (int32_t)((v + WPB - 1) / WPB * WPB) : 0;
     }();
     const int32_t st1 = s1 > 0 && nseg_max > s1 ? s1 : 0;
+    // the fast class-0 proof (fast_class0; SCCG_LOCAL_FAST=0: every segment takes the full pass)
+    static const int32_t local_fast = [] { const char* e = getenv("SCCG_LOCAL_FAST"); return e ? (int32_t)(atoi(e) != 0) : 1; }();
     unsigned g = grid_for(nseg_max - st1, WPB);
     if (g > cap) g = cap;
     static const bool dbg = getenv("SCCG_DEBUG") != nullptr;
     if (st1)
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3((unsigned)(st1 / WPB)), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT,
-                    recs, stat, cls, gen, ctl, 0, st1);
+                    recs, stat, cls, gen, ctl, 0, st1, local_fast);
     if (dbg) {
         const unsigned long long z[16] = {};
         SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl, st1, INT32_MAX);
+                    gen, ctl, st1, INT32_MAX, local_fast);
         unsigned long long d[16];
         SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
         SCCG_HIP(hipStreamSynchronize(s));
@@ -707,7 +785,7 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
                 d[8] / 100.0, d[9] / 100.0, d[10] / 100.0, d[11] / 100.0, d[12] / 100.0);
     } else {
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl, st1, INT32_MAX);
+                    gen, ctl, st1, INT32_MAX, local_fast);
     }
     if (nseg_max > 4) {
         const unsigned gs = grid_for(nseg_max - 4, 256) > 2048 ? 2048 : grid_for(nseg_max - 4, 256);
