@@ -128,28 +128,56 @@ __device__ __forceinline__ void seg_words_load(SegWords& W, int64_t seg, const u
     }
 }
 
-// Fast class-0 proof (switch detection only).  A full segment pair whose target is, on one diagonal
-// d of the reference segment, equal but for `mism` bytes: every target position whose k-mer lies
-// inside the overlap and holds none of those bytes has a candidate (the diagonal's own copy), so
-// the walk's literal steps are among the <= K * mism blocked positions, the |d| positions off the
-// overlap and the K - 1 positions at each end of it -- at most B = K * mism + |d| + 2 (K - 1).  When
-// 2 B <= nt the k = 14 pass matches (literals < nt) with a literal ratio <= T1 = 0.5: class 0
-// (compression.cpp:402-416), whatever the records are.  The diagonal comes from three probe k-mers
-// of the target searched in the reference segment's keys (the first k-mer of the hash build,
-// computed anyway).  Only the switch state machine needs the class; a pair that stays local gets
-// these segments' records from a second pass (k_local_pass, pass 3) before its record text.
+// Fast class-0 proof (switch detection only).  A target position whose k-mer equals the reference
+// segment's k-mer on some diagonal d (T[j, j+K) == R[j+d, j+d+K), both inside their segments) has a
+// candidate, so the walk never takes a literal step there: the literal bases of the k = 14 pass are
+// at most the positions covered by none of the probed diagonals (those whose window leaves either
+// segment, or holds a mismatch, on every one of them) -- the walk's final literal tail included.
+// When twice that count is <= nt, the pass matches (literals < nt) with a literal ratio <= T1 = 0.5:
+// class 0 (compression.cpp:402-416), whatever the records are.  The diagonals come from FAST_PROBES
+// target k-mers searched in the reference segment's keys (the hash build's first step, computed
+// anyway): an indel inside the segment gives two diagonals, both counted.  Only the switch state
+// machine needs the class; a pair that stays local gets these segments' records from a second pass
+// (k_local_pass, pass 3) before its record text.  tests/test_local_fast_proof.py restates this and
+// checks it against the oracle's match_sequences.
 constexpr int FAST_NREC = -1;   // SegStat.nrec of a segment classified by the proof (records not written)
+constexpr int FAST_PROBES = 5;
+__device__ constexpr int FAST_PROBE_AT[FAST_PROBES] = {40, 260, 480, 700, 920};
+// bit i: T[j0 + i] == R[j0 + i + d] for the 32 bytes from j0 (false outside either segment)
+__device__ __forceinline__ uint32_t diag_eq32(const SegLds& L, int nr, int nt, int j0, int d) {
+    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
+    const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
+    uint32_t eq = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int j = j0 + 4 * q, a = j + d;
+        uint32_t tv = 0, rv = 0;
+        if (j < SEGB - 4) tv = __builtin_amdgcn_alignbyte(t4[(j >> 2) + 1], t4[j >> 2], (uint32_t)(j & 3));
+        if (a >= 0 && a < SEGB - 4) rv = __builtin_amdgcn_alignbyte(r4[(a >> 2) + 1], r4[a >> 2], (uint32_t)(a & 3));
+        const uint32_t x = tv ^ rv;
+        const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;   // bit 7 of each equal byte
+        uint32_t b4 = ((z >> 7) * 0x01020408u) >> 24 & 0xfu;                            // -> 4 bits
+        // bytes outside either segment are never equal
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (j + i >= nt || a + i < 0 || a + i >= nr) b4 &= ~(1u << i);
+        eq |= b4 << (4 * q);
+    }
+    return eq;
+}
 template <int K>
 __device__ __forceinline__ bool fast_class0(const SegLds& L, int nr, int nt, uint64_t code, uint32_t bad) {
+    static_assert(K == 14, "the window AND below is for K = 14");
     constexpr uint32_t MASK = (1u << (2 * K)) - 1u, KM = (1u << K) - 1u;
     const int lane = lane_id();
     const int p0 = lane * 16, lastr = nr - K;
-    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
     const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
-    constexpr int PROBES[3] = {40, 480, 920};
+    uint32_t covered = 0;   // bit i: position p0 + i has a candidate on a probed diagonal
+    int dprev[FAST_PROBES];
 #pragma unroll
-    for (int pi = 0; pi < 3; pi++) {
-        const int sp = PROBES[pi];
+    for (int pi = 0; pi < FAST_PROBES; pi++) {
+        dprev[pi] = INT32_MIN;
+        const int sp = FAST_PROBE_AT[pi];
         if (sp + K > nt) continue;
         uint32_t w[4];
 #pragma unroll
@@ -166,27 +194,23 @@ __device__ __forceinline__ bool fast_class0(const SegLds& L, int nr, int nt, uin
         const unsigned long long hm = __ballot(hit != 0);
         if (!hm) continue;
         const int fl = first_lane(hm);
-        const int c = fl * 16 + (__builtin_ctz(lane_val(hit, fl)));
-        const int d = c - sp;   // T[j] against R[j + d]
-        const int j0 = d < 0 ? -d : 0, j1 = nt < nr - d ? nt : nr - d;
-        int cnt = 0;
+        const int d = fl * 16 + __builtin_ctz(lane_val(hit, fl)) - sp;   // T[j] against R[j + d]
+        bool seen = false;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int j = j0 + 16 * lane + 4 * q;
-            if (j >= j1) continue;
-            const int a = j + d;
-            const uint32_t tv = __builtin_amdgcn_alignbyte(t4[(j >> 2) + 1], t4[j >> 2], (uint32_t)(j & 3));
-            const uint32_t rv = __builtin_amdgcn_alignbyte(r4[(a >> 2) + 1], r4[a >> 2], (uint32_t)(a & 3));
-            uint32_t x = tv ^ rv;
-            if (j1 - j < 4) x &= (1u << (8 * (j1 - j))) - 1u;
-            const uint32_t nz = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu | x) & 0x80808080u;   // bytes != 0
-            cnt += __builtin_popcount(nz);
-        }
-        const int mism = wave_sum(cnt);
-        const int bound = K * mism + (d < 0 ? -d : d) + 2 * (K - 1);
-        if (2 * bound <= nt) return true;
+        for (int q = 0; q < pi; q++) seen |= dprev[q] == d;
+        dprev[pi] = d;
+        if (seen) continue;
+        uint32_t e = diag_eq32(L, nr, nt, p0, d);
+        e &= e >> 1;
+        e &= e >> 2;
+        e &= e >> 4;    // bit i: bytes i .. i+7 equal
+        e &= e >> 6;    // bit i: bytes i .. i+13 equal (bits 0..15 are exact: 15 + 13 < 32)
+        covered |= e & 0xffffu;
     }
-    return false;
+    const int mine = p0 < nt ? (nt - p0 < 16 ? nt - p0 : 16) : 0;
+    const uint32_t lim = mine >= 16 ? 0xffffu : (1u << mine) - 1u;
+    const int uncovered = wave_sum(mine - __builtin_popcount(covered & lim));
+    return 2 * uncovered <= nt;
 }
 
 template <int K, bool DBG>
@@ -237,7 +261,8 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     uint64_t code = 0;
     uint32_t bad = 0;
     if (lane * 16 <= lastr) keys16<K>(&L.r[lane * 16], code, bad);   // lanes past lastr own no k-mer
-    if (K == 14 && fast && pass == 1 && nr == SEG_L && nt == SEG_L && fast_class0<K>(L, nr, nt, code, bad)) {
+    if constexpr (K == 14) {
+    if (fast && pass == 1 && nr == SEG_L && nt == SEG_L && fast_class0<14>(L, nr, nt, code, bad)) {
         SegStat s;
         s.nrec = FAST_NREC;
         s.nmatch = 0;
@@ -248,6 +273,7 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
         s.last_p = -1;
         s.pad = nt;
         return s;
+    }
     }
     uint32_t* cnt = L.skey;   // bucket counters live where the keys go later
     for (int i = lane; i < NB; i += 64) cnt[i] = 0;
