@@ -378,8 +378,6 @@ __device__ __forceinline__ TileSum ts_shfl_up(const TileSum& v, int d) {
 // (2) one block: exclusive prefix of the block totals; (3) per tile: stream prefix = "carry 1"
 // then block prefix then local prefix -> output offsets (strip and filter) and carry-in status.
 constexpr int SCAN_B = 1024;
-constexpr bool STRIP_ONEPASS_DEFAULT = false;
-constexpr bool RUNS_ONEPASS_DEFAULT = false;
 __device__ __forceinline__ TileSum block_scan_tiles(TileSum v, TileSum* wsum, TileSum* total) {
     const TileSum id{0, 0, 0, 0, -1};
     const int lane = lane_id(), w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
@@ -516,151 +514,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
 }
 
 // ---------------------------------------------------------------------------------------------
-// Single-pass strip (decoupled look-back).  One launch per FASTA instead of summary + three scan
-// launches + write: a wave takes the next tile from a ticket, computes its summary (as
-// k_strip_summary), publishes it, finds its exclusive prefix from its predecessors' published
-// summaries (64 at a time, one per lane), publishes its inclusive prefix and writes its output
-// (as k_strip_write) from the words it still holds -- the FASTA is read once, not twice.
-// Progress: tiles are taken in ticket order, so every tile a wave waits for belongs to a wave that
-// is already running, and tile 0 waits for nobody.
-// Status word of tile t (lb[1 + t], zeroed before the launch; lb[0] is the ticket):
-//   AGG  flag 1 | last + 1 << 2 | a << 4 | b << 17 | fa << 30 | fb << 43   (13 bits each: <= 4096)
-//   INC  flag 2 | last + 1 << 2 | b << 4, with fb in incf[t] (stored before the flag, released)
-// An inclusive prefix always starts with the stream start (a kept line), so its a and fa are 0.
-// ---------------------------------------------------------------------------------------------
-constexpr uint64_t LB_AGG = 1, LB_INC = 2;
-__device__ __forceinline__ uint64_t lb_agg(const TileSum& v) {
-    return LB_AGG | ((uint64_t)(v.last + 1) << 2) | ((uint64_t)v.a << 4) | ((uint64_t)v.b << 17) | ((uint64_t)v.fa << 30) |
-           ((uint64_t)v.fb << 43);
-}
-__device__ __forceinline__ TileSum ts_shfl_down(const TileSum& v, int d) {
-    TileSum r;
-    r.a = __shfl_down(v.a, d, 64); r.b = __shfl_down(v.b, d, 64);
-    r.fa = __shfl_down(v.fa, d, 64); r.fb = __shfl_down(v.fb, d, 64);
-    r.last = __shfl_down(v.last, d, 64);
-    return r;
-}
-
-// Exclusive prefix of `tile` (>= 1), composed with the stream start, from the predecessors' words.
-__device__ __forceinline__ TileSum lb_prefix(unsigned long long* __restrict__ lb, int64_t* __restrict__ incf, int64_t tile) {
-    const TileSum id{0, 0, 0, 0, -1};
-    const int lane = lane_id();
-    TileSum acc = id;   // tiles j + 1 .. tile - 1
-    for (int64_t j = tile - 1;; j -= 64) {
-        const int64_t mine = j - lane;   // lane l: tile j - l (every window reaches an INC before tile 0)
-        uint64_t s;
-        int fi;
-        for (;;) {
-            s = mine >= 0 ? __hip_atomic_load(&lb[1 + mine], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : (LB_INC | (2ull << 2));
-            const uint64_t inc = __ballot((s & 3) == LB_INC);
-            fi = inc ? __builtin_ctzll(inc) : 64;
-            if ((__ballot((s & 3) == 0) & below64(fi + 1)) == 0) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        TileSum v = id;
-        if (lane <= fi) {
-            v.last = (int32_t)((s >> 2) & 3) - 1;
-            if ((s & 3) == LB_INC) {
-                v.a = 0;
-                v.fa = 0;
-                v.b = (int64_t)(s >> 4);
-                v.fb = mine >= 0 ? __hip_atomic_load(&incf[mine], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-            } else {
-                v.a = (int64_t)((s >> 4) & 0x1fff);
-                v.b = (int64_t)((s >> 17) & 0x1fff);
-                v.fa = (int64_t)((s >> 30) & 0x1fff);
-                v.fb = (int64_t)((s >> 43) & 0x1fff);
-            }
-        }
-        // ordered reduction: lane 0 ends with v[63] o ... o v[0] (higher lanes are earlier tiles)
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const TileSum o = ts_shfl_down(v, d);
-            if (lane + d < 64) v = ts_compose(o, v);
-        }
-        TileSum w;
-        w.a = __shfl(v.a, 0, 64); w.b = __shfl(v.b, 0, 64); w.fa = __shfl(v.fa, 0, 64); w.fb = __shfl(v.fb, 0, 64);
-        w.last = __shfl(v.last, 0, 64);
-        acc = ts_compose(w, acc);
-        if (fi < 64) return acc;
-    }
-}
-
-template <IngestMode MODE>
-__global__ __launch_bounds__(SCCG_BLOCK) void k_strip_onepass(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n,
-                                                              const int64_t* __restrict__ hdr, int64_t ntiles,
-                                                              unsigned long long* __restrict__ lb, int64_t* __restrict__ incf,
-                                                              uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
-                                                              int32_t* __restrict__ flags, int64_t* __restrict__ d_len,
-                                                              int64_t* __restrict__ d_len2) {
-    __shared__ uint4 stage_all4[WPB][(STAGE_WORDS + 3) / 4];   // (also the coalesced load's transpose)
-    __shared__ uint32_t tab[16];
-    if (threadIdx.x < 16) tab[threadIdx.x] = compact_sel(threadIdx.x);
-    __syncthreads();
-    const int lane = lane_id();
-    unsigned long long tk = 0;
-    if (lane == 0) tk = atomicAdd(lb, 1ull);
-    const int64_t tile = (int64_t)__shfl(tk, 0, 64);
-    if (tile >= ntiles) return;
-    uint32_t* st4 = reinterpret_cast<uint32_t*>(stage_all4[wave_in_block()]);
-    uint8_t* s1 = reinterpret_cast<uint8_t*>(st4);
-    const int64_t off = tile * STRIP_WTILE + (int64_t)lane * SL;
-    const int64_t h = MODE == INGEST_TGT ? hdr[0] : 0, he = MODE == INGEST_TGT ? hdr[1] : 0;
-    uint32_t w[SNW];
-    int32_t prior;
-    uint64_t lsm;
-    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm, stage_all4[wave_in_block()]);
-    // the tile's summary (k_strip_summary)
-    TileSum agg;
-    {
-        const uint64_t ra = (uint64_t)__popcll(r.unknown), rb = (uint64_t)__popcll(r.known);
-        const uint64_t rfa = (uint64_t)__popcll(r.unknown & r.fk), rfb = (uint64_t)__popcll(r.known & r.fk);
-        const uint64_t A = prior < 0 ? ra : 0, B = rb + (prior == 1 ? ra : 0);
-        const uint64_t FA = prior < 0 ? rfa : 0, FB = rfb + (prior == 1 ? rfa : 0);
-        const uint64_t tot = wave_sum<uint64_t>(A | (B << 16) | (FA << 32) | (FB << 48));
-        agg.a = (int64_t)(tot & 0xffff);
-        agg.b = (int64_t)((tot >> 16) & 0xffff);
-        agg.fa = (int64_t)((tot >> 32) & 0xffff);
-        agg.fb = (int64_t)(tot >> 48);
-        agg.last = (MODE == INGEST_REF && lsm) ? __shfl(r.last, 63 - __builtin_clzll(lsm), 64) : -1;
-    }
-    const TileSum start{0, 0, 0, 0, 1};   // the stream starts as if after a kept line
-    TileSum pre = start;
-    if (tile > 0) {
-        if (lane == 0) __hip_atomic_store(&lb[1 + tile], lb_agg(agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pre = ts_compose(start, lb_prefix(lb, incf, tile));
-    }
-    const TileSum inc = ts_compose(pre, agg);
-    if (lane == 0) {
-        __hip_atomic_store(&incf[tile], inc.fb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&lb[1 + tile], LB_INC | ((uint64_t)(inc.last + 1) << 2) | ((uint64_t)inc.b << 4), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        if (tile == ntiles - 1) {
-            *d_len = inc.b;
-            if (d_len2) *d_len2 = inc.fb;
-        }
-    }
-    // the tile's output (k_strip_write)
-    if (MODE == INGEST_REF && prior < 0) prior = pre.last;
-    const uint64_t keep = r.known | (prior == 1 ? r.unknown : 0ull), fkeep = keep & r.fk;
-    const uint32_t c = (uint32_t)__popcll(keep) | ((uint32_t)__popcll(fkeep) << 16);
-    const uint32_t incl = wave_incl_add<uint32_t>(c), tot = lane_val(incl, 63);
-    const uint32_t ex = incl - c;
-    if (flags && __ballot((keep & r.par) != 0) && lane == 0) atomicOr(flags, 1);
-    if (out) {
-        stage_lane<false>(s1, tab, w, keep, (int)(ex & 0xffff));
-        wave_sync();
-        stage_out(st4, (int)(tot & 0xffff), out, pre.b);
-    }
-    if (out2) {
-        wave_sync();
-        stage_lane<true>(s1, tab, w, fkeep, (int)(ex >> 16));
-        wave_sync();
-        stage_out(st4, (int)(tot >> 16), out2, pre.fb);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // runs of a predicate
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool run_pred(RunPred p, uint8_t c) {
@@ -730,75 +583,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_runs_write(const uint8_t* __rest
     put_positions(el, off, re_l, toff_l[blockIdx.x] - (open_l ? 1 : 0) + (xe & 0xffff));
     put_positions(sn, off, rs_n, toff_n[blockIdx.x] + (xs >> 16));
     put_positions(en, off, re_n, toff_n[blockIdx.x] - (open_n ? 1 : 0) + (xe >> 16));
-}
-
-// Both run lists in one pass (SCCG_RUNS_ONEPASS): k_runs_count + the two offset scans + k_runs_write
-// as one launch with a decoupled look-back over the tiles' run counts (T is read once, not twice).
-// Block tiles come from a ticket (lb[0]); tile t's word lb[1 + t] = flag (1 counts of the tile,
-// 2 counts of tiles 0..t) | lowercase count << 2 | N count << 33.  Wave 0 looks back while the
-// block's other waves wait at the barrier; the tiles it waits for belong to running blocks.
-__global__ __launch_bounds__(SCCG_BLOCK) void k_runs_onepass(const uint8_t* __restrict__ in, int64_t n, int64_t ntiles,
-                                                             unsigned long long* __restrict__ lb, int32_t* __restrict__ rs_l,
-                                                             int32_t* __restrict__ re_l, int32_t* __restrict__ rs_n,
-                                                             int32_t* __restrict__ re_n, int64_t* __restrict__ d_nruns) {
-    __shared__ int32_t tmp32[8];
-    __shared__ int64_t s_tile, s_pl, s_pn;
-    if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(lb, 1ull);
-    __syncthreads();
-    const int64_t blk = s_tile;
-    if (blk >= ntiles) return;
-    const int64_t tile0 = blk * INGEST_TILE;
-    const int64_t off = tile0 + (int64_t)threadIdx.x * PER_T;
-    uint32_t ml, mn;
-    pred_masks(in, n, off, ml, mn);
-    const bool in_prev = off > 0 && off - 1 < n, in_next = off + PER_T < n;
-    const uint32_t pl = in_prev && run_pred(RUN_LOWER, in[off - 1]), pn = in_prev && run_pred(RUN_N, in[off - 1]);
-    const uint32_t nl = in_next && run_pred(RUN_LOWER, in[off + PER_T]), nn = in_next && run_pred(RUN_N, in[off + PER_T]);
-    const uint32_t sl = ml & ~((ml << 1) | pl), el = ml & ~((ml >> 1) | (nl << 31));
-    const uint32_t sn = mn & ~((mn << 1) | pn), en = mn & ~((mn >> 1) | (nn << 31));
-    const bool t_in = tile0 > 0 && tile0 < n;
-    const bool open_l = t_in && run_pred(RUN_LOWER, in[tile0 - 1]) && run_pred(RUN_LOWER, in[tile0]);
-    const bool open_n = t_in && run_pred(RUN_N, in[tile0 - 1]) && run_pred(RUN_N, in[tile0]);
-    int32_t tot;
-    const int32_t xs = block_excl_add<int32_t>(__popc(sl) | (__popc(sn) << 16), tmp32, &tot);
-    const int32_t xe = block_excl_add<int32_t>(__popc(el) | (__popc(en) << 16), tmp32, nullptr);
-    if (threadIdx.x < 64) {
-        const int lane = lane_id();
-        const uint64_t cl = (uint64_t)(tot & 0xffff), cn = (uint64_t)((uint32_t)tot >> 16);
-        uint64_t pre_l = 0, pre_n = 0;
-        if (blk > 0) {
-            if (lane == 0) __hip_atomic_store(&lb[1 + blk], 1ull | (cl << 2) | (cn << 33), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t j = blk - 1;; j -= 64) {
-                const int64_t mine = j - lane;
-                uint64_t w;
-                int fi;
-                for (;;) {
-                    w = mine >= 0 ? __hip_atomic_load(&lb[1 + mine], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : 2ull;
-                    const uint64_t inc = __ballot((w & 3) == 2);
-                    fi = inc ? __builtin_ctzll(inc) : 64;
-                    if ((__ballot((w & 3) == 0) & below64(fi + 1)) == 0) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                const bool use = lane <= fi;
-                pre_l += wave_sum<uint64_t>(use ? (w >> 2) & 0x7fffffffull : 0ull);
-                pre_n += wave_sum<uint64_t>(use ? (w >> 33) : 0ull);
-                if (fi < 64) break;
-            }
-        }
-        if (lane == 0) {
-            const uint64_t il = pre_l + cl, in_ = pre_n + cn;
-            __hip_atomic_store(&lb[1 + blk], 2ull | (il << 2) | (in_ << 33), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            if (blk == ntiles - 1) { d_nruns[0] = (int64_t)il; d_nruns[1] = (int64_t)in_; }
-            s_pl = (int64_t)pre_l;
-            s_pn = (int64_t)pre_n;
-        }
-    }
-    __syncthreads();
-    const int64_t ol = s_pl, on = s_pn;
-    put_positions(sl, off, rs_l, ol + (xs & 0xffff));
-    put_positions(el, off, re_l, ol - (open_l ? 1 : 0) + (xe & 0xffff));
-    put_positions(sn, off, rs_n, on + (xs >> 16));
-    put_positions(en, off, re_n, on - (open_n ? 1 : 0) + (xe >> 16));
 }
 
 // text of one run: "d," | "(d,len)" | final singleton "d" (compression.cpp:351-366)
@@ -909,20 +693,6 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     if (!out2) fmode = FILTER_UPPER;   // second output unused
     const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE;
     const unsigned g = grid_for(ntiles, WPB);
-    static const bool onepass = [] { const char* e = getenv("SCCG_STRIP_ONEPASS"); return e ? atoi(e) != 0 : STRIP_ONEPASS_DEFAULT; }();
-    if (onepass) {
-        if ((ntiles + SCAN_B - 1) / SCAN_B > SCAN_B) return SCCG_E_UNSUPPORTED;   // > 4 GiB of FASTA (as the scan path)
-        unsigned long long* lb = reinterpret_cast<unsigned long long*>(sc.tile_a);   // ticket + ntiles status words
-        SCCG_HIP(hipMemsetAsync(lb, 0, (size_t)(ntiles + 1) * sizeof(unsigned long long), s));
-        if (mode == INGEST_TGT)
-            PROF_LAUNCH(PROF_STRIP, s, k_strip_onepass<INGEST_TGT>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                        ntiles, lb, sc.tile_fb, out, out2, d_flags, d_len, d_len2);
-        else
-            PROF_LAUNCH(PROF_STRIP, s, k_strip_onepass<INGEST_REF>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                        ntiles, lb, sc.tile_fb, out, out2, d_flags, d_len, d_len2);
-        SCCG_HIP(hipGetLastError());
-        return 0;
-    }
     if (mode == INGEST_TGT)
         hipLaunchKernelGGL(k_strip_summary<INGEST_TGT>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header, sc.tile_a,
                            sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last);
@@ -955,15 +725,6 @@ int launch_runs2(const uint8_t* in, int64_t n, int32_t* rs_l, int32_t* re_l, int
         return 0;
     }
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE;
-    static const bool onepass = [] { const char* e = getenv("SCCG_RUNS_ONEPASS"); return e ? atoi(e) != 0 : RUNS_ONEPASS_DEFAULT; }();
-    if (onepass) {   // d_cnt_l: ticket + ntiles status words (the caller sizes it for ntiles + 1)
-        unsigned long long* lb = reinterpret_cast<unsigned long long*>(d_cnt_l);
-        SCCG_HIP(hipMemsetAsync(lb, 0, (size_t)(ntiles + 1) * sizeof(unsigned long long), s));
-        PROF_LAUNCH(PROF_RUNS, s, k_runs_onepass, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, in, n, ntiles, lb, rs_l, re_l,
-                    rs_n, re_n, d_nruns);
-        SCCG_HIP(hipGetLastError());
-        return 0;
-    }
     hipLaunchKernelGGL(k_runs_count, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, in, n, d_cnt_l, d_cnt_n);
     int rc = dev_excl_sum(d_cnt_l, d_cnt_l, ntiles, d_nruns, d_partial, s);
     if (!rc) rc = dev_excl_sum(d_cnt_n, d_cnt_n, ntiles, d_nruns + 1, d_partial, s);

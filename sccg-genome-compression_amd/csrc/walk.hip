@@ -1490,6 +1490,7 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
     const int32_t blo = P - half < 0 ? 0 : P - half;
     const int32_t bhi = P + half < A.nR - k ? P + half : A.nR - k;
     if (blockIdx.x == 0 && tid == 0) { A.chs[6] = blo; A.chs[7] = bhi; }
+    // chs[14]: where this generation's bounded span ends before the target's (INT32_MAX: it does not)
     for (int i = tid; i < (1 << CH_TBITS); i += 1024) tab[i] = CH_EMPTY;
     if (tid == 0) trunc_s = INT32_MAX;
     __syncthreads();
@@ -1528,6 +1529,7 @@ __global__ __launch_bounds__(1024) void k_chain_scan(WalkPtrs A) {
     // target (round 3) spent ~0.8 ms per generation on a 243 Mb T2T-like target for hits it never used
     if (total > CH_FF_SPAN * CH_GRID) total = CH_FF_SPAN * CH_GRID;
     const int64_t end = (int64_t)x + (total > 0 ? total : 0);   // < lastk1: the next generation goes on from end
+    if (blockIdx.x == 0 && tid == 0) A.chs[14] = end < lastk1 ? (int32_t)end : INT32_MAX;
     int64_t span = total > 0 ? (total + CH_GRID - 1) / CH_GRID : 0;
     span = (span + 15) & ~(int64_t)15;
     const int64_t b0 = (int64_t)x + (int64_t)blockIdx.x * span;
@@ -1748,10 +1750,17 @@ __global__ __launch_bounds__(64) void k_chain_step(WalkPtrs A) {
         if (!gen_end && !reason && tr != INT32_MAX) {   // hits past tr were not kept
             gen_end = true;
             if (x < tr) x = tr;   // every position before tr is settled (a literal step or a visited hit)
-            // band hits this dense twice running: the chunk rounds are the better engine here
-            // (find-first generations stop at their first hit by design)
-            if (A.chs[11] >= 1 && !A.chs[12]) reason = 2;
-            if (lane == 0) A.chs[11] += 1;
+            if (tr == A.chs[14]) {
+                // the generation's bounded span ended (no overflow): a long stuck stretch, not dense
+                // hits -- counting it as an overflow handed every chain longer than two spans back
+                // to the rounds (T2T-like genome 0.52 -> 1.1 s)
+                if (lane == 0) A.chs[11] = 0;
+            } else {
+                // band hits this dense twice running: the chunk rounds are the better engine here
+                // (find-first generations stop at their first hit by design)
+                if (A.chs[11] >= 1 && !A.chs[12]) reason = 2;
+                if (lane == 0) A.chs[11] += 1;
+            }
         } else if (lane == 0 && b == 0) {
             A.chs[11] = 0;
         }
