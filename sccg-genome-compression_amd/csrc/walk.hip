@@ -1094,110 +1094,35 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
 // Frozen chunks (committed fix-ups that ended in a long literal run with P unchanged up to their
 // chunk end; k_commit lists them): for each of the first FROZEN_MAX, the first position after its
 // exit whose k-mer key occurs in its window of P, over the whole rest of the target (grid.y picks
-// the frozen chunk).  A block holds the window's keys (<= 2m+1) and a one-hash 2^17-bit LDS
-// prefilter of them; every thread tests 64 consecutive target positions per step (five aligned
-// 16-byte loads, 2-bit codes, one prefilter bit per position; the prefilter hits -- 0.15 % of the
-// positions, ~6 per wave step -- are checked in a 512-slot LDS hash table of the keys, one or two
-// probes: a linear pass over the 201 keys per prefilter hit serialised every wave step and made
-// the scan 70x slower), the grid striding over the target so the scan front moves evenly and stops
-// one step after the first hit.  (Round 3: a wave per 1024 positions with a 3-hash Bloom test and
-// 4 waves per CU -- 0.8 ms to scan a 243 Mb target to its end.)  For k > KEY_K a key hit is a
-// superset of a window hit (the first KEY_K bases), which only makes the fills conservative.
-constexpr int FZ_BITS = 17;
-constexpr int FZ_TAB_BITS = 9;                 // exact check: the <= WCAP window keys in 512 slots
-constexpr int FZ_TAB = 1 << FZ_TAB_BITS;
-static_assert(FZ_TAB >= 2 * WCAP, "load factor <= 1/2");
-constexpr uint32_t FZ_EMPTY = 0xffffffffu;
-// (an exotic hash key equal to FZ_EMPTY shares a slot value with 0xfffffffe: a key match is then a
-// superset of a window hit, which only makes the scan's first hit conservative)
-__device__ __forceinline__ uint32_t fz_key(uint32_t key) { return key == FZ_EMPTY ? FZ_EMPTY - 1 : key; }
-constexpr int FZ_T = 256;
+// the frozen chunk; every wave builds its own copy of the window -- registers and a 2 KiB Bloom
+// filter -- and scans a strided share, 1024 positions per wave step, stopping one step after the
+// first hit).  Round 4 tried a block-wide variant (one 2^17-bit one-hash LDS prefilter and a key
+// table per block, 64 positions per thread and step): exact, but 10-15x slower per batch on the
+// T2T-like genome (a 256-chunk batch 10-15 ms against 0.8 ms; profiles/r04/), so this one stays.
+// For k > KEY_K a key hit is a superset of a window hit (the first KEY_K bases), which only makes
+// the fills conservative.
 constexpr unsigned FZ_GRID = 256;
-__global__ __launch_bounds__(FZ_T) void k_frozen_scan(WalkPtrs A, int fbase) {
-    __shared__ uint32_t fbits[1 << (FZ_BITS - 5)];
-    __shared__ uint32_t wtab[FZ_TAB];   // the window's keys, open addressing (FZ_EMPTY: free)
+constexpr int FZ_T = SCCG_BLOCK;
+__global__ __launch_bounds__(SCCG_BLOCK) void k_frozen_scan(WalkPtrs A, int fbase) {
+    __shared__ WalkLds lds_all[WPB];
     if (A.scal[9]) return;   // void pre-queued round
     const int fi = (int)blockIdx.y, f = fbase + fi;
     if (f >= A.scal[5]) return;
-    const int tid = (int)threadIdx.x, kp = A.kp;
     const int32_t j = A.flist[f];
     const int32_t x0 = A.exitX[j], P = A.exitP[j];
-    const uint32_t MASK = (1u << (2 * kp)) - 1u, KM = (1u << kp) - 1u;
-    const int32_t wlo = P - A.m < 0 ? 0 : P - A.m;
-    const int32_t whi = (P + A.m < A.nR - A.k) ? P + A.m : A.nR - A.k;
-    const int nwin = whi - wlo + 1;
-    if (nwin <= 0) return;
-    {
-        uint4* b4 = reinterpret_cast<uint4*>(fbits);
-        for (int i = tid; i < (1 << (FZ_BITS - 5)) / 4; i += FZ_T) b4[i] = make_uint4(0, 0, 0, 0);
-        for (int i = tid; i < FZ_TAB; i += FZ_T) wtab[i] = FZ_EMPTY;
-    }
-    __syncthreads();
-    for (int c = tid; c < nwin; c += FZ_T) {
-        uint32_t wv[4], bad;
-        uint64_t code;
-        loadw<4>(A.R + wlo + c, wv);   // (R' has 4 KiB of readable slack)
-        pack_codes<4>(wv, code, bad);
-        const uint32_t key = fz_key((bad & KM) ? exotic_key(A.R + wlo + c, kp) : (uint32_t)code & MASK);
-        const uint32_t h = slot_hash(key, FZ_BITS);
-        atomicOr(&fbits[h >> 5], 1u << (h & 31));
-        for (uint32_t t = slot_hash(key, FZ_TAB_BITS);; t = (t + 1) & (FZ_TAB - 1)) {
-            const uint32_t old = atomicCAS(&wtab[t], FZ_EMPTY, key);
-            if (old == FZ_EMPTY || old == key) break;
-        }
-    }
-    __syncthreads();
+    WalkLds& L = lds_all[wave_in_block()];
+    RegWin W;
+    reg_window(A, P, W);
+    if (W.n <= 0) return;
+    bloom_window(W, L);
     const int32_t end = A.nT - A.k + 1 < A.xhi ? A.nT - A.k + 1 : A.xhi;   // (a range walk stops at xhi)
-    const int64_t g0 = (int64_t)(x0 & ~63);
-    const int64_t gid = (int64_t)blockIdx.x * FZ_T + tid, G = (int64_t)gridDim.x * FZ_T;
-    for (int64_t base = g0 + 64 * gid; base < end; base += 64 * G) {
-        if (base > (int64_t)__hip_atomic_load(&A.fy[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-        uint32_t cw[20], acc = 0, dw[20];
-        {
-            const uint4* src = reinterpret_cast<const uint4*>(A.T + base);   // 4 KiB readable slack after T'
-#pragma unroll
-            for (int i = 0; i < 5; i++) {
-                const uint4 v = src[i];
-                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int q = 0; q < 4; q++) { cw[4 * i + q] = swar_codes(wv[q], dw[4 * i + q]); acc |= dw[4 * i + q]; }
-            }
-        }
-        int32_t hit = -1;
-#pragma unroll
-        for (int g = 0; g < 4 && hit < 0; g++) {
-            uint64_t code = 0;
-            uint32_t bad = 0;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                code |= (uint64_t)cw[4 * g + i] << (8 * i);
-                if (acc) bad |= nz_bytes(dw[4 * g + i]) << (4 * i);
-            }
-            uint32_t cand = 0;
-#pragma unroll
-            for (int st = 0; st < 16; st++) {
-                const uint32_t key = (uint32_t)(code >> (2 * st)) & MASK;
-                const uint32_t h = slot_hash(key, FZ_BITS);
-                // a k-mer with a non-ACGT byte always goes to the exact check (its key needs the bytes)
-                if (((bad >> st) & KM) || ((fbits[h >> 5] >> (h & 31)) & 1u)) cand |= 1u << st;
-            }
-            while (cand) {
-                const int st = __ffs((int)cand) - 1;
-                cand &= cand - 1;
-                const int64_t y = base + 16 * g + st;
-                if (y < x0 || y >= end) continue;
-                const uint32_t key = fz_key(((bad >> st) & KM) ? walk_key(A.T + y, kp) : (uint32_t)(code >> (2 * st)) & MASK);
-                bool in = false;
-                for (uint32_t t = slot_hash(key, FZ_TAB_BITS);; t = (t + 1) & (FZ_TAB - 1)) {
-                    const uint32_t v = wtab[t];
-                    if (v == key) { in = true; break; }
-                    if (v == FZ_EMPTY) break;
-                }
-                if (in) { hit = (int32_t)y; break; }
-            }
-        }
-        if (hit >= 0) {
-            atomicMin(&A.fy[fi], hit);
+    const int64_t gw = (int64_t)blockIdx.x * WPB + wave_in_block(), G = (int64_t)gridDim.x * WPB;
+    for (int64_t base = x0 + gw * 64 * WIDE; base < end; base += G * 64 * WIDE) {
+        if (base >= (int64_t)__hip_atomic_load(&A.fy[fi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        const int32_t seg_end = base + 64 * WIDE < end ? (int32_t)(base + 64 * WIDE) : end;
+        const int32_t y = wide_scan(A, L, W, (int32_t)base, seg_end);
+        if (y < seg_end) {
+            if (lane_id() == 0) atomicMin(&A.fy[fi], y);
             return;
         }
     }
