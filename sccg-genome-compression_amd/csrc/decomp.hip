@@ -950,14 +950,13 @@ __device__ __forceinline__ void store16(uint8_t* p, uint64_t lo, uint64_t hi) {
     }
 }
 
+// format_out16 with the position (j, col of oc = max(o0, 0)) and the first N / lowercase runs
+// ending after j (rn, rl) given by the caller
 template <typename V, bool NT = false>
-__device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t nres, const uint8_t* sdec, int64_t dbase,
-                                             const V& N, int64_t cn, int64_t ntot, const V& L, int64_t cl, uint8_t* out) {
+__device__ __forceinline__ void format_out16_at(int64_t o0, int64_t total, const uint8_t* sdec, int64_t dbase, const V& N,
+                                                int64_t cn, int64_t ntot, const V& L, int64_t cl, uint8_t* out, int64_t j,
+                                                int col, int64_t rn, int64_t rl) {
     const int64_t oc = o0 < 0 ? 0 : o0;
-    if (oc >= total || o0 + OPT <= 0) return;
-    int64_t j = oc - oc / 51;
-    int col = (int)(oc % 51);
-    int64_t rn = first_end_after(N, 0, cn, j), rl = first_end_after(L, 0, cl, j);
     int64_t n_s = INT64_MAX, n_e = INT64_MAX, n_b = ntot, l_s = INT64_MAX, l_e = INT64_MAX;
     if (rn < cn) { n_s = N.st(rn); n_e = N.en(rn); n_b = N.nb(rn); }
     if (rl < cl) { l_s = L.st(rl); l_e = L.en(rl); }
@@ -965,37 +964,69 @@ __device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t 
     const int k0 = (int)(oc - o0), k1 = total - o0 < OPT ? (int)(total - o0) : OPT;
     if (k0 == 0 && k1 == OPT) {
         // Fast path: the thread's 16 output bytes are at most one '\n' (at knl) and 15-16 sequence
-        // bytes j .. jl-1; when no N-run or lowercase-run boundary falls inside them (runs are
-        // tens to thousands of bases long), they are one unaligned 16-byte LDS read (or all 'N'),
-        // a SWAR tolower and a byte shift -- instead of a per-byte loop with run bookkeeping.
+        // bytes j .. jl-1.  Lowercase runs (any number) and at most one N run inside them become
+        // byte masks: the sequence bytes are the decoded bytes from j's decoded offset, those after
+        // an N run inside the group from an offset shifted back by the run's length, N inside the
+        // run, tolower where lowercase -- SWAR on four words, then a byte shift for the '\n'.  (A
+        // per-byte loop with run bookkeeping ran whenever any lane of a wave met a run boundary:
+        // with soft-masked runs every ~650 bases, nearly every wave; 620-680 VALU per wave.)
         const int knl = 50 - col;   // col in [0, 50]: the line's '\n' is output byte knl (if < 16)
         const int nseq = knl < OPT ? OPT - 1 : OPT;
         const int64_t jl = j + nseq;
-        const bool allN = n_s <= j && n_e >= jl, noN = n_s >= jl;
-        const bool allL = l_s <= j && l_e >= jl, noL = l_s >= jl;
-        if ((allN || noN) && (allL || noL)) {
-            uint32_t w[4];
-            if (allN) {
-                w[0] = w[1] = w[2] = w[3] = 0x4E4E4E4Eu;   // 'N'
-            } else {
-                const int64_t at = j - n_b - dbase;
+        // N runs meeting [j, jl): one at most for this path
+        int na = OPT, nbnd = OPT, nin = 0;   // N bytes [na, nbnd) of the group (relative)
+        int64_t r = rn;
+        int64_t nbj;                          // N bases before j
+        if (rn < cn && n_s < j) nbj = n_b + (j - n_s);
+        else nbj = rn < cn ? n_b : ntot;
+        while (r < cn && (r == rn ? n_s : N.st(r)) < jl) {
+            const int64_t rs = r == rn ? n_s : N.st(r), re = r == rn ? n_e : N.en(r);
+            na = (int)((rs > j ? rs : j) - j);
+            nbnd = (int)((re < jl ? re : jl) - j);
+            nin++;
+            r++;
+        }
+        const int64_t at1 = j - nbj - dbase;             // decoded offset of byte 0 (bytes before the N run)
+        const int64_t at2 = at1 - (nbnd - na);            // (bytes after it: byte p at at2 + p)
+        const uint32_t nm = nin ? (((1u << nbnd) - 1u) & ~((1u << na) - 1u)) : 0u;
+        const uint32_t after = nin ? (~((1u << nbnd) - 1u) & 0xffffu) : 0u;   // bytes from the shifted window
+        const bool use1 = (~after & ~nm & 0xffffu) != 0, use2 = after != 0;
+        if (nin <= 1 && (!use1 || at1 >= 0) && (!use2 || at2 >= 0)) {
+            // lowercase byte mask (bit per byte)
+            uint32_t lm = 0;
+            for (int64_t q = rl; q < cl; q++) {
+                const int64_t ls = q == rl ? l_s : L.st(q);
+                if (ls >= jl) break;
+                const int64_t le = q == rl ? l_e : L.en(q);
+                const int s0 = (int)((ls > j ? ls : j) - j), e0 = (int)((le < jl ? le : jl) - j);
+                if (e0 > s0) lm |= ((1u << e0) - 1u) & ~((1u << s0) - 1u);
+            }
+            uint32_t w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0};
+            auto load16 = [&](int64_t at, uint32_t (&w)[4]) {
                 const uint32_t* sw = reinterpret_cast<const uint32_t*>(sdec) + (at >> 2);
                 const uint32_t sh = (uint32_t)(at & 3);
                 uint32_t v[5];
 #pragma unroll
-                for (int q = 0; q < 5; q++) v[q] = sw[q];
+                for (int qq = 0; qq < 5; qq++) v[qq] = sw[qq];
 #pragma unroll
-                for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbyte(v[q + 1], v[q], sh);
-            }
-            if (allL) {
+                for (int qq = 0; qq < 4; qq++) w[qq] = __builtin_amdgcn_alignbyte(v[qq + 1], v[qq], sh);
+            };
+            if (use1) load16(at1, w1);
+            if (use2) load16(at2, w2);
+            uint32_t w[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++) {   // tolower of 'A'..'Z' only (bit 7 of a byte set where upper)
-                    const uint32_t x = w[q];
-                    const uint32_t ge_a = ((x | 0x80808080u) - 0x41414141u) & 0x80808080u;   // byte >= 'A' (7-bit)
-                    const uint32_t gt_z = ((x | 0x80808080u) - 0x5B5B5B5Bu) & 0x80808080u;   // byte >= 'Z' + 1
-                    const uint32_t up = ge_a & ~gt_z & ~x;   // (bytes >= 0x80 are no letters)
-                    w[q] = x + (up >> 2);
-                }
+            for (int qq = 0; qq < 4; qq++) {
+                // bit masks -> byte masks for bytes 4qq .. 4qq+3
+                const uint32_t nb4 = (nm >> (4 * qq)) & 0xfu, ab4 = (after >> (4 * qq)) & 0xfu, lb4 = (lm >> (4 * qq)) & 0xfu;
+                const uint32_t nB = (nb4 * 0x00204081u & 0x01010101u) * 0xffu;   // bit i -> byte i = 0xff
+                const uint32_t aB = (ab4 * 0x00204081u & 0x01010101u) * 0xffu;
+                const uint32_t lB = (lb4 * 0x00204081u & 0x01010101u) * 0xffu;
+                uint32_t x = (w1[qq] & ~aB) | (w2[qq] & aB);
+                x = (x & ~nB) | (0x4E4E4E4Eu & nB);                               // 'N'
+                const uint32_t ge_a = ((x | 0x80808080u) - 0x41414141u) & 0x80808080u;   // byte >= 'A' (7-bit)
+                const uint32_t gt_z = ((x | 0x80808080u) - 0x5B5B5B5Bu) & 0x80808080u;   // byte >= 'Z' + 1
+                const uint32_t up = ge_a & ~gt_z & ~x & lB;                       // tolower where lowercase
+                w[qq] = x + (up >> 2);
             }
             uint64_t slo = (uint64_t)w[0] | ((uint64_t)w[1] << 32), shi = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
             if (knl < OPT) {   // bytes from knl on move up by one; '\n' at knl
@@ -1035,12 +1066,39 @@ __device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t 
         if (k < 8) lo |= (uint64_t)c << (8 * k);
         else hi |= (uint64_t)c << (8 * (k - 8));
     }
-    (void)nres;
     if (k0 == 0 && k1 == OPT) {
         store16<NT>(out + o0, lo, hi);
     } else {
         for (int k = k0; k < k1; k++) out[o0 + k] = (uint8_t)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xff);
     }
+}
+
+template <typename V, bool NT = false>
+__device__ __forceinline__ void format_out16(int64_t o0, int64_t total, int64_t nres, const uint8_t* sdec, int64_t dbase,
+                                             const V& N, int64_t cn, int64_t ntot, const V& L, int64_t cl, uint8_t* out) {
+    (void)nres;
+    const int64_t oc = o0 < 0 ? 0 : o0;
+    if (oc >= total || o0 + OPT <= 0) return;
+    const int64_t j = oc - oc / 51;
+    const int col = (int)(oc % 51);
+    format_out16_at<V, NT>(o0, total, sdec, dbase, N, cn, ntot, L, cl, out, j, col, first_end_after(N, 0, cn, j),
+                           first_end_after(L, 0, cl, j));
+}
+
+// first r in [0, c) with e[r] > j over an LDS run list: short lists (a tile holds a few runs) by a
+// linear pass, long ones by bisection
+__device__ __forceinline__ int32_t lds_first_end_after(const int32_t* e, int32_t c, int32_t j) {
+    if (c <= 16) {
+        int32_t r = 0;
+        while (r < c && e[r] <= j) r++;
+        return r;
+    }
+    int32_t a = 0, b = c;
+    while (a < b) {
+        const int32_t m = (a + b) >> 1;
+        if (e[m] > j) b = m; else a = m + 1;
+    }
+    return a;
 }
 
 // runs of the global lists from index a on, as views starting at 0 (format_out16's fallback)
@@ -1102,12 +1160,26 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
     }
     __syncthreads();
     const uint8_t* sdec = reinterpret_cast<const uint8_t*>(sdec_w);
+    // the block's first output offset (clamped) and its (j, col): a thread's (j, col) follow in 32-bit
+    // arithmetic from its offset inside the block (no 64-bit division per thread)
+    const int64_t ob = o_first + b * (U * OB), obc = ob < 0 ? 0 : ob;
+    const int64_t Jb = st[3];   // obc - obc / 51 (k_out_index)
+    const int32_t colb = (int32_t)(obc - 51 * (obc - Jb));
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const int64_t o0 = o_first + b * (U * OB) + (int64_t)(u * 256 + tid) * OPT;
+        const int64_t o0 = ob + (int64_t)(u * 256 + tid) * OPT;
         if (lds_runs) {
+            const int64_t oc = o0 < 0 ? 0 : o0;
+            if (oc >= total || o0 + OPT <= 0) continue;
+            const int32_t q = colb + (int32_t)(oc - obc);
+            const int32_t nl51 = q / 51;
+            const int64_t j = Jb + (oc - obc) - nl51;
+            const int col = q - 51 * nl51;
+            const int32_t jr = (int32_t)j;   // (positions are int32 in the run lists)
             const LdsRuns N{s_ns, s_ne, s_nb}, L{s_ls, s_le, nullptr};
-            format_out16<LdsRuns, NT>(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
+            format_out16_at<LdsRuns, NT>(o0, total, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out, j, col,
+                                         lds_first_end_after(s_ne, (int32_t)(n_hi - n_lo), jr),
+                                         lds_first_end_after(s_le, (int32_t)(l_hi - l_lo), jr));
         } else {
             const GlobalRunsAt N{ns, nl, ncum, n_lo}, L{ls, ll, nullptr, l_lo};
             format_out16<GlobalRunsAt, NT>(o0, total, nres, sdec, a0, N, n_hi - n_lo, ntot, L, l_hi - l_lo, out);
