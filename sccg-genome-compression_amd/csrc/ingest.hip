@@ -209,23 +209,33 @@ __device__ __forceinline__ uint64_t below64(int k) { return k >= 64 ? ~0ull : (1
 
 template <IngestMode MODE>
 __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t (&w)[SNW], uint8_t prev, int64_t off,
-                                                  int64_t n, int64_t h, int64_t he) {
-    // byte classes four at a time (SWAR); flags gathered into one bit per byte
-    const uint32_t dn_up = fm != FILTER_UPPER ? 0x80808080u : 0u, dn_lo = fm == FILTER_DROP_N_UPPER ? 0x80808080u : 0u;
-    uint64_t ws = 0, nl = 0, gt = 0, fk = 0, par = 0;
+                                                  int64_t n, int64_t h, int64_t he, const uint8_t* __restrict__ lbytes) {
+    // Byte classes.  Every byte that matters (whitespace, '\n', '>', '(', N / n) is outside
+    // {A,C,G,T,a,c,g,t}, which one 2-bit-code round trip per word flags (on the word with bit 5
+    // cleared: the case fold); only the flagged bytes -- a line's '\n' per ~60 bases, N runs -- are
+    // classified, one at a time from the lane's LDS copy (lbytes).  (Classifying every byte with
+    // SWAR compares cost ~45 VALU per word: the strip kernels were VALU-bound.)
+    uint64_t sp = 0;
 #pragma unroll
     for (int q = 0; q < SNW; q++) {
-        const uint32_t x = w[q];
-        const int sh = 4 * q;
-        ws |= (uint64_t)sw_bits(sw_eq(x, ' ') | (sw_lt(x, 14) & ~sw_lt(x, 9))) << sh;   // isspace: ' ', \t..\r
-        if (MODE == INGEST_REF) {
-            nl |= (uint64_t)sw_bits(sw_eq(x, '\n')) << sh;
-            gt |= (uint64_t)sw_bits(sw_eq(x, '>')) << sh;
-        }
-        const uint32_t nn = (sw_eq(x, 'N') & dn_up) | (sw_eq(x, 'n') & dn_lo);
-        fk |= (uint64_t)(sw_bits(nn) ^ 0xfu) << sh;
-        par |= (uint64_t)sw_bits(sw_eq(x, '(')) << sh;
+        uint32_t d;
+        (void)swar_codes(w[q] & 0xDFDFDFDFu, d);
+        sp |= (uint64_t)nz_bytes(d) << (4 * q);
     }
+    uint64_t ws = 0, nl = 0, gt = 0, drop = 0, par = 0;
+    for (uint64_t m = sp; m; m &= m - 1) {
+        const int i = __builtin_ctzll(m);
+        const uint32_t c = lbytes[i];
+        const uint64_t bit = 1ull << i;
+        if (c == ' ' || (c >= 9 && c <= 13)) ws |= bit;   // isspace
+        if (MODE == INGEST_REF) {
+            if (c == '\n') nl |= bit;
+            if (c == '>') gt |= bit;
+        }
+        if ((c == 'N' && fm != FILTER_UPPER) || (c == 'n' && fm == FILTER_DROP_N_UPPER)) drop |= bit;
+        if (c == '(') par |= bit;
+    }
+    const uint64_t fk = ~drop;
     const int64_t lim = n - off;
     const uint64_t valid = lim >= 64 ? ~0ull : (lim > 0 ? (1ull << lim) - 1ull : 0ull);
     StripMasks r{0, 0, fk, par, -1};
@@ -297,12 +307,22 @@ __device__ __forceinline__ StripMasks strip_tile(FilterMode fm, const uint8_t* _
                                                  uint64_t& lsm, uint4* tin) {
     const int lane = lane_id();
     load_lane64(buf, n, off, tin, w);
+    // the lane's 64 bytes in the wave's LDS buffer, for strip_masks' byte lookups (the coalesced
+    // load leaves them there already, in the same layout)
+    if (!(SCCG_STRIP_COALESCED && tin && off - (int64_t)lane * SL + STRIP_WTILE <= n &&
+          (((uintptr_t)(buf + off - (int64_t)lane * SL)) & 15) == 0)) {
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < SNW / 4; q++) tin[4 * lane + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        wave_sync();
+    }
     uint8_t prev = '\n';
     if (MODE == INGEST_REF) {
         const uint32_t up = (uint32_t)__shfl_up((int)w[SNW - 1], 1, 64) >> 24;
         prev = lane ? (uint8_t)up : ((off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n');
     }
-    const StripMasks r = strip_masks<MODE>(fm, w, prev, off, n, h, he);
+    const StripMasks r = strip_masks<MODE>(fm, w, prev, off, n, h, he, reinterpret_cast<const uint8_t*>(tin + 4 * lane));
+    wave_sync();   // (k_strip_write stages its output in tin next)
     prior = -1;
     lsm = 0;
     if (MODE == INGEST_REF) {
