@@ -128,96 +128,10 @@ __device__ __forceinline__ void seg_words_load(SegWords& W, int64_t seg, const u
     }
 }
 
-// Fast class-0 proof (switch detection only).  A target position whose k-mer equals the reference
-// segment's k-mer on some diagonal d (T[j, j+K) == R[j+d, j+d+K), both inside their segments) has a
-// candidate, so the walk never takes a literal step there: the literal bases of the k = 14 pass are
-// at most the positions covered by none of the probed diagonals (those whose window leaves either
-// segment, or holds a mismatch, on every one of them) -- the walk's final literal tail included.
-// When twice that count is <= nt, the pass matches (literals < nt) with a literal ratio <= T1 = 0.5:
-// class 0 (compression.cpp:402-416), whatever the records are.  The diagonals come from FAST_PROBES
-// target k-mers searched in the reference segment's keys (the hash build's first step, computed
-// anyway): an indel inside the segment gives two diagonals, both counted.  Only the switch state
-// machine needs the class; a pair that stays local gets these segments' records from a second pass
-// (k_local_pass, pass 3) before its record text.  tests/test_local_fast_proof.py restates this and
-// checks it against the oracle's match_sequences.
-constexpr int FAST_NREC = -1;   // SegStat.nrec of a segment classified by the proof (records not written)
-constexpr int FAST_PROBES = 5;
-__device__ constexpr int FAST_PROBE_AT[FAST_PROBES] = {40, 260, 480, 700, 920};
-// bit i: T[j0 + i] == R[j0 + i + d] for the 32 bytes from j0 (false outside either segment)
-__device__ __forceinline__ uint32_t diag_eq32(const SegLds& L, int nr, int nt, int j0, int d) {
-    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
-    const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
-    uint32_t eq = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-        const int j = j0 + 4 * q, a = j + d;
-        uint32_t tv = 0, rv = 0;
-        if (j < SEGB - 4) tv = __builtin_amdgcn_alignbyte(t4[(j >> 2) + 1], t4[j >> 2], (uint32_t)(j & 3));
-        if (a >= 0 && a < SEGB - 4) rv = __builtin_amdgcn_alignbyte(r4[(a >> 2) + 1], r4[a >> 2], (uint32_t)(a & 3));
-        const uint32_t x = tv ^ rv;
-        const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;   // bit 7 of each equal byte
-        uint32_t b4 = ((z >> 7) * 0x01020408u) >> 24 & 0xfu;                            // -> 4 bits
-        // bytes outside either segment are never equal
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            if (j + i >= nt || a + i < 0 || a + i >= nr) b4 &= ~(1u << i);
-        eq |= b4 << (4 * q);
-    }
-    return eq;
-}
-template <int K>
-__device__ __forceinline__ bool fast_class0(const SegLds& L, int nr, int nt, uint64_t code, uint32_t bad) {
-    static_assert(K == 14, "the window AND below is for K = 14");
-    constexpr uint32_t MASK = (1u << (2 * K)) - 1u, KM = (1u << K) - 1u;
-    const int lane = lane_id();
-    const int p0 = lane * 16, lastr = nr - K;
-    const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
-    uint32_t covered = 0;   // bit i: position p0 + i has a candidate on a probed diagonal
-    int dprev[FAST_PROBES];
-#pragma unroll
-    for (int pi = 0; pi < FAST_PROBES; pi++) {
-        dprev[pi] = INT32_MIN;
-        const int sp = FAST_PROBE_AT[pi];
-        if (sp + K > nt) continue;
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) w[i] = t4[(sp >> 2) + i];
-        uint64_t pc;
-        uint32_t pb;
-        pack_codes<4>(w, pc, pb);
-        if (pb & KM) continue;   // (an exotic probe: its key needs the bytes)
-        const uint32_t pkey = (uint32_t)pc & MASK;
-        uint32_t hit = 0;
-#pragma unroll
-        for (int st = 0; st < 16; st++)
-            if (p0 + st <= lastr && !((bad >> st) & KM) && ((uint32_t)(code >> (2 * st)) & MASK) == pkey) hit |= 1u << st;
-        const unsigned long long hm = __ballot(hit != 0);
-        if (!hm) continue;
-        const int fl = first_lane(hm);
-        const int d = fl * 16 + __builtin_ctz(lane_val(hit, fl)) - sp;   // T[j] against R[j + d]
-        bool seen = false;
-#pragma unroll
-        for (int q = 0; q < pi; q++) seen |= dprev[q] == d;
-        dprev[pi] = d;
-        if (seen) continue;
-        uint32_t e = diag_eq32(L, nr, nt, p0, d);
-        e &= e >> 1;
-        e &= e >> 2;
-        e &= e >> 4;    // bit i: bytes i .. i+7 equal
-        e &= e >> 6;    // bit i: bytes i .. i+13 equal (bits 0..15 are exact: 15 + 13 < 32)
-        covered |= e & 0xffffu;
-    }
-    const int mine = p0 < nt ? (nt - p0 < 16 ? nt - p0 : 16) : 0;
-    const uint32_t lim = mine >= 16 ? 0xffffu : (1u << mine) - 1u;
-    const int uncovered = wave_sum(mine - __builtin_popcount(covered & lim));
-    return 2 * uncovered <= nt;
-}
-
 template <int K, bool DBG>
 __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pass, int non_n_prev, int upper,
                                                  const uint8_t* __restrict__ R, int64_t nR, const uint8_t* __restrict__ T,
-                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr,
-                                                 bool fast = false) {
+                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr) {
     const int lane = lane_id();
     const int64_t base = seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
@@ -258,28 +172,14 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     // ---- H: every k-mer of the reference segment (compression.cpp:41-47), counting-sorted by
     //      bucket; lane l owns starts 16l..16l+15
     const int lastr = nr - K;
-    uint64_t code = 0;
-    uint32_t bad = 0;
-    if (lane * 16 <= lastr) keys16<K>(&L.r[lane * 16], code, bad);   // lanes past lastr own no k-mer
-    if constexpr (K == 14) {
-    if (fast && pass == 1 && nr == SEG_L && nt == SEG_L && fast_class0<14>(L, nr, nt, code, bad)) {
-        SegStat s;
-        s.nrec = FAST_NREC;
-        s.nmatch = 0;
-        s.lit = 0;
-        s.pass = 1;
-        s.non_n = (int)non_n;
-        s.first_p = -1;
-        s.last_p = -1;
-        s.pad = nt;
-        return s;
-    }
-    }
     uint32_t* cnt = L.skey;   // bucket counters live where the keys go later
     for (int i = lane; i < NB; i += 64) cnt[i] = 0;
     wave_sync();
     {
         const int p0 = lane * 16;
+        uint64_t code = 0;
+        uint32_t bad = 0;
+        if (p0 <= lastr) keys16<K>(&L.r[p0], code, bad);   // lanes past lastr own no k-mer
         uint32_t key[16], rank[16];
 #pragma unroll
         for (int st = 0; st < 16; st++) {
@@ -495,9 +395,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
     const int64_t G = (int64_t)gridDim.x * WPB;
     for (int64_t seg = seg0 + (int64_t)blockIdx.x * WPB + w; seg < seg_end; seg += G) {
         if (pass == 2 && stat[seg].pass != 0) continue;
-        if (pass == 3 && stat[seg].nrec != FAST_NREC) continue;   // (3: the records of fast-classified segments)
-        const int ps = pass == 3 ? 1 : pass;
-        const SegStat st = local_segment<K, DBG>(lds_all[w], seg, ps, ps == 2 ? stat[seg].non_n : 0, upper, R, nR, T,
+        const SegStat st = local_segment<K, DBG>(lds_all[w], seg, pass, pass == 2 ? stat[seg].non_n : 0, upper, R, nR, T,
                                                  nT, recs);
         if (lane_id() == 0) stat[seg] = st;
         wave_sync();   // the next segment reuses this wave's LDS
@@ -532,8 +430,6 @@ __device__ __forceinline__ int32_t seg_count(int64_t nR, int64_t nT) {
     return n >= INT32_MAX / 2 ? 0 : (int32_t)n;   // beyond int positions: the host reports it
 }
 
-constexpr int LOCAL_STAGE1_DEFAULT = 0;    // segments of launch_local_all's first stage
-
 #ifndef LOCAL_WAVES_PER_EU
 #define LOCAL_WAVES_PER_EU 4   // the LDS allows 4 waves/SIMD (4 blocks of SegLds x 4); VGPRs must fit 128
 #endif
@@ -541,22 +437,20 @@ template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_all(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
                                                           const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
                                                           uint32_t* __restrict__ recs, SegStat* __restrict__ stat,
-                                                          int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl,
-                                                          int32_t seg_lo, int32_t seg_hi, int32_t fast) {
+                                                          int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl) {
     __shared__ SegLds lds_all[WPB];
     const int64_t nR = *dnR, nT = *dnT;
-    const int32_t nseg_all = seg_count(nR, nT);
-    const int32_t nseg = nseg_all < seg_hi ? nseg_all : seg_hi;
+    const int32_t nseg = seg_count(nR, nT);
     const int w = wave_in_block(), lane = lane_id();
     SegLds& L = lds_all[w];
     const int32_t G = (int32_t)gridDim.x * WPB;
     SegWords cur, nxt;
-    int32_t seg = seg_lo + (int32_t)blockIdx.x * WPB + w;
+    int32_t seg = (int32_t)blockIdx.x * WPB + w;
     if (seg < nseg) seg_words_load(cur, seg, R, nR, T, nT);
     for (; seg < nseg; seg += G) {
         if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
         if (seg + G < nseg) seg_words_load(nxt, seg + G, R, nR, T, nT);   // in flight during this segment
-        SegStat st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, &cur, fast != 0);
+        SegStat st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, &cur);
         if (!st.pass) {
             wave_sync();
             st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs);
@@ -567,7 +461,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
         // classes of seg-4 .. seg+4 (lane i holds seg-4+i; -1 = not published in this call)
         const int32_t idx = seg - 4 + lane;
         int v = -1;
-        if (lane < 9 && lane != 4 && idx >= 0 && idx < nseg_all) {
+        if (lane < 9 && lane != 4 && idx >= 0 && idx < nseg) {
             const int32_t t = __hip_atomic_load(&cls[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             v = (t >> 2) == gen ? (t & 3) : -1;
         }
@@ -777,30 +671,14 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
         if (bpc >= 1 && bpc < per) per = bpc;
         return (unsigned)(cus * per);
     }();
-    // Two stages: segments [0, s1) first, one per wave, then the rest behind them on the stream.  A
-    // switch among the first segments (every hg-like pair: the counter can switch at segment 4 at
-    // the earliest, and does) lowers ctl[1] before the second stage starts, so its waves exit at
-    // once -- instead of ~2 segments for every resident wave (~4,000 segment passes per pair, all
-    // discarded) before segment 4's window completes.  SCCG_LOCAL_STAGE1 = 0: one launch.
-    static const int32_t s1 = [] {
-        const char* e = getenv("SCCG_LOCAL_STAGE1");
-        const int v = e ? atoi(e) : LOCAL_STAGE1_DEFAULT;
-        return v > 0 ? (int32_t)((v + WPB - 1) / WPB * WPB) : 0;
-    }();
-    const int32_t st1 = s1 > 0 && nseg_max > s1 ? s1 : 0;
-    // the fast class-0 proof (fast_class0; SCCG_LOCAL_FAST=0: every segment takes the full pass)
-    static const int32_t local_fast = [] { const char* e = getenv("SCCG_LOCAL_FAST"); return e ? (int32_t)(atoi(e) != 0) : 1; }();
-    unsigned g = grid_for(nseg_max - st1, WPB);
+    unsigned g = grid_for(nseg_max, WPB);
     if (g > cap) g = cap;
     static const bool dbg = getenv("SCCG_DEBUG") != nullptr;
-    if (st1)
-        PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3((unsigned)(st1 / WPB)), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT,
-                    recs, stat, cls, gen, ctl, 0, st1, local_fast);
     if (dbg) {
         const unsigned long long z[16] = {};
         SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl, st1, INT32_MAX, local_fast);
+                    gen, ctl);
         unsigned long long d[16];
         SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
         SCCG_HIP(hipStreamSynchronize(s));
@@ -811,7 +689,7 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
                 d[8] / 100.0, d[9] / 100.0, d[10] / 100.0, d[11] / 100.0, d[12] / 100.0);
     } else {
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl, st1, INT32_MAX, local_fast);
+                    gen, ctl);
     }
     if (nseg_max > 4) {
         const unsigned gs = grid_for(nseg_max - 4, 256) > 2048 ? 2048 : grid_for(nseg_max - 4, 256);

@@ -662,8 +662,6 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
             GET(uint8_t, xb, B_DX, out_cap - pos);
             XL = xb;
         }
-        // the segments the switch scan classified by the fast proof have no records yet (local.hip)
-        TRY(launch_local_pass(14, 3, 1, R, nR, T, nT, 0, iters, recs, stat, s));
         TRY(launch_local_emit(T, nT, iters, recs, stat, XL, sc + 5, sa, sb, part, s, paren));
         int64_t rlen = 0;
         TRY(d2h_i64(ctx, sc + 5, &rlen, 1));

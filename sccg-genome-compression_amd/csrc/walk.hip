@@ -172,8 +172,7 @@ struct WalkPtrs {
     int32_t* fy;          // per listed frozen chunk: first window hit after its exit (k_frozen_scan)
     int32_t* scal;        // [0] pending count, [1] escalation count, [2] startX, [3] startP, [4] round,
                           // [5] frozen count, [6] frozen-scan first hit, [9] void round, [11] carry count,
-                          // [12] trapped triggers of the round end, [13] frozen fills of the round end,
-                          // [14] first pending chunk of the round end
+                          // [12] trapped triggers of the round end, [13] frozen fills of the round end
     int32_t* trig;        // the round end's trapped triggers (RESPEC_MAX_TRIGGERS)
     int32_t unguessed_spec;   // SCCG_UNGUESSED_SPEC: k_round_pending speculates chunks left without a trajectory
     int32_t* fa_j;        // the round end's frozen fills: chunks fa_j+1 .. fa_l literal with P fa_p (scal[13])
@@ -182,7 +181,6 @@ struct WalkPtrs {
     int32_t* hintY;       // per chunk: a frozen scan's first window hit of P = hintP in this chunk (-1: none);
     int32_t* hintP;       // a walk at (x <= hintY, hintP) in the chunk may jump to hintY (all literal steps)
     int32_t skip_hints;   // SCCG_SKIP_HINTS (default on)
-    int32_t chain_final;  // SCCG_CHAIN_FINAL: chains only from a frozen chunk before the first pending one
     uint64_t* atab;
     uint32_t agen;            // anchor tag generation (one per call)
     int32_t round;            // walk round of the launch (kernel argument copy)
@@ -1248,7 +1246,6 @@ __global__ __launch_bounds__(FROZEN_MAX) void k_round_fill(WalkPtrs A, int fbase
         A.scal[13] = na;
         A.scal[0] = 0;
         A.scal[12] = 0;
-        A.scal[14] = INT32_MAX;   // first pending chunk of the round end (k_round_pending)
     }
 }
 
@@ -1324,7 +1321,6 @@ __global__ __launch_bounds__(256) void k_round_pending(WalkPtrs A) {
     A.kind[j] = KIND_FIX;
     A.lround[j] = next;
     A.plist[atomicAdd(&A.scal[0], 1)] = j;
-    atomicMin(&A.scal[14], j);
     if (j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round) {
         const int t = atomicAdd(&A.scal[12], 1);
         if (t < RESPEC_MAX_TRIGGERS) A.trig[t] = j;
@@ -1396,9 +1392,6 @@ __global__ void k_chain_init(WalkPtrs A) {
     jm = wave_min(jm);
     if (lane) return;
     if (jm == INT32_MAX) { A.chs[0] = 0; A.chs[5] = 0; return; }
-    // (SCCG_CHAIN_FINAL) only from a final state: every chunk before jm settled (none pending) --
-    // a chain from a speculative exit is redone when that exit changes
-    if (A.chain_final && jm > A.scal[14]) { A.chs[0] = 0; A.chs[5] = 0; return; }
     const int32_t x0 = A.exitX[jm], P0 = A.exitP[jm];
     A.chs[0] = 1; A.chs[1] = x0; A.chs[2] = P0; A.chs[3] = 0; A.chs[4] = jm; A.chs[5] = 0;
     A.chs[8] = 0; A.chs[9] = x0; A.chs[10] = P0; A.chs[11] = 0; A.chs[12] = 0; A.chs[13] = INT32_MAX;
@@ -2634,7 +2627,6 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.fa_j = c.take<int32_t>(FROZEN_MAX); A.fa_l = c.take<int32_t>(FROZEN_MAX); A.fa_p = c.take<int32_t>(FROZEN_MAX);
     A.hintY = c.take<int32_t>(C); A.hintP = c.take<int32_t>(C);
     A.skip_hints = env_int("SCCG_SKIP_HINTS", 1);
-    A.chain_final = env_int("SCCG_CHAIN_FINAL", 0);
     A.flat_off = c.take<int64_t>(C + 1);
     const size_t maxm = (size_t)(nT / k + 2);
     A.ft = c.take<int32_t>(maxm); A.fp = c.take<int32_t>(maxm); A.fl = c.take<int32_t>(maxm);
