@@ -83,11 +83,3 @@ int64_t dc_format_span_words(int64_t nres);
 // waits for wait_before (the reference strip) between the block index and the formatter.
 int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out,
               hipStream_t s, const DcFmtSrc* fz = nullptr, hipEvent_t wait_before = nullptr);
-// dc_decode_fill + dc_format pipelined (tiled record line): the output in SCCG_FILL_PARTS parts, the
-// format of part k on s2 beside the fill of part k+1 on s (ev: an event to reuse); d_tr: 9 int64 of
-// device scratch (the parts' record-tile bounds).  s is ordered after both when it returns.
-int dc_fill_format(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
-                   const int64_t* d_dlt, const int64_t* d_contrib,
-                   const uint8_t* d_R, uint8_t* d_dec, const int64_t* d_nref, int32_t* d_err, int64_t nres, const DcRuns& nr,
-                   const DcRuns& lr, int64_t* d_span, uint8_t* d_out, int64_t* d_tr, hipStream_t s, hipStream_t s2,
-                   hipEvent_t ev);

@@ -563,21 +563,21 @@ __global__ __launch_bounds__(256) void k_tok_blocks(const uint8_t* __restrict__ 
 // the reference (p < 0 or p + l > |R'|, decompression.cpp:223-229) set d_err bit 2 and copy nothing.
 // WRITE = false: the range check alone (no dec; a size query or an early error must report
 // SCCG_E_RANGE exactly as the full decode would)
-// one 64-byte record tile b, one wave (stg: the wave's 128 bytes of LDS)
 template <bool WRITE>
-__device__ __forceinline__ void tok_fill_tile(int64_t b, uint8_t* stg_w, const uint8_t* __restrict__ s, int64_t n,
-                                              const int64_t* __restrict__ bin, const int64_t* __restrict__ boff,
-                                              const int64_t* __restrict__ bdsum, const int64_t* __restrict__ d_nref,
-                                              const uint8_t* __restrict__ R, uint8_t* __restrict__ dec,
-                                              int32_t* __restrict__ err) {
+__global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restrict__ s, int64_t n,
+                                                          const int64_t* __restrict__ bin, const int64_t* __restrict__ boff,
+                                                          const int64_t* __restrict__ bdsum, const int64_t* __restrict__ d_nref,
+                                                          const uint8_t* __restrict__ R, uint8_t* __restrict__ dec,
+                                                          int32_t* __restrict__ err) {
+    __shared__ uint8_t stg[WPB][2 * TK_B];
+    const int64_t b = (int64_t)blockIdx.x * WPB + wave_in_block();
     const int64_t base = b * TK_B;
     if (base >= n) return;
     const int lane = lane_id();
     const int64_t i = base + lane;
     // the block's 64 bytes and the 64 after them (a token starting in the block ends within 32) in
     // LDS: the token parses below read LDS, not one dependent HBM byte after the other
-    uint8_t* st = stg_w;
-    wave_sync();   // (the wave's previous tile is done with the staging bytes)
+    uint8_t* st = stg[wave_in_block()];
     const uint8_t c = i < n ? s[i] : (uint8_t)',';
     st[lane] = c;
     st[TK_B + lane] = i + TK_B < n ? s[i + TK_B] : (uint8_t)0;
@@ -624,30 +624,6 @@ __device__ __forceinline__ void tok_fill_tile(int64_t b, uint8_t* stg_w, const u
         const int64_t pj = __shfl(p, j), lj = __shfl(contrib, j), oj = __shfl(o, j);
         wave_copy(dec + oj, R + pj, lj, lane);
     }
-}
-
-template <bool WRITE>
-__global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restrict__ s, int64_t n,
-                                                          const int64_t* __restrict__ bin, const int64_t* __restrict__ boff,
-                                                          const int64_t* __restrict__ bdsum, const int64_t* __restrict__ d_nref,
-                                                          const uint8_t* __restrict__ R, uint8_t* __restrict__ dec,
-                                                          int32_t* __restrict__ err) {
-    __shared__ uint8_t stg[WPB][2 * TK_B];
-    const int64_t b = (int64_t)blockIdx.x * WPB + wave_in_block();
-    tok_fill_tile<WRITE>(b, stg[wave_in_block()], s, n, bin, boff, bdsum, d_nref, R, dec, err);
-}
-
-// The fill of the record tiles [trange[0], trange[1]) (device values), grid-stride: one part of the
-// pipelined fill + format (dc_fill_format).
-__global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill_range(const uint8_t* __restrict__ s, int64_t n,
-                                                               const int64_t* __restrict__ bin, const int64_t* __restrict__ boff,
-                                                               const int64_t* __restrict__ bdsum, const int64_t* __restrict__ d_nref,
-                                                               const uint8_t* __restrict__ R, uint8_t* __restrict__ dec,
-                                                               int32_t* __restrict__ err, const int64_t* __restrict__ trange) {
-    __shared__ uint8_t stg[WPB][2 * TK_B];
-    const int64_t t0 = trange[0], t1 = trange[1];
-    for (int64_t b = t0 + (int64_t)blockIdx.x * WPB + wave_in_block(); b < t1; b += (int64_t)gridDim.x * WPB)
-        tok_fill_tile<true>(b, stg[wave_in_block()], s, n, bin, boff, bdsum, d_nref, R, dec, err);
 }
 
 // Token table of the fused reconstruction (opt-in, SCCG_DC_FUSED=1): instead of copying bytes into a decoded
@@ -929,7 +905,6 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
 constexpr int OPT = 16, OB = 256 * OPT, OFRUNS = 384;
 constexpr int TW = 5;   // k_out_index entries per block boundary
 constexpr int FMT_U_DEFAULT = 1;
-constexpr int FILL_PARTS_DEFAULT = 4;   // dc_fill_format: fill / format parts in flight together
 constexpr bool FMT_NT_DEFAULT = false;
 
 // Block boundaries: output offset o_b = o_first + b * OB clamped to [0, total]; its position
@@ -1144,8 +1119,7 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
                                                     const int32_t* __restrict__ ns, const int32_t* __restrict__ nl,
                                                     const int64_t* __restrict__ ncum, int64_t nn,
                                                     const int32_t* __restrict__ ls, const int32_t* __restrict__ ll,
-                                                    int64_t nlr, const int64_t* __restrict__ tab, uint8_t* __restrict__ out,
-                                                    int64_t b_off) {
+                                                    int64_t nlr, const int64_t* __restrict__ tab, uint8_t* __restrict__ out) {
     // the tile's decoded bytes from a 16-byte-aligned base, 16 bytes per thread and load, with
     // 16 bytes of slack for format_out16's unaligned 16-byte reads (dec holds >= 64 bytes of slack)
     __shared__ uint4 sdec4[(U * OB + 64) / 16];
@@ -1154,7 +1128,7 @@ __global__ __launch_bounds__(256) void k_format_out(const uint8_t* __restrict__ 
     __shared__ int64_t st[2 * TW];
     uint32_t* sdec_w = reinterpret_cast<uint32_t*>(sdec4);
     const int tid = threadIdx.x;
-    const int64_t b = b_off + blockIdx.x;   // (a grid-stride loop over blocks: 0.35-0.43 ms instead of 0.27)
+    const int64_t b = blockIdx.x;   // (a grid-stride loop over blocks: 0.35-0.43 ms instead of 0.27)
     if (tid < 2 * TW) st[tid] = tab[TW * b + tid];
     __syncthreads();
     const int64_t d0 = st[0], d1 = st[TW];
@@ -1685,71 +1659,6 @@ int dc_tok_range_tiled(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const
     return 0;
 }
 
-namespace {
-// Part bounds of the pipelined fill + format: format part k takes output blocks [B_k, B_k+1) with
-// B_k = k * nblk / K; it needs the decoded bytes below D_k+1 (the decoded offset of block B_k+1's
-// first position, tab), which the record tiles with boff < D_k+1 produce -- so fill part k takes
-// the tiles [T_k, T_k+1), T_k = the first tile with boff >= D_k (T_0 = 0, T_K = ntiles): the fills
-// run in order on one stream, and after fill part k every byte format part k reads is written.
-__global__ void k_fill_bounds(const int64_t* __restrict__ tab, int64_t nblk, int K, const int64_t* __restrict__ boff,
-                              int64_t ntiles, int64_t* __restrict__ tr) {
-    const int k = (int)threadIdx.x;
-    if (k > K) return;
-    if (k == 0) { tr[0] = 0; return; }
-    if (k == K) { tr[K] = ntiles; return; }
-    const int64_t Bk = (int64_t)k * nblk / K;
-    const int64_t D = tab[TW * Bk + 0];
-    int64_t lo = 0, hi = ntiles;   // first tile with boff >= D
-    while (lo < hi) {
-        const int64_t m = (lo + hi) >> 1;
-        if (boff[m] >= D) hi = m; else lo = m + 1;
-    }
-    tr[k] = lo;
-}
-}  // namespace
-
-int dc_fill_format(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
-                   const int64_t* d_dlt, const int64_t* d_contrib,
-                   const uint8_t* d_R, uint8_t* d_dec, const int64_t* d_nref, int32_t* d_err, int64_t nres, const DcRuns& nr,
-                   const DcRuns& lr, int64_t* d_span, uint8_t* d_out, int64_t* d_tr, hipStream_t s, hipStream_t s2,
-                   hipEvent_t ev) {
-    static const int parts = [] {
-        const char* e = getenv("SCCG_FILL_PARTS");
-        const int v = e ? atoi(e) : FILL_PARTS_DEFAULT;
-        return v >= 1 && v <= 8 ? v : FILL_PARTS_DEFAULT;
-    }();
-    const int64_t total = nres + (nres > 0 ? (nres - 1) / 50 : 0);
-    const int64_t o_first = -(int64_t)((uintptr_t)d_out & 15);
-    const int64_t nblk = nres > 0 ? (total - o_first + OB - 1) / OB : 0;
-    const int64_t ntiles = (n + TK_B - 1) / TK_B;
-    if (parts <= 1 || nblk < 64 * parts || ntiles < 64 * parts || n <= 0 || !dc_tok_tiled() || nres <= 0) {
-        const int rc = dc_decode_fill(d_s, n, d_lp, d_off, d_dsum, d_dlt, d_contrib, d_R, d_dec, s, d_nref, d_err);
-        if (rc) return rc;
-        return dc_format(d_dec, nres, nr, lr, d_span, d_out, s);
-    }
-    hipLaunchKernelGGL(k_out_index, dim3(grid_for(2 * (nblk + 1), 256)), dim3(256), 0, s, nres, total, o_first, nblk, (int64_t)OB,
-                       (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
-                       (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)nullptr,
-                       (const int64_t*)nullptr, d_span);
-    hipLaunchKernelGGL(k_fill_bounds, dim3(1), dim3(64), 0, s, (const int64_t*)d_span, nblk, parts, d_off, ntiles, d_tr);
-    SCCG_HIP(hipGetLastError());
-    const unsigned fg = grid_for((ntiles + parts - 1) / parts, WPB) > 4096 ? 4096 : grid_for((ntiles + parts - 1) / parts, WPB);
-    for (int k = 0; k < parts; k++) {
-        PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_fill_range, dim3(fg), dim3(SCCG_BLOCK), 0, s, d_s, n, d_lp, d_off, d_dsum, d_nref,
-                    d_R, d_dec, d_err, (const int64_t*)(d_tr + k));
-        SCCG_HIP(hipEventRecord(ev, s));
-        SCCG_HIP(hipStreamWaitEvent(s2, ev, 0));
-        const int64_t b0 = (int64_t)k * nblk / parts, b1 = (int64_t)(k + 1) * nblk / parts;
-        PROF_LAUNCH(PROF_DC_FORMAT, s2, (k_format_out<1, false>), dim3((unsigned)(b1 - b0)), dim3(256), 0, s2, d_dec, nres, total,
-                    o_first, (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
-                    (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out, b0);
-    }
-    SCCG_HIP(hipGetLastError());
-    SCCG_HIP(hipEventRecord(ev, s2));
-    SCCG_HIP(hipStreamWaitEvent(s, ev, 0));
-    return 0;
-}
-
 int64_t dc_format_span_words(int64_t nres) {   // (both formatters' tables; the output's misalignment adds a block)
     const int64_t a = 3 * ((nres + FSPAN - 1) / FSPAN + 2), o = TW * ((nres + nres / 50 + 16) / OB + 3);
     return a > o ? a : o;
@@ -1818,7 +1727,7 @@ int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns
 #define SCCG_FMT_LAUNCH(U, NT)                                                                                       \
     PROF_LAUNCH(PROF_DC_FORMAT, s, (k_format_out<U, NT>), dim3((unsigned)nblk), dim3(256), 0, s, d_dec, nres, total, o_first, \
                 (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,                          \
-                (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out, (int64_t)0)
+                (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out)
         if (fmt_u == 1) { if (fmt_nt) SCCG_FMT_LAUNCH(1, true); else SCCG_FMT_LAUNCH(1, false); }
         else if (fmt_u == 2) { if (fmt_nt) SCCG_FMT_LAUNCH(2, true); else SCCG_FMT_LAUNCH(2, false); }
         else { if (fmt_nt) SCCG_FMT_LAUNCH(4, true); else SCCG_FMT_LAUNCH(4, false); }

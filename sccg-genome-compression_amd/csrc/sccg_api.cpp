@@ -1091,16 +1091,11 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     }
     GET(uint8_t, dec, B_D_DEC, D + 64);
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // the fill copies from R'
+    TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s, sc + 9, d_err));
     if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
     TRY(dev_put_bytes(out + hlen, "\n", 1, s));
     GET(int64_t, span, B_D_SPAN, dc_format_span_words(nres));
-    if (dc_tok_tiled()) {   // fill and format in parts, the format of one beside the fill of the next
-        TRY(dc_fill_format(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, sc + 9, d_err, nres, nr, lr, span,
-                           out + hlen + 1, sc + 48, s, ctx->side, ctx->ev_join));
-    } else {
-        TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s, sc + 9, d_err));
-        TRY(dc_format(dec, nres, nr, lr, span, out + hlen + 1, s));
-    }
+    TRY(dc_format(dec, nres, nr, lr, span, out + hlen + 1, s));
     TRY(dev_put_bytes(out + total - 1, "\n", 1, s));
     {   // (tiled record line: the range check ran with the fill) error bits and |R'| behind the output
         const RbItem it[2] = {{d_err, &err, (int)sizeof err}, {sc + 9, &nRp, (int)sizeof nRp}};
