@@ -791,7 +791,7 @@ def load_pmc(kernel: str) -> dict | None:
     try:
         doc = json.load(open(path))
         v = doc.get(kernel, {}).get("hbm_bytes_per_launch")
-        return {"hbm_bytes_per_launch": v, "source": doc.get("_source", path)} if v else None
+        return {"hbm_bytes_per_launch": v, "source": doc.get("_source", "profiles/pmc_summary.json")} if v else None
     except Exception:
         return None
 

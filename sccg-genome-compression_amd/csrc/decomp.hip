@@ -1585,9 +1585,8 @@ int dc_decode_prepare(const uint8_t* d_s, int64_t n, int64_t* d_lp, int64_t* d_c
         hipLaunchKernelGGL(k_tok_blocks, dim3(g), dim3(256), 0, s, d_s, n, d_lp, d_contrib, d_dlt, d_err,
                            tk ? tk->btok : nullptr);
         SCCG_HIP(hipGetLastError());
-        int rc = dev_excl_sum(d_contrib, d_off, nb, d_total, d_partial, s);
-        if (rc) return rc;
-        rc = dev_excl_sum(d_dlt, d_dsum, nb, nullptr, d_partial, s);
+        // (d_partial: scan_partials_needed(n + 1) + 16 >= 2 * scan_partials_needed(nb))
+        int rc = dev_excl_sum2(d_contrib, d_off, d_total, d_dlt, d_dsum, nullptr, nb, d_partial, s);
         if (rc || !tk) return rc;   // (unfused: the range check is in the fill, dc_decode_fill)
         rc = dev_excl_sum(tk->btok, tk->btoff, nb, tk->d_ntok, d_partial, s);
         if (rc) return rc;

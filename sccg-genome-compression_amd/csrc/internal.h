@@ -52,6 +52,10 @@ int dev_put_framed(uint8_t* dst, const uint8_t* src, int64_t n, char pre, char p
 int64_t scan_partials_needed(int64_t n);
 int dev_excl_sum(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
                  hipStream_t s);
+// two independent exclusive sums of n elements in the same three launches; d_partial holds
+// 2 * scan_partials_needed(n)
+int dev_excl_sum2(const int64_t* in0, int64_t* out0, int64_t* d_total0, const int64_t* in1, int64_t* out1,
+                  int64_t* d_total1, int64_t n, int64_t* d_partial, hipStream_t s);
 int dev_excl_max(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
                  hipStream_t s);
 

@@ -53,10 +53,19 @@ __device__ int64_t block_excl(int64_t v, int64_t* tmp /*17*/, int64_t* total) {
     return r;
 }
 
+// Up to two independent scans of the same length share each launch (blockIdx.y picks the array):
+// the record line's two block-prefix scans run as three launches instead of six.
+struct ScanArrays {
+    const int64_t* in[2];
+    int64_t* out[2];
+    int64_t* total[2];
+    int64_t* partial[2];
+};
+
 template <class Op>
-__global__ __launch_bounds__(SCCG_BLOCK) void k_tile_reduce(const int64_t* __restrict__ in, int64_t n,
-                                                            int64_t* __restrict__ partial) {
+__global__ __launch_bounds__(SCCG_BLOCK) void k_tile_reduce(ScanArrays a, int64_t n) {
     __shared__ int64_t tmp[17];
+    const int64_t* __restrict__ in = a.in[blockIdx.y];
     const int64_t base = (int64_t)blockIdx.x * TILE;
     int64_t acc = Op::id();
 #pragma unroll
@@ -66,7 +75,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_reduce(const int64_t* __res
     }
     int64_t tot;
     block_excl<Op>(acc, tmp, &tot);
-    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+    if (threadIdx.x == 0) a.partial[blockIdx.y][blockIdx.x] = tot;
 }
 
 // Single-block scans: SCCG_SB_T threads (256-thread builds do not wait for a whole free CU beside
@@ -76,9 +85,10 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_reduce(const int64_t* __res
 #endif
 constexpr int SB_T = SCCG_SB_T, PART_PER = 4;
 template <class Op>
-__global__ __launch_bounds__(SB_T) void k_partials_scan(int64_t* __restrict__ partial, int64_t nb,
-                                                        int64_t* __restrict__ total) {
+__global__ __launch_bounds__(SB_T) void k_partials_scan(ScanArrays a, int64_t nb) {
     __shared__ int64_t tmp[17];
+    int64_t* __restrict__ partial = a.partial[blockIdx.y];
+    int64_t* total = a.total[blockIdx.y];
     int64_t carry = Op::id();
     for (int64_t base = 0; base < nb; base += SB_T * PART_PER) {
         const int64_t i0 = base + (int64_t)threadIdx.x * PART_PER;
@@ -101,10 +111,10 @@ __global__ __launch_bounds__(SB_T) void k_partials_scan(int64_t* __restrict__ pa
 }
 
 template <class Op>
-__global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(const int64_t* __restrict__ in, int64_t n,
-                                                          const int64_t* __restrict__ partial,
-                                                          int64_t* __restrict__ out) {
+__global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(ScanArrays a, int64_t n) {
     __shared__ int64_t tmp[17];
+    const int64_t* __restrict__ in = a.in[blockIdx.y];
+    int64_t* __restrict__ out = a.out[blockIdx.y];
     // each thread owns ITEMS consecutive elements
     const int64_t base = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * ITEMS;
     int64_t v[ITEMS];
@@ -115,7 +125,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(const int64_t* __restr
         acc = Op::f(acc, v[i]);
     }
     int64_t ex = block_excl<Op>(acc, tmp, nullptr);
-    int64_t run = Op::f(partial[blockIdx.x], ex);
+    int64_t run = Op::f(a.partial[blockIdx.y][blockIdx.x], ex);
 #pragma unroll
     for (int i = 0; i < ITEMS; i++) {
         if (base + i < n) out[base + i] = run;
@@ -128,9 +138,11 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(const int64_t* __restr
 // (L2-hot) for the prefixes
 constexpr int SMALL_PER = 16, SMALL_MAX = 16384;   // (<= 64 elements per thread at 256 threads)
 template <class Op>
-__global__ __launch_bounds__(SB_T) void k_small_scan(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ out,
-                                                     int64_t* __restrict__ total) {
+__global__ __launch_bounds__(SB_T) void k_small_scan(ScanArrays a, int64_t n) {
     __shared__ int64_t tmp[17];
+    const int64_t* __restrict__ in = a.in[blockIdx.y];
+    int64_t* __restrict__ out = a.out[blockIdx.y];
+    int64_t* total = a.total[blockIdx.y];
     const int64_t per = (n + SB_T - 1) / SB_T, base = (int64_t)threadIdx.x * per;
     int64_t acc = Op::id();
     for (int64_t g = 0; g < per; g += SMALL_PER) {
@@ -156,24 +168,32 @@ __global__ __launch_bounds__(SB_T) void k_small_scan(const int64_t* __restrict__
 }
 
 template <class Op>
-int scan_impl(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
-              hipStream_t s) {
+int scan_impl(const ScanArrays& a, int m, int64_t n, hipStream_t s) {
     if (n <= 0) {
-        if (d_total) return dev_set_i64(d_total, 1, {0}, s);
+        for (int i = 0; i < m; i++)
+            if (a.total[i]) {
+                const int rc = dev_set_i64(a.total[i], 1, {0}, s);
+                if (rc) return rc;
+            }
         return 0;
     }
     if (n <= SMALL_MAX) {
-        hipLaunchKernelGGL(k_small_scan<Op>, dim3(1), dim3(SB_T), 0, s, in, n, out, d_total);
+        hipLaunchKernelGGL(k_small_scan<Op>, dim3(1, m), dim3(SB_T), 0, s, a, n);
         SCCG_HIP(hipGetLastError());
         return 0;
     }
     const int64_t nb = (n + TILE - 1) / TILE;
-    hipLaunchKernelGGL(k_tile_reduce<Op>, dim3((unsigned)nb), dim3(SCCG_BLOCK), 0, s, in, n, d_partial);
-    hipLaunchKernelGGL(k_partials_scan<Op>, dim3(1), dim3(SB_T), 0, s, d_partial, nb, d_total);
-    hipLaunchKernelGGL(k_tile_scan<Op>, dim3((unsigned)nb), dim3(SCCG_BLOCK), 0, s, in, n,
-                       (const int64_t*)d_partial, out);
+    hipLaunchKernelGGL(k_tile_reduce<Op>, dim3((unsigned)nb, m), dim3(SCCG_BLOCK), 0, s, a, n);
+    hipLaunchKernelGGL(k_partials_scan<Op>, dim3(1, m), dim3(SB_T), 0, s, a, nb);
+    hipLaunchKernelGGL(k_tile_scan<Op>, dim3((unsigned)nb, m), dim3(SCCG_BLOCK), 0, s, a, n);
     SCCG_HIP(hipGetLastError());
     return 0;
+}
+
+template <class Op>
+int scan_one(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial, hipStream_t s) {
+    const ScanArrays a{{in, in}, {out, out}, {d_total, d_total}, {d_partial, d_partial}};
+    return scan_impl<Op>(a, 1, n, s);
 }
 
 struct Vals8 {
@@ -246,12 +266,19 @@ int64_t scan_partials_needed(int64_t n) { return (n + TILE - 1) / TILE + 1; }
 
 int dev_excl_sum(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
                  hipStream_t s) {
-    return scan_impl<OpSum>(in, out, n, d_total, d_partial, s);
+    return scan_one<OpSum>(in, out, n, d_total, d_partial, s);
+}
+
+int dev_excl_sum2(const int64_t* in0, int64_t* out0, int64_t* d_total0, const int64_t* in1, int64_t* out1,
+                  int64_t* d_total1, int64_t n, int64_t* d_partial, hipStream_t s) {
+    const int64_t np = scan_partials_needed(n);
+    const ScanArrays a{{in0, in1}, {out0, out1}, {d_total0, d_total1}, {d_partial, d_partial + np}};
+    return scan_impl<OpSum>(a, 2, n, s);
 }
 
 int dev_excl_max(const int64_t* in, int64_t* out, int64_t n, int64_t* d_total, int64_t* d_partial,
                  hipStream_t s) {
-    return scan_impl<OpMax>(in, out, n, d_total, d_partial, s);
+    return scan_one<OpMax>(in, out, n, d_total, d_partial, s);
 }
 
 // ---------------------------------------------------------------------------------------------
