@@ -36,7 +36,8 @@ struct DcFmtSrc {
 // every '\n' of the record text, unordered: d_buf[0] = their count, d_buf[1, 1 + DC_NL_CAP) the
 // first DC_NL_CAP found (one pass; the caller sorts them, or uses dc_find_lines when there are more)
 constexpr int DC_NL_CAP = 32;
-int dc_newlines(const uint8_t* d_rec, int64_t n, int64_t* d_buf, hipStream_t s);
+// (d_err, if given, is zeroed in the same stream-ordered launch as the count)
+int dc_newlines(const uint8_t* d_rec, int64_t n, int64_t* d_buf, hipStream_t s, int32_t* d_err = nullptr);
 // positions of the first four '\n' of the record text (n when absent) -> d_nl[0..3]
 int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl, hipStream_t s);
 // exclusive max-scan of parenthesis positions: d_lp[i] = last '(' or ')' strictly before i
@@ -81,5 +82,11 @@ bool dc_tok_tiled();
 int64_t dc_format_span_words(int64_t nres);
 // With fz (fused path) d_dec is unused: the decoded bytes come from fz's token table; the stream
 // waits for wait_before (the reference strip) between the block index and the formatter.
+// index_ready: dc_format_index already wrote the block index into d_span (on another stream,
+// ordered before wait_before).
 int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out,
-              hipStream_t s, const DcFmtSrc* fz = nullptr, hipEvent_t wait_before = nullptr);
+              hipStream_t s, const DcFmtSrc* fz = nullptr, hipEvent_t wait_before = nullptr, bool index_ready = false);
+// The unfused formatter's block index alone (it needs the run lists, not the decoded bytes, so it
+// can run beside the token fill); returns false (nothing launched) where dc_format builds its own.
+bool dc_format_index(int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out, hipStream_t s,
+                     int* rc);

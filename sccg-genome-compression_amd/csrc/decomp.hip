@@ -118,7 +118,10 @@ __global__ void k_run_items_parse(const uint8_t* __restrict__ s, int64_t n, cons
 // of a parenthesis max-scan, an item-rank scan and three prefix sums (decompression.cpp:126-207 per
 // item, running start, sorted).
 // ---------------------------------------------------------------------------------------------
-constexpr int RL_LANE = 16, RL_TILE = 64 * RL_LANE, RL_BEHIND = 32, RL_AHEAD = 64;
+#ifndef SCCG_RL_LANE
+#define SCCG_RL_LANE 8   // (16: ~5 us slower on the chr1 reconstruction, more serial bytes per lane)
+#endif
+constexpr int RL_LANE = SCCG_RL_LANE, RL_TILE = 64 * RL_LANE, RL_BEHIND = 32, RL_AHEAD = 64;
 constexpr int RL_STAGE = RL_BEHIND + RL_TILE + RL_AHEAD;
 
 // the wave's staged bytes: global positions [t0 - RL_BEHIND, t0 + tile + RL_AHEAD), 0 outside [0, n)
@@ -434,6 +437,9 @@ constexpr int WPB = 4;
 // one per lane, the rest 16 bytes per lane as aligned stores built from five dword loads of the
 // (unaligned) source combined with v_alignbyte.  The source may be read up to 19 bytes past
 // src + l (the reference buffers carry 64 bytes of slack).
+#ifndef WC_DEPTH
+#define WC_DEPTH 2
+#endif
 __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t l, int lane) {
     const int64_t h = ((16 - ((uintptr_t)dst & 15)) & 15) < l ? ((16 - ((uintptr_t)dst & 15)) & 15) : l;
     const int64_t nb = (l - h) >> 4;
@@ -444,15 +450,31 @@ __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8
     const unsigned sh = (unsigned)((uintptr_t)s0 & 3);
     const uint32_t* sa = reinterpret_cast<const uint32_t*>((uintptr_t)s0 & ~(uintptr_t)3);
     uint4* d = reinterpret_cast<uint4*>(dst + h);
-    for (int64_t c = lane; c < nb; c += 64) {
-        const uint32_t* w = sa + 4 * c;
-        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-        uint4 v;
-        v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
-        v.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
-        d[c] = v;
+    // WC_DEPTH KiB of loads in flight per wave before the stores (one 1 KiB step at a time left the
+    // fill bound by the bytes in flight: ~3 TB/s)
+    for (int64_t c0 = lane; c0 < nb; c0 += 64 * WC_DEPTH) {
+        uint32_t w[WC_DEPTH][5];
+#pragma unroll
+        for (int u = 0; u < WC_DEPTH; u++) {
+            const int64_t c = c0 + 64 * u;
+            if (c < nb) {
+                const uint32_t* ws = sa + 4 * c;
+#pragma unroll
+                for (int i = 0; i < 5; i++) w[u][i] = ws[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < WC_DEPTH; u++) {
+            const int64_t c = c0 + 64 * u;
+            if (c < nb) {
+                uint4 v;
+                v.x = __builtin_amdgcn_alignbyte(w[u][1], w[u][0], sh);
+                v.y = __builtin_amdgcn_alignbyte(w[u][2], w[u][1], sh);
+                v.z = __builtin_amdgcn_alignbyte(w[u][3], w[u][2], sh);
+                v.w = __builtin_amdgcn_alignbyte(w[u][4], w[u][3], sh);
+                d[c] = v;
+            }
+        }
     }
 }
 
@@ -1466,8 +1488,18 @@ int dc_find_lines(const uint8_t* d_rec, int64_t n, int64_t* d_nl /*8: 4 results 
     return 0;
 }
 
-int dc_newlines(const uint8_t* d_rec, int64_t n, int64_t* d_buf, hipStream_t s) {
-    SCCG_HIP(hipMemsetAsync(d_buf, 0, sizeof(int64_t), s));
+namespace {
+__global__ void k_nl_init(int64_t* cnt, int32_t* err) {
+    if (threadIdx.x == 0) {
+        *cnt = 0;
+        if (err) *err = 0;
+    }
+}
+}  // namespace
+
+int dc_newlines(const uint8_t* d_rec, int64_t n, int64_t* d_buf, hipStream_t s, int32_t* d_err) {
+    hipLaunchKernelGGL(k_nl_init, dim3(1), dim3(64), 0, s, d_buf, d_err);   // (one launch zeroes both)
+    SCCG_HIP(hipGetLastError());
     if (n <= 0) return 0;
     const unsigned g = grid_for(n, 256) > 4096 ? 4096 : grid_for(n, 256);
     hipLaunchKernelGGL(k_newlines, dim3(g), dim3(256), 0, s, d_rec, n, reinterpret_cast<unsigned long long*>(d_buf), d_buf + 1);
@@ -1663,34 +1695,69 @@ int64_t dc_format_span_words(int64_t nres) {   // (both formatters' tables; the 
     return a > o ? a : o;
 }
 
+namespace {
+bool fmt_span_path() {   // (A/B runs: the position-centric writer)
+    static const bool v = getenv("SCCG_FMT_SPAN") != nullptr;
+    return v;
+}
+bool fmt_pipe() { return getenv("SCCG_FMT_PIPE") != nullptr; }
+int fmt_u() {   // output bytes per k_format_out block: U * OB (the fused and pipelined formatters use OB)
+    static const int v = [] {
+        const char* e = getenv("SCCG_FMT_U");
+        const int u = e ? atoi(e) : FMT_U_DEFAULT;
+        return u == 1 || u == 2 || u == 4 ? u : FMT_U_DEFAULT;
+    }();
+    return v;
+}
+struct FmtGeom {
+    int64_t total, o_first, ob, nblk;
+};
+FmtGeom fmt_geom(int64_t nres, const uint8_t* d_out, bool ob1) {
+    FmtGeom g;
+    g.total = nres + (nres - 1) / 50;   // the final '\n' is the caller's
+    g.o_first = -(int64_t)((uintptr_t)d_out & 15);
+    g.ob = ob1 ? OB : (int64_t)fmt_u() * OB;
+    g.nblk = (g.total - g.o_first + g.ob - 1) / g.ob;
+    return g;
+}
+int launch_out_index(const FmtGeom& g, int64_t nres, const DcRuns& nr, const DcRuns& lr, const DcFmtSrc* fz,
+                     int64_t* d_span, hipStream_t s) {
+    hipLaunchKernelGGL(k_out_index, dim3(grid_for(2 * (g.nblk + 1), 256)), dim3(256), 0, s, nres, g.total, g.o_first, g.nblk,
+                       g.ob, (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
+                       (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, fz ? (const int64_t*)fz->tk.o : nullptr,
+                       fz ? fz->d_ntok : nullptr, d_span);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+}  // namespace
+
+bool dc_format_index(int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out, hipStream_t s,
+                     int* rc) {
+    *rc = 0;
+    if (nres <= 0 || fmt_span_path() || fmt_pipe()) return false;
+    *rc = launch_out_index(fmt_geom(nres, d_out, false), nres, nr, lr, nullptr, d_span, s);
+    return true;
+}
+
 int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns& lr, int64_t* d_span, uint8_t* d_out,
-              hipStream_t s, const DcFmtSrc* fz, hipEvent_t wait_before) {
+              hipStream_t s, const DcFmtSrc* fz, hipEvent_t wait_before, bool index_ready) {
     if (nres <= 0) {
         if (wait_before) SCCG_HIP(hipStreamWaitEvent(s, wait_before, 0));
         return 0;
     }
-    static const bool span_path = getenv("SCCG_FMT_SPAN") != nullptr;   // (A/B runs: the position-centric writer)
+    const bool span_path = fmt_span_path();
     if (fz || !span_path) {
-        const int64_t total = nres + (nres - 1) / 50;   // the final '\n' is the caller's
-        const int64_t o_first = -(int64_t)((uintptr_t)d_out & 15);
-        // output bytes per k_format_out block (U * OB; the fused and pipelined formatters use OB)
-        static const int fmt_u = [] {
-            const char* e = getenv("SCCG_FMT_U");
-            const int u = e ? atoi(e) : FMT_U_DEFAULT;
-            return u == 1 || u == 2 || u == 4 ? u : FMT_U_DEFAULT;
-        }();
         static const bool fmt_nt = [] {
             const char* e = getenv("SCCG_FMT_NT");
             return e ? atoi(e) != 0 : FMT_NT_DEFAULT;
         }();
-        const bool pipe = getenv("SCCG_FMT_PIPE") != nullptr;
-        const int64_t ob = (fz || pipe) ? OB : (int64_t)fmt_u * OB;
-        const int64_t nblk = (total - o_first + ob - 1) / ob;
-        hipLaunchKernelGGL(k_out_index, dim3(grid_for(2 * (nblk + 1), 256)), dim3(256), 0, s, nres, total, o_first, nblk, ob,
-                           (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,
-                           (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, fz ? (const int64_t*)fz->tk.o : nullptr,
-                           fz ? fz->d_ntok : nullptr, d_span);
-        SCCG_HIP(hipGetLastError());
+        const bool pipe = fmt_pipe();
+        const FmtGeom g = fmt_geom(nres, d_out, fz || pipe);
+        const int64_t total = g.total, o_first = g.o_first, nblk = g.nblk;
+        if (!index_ready || fz || pipe) {
+            const int rc = launch_out_index(g, nres, nr, lr, fz, d_span, s);
+            if (rc) return rc;
+        }
         if (wait_before) SCCG_HIP(hipStreamWaitEvent(s, wait_before, 0));
         if (fz) {
             PROF_LAUNCH(PROF_DC_FORMAT, s, k_format_fused, dim3((unsigned)nblk), dim3(256), 0, s, *fz, nres, total, o_first,
@@ -1727,8 +1794,9 @@ int dc_format(const uint8_t* d_dec, int64_t nres, const DcRuns& nr, const DcRuns
     PROF_LAUNCH(PROF_DC_FORMAT, s, (k_format_out<U, NT>), dim3((unsigned)nblk), dim3(256), 0, s, d_dec, nres, total, o_first, \
                 (const int32_t*)nr.start, (const int32_t*)nr.len, (const int64_t*)nr.cum, nr.n,                          \
                 (const int32_t*)lr.start, (const int32_t*)lr.len, lr.n, (const int64_t*)d_span, d_out)
-        if (fmt_u == 1) { if (fmt_nt) SCCG_FMT_LAUNCH(1, true); else SCCG_FMT_LAUNCH(1, false); }
-        else if (fmt_u == 2) { if (fmt_nt) SCCG_FMT_LAUNCH(2, true); else SCCG_FMT_LAUNCH(2, false); }
+        const int fu = fmt_u();
+        if (fu == 1) { if (fmt_nt) SCCG_FMT_LAUNCH(1, true); else SCCG_FMT_LAUNCH(1, false); }
+        else if (fu == 2) { if (fmt_nt) SCCG_FMT_LAUNCH(2, true); else SCCG_FMT_LAUNCH(2, false); }
         else { if (fmt_nt) SCCG_FMT_LAUNCH(4, true); else SCCG_FMT_LAUNCH(4, false); }
 #undef SCCG_FMT_LAUNCH
         SCCG_HIP(hipGetLastError());

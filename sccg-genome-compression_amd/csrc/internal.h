@@ -47,6 +47,8 @@ int dev_set_i64(int64_t* p, int n, std::initializer_list<int64_t> vals, hipStrea
 int dev_set_i32(int32_t* p, int n, std::initializer_list<int32_t> vals, hipStream_t s);
 // stream-ordered write of up to 16 bytes (copied into the kernel arguments)
 int dev_put_bytes(uint8_t* p, const char* bytes, int n, hipStream_t s);
+// out[0, hlen) = hdr, out[hlen] = '\n', out[total - 1] = '\n' (one launch; total >= hlen + 2)
+int dev_put_frame(uint8_t* out, const uint8_t* hdr, int64_t hlen, int64_t total, hipStream_t s);
 // stream-ordered dst = pre, src[0, n), post (one launch)
 int dev_put_framed(uint8_t* dst, const uint8_t* src, int64_t n, char pre, char post, hipStream_t s);
 int64_t scan_partials_needed(int64_t n);

@@ -22,6 +22,7 @@ struct Pending {
 struct Registry {
     std::mutex mu;
     bool on = false;
+    uint32_t mask = ~0u;   // families bracketed while on (bit = family index)
     std::vector<hipEvent_t> pool;
     std::vector<Pending> pending;
     double ms[PROF_COUNT] = {};
@@ -75,7 +76,7 @@ thread_local Open t_open;
 
 void prof_begin(hipStream_t s, int id) {
     Registry& r = reg();
-    if (!r.on) return;
+    if (!r.on || !((r.mask >> id) & 1u)) return;
     std::lock_guard<std::mutex> g(r.mu);
     hipEvent_t e = r.take();
     (void)hipEventRecord(e, s);
@@ -85,7 +86,7 @@ void prof_begin(hipStream_t s, int id) {
 
 void prof_end(hipStream_t s, int id) {
     Registry& r = reg();
-    if (!r.on) return;
+    if (!r.on || !((r.mask >> id) & 1u)) return;
     std::lock_guard<std::mutex> g(r.mu);
     if (!t_open.e[id]) return;
     if (t_open.epoch[id] != r.epoch) { r.pool.push_back(t_open.e[id]); t_open.e[id] = nullptr; return; }
@@ -103,6 +104,7 @@ int sccg_profile(sccg_ctx* /*ctx*/, int enable) {
     std::lock_guard<std::mutex> g(r.mu);
     r.drain();
     r.on = enable != 0;
+    r.mask = enable == 1 ? ~0u : (uint32_t)enable;   // (> 1: a bit mask of families, sccg_profile_name order)
     r.epoch++;
     for (int i = 0; i < PROF_COUNT; i++) { r.ms[i] = 0; r.n[i] = 0; }
     return SCCG_OK;

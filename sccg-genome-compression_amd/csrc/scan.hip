@@ -234,6 +234,22 @@ int dev_put_framed(uint8_t* dst, const uint8_t* src, int64_t n, char pre, char p
     return 0;
 }
 
+namespace {
+// out[0, hlen) = hdr, out[hlen] = '\n', out[total - 1] = '\n'
+__global__ void k_put_frame(uint8_t* __restrict__ out, const uint8_t* __restrict__ hdr, int64_t hlen, int64_t total) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= hlen; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = i < hlen ? hdr[i] : (uint8_t)'\n';
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[total - 1] = '\n';
+}
+}  // namespace
+
+int dev_put_frame(uint8_t* out, const uint8_t* hdr, int64_t hlen, int64_t total, hipStream_t s) {
+    const unsigned g = grid_for(hlen + 1, 256) > 64 ? 64 : grid_for(hlen + 1, 256);
+    hipLaunchKernelGGL(k_put_frame, dim3(g), dim3(256), 0, s, out, hdr, hlen, total);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
 int dev_put_bytes(uint8_t* p, const char* bytes, int n, hipStream_t s) {
     Bytes16 v{};
     if (n > 16) return SCCG_E_INTERNAL;

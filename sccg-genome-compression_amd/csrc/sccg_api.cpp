@@ -948,7 +948,8 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     int64_t nlb[1 + DC_NL_CAP];
     uint8_t first = 0;
     GET(int64_t, dnl, B_D_NLPOS, 1 + DC_NL_CAP);
-    TRY(dc_newlines(rec, n, dnl, s));
+    int32_t* d_err = reinterpret_cast<int32_t*>(sc + 40);
+    TRY(dc_newlines(rec, n, dnl, s, d_err));   // (also zeroes the error bits)
     {
         const RbItem it[2] = {{dnl, nlb, (int)sizeof nlb}, {rec, &first, n > 0 ? 1 : 0}};
         TRY(dev_readback(it, 2, s));
@@ -995,8 +996,6 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     }
 
     // ---- record line on side2 (own scratch) beside the run-line parses, which read counts back
-    int32_t* d_err = reinterpret_cast<int32_t*>(sc + 40);
-    HIPTRY(hipMemsetAsync(d_err, 0, sizeof(int32_t), s));
     GET(int64_t, lp2, B_D_LP2, nenc + 1);
     GET(int64_t, dlt2, B_D_DLT2, nenc + 1);
     GET(int64_t, part2, B_PARTIAL2, scan_partials_needed(nenc + 1) + 16);
@@ -1092,13 +1091,20 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
         return SCCG_OK;
     }
     GET(uint8_t, dec, B_D_DEC, D + 64);
+    GET(int64_t, span, B_D_SPAN, dc_format_span_words(nres));
+    // side2, beside the token fill: the output's frame (header, its '\n', the final '\n' -- bytes
+    // the formatter does not write) and the formatter's block index (run lists only)
+    // (the fill is launched first: it is the critical path)
+    HIPTRY(hipEventRecord(ctx->ev_fork2, s));
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // the fill copies from R'
     TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s, sc + 9, d_err));
-    if (hlen) HIPTRY(hipMemcpyAsync(out, rec, (size_t)hlen, hipMemcpyDeviceToDevice, s));
-    TRY(dev_put_bytes(out + hlen, "\n", 1, s));
-    GET(int64_t, span, B_D_SPAN, dc_format_span_words(nres));
-    TRY(dc_format(dec, nres, nr, lr, span, out + hlen + 1, s));
-    TRY(dev_put_bytes(out + total - 1, "\n", 1, s));
+    HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
+    TRY(dev_put_frame(out, rec, hlen, total, ctx->side2));
+    int irc = 0;
+    const bool index_ready = dc_format_index(nres, nr, lr, span, out + hlen + 1, ctx->side2, &irc);
+    TRY(irc);
+    HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
+    TRY(dc_format(dec, nres, nr, lr, span, out + hlen + 1, s, nullptr, ctx->ev_lines, index_ready));
     {   // (tiled record line: the range check ran with the fill) error bits and |R'| behind the output
         const RbItem it[2] = {{d_err, &err, (int)sizeof err}, {sc + 9, &nRp, (int)sizeof nRp}};
         TRY(dev_readback(it, 2, s));

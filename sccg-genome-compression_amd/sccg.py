@@ -219,8 +219,22 @@ class Context:
             self._err(rc)
         return n.value
 
-    def profile(self, enable: bool = True) -> None:
-        """Reset and enable (or disable) per-kernel HIP-event timing."""
+    def profile(self, enable: bool = True, families: list | None = None) -> None:
+        """Reset and enable (or disable) per-kernel HIP-event timing; `families` (names from
+        sccg_profile_name) limits the bracketed launches to those families."""
+        if enable and families:
+            mask, i = 0, 0
+            while True:
+                name = self.lib.sccg_profile_name(i)
+                if not name:
+                    break
+                if name.decode() in families:
+                    mask |= 1 << i
+                i += 1
+            if mask <= 1:
+                raise ValueError(f"profile: unknown kernel families {families}")
+            self.lib.sccg_profile(self.ptr, mask)
+            return
         self.lib.sccg_profile(self.ptr, int(enable))
 
     def profile_get(self) -> dict:
