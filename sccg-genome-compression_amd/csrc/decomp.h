@@ -74,7 +74,7 @@ int dc_tok_range_tiled(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const
                        const int64_t* d_nref, int32_t* d_err, hipStream_t s);
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
                    const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s,
-                   const int64_t* d_nref, int32_t* d_err);
+                   const int64_t* d_nref, int32_t* d_err, int64_t dcap = INT64_MAX);
 // true: the record line takes the per-block path (its range errors are known only after the fill)
 bool dc_tok_tiled();
 // N insertion + lowercase + 50-column wrap of nres result bytes into d_out (no final '\n');

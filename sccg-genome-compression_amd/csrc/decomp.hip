@@ -590,7 +590,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restr
                                                           const int64_t* __restrict__ bin, const int64_t* __restrict__ boff,
                                                           const int64_t* __restrict__ bdsum, const int64_t* __restrict__ d_nref,
                                                           const uint8_t* __restrict__ R, uint8_t* __restrict__ dec,
-                                                          int32_t* __restrict__ err) {
+                                                          int32_t* __restrict__ err, int64_t dcap) {
     __shared__ uint8_t stg[WPB][2 * TK_B];
     const int64_t b = (int64_t)blockIdx.x * WPB + wave_in_block();
     const int64_t base = b * TK_B;
@@ -638,12 +638,16 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restr
         tok = false;
     }
     if (!WRITE) return;
-    if (!tok && contrib == 1 && c != '(') dec[o] = c;   // literals, a stray ')' included
+    // (dcap: dec's capacity -- a fill queued before the decoded length is known writes nothing past
+    // it; only a call that then fails its output-capacity check can reach it)
+    if (!tok && contrib == 1 && c != '(' && o < dcap) dec[o] = c;   // literals, a stray ')' included
     unsigned long long tm = __ballot(tok);
     while (tm) {
         const int j = __ffsll((long long)tm) - 1;
         tm &= tm - 1;
-        const int64_t pj = __shfl(p, j), lj = __shfl(contrib, j), oj = __shfl(o, j);
+        const int64_t pj = __shfl(p, j), oj = __shfl(o, j);
+        int64_t lj = __shfl(contrib, j);
+        if (lj > dcap - oj) lj = dcap - oj > 0 ? dcap - oj : 0;
         wave_copy(dec + oj, R + pj, lj, lane);
     }
 }
@@ -926,7 +930,7 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
 // ---------------------------------------------------------------------------------------------
 constexpr int OPT = 16, OB = 256 * OPT, OFRUNS = 384;
 constexpr int TW = 5;   // k_out_index entries per block boundary
-constexpr int FMT_U_DEFAULT = 1;
+constexpr int FMT_U_DEFAULT = 4;   // (U = 1 / 2 / 4 on one box, chr1: 0.638-0.647 / 0.634-0.639 / 0.624-0.626 ms)
 constexpr bool FMT_NT_DEFAULT = false;
 
 // Block boundaries: output offset o_b = o_first + b * OB clamped to [0, total]; its position
@@ -1667,11 +1671,11 @@ bool dc_tok_tiled() {
 
 int dc_decode_fill(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const int64_t* d_off, const int64_t* d_dsum,
                    const int64_t* d_dlt, const int64_t* d_contrib, const uint8_t* d_R, uint8_t* d_dec, hipStream_t s,
-                   const int64_t* d_nref, int32_t* d_err) {
+                   const int64_t* d_nref, int32_t* d_err, int64_t dcap) {
     if (n <= 0) return 0;
     if (dc_tok_tiled()) {
         PROF_LAUNCH(PROF_DC_DECODE, s, k_tok_fill2<true>, dim3(grid_for((n + TK_B - 1) / TK_B, WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n,
-                    d_lp, d_off, d_dsum, d_nref, d_R, d_dec, d_err);
+                    d_lp, d_off, d_dsum, d_nref, d_R, d_dec, d_err, dcap);
         SCCG_HIP(hipGetLastError());
         return 0;
     }
@@ -1685,7 +1689,7 @@ int dc_tok_range_tiled(const uint8_t* d_s, int64_t n, const int64_t* d_lp, const
                        const int64_t* d_nref, int32_t* d_err, hipStream_t s) {
     if (n <= 0 || !dc_tok_tiled()) return 0;   // (the scan path checked the range in dc_decode_prepare)
     hipLaunchKernelGGL(k_tok_fill2<false>, dim3(grid_for((n + TK_B - 1) / TK_B, WPB)), dim3(SCCG_BLOCK), 0, s, d_s, n, d_lp,
-                       d_off, d_dsum, d_nref, (const uint8_t*)nullptr, (uint8_t*)nullptr, d_err);
+                       d_off, d_dsum, d_nref, (const uint8_t*)nullptr, (uint8_t*)nullptr, d_err, (int64_t)0);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

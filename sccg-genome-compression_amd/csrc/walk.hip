@@ -461,9 +461,12 @@ __device__ __forceinline__ int32_t ext_k(const WalkPtrs& A, WalkLds& L, BufPos& 
 // 2m+1 <= 4*64 window positions (m = 100: 201).  Its bytes come from the LDS copy when they lie
 // in it.
 // ---------------------------------------------------------------------------------------------
+// A key no k-mer has: pure keys are < 4^kp <= 2^30 (kp <= 15), exotic ones >= 2^31.  Window slots
+// outside the window hold it, so "some slot equals kk" needs no vmask test.
+constexpr uint32_t KEY_NONE = 0x40000000u;
 struct RegWin {
     int32_t P, lo, n;
-    uint32_t key[4];
+    uint32_t key[4];  // KEY_NONE outside the window
     uint32_t vmask;   // bit q: index 4*lane+q is inside the window
 };
 
@@ -476,7 +479,7 @@ __device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin&
     W.n = hi - W.lo + 1;
     if (W.n < 0) W.n = 0;
     W.vmask = 0;
-    W.key[0] = W.key[1] = W.key[2] = W.key[3] = 0;
+    W.key[0] = W.key[1] = W.key[2] = W.key[3] = KEY_NONE;
     const bool lds = L && B->has_r(W.lo, W.n + 20);
     const int i0 = 4 * lane;
     if (i0 >= W.n) return;
@@ -491,6 +494,7 @@ __device__ __forceinline__ void reg_window(const WalkPtrs& A, int32_t P, RegWin&
     for (int q = 0; q < 4; q++) {
         W.key[q] = (bad >> q) & KM ? exotic_key(A.R + W.lo + i0 + q, kp) : (uint32_t)(code >> (2 * q)) & MASK;
         if (i0 + q < W.n) W.vmask |= 1u << q;
+        else W.key[q] = KEY_NONE;
     }
 }
 
@@ -515,6 +519,11 @@ __device__ __forceinline__ uint32_t win_match(const WalkPtrs& A, const RegWin& W
             if (((m >> q) & 1u) && !bytes_eq(A.R + c0 + q, A.T + y, A.kp)) m &= ~(1u << q);
     }
     return m;
+}
+
+// some window slot holds key kk (exact for pure keys; exotic ones still need win_match's byte check)
+__device__ __forceinline__ bool win_any(const RegWin& W, uint32_t kk) {
+    return (W.key[0] == kk) | (W.key[1] == kk) | (W.key[2] == kk) | (W.key[3] == kk);
 }
 
 // LDS Bloom filter of the register window's keys (only needed for wide literal scans)
@@ -835,11 +844,17 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         if (DBG) dbg_c[1]++;
         // ---- literal steps: first y in [x, scan_end) whose k-mer has a candidate in the window
         const uint32_t key_l = valid ? target_key_w(A, y_l, tw) : 0u;
+        // (after a mismatch the next k-mer usually hits: typically one or two positions.  A hit
+        // needs only "some slot equals the key" -- slots outside the window hold KEY_NONE --; an
+        // exotic key's hit is confirmed by win_match's byte compare)
         int hl = -1;
         const int nb = scan_end - x < 64 ? scan_end - x : 64;
         for (int yy = 0; yy < nb; yy++) {
             const uint32_t kk = lane_val(key_l, yy);
-            if (__ballot(win_match(A, W, kk, x + yy) != 0)) { hl = yy; break; }
+            if (__ballot(win_any(W, kk)) && (kk < KEY_EXOTIC || __ballot(win_match(A, W, kk, x + yy) != 0))) {
+                hl = yy;
+                break;
+            }
         }
         if (hl < 0) {
             x = (x + 64 < scan_end) ? x + 64 : scan_end;
@@ -3054,7 +3069,8 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         const int32_t* nd = dev_nlist ? A.scal : nullptr;
         PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(A.C, WWPB)), dim3(64 * WWPB), 0, s, A, (const int32_t*)A.plist,
                     A.C, nd);
-        RC(launch_carry(A, s));
+        // a round that walks every chunk (round 1) carries nothing: a carry needs an unlisted successor
+        if (dev_nlist) RC(launch_carry(A, s));
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
         if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, fbase_cap), dim3(FZ_T), 0, s, A, 0);
@@ -3292,7 +3308,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                     PROF_LAUNCH(PROF_WALK, s, walk_kernel(A), dim3(grid_for(gl, WWPB)), dim3(64 * WWPB), 0, s, A,
                                 (const int32_t*)A.plist, gl, dev ? (const int32_t*)A.scal : (const int32_t*)nullptr);
                     SCCG_HIP(hipGetLastError());
-                    RC(launch_carry(A, s));
+                    if (dev || gl < A.C) RC(launch_carry(A, s));   // (every chunk listed: no carries)
                     // Commit, fill the first frozen runs and find the next round's pending chunks
                     // without waiting for the host; more frozen chunks and the rare escalated
                     // (pn2 == 0) ones are handled after the batch's one sync.
