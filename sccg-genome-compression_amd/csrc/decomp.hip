@@ -928,7 +928,10 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
 // binary search in LDS and then walks them.  (The position-centric k_format_span wrote each
 // position's byte to LDS, 16 bytes apart per lane, and copied the line-broken range out again.)
 // ---------------------------------------------------------------------------------------------
-constexpr int OPT = 16, OB = 256 * OPT, OFRUNS = 384;
+#ifndef SCCG_OFRUNS
+#define SCCG_OFRUNS 384
+#endif
+constexpr int OPT = 16, OB = 256 * OPT, OFRUNS = SCCG_OFRUNS;   // (a block with more runs takes the global-runs path)
 constexpr int TW = 5;   // k_out_index entries per block boundary
 constexpr int FMT_U_DEFAULT = 4;   // (U = 1 / 2 / 4 on one box, chr1: 0.638-0.647 / 0.634-0.639 / 0.624-0.626 ms)
 constexpr bool FMT_NT_DEFAULT = false;

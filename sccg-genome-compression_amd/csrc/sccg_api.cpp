@@ -927,22 +927,13 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
                      int64_t out_cap, int64_t* out_len, bool size_only) {
     hipStream_t s = ctx->stream;
     GET(int64_t, sc, B_SCAL, 64);
-    // ---- reference (decompression.cpp:47-58, 105-110), right behind the newline search, on the side
-    //      stream beside everything that follows: its filter depends on the N line only when that line is exactly "," (then it
+    // ---- reference (decompression.cpp:47-58, 105-110), first, on the side stream beside everything
+    //      that follows: its filter depends on the N line only when that line is exactly "," (then it
     //      keeps the N's, FILTER_UPPER), so the usual filter starts now and that rare case redoes it
     //      once the lines are known.  (Its length |R'| stays on the device, sc[9], until the range
     //      check and the parse's readback.)
     GET(uint8_t, Rp, B_RP, rn + 64);   // (only R' is read: the strip writes no R here)
-    // the line ends: one pass collects every '\n' (a record file holds 2-3); more than DC_NL_CAP
-    // of them -> four ordered first-match searches.  Queued ahead of the strip (it is the start of
-    // the critical path; the strip has slack until the token fill).
-    int64_t nl[4];
-    int64_t nlb[1 + DC_NL_CAP];
-    uint8_t first = 0;
-    GET(int64_t, dnl, B_D_NLPOS, 1 + DC_NL_CAP);
-    int32_t* d_err = reinterpret_cast<int32_t*>(sc + 40);
     HIPTRY(hipEventRecord(ctx->ev_fork, s));
-    TRY(dc_newlines(rec, n, dnl, s, d_err));   // (also zeroes the error bits)
     HIPTRY(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, nullptr, sc + 8, nullptr, nullptr, FILTER_DROP_UPPERN_ONLY, Rp, 1, ctx->side));
     HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
@@ -951,6 +942,16 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
         hipStream_t st;
         ~JoinSide() { (void)hipStreamWaitEvent(st, c->ev_rstrip, 0); }
     } join_side{ctx, s};
+    // the line ends: one pass collects every '\n' (a record file holds 2-3); more than DC_NL_CAP
+    // of them -> four ordered first-match searches.  (Queued ahead of the strip, the search itself
+    // finished earlier, but its one-wave readback then waited ~40 us for a slot behind the strip's
+    // grid: measured slower.)
+    int64_t nl[4];
+    int64_t nlb[1 + DC_NL_CAP];
+    uint8_t first = 0;
+    GET(int64_t, dnl, B_D_NLPOS, 1 + DC_NL_CAP);
+    int32_t* d_err = reinterpret_cast<int32_t*>(sc + 40);
+    TRY(dc_newlines(rec, n, dnl, s, d_err));   // (also zeroes the error bits)
     {
         const RbItem it[2] = {{dnl, nlb, (int)sizeof nlb}, {rec, &first, n > 0 ? 1 : 0}};
         TRY(dev_readback(it, 2, s));
@@ -1042,12 +1043,13 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
     if (!dc_tok_tiled()) HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // (nenc <= 0 skips the range check's wait)
     TRY(dc_n_check(nr, sc + 16, sc + 12, d_err, s));
-    // The usual call: the token fill goes out right behind the N check, before the host knows the
-    // decoded length D, into a buffer of the output's capacity (D <= nres < out_cap whenever the
-    // call succeeds; the fill writes nothing past it), and the readback below runs on side2 beside
-    // it -- the host round trip leaves the critical path.
+    // Opt-in (SCCG_DC_SPEC=1): the token fill goes out right behind the N check, before the host
+    // knows the decoded length D, into a buffer of the output's capacity (D <= nres < out_cap whenever
+    // the call succeeds; the fill writes nothing past it), and the readback below runs on side2 beside
+    // it.  Measured slower (chr1 0.617-0.619 vs 0.613-0.617 ms): the one-wave readback then waits for
+    // a slot behind the fill's grid, so the host learns D later than without it.
     constexpr int64_t SPEC_FILL_MAX = (int64_t)4 << 30;
-    static const bool spec_env = getenv("SCCG_DC_NO_SPEC") == nullptr;   // (A/B runs: the fill after the readback)
+    static const bool spec_env = getenv("SCCG_DC_SPEC") != nullptr;
     const bool spec_fill = spec_env && !fused && dc_tok_tiled() && !size_only && nenc > 0 && out_cap > 0 &&
                            out_cap <= SPEC_FILL_MAX;
     uint8_t* dec = nullptr;
