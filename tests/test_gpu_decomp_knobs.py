@@ -1,0 +1,99 @@
+"""Opt-in reconstruction paths and the profiler's family mask (GPU).
+
+* SCCG_DC_SPEC=1 queues the token fill before the host knows the decoded length (decompression.cpp
+  :210-236 filled into a buffer of the output's capacity; sccg_api.cpp reconstruct_impl).  It is off
+  by default (measured slower) but must stay exact: round trips against the target FASTA,
+  a too-small output buffer (SCCG_E_NOMEM) and tokens beyond the reference (:223-229, SCCG_E_RANGE).
+  The knob is read once per process, so the checks run in a child process.
+* sccg_profile with a family mask brackets only those families (bench.py's timed region).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from pkg import sccg
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = sccg.Context(0)
+    yield c
+    c.close()
+
+
+CHILD = r"""
+import json, sys
+sys.path.insert(0, HERE)
+import torch
+import synthlib
+from pkg import sccg
+dev = torch.device("cuda", 0)
+torch.zeros(1, device=dev)   # torch's HIP runtime before the library context
+ctx = sccg.Context(0)
+out = {"round_trips": [], "nomem": None, "range": []}
+
+def dev_bytes(b):
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+
+def run(rfa, rec, cap):
+    d_r, d_c = dev_bytes(rfa), dev_bytes(rec)
+    d_o = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+    n = ctx.reconstruct_device(d_r.data_ptr(), len(rfa), d_c.data_ptr(), len(rec), d_o.data_ptr(), cap)
+    torch.cuda.synchronize()
+    return d_o[:n].cpu().numpy().tobytes()
+
+for prof, rl, tl, seed in (("hg", 200_000, 201_000, 3), ("hg", 1_000_000, 1_003_000, 4), ("t2t", 300_000, 300_000, 5)):
+    rfa, tfa = synthlib.synth_pair(prof, rl, tl, seed)
+    rec = ctx.compress(rfa, tfa)
+    need = ctx.reconstruct_device(dev_bytes(rfa).data_ptr(), len(rfa), dev_bytes(rec).data_ptr(), len(rec), 0, 0)
+    got = run(rfa, rec, need + 64)
+    out["round_trips"].append(got == tfa)
+    if seed == 3:
+        try:
+            run(rfa, rec, need - 1)
+            out["nomem"] = 0
+        except sccg.SccgError as e:
+            out["nomem"] = e.rc
+rfa = b">r\n" + b"ACGT" * 50 + b"\n"
+for rec in (b"\n,\n(0,20)(500,30)", b">h\n\n(3,2)\n(0,20)(500,30)", b"\n,\nAC(190,20)"):
+    try:
+        run(rfa, rec, 1 << 16)
+        out["range"].append(0)
+    except sccg.SccgError as e:
+        out["range"].append(e.rc)
+ctx.close()
+print(json.dumps(out))
+"""
+
+
+def test_spec_fill_round_trips_and_errors():
+    env = dict(os.environ, SCCG_DC_SPEC="1")
+    p = subprocess.run([sys.executable, "-c", f"HERE = {HERE!r}\n" + CHILD], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["round_trips"] == [True, True, True], d
+    assert d["nomem"] == sccg.ERR_CODES["SCCG_E_NOMEM"], d
+    assert d["range"] == [sccg.ERR_CODES["SCCG_E_RANGE"]] * 3, d
+
+
+def test_profile_family_mask(ctx):
+    import synthlib
+    rfa, tfa = synthlib.synth_pair("hg", 2_000_000, 2_010_000, 6)
+    ctx.profile(True, families=["walk"])
+    ctx.compress(rfa, tfa)
+    only = ctx.profile_get()
+    ctx.profile(True)
+    ctx.compress(rfa, tfa)
+    every = ctx.profile_get()
+    ctx.profile(False)
+    assert set(only) <= {"walk"}, only
+    assert "walk" in every and len(every) > 1, every
+    with pytest.raises(ValueError):
+        ctx.profile(True, families=["no_such_family"])
