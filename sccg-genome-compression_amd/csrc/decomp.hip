@@ -280,6 +280,8 @@ __global__ __launch_bounds__(256) void k_rl_tiles(RlJob j0, RlJob j1, int32_t* _
 // pass 2 (one block): exclusive prefix over tiles of (count, deltas, lengths) and the last item
 // length before each tile (-1: none); the totals -> d_count[0..1]
 constexpr int RL_SCAN_T = 256;   // (a 1024-thread block waits for a whole CU beside a running strip)
+constexpr int RL_SCAN_B = 8;     // tile summaries per batch of loads
+__device__ __forceinline__ int64_t i64_of(int lo, int hi) { return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo); }
 __global__ __launch_bounds__(RL_SCAN_T) void k_rl_scan(RlJob j0, RlJob j1) {   // block b: line b
     constexpr int NW = RL_SCAN_T / 64;
     __shared__ int64_t wc[NW], wd[NW], wl[NW], wlast[NW];
@@ -293,10 +295,26 @@ __global__ __launch_bounds__(RL_SCAN_T) void k_rl_scan(RlJob j0, RlJob j1) {   /
     }
     const int tid = (int)threadIdx.x, lane = lane_id(), w = wave_in_block();
     const int64_t per = (ntiles + RL_SCAN_T - 1) / RL_SCAN_T, b0 = tid * per;
+    const int64_t b1 = b0 + per < ntiles ? b0 + per : ntiles;
+    // (RL_SCAN_B tiles' summaries loaded together: one tile at a time made this single-block pass
+    // a chain of dependent HBM round trips, ~30 us on the chr1 reconstruction's critical path)
     int64_t c = 0, d = 0, l = 0, last = -1;
-    for (int64_t t = b0; t < b0 + per && t < ntiles; t++) {
-        c += tsum[4 * t]; d += tsum[4 * t + 1]; l += tsum[4 * t + 2];
-        if (tsum[4 * t + 3] >= 0) last = tsum[4 * t + 3];
+    for (int64_t t0 = b0; t0 < b1; t0 += RL_SCAN_B) {
+        int4 q[RL_SCAN_B][2];
+#pragma unroll
+        for (int u = 0; u < RL_SCAN_B; u++)
+            if (t0 + u < b1) {
+                const int4* p4 = reinterpret_cast<const int4*>(tsum + 4 * (t0 + u));
+                q[u][0] = p4[0];
+                q[u][1] = p4[1];
+            }
+#pragma unroll
+        for (int u = 0; u < RL_SCAN_B; u++)
+            if (t0 + u < b1) {
+                c += i64_of(q[u][0].x, q[u][0].y); d += i64_of(q[u][0].z, q[u][0].w); l += i64_of(q[u][1].x, q[u][1].y);
+                const int64_t tl = i64_of(q[u][1].z, q[u][1].w);
+                if (tl >= 0) last = tl;
+            }
     }
     int64_t ic = c, id = d, il = l, ilast = last;
 #pragma unroll
@@ -312,11 +330,25 @@ __global__ __launch_bounds__(RL_SCAN_T) void k_rl_scan(RlJob j0, RlJob j1) {   /
     int64_t ec = pc + ic - c, ed = pd + id - d, el = pl + il - l;
     int64_t elast = __shfl_up(ilast, 1, 64);
     if (lane == 0 || elast < 0) elast = lane == 0 ? plast : (elast < 0 ? plast : elast);
-    for (int64_t t = b0; t < b0 + per && t < ntiles; t++) {
-        const int64_t tc = tsum[4 * t], td = tsum[4 * t + 1], tl = tsum[4 * t + 2], tlast = tsum[4 * t + 3];
-        tsum[4 * t] = ec; tsum[4 * t + 1] = ed; tsum[4 * t + 2] = el; tsum[4 * t + 3] = elast;
-        ec += tc; ed += td; el += tl;
-        if (tlast >= 0) elast = tlast;
+    for (int64_t t0 = b0; t0 < b1; t0 += RL_SCAN_B) {
+        int4 q[RL_SCAN_B][2];
+#pragma unroll
+        for (int u = 0; u < RL_SCAN_B; u++)
+            if (t0 + u < b1) {
+                const int4* p4 = reinterpret_cast<const int4*>(tsum + 4 * (t0 + u));
+                q[u][0] = p4[0];
+                q[u][1] = p4[1];
+            }
+#pragma unroll
+        for (int u = 0; u < RL_SCAN_B; u++)
+            if (t0 + u < b1) {
+                const int64_t t = t0 + u;
+                const int64_t tc = i64_of(q[u][0].x, q[u][0].y), td = i64_of(q[u][0].z, q[u][0].w);
+                const int64_t tl = i64_of(q[u][1].x, q[u][1].y), tlast = i64_of(q[u][1].z, q[u][1].w);
+                tsum[4 * t] = ec; tsum[4 * t + 1] = ed; tsum[4 * t + 2] = el; tsum[4 * t + 3] = elast;
+                ec += tc; ed += td; el += tl;
+                if (tlast >= 0) elast = tlast;
+            }
     }
     if (tid == RL_SCAN_T - 1 && d_count) { d_count[0] = ec; d_count[1] = el; }
 }
@@ -1707,7 +1739,10 @@ bool fmt_span_path() {   // (A/B runs: the position-centric writer)
     static const bool v = getenv("SCCG_FMT_SPAN") != nullptr;
     return v;
 }
-bool fmt_pipe() { return getenv("SCCG_FMT_PIPE") != nullptr; }
+bool fmt_pipe() {   // (SCCG_FMT_PIPE=1, A/B runs: the resident pipelined grid)
+    static const bool v = getenv("SCCG_FMT_PIPE") != nullptr;
+    return v;
+}
 int fmt_u() {   // output bytes per k_format_out block: U * OB (the fused and pipelined formatters use OB)
     static const int v = [] {
         const char* e = getenv("SCCG_FMT_U");
