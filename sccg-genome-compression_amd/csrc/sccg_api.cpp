@@ -1043,26 +1043,28 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     TRY(dc_decode_prepare(enc, nenc, lp2, contrib, dlt2, doff, dsum, sc + 9, ctx->ev_rstrip, part2, d_err, sc + 12,
                           s, fused ? &tk : nullptr));
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
-    if (!dc_tok_tiled()) HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // (nenc <= 0 skips the range check's wait)
-    TRY(dc_n_check(nr, sc + 16, sc + 12, d_err, s));
-    // Opt-in (SCCG_DC_SPEC=1): the token fill goes out right behind the N check, before the host
-    // knows the decoded length D, into a buffer of the output's capacity (D <= nres < out_cap whenever
-    // the call succeeds; the fill writes nothing past it), and the readback below runs on side2 beside
-    // it.  Measured slower (chr1 0.617-0.619 vs 0.613-0.617 ms): the one-wave readback then waits for
-    // a slot behind the fill's grid, so the host learns D later than without it.
+    // The usual call queues the token fill right behind the N check, before the host knows the
+    // decoded length D, into a buffer of the output's capacity (D <= nres < out_cap whenever the
+    // call succeeds; the fill writes nothing past it), and reads the lengths back on side2 beside
+    // it: the fill no longer waits for a host round trip.  (SCCG_DC_SPEC=0: the fill after the
+    // readback.  Queued behind the readback copy on the same stream it gained nothing: the copy,
+    // an event and a cross-stream wait still sat between the N check and the fill.)
     constexpr int64_t SPEC_FILL_MAX = (int64_t)4 << 30;
-    static const bool spec_env = getenv("SCCG_DC_SPEC") != nullptr;
-    const bool spec_fill = spec_env && !fused && dc_tok_tiled() && !size_only && nenc > 0 && out_cap > 0 &&
+    static const bool spec_on = [] { const char* e = getenv("SCCG_DC_SPEC"); return !e || atoi(e) != 0; }();
+    const bool spec_fill = spec_on && !fused && dc_tok_tiled() && !size_only && nenc > 0 && out_cap > 0 &&
                            out_cap <= SPEC_FILL_MAX;
+    // (the strip's wait goes ahead of the N check, so nothing but the fork's event sits between the
+    // check and the fill; the strip has long finished by then on genome-sized records)
+    if (!dc_tok_tiled() || spec_fill) HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
+    TRY(dc_n_check(nr, sc + 16, sc + 12, d_err, s));
     uint8_t* dec = nullptr;
     hipStream_t rbs = s;
     if (spec_fill) {
         GET(uint8_t, dec0, B_D_DEC, out_cap + 64);
         dec = dec0;
         HIPTRY(hipEventRecord(ctx->ev_fork2, s));
-        HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
-        HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));   // the fill copies from R'
         TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s, sc + 9, d_err, out_cap));
+        HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
         rbs = ctx->side2;
     }
     // one readback: decoded length, error bits, both run lines' counts and totals -- with the tiled

@@ -1,10 +1,11 @@
 """Opt-in reconstruction paths and the profiler's family mask (GPU).
 
-* SCCG_DC_SPEC=1 queues the token fill before the host knows the decoded length (decompression.cpp
-  :210-236 filled into a buffer of the output's capacity; sccg_api.cpp reconstruct_impl).  It is off
-  by default (measured slower) but must stay exact: round trips against the target FASTA,
-  a too-small output buffer (SCCG_E_NOMEM) and tokens beyond the reference (:223-229, SCCG_E_RANGE).
-  The knob is read once per process, so the checks run in a child process.
+* The token fill (decompression.cpp:210-236) is queued before the host knows the decoded length,
+  into a buffer of the output's capacity, beside the readback (the default, exercised by every
+  other reconstruction test); SCCG_DC_SPEC=0 queues it after the host read the length.  Both must
+  stay exact: round trips against the target FASTA, a too-small output buffer (SCCG_E_NOMEM) and
+  tokens beyond the reference (:223-229, SCCG_E_RANGE).  The knob is read once per process, so the
+  checks run in a child process.
 * sccg_profile with a family mask brackets only those families (bench.py's timed region).
 """
 import json
@@ -72,8 +73,8 @@ print(json.dumps(out))
 """
 
 
-def test_spec_fill_round_trips_and_errors():
-    env = dict(os.environ, SCCG_DC_SPEC="1")
+def test_fill_after_readback_round_trips_and_errors():
+    env = dict(os.environ, SCCG_DC_SPEC="0")
     p = subprocess.run([sys.executable, "-c", f"HERE = {HERE!r}\n" + CHILD], env=env, capture_output=True, text=True,
                        timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
