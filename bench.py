@@ -195,24 +195,42 @@ def cpu_baseline_pointer() -> dict | None:
     return out
 
 
-def cpu_genome_estimate(cores: int | None = None) -> dict | None:
-    """The whole hg19-vs-hg18 genome on host cores, from the 24 reference walls in the manifest
-    (measured by tests/golden/pin_genome.py in the build container, concurrently under a RAM
-    budget): total CPU-seconds, single-core rate, and the LPT makespan over P cores."""
+def box_cpu_share() -> int:
+    """Host cores this process may use: its affinity mask, capped at the GPU box's share per GPU
+    (16; the box's os.cpu_count() is the whole machine's)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def cpu_genome_estimate(box_chr21_wall_s: float | None = None, cores: int | None = None) -> dict | None:
+    """The whole hg19-vs-hg18 genome on THIS host's cores, from the reference's own walls: the 24
+    per-pair walls in the manifest (compiled reference, measured once by tests/golden/pin_genome.py
+    in the build container) give the pairs' relative costs; they are scaled to this host by its own
+    chr21 wall measured in this run (cpu_baseline, the same compiled reference on the same pair) over
+    the manifest's chr21 wall.  Makespan = LPT of the scaled walls over P = this host's core share.
+    Without this run's chr21 wall nothing is estimated (no field mixes two machines)."""
     import multigpu
     pins = load_manifest()
     walls = [pins[n]["reference_wall_s"] for n in multigpu.CHROMS if n in pins and "reference_wall_s" in pins[n]]
-    if len(walls) < len(multigpu.CHROMS):
+    c21 = pins.get("chr21", {}).get("reference_wall_s")
+    if len(walls) < len(multigpu.CHROMS) or not c21 or not box_chr21_wall_s:
         return None
+    scale = box_chr21_wall_s / c21
+    walls = [w * scale for w in walls]
     nT = sum(multigpu.HG19)
-    P = cores or 8
+    P = cores or box_cpu_share()
     loads = [sum(walls[i] for i in part) for part in multigpu.lpt_shard(walls, P)]
     return {"cpu_seconds": round(sum(walls), 1), "target_bases": nT, "bases_per_s_one_core": nT / sum(walls),
             "cores": P, "lpt_makespan_s": round(max(loads), 1), "bases_per_s_on_P_cores": nT / max(loads),
-            "note": "compiled reference (oracle/_ref, g++ -O2, stub 7z) walls from tests/golden/genome_manifest.json, "
-                    "measured in the build container (8x 'Intel(R) Xeon(R) Processor', 62 GB; pairs run concurrently "
-                    "under a 46 GB RAM budget); makespan = LPT of those walls over P cores, RAM permitting "
-                    "(chr1 alone needs 17.4 GB)"}
+            "host": {"cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "core_share": box_cpu_share()},
+            "scale_from_chr21": round(scale, 4),
+            "note": f"compiled reference (oracle/_ref, g++ -O2, stub 7z) on this host: its chr21 wall in this run "
+                    f"({box_chr21_wall_s:.1f} s) x the 24 pairs' relative walls from tests/golden/genome_manifest.json "
+                    f"(one machine's ratios, chr21 there {c21:.1f} s); makespan = LPT over P cores of this host, "
+                    f"RAM permitting (chr1 alone needs 17.4 GB)"}
 
 
 def cpu_baseline(timeout_s: int) -> dict | None:
@@ -258,10 +276,45 @@ def cpu_baseline(timeout_s: int) -> dict | None:
     finally:
         shutil.rmtree(d, ignore_errors=True)
     pin = load_manifest().get("chr21", {}).get("record_sha256")
-    return {"value": tl / dt, "unit": "target bases/s", "cores": 1, "kind": kind,
+    return {"value": tl / dt, "unit": "target bases/s", "cores": 1, "kind": kind, "wall_s": dt,
             "sample": f"BASELINE configs[0]: hg19-vs-hg18 chr21-sized synthetic pair |R|={rl:,} |T|={tl:,} (seed 21), "
                       f"wall {dt:.1f} s, single-threaded ({cpu_model()}), stub 7z, stdout to /dev/null",
             "record_matches_pinned": (sha == pin) if pin else None}
+
+
+def chr1_k21(lane: Lane, pair: tuple, tfa: bytes, dev, reps: int = 5) -> dict:
+    """BASELINE configs[1] as written: the chr1 pair with k = 21 (a non-parity override -- the
+    reference hard-codes k = 14, compression.cpp:373 -- so the global walk runs with local = 0),
+    HBM-resident inputs, one lane; the record stream is reconstructed on the GPU and compared with
+    the target FASTA byte for byte."""
+    import torch
+    dr, rn, dt_, tn = pair
+    ctx, s = lane.ctx, lane.stream
+
+    def once():
+        return ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, lane.out.data_ptr(), lane.cap, s.cuda_stream,
+                                   k=21, local=0)
+    once()
+    s.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        n = once()
+        s.synchronize()
+        ts.append(time.perf_counter() - t0)
+    st = ctx.stats()
+    rec = lane.out[:n].clone()
+    need = ctx.reconstruct_device(dr.data_ptr(), rn, rec.data_ptr(), n, 0, 0, s.cuda_stream)
+    d_fa = torch.empty(need + 64, dtype=torch.uint8, device=dev)
+    n_fa = ctx.reconstruct_device(dr.data_ptr(), rn, rec.data_ptr(), n, d_fa.data_ptr(), need + 64, s.cuda_stream)
+    s.synchronize()
+    exact = d_fa[:n_fa].cpu().numpy().tobytes() == tfa
+    dt = sorted(ts)[len(ts) // 2]
+    return {"workload": "BASELINE configs[1]: hg19-vs-hg18 chr1-sized pair, k = 21 (non-parity override, local = 0), "
+                        "1 GPU, one lane", "k": 21, "target_bases": st["target_bases"], "ms": dt * 1e3,
+            "ms_all": [round(t * 1e3, 3) for t in ts], "bases_per_s": st["target_bases"] / dt,
+            "walk_rounds": st["walk_rounds"], "matches": st["n_matches"], "record_bytes": n,
+            "record_sha256": hashlib.sha256(rec.cpu().numpy().tobytes()).hexdigest(), "roundtrip_exact": exact}
 
 
 def end_to_end(ctx, rfa: bytes, tfa: bytes, pinned_sha: str | None, reps: int = 3) -> dict:
@@ -408,6 +461,43 @@ def device_job(pairs: dict, results: dict, dev):
     return job
 
 
+def standalone_costs(lane: Lane, pairs: dict, order: list) -> dict:
+    """Each pair alone on one lane, one after the other (an untimed pass after the timed steps): its
+    compress call's wall time in ms, device-resident inputs -- the per-pair cost a multi-GPU shard
+    plan needs (a T2T-like pair's cost is not proportional to its length)."""
+    import torch
+    out = {}
+    for n in order:
+        dr, rn, dt_, tn = pairs[n]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lane.ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, lane.out.data_ptr(), lane.cap,
+                                 lane.stream.cuda_stream)
+        lane.stream.synchronize()
+        out[n] = round((time.perf_counter() - t0) * 1e3, 3)
+    return out
+
+
+def predicted_makespans(cost: dict, sizes: dict, step_ms: float, worlds=(1, 2, 4, 8)) -> dict:
+    """The N-GPU job time predicted from one GPU's measurements: per-pair standalone costs, LPT-sharded
+    over N GPUs (by measured cost, and by target size as bench.py / genome.py shard by default), each
+    GPU's load divided by the overlap its lanes gain on one GPU (sum of standalone costs / measured
+    step), and never below the costliest single pair (a pair is one GPU's work unless its walk is
+    split, multigpu.split_walk)."""
+    import multigpu
+    names = sorted(cost)
+    gain = sum(cost.values()) / step_ms if step_ms > 0 else 1.0
+    out = {"lane_overlap_gain": round(gain, 3), "costliest_pair": max(names, key=lambda n: cost[n]),
+           "costliest_pair_ms": max(cost.values())}
+    for key, w8 in (("lpt_by_cost", [cost[n] for n in names]), ("lpt_by_size", [sizes[n] for n in names])):
+        e = {}
+        for w in worlds:
+            loads = [sum(cost[names[i]] for i in part) for part in multigpu.lpt_shard(w8, w)]
+            e[str(w)] = round(max(max(loads) / gain, max(cost.values())), 3)
+        out[key + "_ms"] = e
+    return out
+
+
 def t2t_genome(pool: LanePool, jobs: list, world: int, rank: int, dev, steps: int) -> dict:
     """BASELINE configs[4]'s shape: the same 24 UCSC length pairs with the T2T-like profile (the
     stuck, literal-heavy walk of compression.cpp:83-101), each rank its LPT shard; one warm pass,
@@ -423,14 +513,21 @@ def t2t_genome(pool: LanePool, jobs: list, world: int, rank: int, dev, steps: in
     order = sorted(pairs, key=lambda n: -pairs[n][3])
     results: dict = {}
     job = device_job(pairs, results, dev)
+    rounds_per_step: list = []
+
     def step():
         pool.run(order, job)
         pool.sync()
+        rounds_per_step.append({n: results[n][1]["walk_rounds"] for n in order})
 
     dt = timed_region(step, steps, 1, world, torch.cuda.synchronize, dev)
+    timed_rounds = rounds_per_step[1:]   # (the warm pass first)
+    cost = standalone_costs(pool.lanes[0], pairs, order)
     shas = {n: hashlib.sha256(results[n][0].cpu().numpy().tobytes()).hexdigest() for n in order}
-    per = {n: {"rounds": results[n][1]["walk_rounds"], "chains": results[n][1]["walk_chains"],
-               "matches": results[n][1]["n_matches"], "mode": "global" if results[n][1]["mode_global"] else "local"}
+    per = {n: {"rounds": results[n][1]["walk_rounds"], "rounds_per_timed_step": [r[n] for r in timed_rounds],
+               "chains": results[n][1]["walk_chains"], "matches": results[n][1]["n_matches"],
+               "mode": "global" if results[n][1]["mode_global"] else "local", "ms_alone": cost[n],
+               "target_bases": results[n][1]["target_bases"]}
            for n in order}
     nT = sum(results[n][1]["target_bases"] for n in order)
     if world > 1:
@@ -448,13 +545,17 @@ def t2t_genome(pool: LanePool, jobs: list, world: int, rank: int, dev, steps: in
     bad = [n for n in checked if shas[n] != pins[n]["record_sha256"]]
     ms = dt / steps * 1e3
     worst = max(per, key=lambda n: per[n]["rounds"]) if per else None
+    stable = all(len(set(p["rounds_per_timed_step"])) <= 1 for p in per.values())
     return {"workload": "BASELINE configs[4] shape: T2T-like profile (tandem arrays, 1e-2 SNPs, >100-bp deletions "
                         "every ~100 kb) on the 24 hg18/hg19 UCSC length pairs, seed = chromosome index",
             "target_bases": nT, "ms": ms, "bases_per_s": nT / (ms * 1e-3), "steps": steps,
             "pinned_checked": len(checked), "pinned_mismatch": bad,
             "max_rounds": per[worst]["rounds"] if worst else None, "max_rounds_chrom": worst,
+            "rounds_same_every_timed_step": stable,
             "generate_s": round(gen_s, 1), "per_chromosome": per,
-            "lpt_max_over_mean_8gpu": multigpu.max_over_mean([j[2] for j in jobs], 8)}
+            "lpt_max_over_mean_8gpu": multigpu.max_over_mean([j[2] for j in jobs], 8),
+            "predicted": predicted_makespans({n: per[n]["ms_alone"] for n in per},
+                                             {n: per[n]["target_bases"] for n in per}, ms) if world == 1 else None}
 
 
 def end_to_end_genome(pool: LanePool, host_fa: dict, order: list, pins: dict, reps: int = 2) -> dict:
@@ -536,6 +637,7 @@ def main() -> None:
     ap.add_argument("--no-t2t", action="store_true", help="skip the T2T-like genome (configs[4] shape)")
     ap.add_argument("--t2t-steps", type=int, default=2)
     ap.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events in the timed region")
+    ap.add_argument("--no-k21", action="store_true", help="skip the configs[1] leg (chr1 at k = 21)")
     args = ap.parse_args()
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))   # before HIP initialises
@@ -608,6 +710,9 @@ def main() -> None:
         prof_all = lanes[0].ctx.profile_get()
         lanes[0].ctx.profile(False)
 
+    # ---- per-pair standalone costs (untimed) and the N-GPU makespans they predict (N = 1 lines)
+    hg_cost = standalone_costs(lanes[0], pairs, order) if world == 1 else {}
+
     # ---- per-rank totals (all ranks' target bases make up the whole job)
     tot = {"target_bases": sum(results[n][1]["target_bases"] for n in order),
            "reference_bases": sum(results[n][1]["reference_bases"] for n in order),
@@ -679,6 +784,15 @@ def main() -> None:
         del d_fa
         if not exact:
             raise SystemExit("bench: chr1 reconstruction differs from the target FASTA")
+
+    # ---- configs[1] as named: chr1 at k = 21 through the global walk (non-parity: the reference
+    #      hard-codes k = 14, compression.cpp:373; local = 0), round trip checked on the GPU
+    k21 = None
+    if rank == 0 and not args.no_k21 and keep_chr1 is not None:
+        name = "chr1" if "chr1" in pairs else f"chr1_r{rank}"
+        k21 = chr1_k21(lanes[0], pairs[name], keep_chr1[1], dev)
+        if not k21["roundtrip_exact"]:
+            raise SystemExit("bench: chr1 k=21 record stream does not reconstruct the target FASTA")
 
     e2e = None
     if rank == 0 and not args.no_e2e and keep_chr1 is not None:
@@ -784,12 +898,19 @@ def main() -> None:
             "roofline_kernels": kroof,
             "roofline_job": roof_job,
             "cpu_baseline": cpu,
-            "cpu_genome_estimate": cpu_genome_estimate(),
+            "cpu_genome_estimate": cpu_genome_estimate(cpu.get("wall_s") if cpu and world == 1 else None),
             "parity": parity,
             "decompress": decomp,
             "end_to_end": e2e,
             "end_to_end_genome": e2e_genome,
             "t2t_genome": t2t,
+            "chr1_k21": k21,
+            "predicted_multi_gpu": {"hg_genome": predicted_makespans(hg_cost, {n: pairs[n][3] for n in hg_cost}, ms_step)
+                                    if hg_cost else None,
+                                    "t2t_genome": (t2t or {}).get("predicted"),
+                                    "model": "bench.predicted_makespans: per-pair standalone ms, LPT over N GPUs, "
+                                             "loads / the lanes' overlap gain on one GPU, floor = costliest pair"},
+            "hip_runtime": sccg.hip_runtimes(),
             "kernels": kernels,
             "per_chromosome_rank0": per,
         }

@@ -170,11 +170,13 @@ int sccg_reconstruct_device(sccg_ctx* ctx, const void* d_ref_fa, size_t ref_len,
 void sccg_buf_free(sccg_buf* b);
 
 /* Per-kernel device timing with HIP events recorded on the launching stream (process-wide).
- * sccg_profile(ctx, 1) resets and enables it for every family; enable > 1 is a bit mask of the
- * families to bracket (bit i = sccg_profile_name(i)), 0 disables it.  sccg_profile_get returns
- * the summed duration and launch count of one kernel family by name (sccg_profile_name(i),
- * i = 0.. until NULL). */
+ * sccg_profile(ctx, 1) resets and enables it for every family, 0 disables it (enable > 1: a bit
+ * mask as below, kept for old callers -- it cannot select family 0 alone).  sccg_profile_mask
+ * resets and enables it for the families of `mask` (bit i = sccg_profile_name(i); 0 disables).
+ * sccg_profile_get returns the summed duration and launch count of one kernel family by name
+ * (sccg_profile_name(i), i = 0.. until NULL). */
 int sccg_profile(sccg_ctx* ctx, int enable);
+int sccg_profile_mask(sccg_ctx* ctx, uint32_t mask);
 int sccg_profile_get(sccg_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches);
 const char* sccg_profile_name(int i);
 

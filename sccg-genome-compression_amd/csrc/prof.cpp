@@ -99,15 +99,19 @@ void prof_end(hipStream_t s, int id) {
 
 extern "C" {
 
-int sccg_profile(sccg_ctx* /*ctx*/, int enable) {
+int sccg_profile_mask(sccg_ctx* /*ctx*/, uint32_t mask) {
     Registry& r = reg();
     std::lock_guard<std::mutex> g(r.mu);
     r.drain();
-    r.on = enable != 0;
-    r.mask = enable == 1 ? ~0u : (uint32_t)enable;   // (> 1: a bit mask of families, sccg_profile_name order)
+    r.on = mask != 0;
+    r.mask = mask;   // bit i: family sccg_profile_name(i)
     r.epoch++;
     for (int i = 0; i < PROF_COUNT; i++) { r.ms[i] = 0; r.n[i] = 0; }
     return SCCG_OK;
+}
+
+int sccg_profile(sccg_ctx* ctx, int enable) {
+    return sccg_profile_mask(ctx, enable == 1 ? ~0u : (uint32_t)enable);
 }
 
 int sccg_profile_get(sccg_ctx* /*ctx*/, const char* kernel, double* total_ms, int64_t* launches) {

@@ -1051,8 +1051,17 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     // an event and a cross-stream wait still sat between the N check and the fill.)
     constexpr int64_t SPEC_FILL_MAX = (int64_t)4 << 30;
     static const bool spec_on = [] { const char* e = getenv("SCCG_DC_SPEC"); return !e || atoi(e) != 0; }();
-    const bool spec_fill = spec_on && !fused && dc_tok_tiled() && !size_only && nenc > 0 && out_cap > 0 &&
-                           out_cap <= SPEC_FILL_MAX;
+    // The speculative buffer is sized by the caller's capacity, not by D: a caller passing a far
+    // larger output buffer than the record can need (D rarely exceeds |R| + |rec|: every token
+    // copies reference bytes, every literal is a record byte) takes the non-speculative path, which
+    // sizes it by D; so does a call whose speculative allocation fails.
+    bool spec_fill = spec_on && !fused && dc_tok_tiled() && !size_only && nenc > 0 && out_cap > 0 &&
+                     out_cap <= SPEC_FILL_MAX && out_cap <= 2 * (rn + n) + ((int64_t)64 << 20);
+    uint8_t* dec_spec = nullptr;
+    if (spec_fill) {
+        dec_spec = reinterpret_cast<uint8_t*>(ctx->get(B_D_DEC, (size_t)out_cap + 64));
+        if (!dec_spec) spec_fill = false;
+    }
     // (the strip's wait goes ahead of the N check, so nothing but the fork's event sits between the
     // check and the fill; the strip has long finished by then on genome-sized records)
     if (!dc_tok_tiled() || spec_fill) HIPTRY(hipStreamWaitEvent(s, ctx->ev_rstrip, 0));
@@ -1060,8 +1069,7 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     uint8_t* dec = nullptr;
     hipStream_t rbs = s;
     if (spec_fill) {
-        GET(uint8_t, dec0, B_D_DEC, out_cap + 64);
-        dec = dec0;
+        dec = dec_spec;
         HIPTRY(hipEventRecord(ctx->ev_fork2, s));
         TRY(dc_decode_fill(enc, nenc, lp2, doff, dsum, dlt2, contrib, Rp, dec, s, sc + 9, d_err, out_cap));
         HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
@@ -1285,13 +1293,20 @@ int walk_range_dev(sccg_ctx* ctx, const uint8_t* R, int64_t nr, const uint8_t* T
     out->len = (int32_t*)malloc((n ? n : 1) * 4);
     out->t = (int64_t*)malloc((n ? n : 1) * 8);
     std::vector<int32_t> ht(n ? n : 1);
-    if (!out->kind || !out->pos || !out->len || !out->t) return ctx->fail(SCCG_E_NOMEM, "host allocation");
-    if (n) {
-        HIPTRY(hipMemcpyAsync(ht.data(), dt, n * 4, hipMemcpyDeviceToHost, s));
-        HIPTRY(hipMemcpyAsync(out->pos, dp, n * 4, hipMemcpyDeviceToHost, s));
-        HIPTRY(hipMemcpyAsync(out->len, dl, n * 4, hipMemcpyDeviceToHost, s));
+    const int rc = [&]() -> int {   // every error after the allocations frees them
+        if (!out->kind || !out->pos || !out->len || !out->t) return ctx->fail(SCCG_E_NOMEM, "host allocation");
+        if (n) {
+            HIPTRY(hipMemcpyAsync(ht.data(), dt, n * 4, hipMemcpyDeviceToHost, s));
+            HIPTRY(hipMemcpyAsync(out->pos, dp, n * 4, hipMemcpyDeviceToHost, s));
+            HIPTRY(hipMemcpyAsync(out->len, dl, n * 4, hipMemcpyDeviceToHost, s));
+        }
+        HIPTRY(hipStreamSynchronize(s));
+        return SCCG_OK;
+    }();
+    if (rc) {
+        sccg_records_free(out);
+        return rc;
     }
-    HIPTRY(hipStreamSynchronize(s));
     for (size_t i = 0; i < n; i++) { out->kind[i] = 1; out->t[i] = ht[i]; }
     exit_state[0] = ex;
     exit_state[1] = ep;

@@ -23,7 +23,8 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-SCCG_E_IO = 100   # a FASTA file could not be read (host side; no library call was made)
+SCCG_E_IO = 100    # a FASTA file could not be read (host side; no library call was made)
+SCCG_E_OUT = 101   # the output folder could not be written (host side)
 
 
 class Emitter:
@@ -51,7 +52,8 @@ class Emitter:
         import sccg
         self.done.add(name)
         if rc_n and rc_n != sccg.SCCG_E_DELTA_STOI:
-            what = "cannot read the FASTA files" if rc_n == SCCG_E_IO else sccg.ERRORS.get(rc_n, rc_n)
+            what = {SCCG_E_IO: "cannot read the FASTA files",
+                    SCCG_E_OUT: "cannot write the output folder"}.get(rc_n) or sccg.ERRORS.get(rc_n, rc_n)
             print(f"Error: {name}: {what}", file=sys.stderr)
             self.rc = 1
             return
@@ -91,14 +93,20 @@ def compress_pair_files(ctx, ref_path: str, tgt_path: str, out_dir: str, name: s
     the Emitter.  Returns the pair's stats with its rc (the CLI's failure points as error codes)."""
     import sccg
     d = os.path.join(out_dir, name)
-    os.makedirs(d, exist_ok=True)
     path = os.path.join(d, "compressed_genome.txt")
     rc_n, st = 0, {}
     try:
+        os.makedirs(d, exist_ok=True)
         ctx.compress_files(ref_path, tgt_path, path)
         st = ctx.stats()
     except sccg.SccgError as e:
         rc_n = e.rc
+    except OSError as e:   # an unwritable output folder: this chromosome fails, the job goes on
+        print(f"Error: {name}: {e}", file=sys.stderr)
+        rc_n = SCCG_E_OUT
+    except Exception as e:   # noqa: BLE001  (anything else still fails only this pair)
+        print(f"Error: {name}: {e}", file=sys.stderr)
+        rc_n = sccg.ERR_CODES["SCCG_E_HIP"]
     if em is not None:
         if rc_n and rc_n != sccg.SCCG_E_DELTA_STOI:
             em.emit(name, b"", rc_n)
@@ -172,29 +180,35 @@ def compress_shard_files(mine: list[str], ref_dir: str, tgt_dir: str, make_ctx, 
             ctx = make_ctx()
         except Exception as e:   # noqa: BLE001
             print(f"Error: no context: {e}", file=sys.stderr)
-        while True:
-            with lock:
-                if not todo:
-                    break
-                n = todo.pop(0)
-            if ctx is None:
+        try:
+            while True:
                 with lock:
-                    stats[n] = {"rc": err_hip}
-                    em.emit(n, b"", err_hip)
-                continue
-            st = compress_pair_files(ctx, os.path.join(ref_dir, n + ".fa"), os.path.join(tgt_dir, n + ".fa"),
-                                     em.out_dir, n, None)
-            with lock:
-                stats[n] = st
-                if st["rc"] and st["rc"] != sccg_delta_stoi():
-                    em.emit(n, b"", st["rc"])
-                else:
-                    em.written(n, os.path.join(em.out_dir, n, "compressed_genome.txt"), st["rc"])
-        if ctx is not None:
-            try:
-                ctx.close()
-            except Exception:   # noqa: BLE001
-                pass
+                    if not todo:
+                        break
+                    n = todo.pop(0)
+                if ctx is None:
+                    with lock:
+                        stats[n] = {"rc": err_hip}
+                        em.emit(n, b"", err_hip)
+                    continue
+                try:
+                    st = compress_pair_files(ctx, os.path.join(ref_dir, n + ".fa"), os.path.join(tgt_dir, n + ".fa"),
+                                             em.out_dir, n, None)
+                except Exception as e:   # noqa: BLE001  (never lose a pair: it is reported failed)
+                    print(f"Error: {n}: {e}", file=sys.stderr)
+                    st = {"rc": err_hip}
+                with lock:
+                    stats[n] = st
+                    if st["rc"] and st["rc"] != sccg_delta_stoi():
+                        em.emit(n, b"", st["rc"])
+                    else:
+                        em.written(n, os.path.join(em.out_dir, n, "compressed_genome.txt"), st["rc"])
+        finally:
+            if ctx is not None:
+                try:
+                    ctx.close()
+                except Exception:   # noqa: BLE001
+                    pass
 
     ths = [threading.Thread(target=worker) for _ in range(max(1, contexts))]
     for t in ths:
@@ -235,6 +249,37 @@ def collect(names: list[str], parts: dict, stats: dict, em: Emitter | None, dev,
     return all_stats
 
 
+def run_job(names: list[str], ref_dir: str, tgt_dir: str, out_dir: str, make_ctx, rank: int, world: int, dev,
+            contexts: int = 2, run_7z: bool = True, seven_zip: str = "7z", err_hip: int | None = None,
+            cost: dict | None = None) -> tuple[int, dict | None]:
+    """The whole job on one rank: shard, compress, gather, emit.  Rank 0 writes its own pairs'
+    record files straight from the library (sccg_compress_files) and the other ranks' after the
+    gather.  `cost` (name -> measured cost, e.g. per-pair GPU ms) shards by cost instead of target
+    size (a T2T-like pair's walk time is not proportional to its length).  Returns (rc, summary)
+    on rank 0 and (0, None) elsewhere."""
+    import multigpu
+    if err_hip is None:
+        import sccg
+        err_hip = sccg.ERR_CODES["SCCG_E_HIP"]
+    sizes = [os.path.getsize(os.path.join(tgt_dir, n + ".fa")) if os.path.exists(os.path.join(tgt_dir, n + ".fa"))
+             else 0 for n in names]
+    weights = [cost.get(n, s) for n, s in zip(names, sizes)] if cost else sizes
+    mine = [names[i] for i in multigpu.lpt_shard(weights, world)[rank]]
+    em = Emitter(out_dir, run_7z, seven_zip) if rank == 0 else None
+    t0 = time.perf_counter()
+    if em is not None:   # rank 0: files straight to record files (sccg_compress_files)
+        parts, stats = {}, compress_shard_files(mine, ref_dir, tgt_dir, make_ctx, em, err_hip, contexts)
+    else:
+        parts, stats = compress_shard(mine, ref_dir, tgt_dir, make_ctx, em, err_hip)
+    t_comp = time.perf_counter() - t0
+    all_stats = collect(names, parts, stats, em, dev, world)
+    if rank != 0:
+        return 0, None
+    rc = em.wait()
+    return rc, {"chromosomes": len(names), "target_fasta_bytes": sum(sizes), "ranks": world,
+                "compress_seconds_rank0": t_comp, "per_chrom": all_stats}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref-dir", required=True)
@@ -243,6 +288,7 @@ def main(argv=None) -> int:
     ap.add_argument("--names", default="", help="comma-separated subset (default: all common *.fa)")
     ap.add_argument("--no-7z", action="store_true")
     ap.add_argument("--contexts", type=int, default=2, help="rank 0: library contexts (host threads) on its GPU")
+    ap.add_argument("--cost", default="", help="JSON file {name: measured cost} to shard by (default: target size)")
     args = ap.parse_args(argv)
 
     import torch
@@ -263,24 +309,11 @@ def main(argv=None) -> int:
     if args.names:
         keep = set(args.names.split(","))
         names = [n for n in names if n in keep]
-    sizes = [os.path.getsize(os.path.join(args.tgt_dir, n + ".fa")) for n in names]
-    mine = [names[i] for i in multigpu.lpt_shard(sizes, world)[rank]]
-    em = Emitter(args.out, not args.no_7z) if rank == 0 else None
-
-    t0 = time.perf_counter()
-    if em is not None:   # rank 0: files straight to record files (sccg_compress_files)
-        parts, stats = {}, compress_shard_files(mine, args.ref_dir, args.tgt_dir, lambda: sccg.Context(local), em,
-                                                sccg.ERR_CODES["SCCG_E_HIP"], args.contexts)
-    else:
-        parts, stats = compress_shard(mine, args.ref_dir, args.tgt_dir, lambda: sccg.Context(local), em,
-                                      sccg.ERR_CODES["SCCG_E_HIP"])
-    t_comp = time.perf_counter() - t0
-    all_stats = collect(names, parts, stats, em, dev, world)
-    rc = 0
+    rc, summary = run_job(names, args.ref_dir, args.tgt_dir, args.out, lambda: sccg.Context(local), rank, world, dev,
+                          contexts=args.contexts, run_7z=not args.no_7z,
+                          cost=json.load(open(args.cost)) if args.cost else None)
     if rank == 0:
-        rc = em.wait()
-        print(json.dumps({"chromosomes": len(names), "target_fasta_bytes": sum(sizes), "ranks": world,
-                          "compress_seconds_rank0": t_comp, "per_chrom": all_stats}))
+        print(json.dumps(summary))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -62,14 +62,39 @@ class Params(ctypes.Structure):
 _lib = None
 
 
+def hip_runtimes() -> list[str]:
+    """The distinct libamdhip64 files mapped into this process (/proc/self/maps)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln and "/" in ln})
+    except OSError:
+        return []
+
+
 def load_library():
-    """Load libsccg.so (raises if it was not built: no silent fallback)."""
+    """Load libsccg.so (raises if it was not built: no silent fallback).
+
+    One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7, the same
+    as /opt/rocm's that libsccg links), and whichever is loaded first serves every later user of
+    that SONAME -- but torch's libraries name the file (libamdhip64.so, RPATH $ORIGIN), so loading
+    libsccg before torch maps BOTH runtimes, and torch then sees no GPU.  So torch (when installed)
+    is imported first and its runtime serves libsccg too; a process that still ends up with two
+    runtimes mapped is refused with a clear message instead of failing later in a HIP call.  The
+    C CLIs (no torch) run on /opt/rocm's runtime."""
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} not built: run `make` or __graft_entry__.build()")
+    try:
+        import torch  # noqa: F401  (its HIP runtime first: see above)
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
+    rts = hip_runtimes()
+    if len({os.path.realpath(r) for r in rts}) > 1:
+        raise RuntimeError("two HIP runtimes are mapped into this process (" + ", ".join(rts) + "): libsccg was "
+                           "loaded before torch; import torch (or sccg) before loading libsccg.so yourself")
     vp, sz, c, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int64
     lib.sccg_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     lib.sccg_ctx_destroy.argtypes = [vp]
@@ -98,6 +123,7 @@ def load_library():
     lib.sccg_reconstruct_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
     lib.sccg_buf_free.argtypes = [ctypes.POINTER(Buf)]
     lib.sccg_profile.argtypes = [vp, ctypes.c_int]
+    lib.sccg_profile_mask.argtypes = [vp, ctypes.c_uint32]
     lib.sccg_profile_get.argtypes = [vp, c, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64)]
     lib.sccg_profile_name.argtypes = [ctypes.c_int]
     lib.sccg_profile_name.restype = ctypes.c_char_p
@@ -231,9 +257,9 @@ class Context:
                 if name.decode() in families:
                     mask |= 1 << i
                 i += 1
-            if mask <= 1:
+            if not mask:
                 raise ValueError(f"profile: unknown kernel families {families}")
-            self.lib.sccg_profile(self.ptr, mask)
+            self.lib.sccg_profile_mask(self.ptr, mask)
             return
         self.lib.sccg_profile(self.ptr, int(enable))
 
@@ -259,10 +285,12 @@ class Context:
         return load_library().sccg_compress_bound(ref_len, tgt_len)
 
     def _walk_out(self, rc: int, recs: Records, ex) -> tuple[list, tuple[int, int]]:
-        if rc:
-            self._err(rc)
-        out = [(recs.t[i], recs.pos[i], recs.len[i]) for i in range(recs.n)]
-        self.lib.sccg_records_free(ctypes.byref(recs))
+        try:
+            if rc:
+                self._err(rc)
+            out = [(recs.t[i], recs.pos[i], recs.len[i]) for i in range(recs.n)]
+        finally:   # (the library frees on its own error paths too; freeing zeroed records is a no-op)
+            self.lib.sccg_records_free(ctypes.byref(recs))
         return out, (ex[0], ex[1])
 
     def walk_range(self, sr: bytes, st: bytes, k: int, m: int, x0: int, p0: int, x_end: int):

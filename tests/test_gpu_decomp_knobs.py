@@ -3,8 +3,9 @@
 * The token fill (decompression.cpp:210-236) is queued before the host knows the decoded length,
   into a buffer of the output's capacity, beside the readback (the default, exercised by every
   other reconstruction test); SCCG_DC_SPEC=0 queues it after the host read the length.  Both must
-  stay exact: round trips against the target FASTA, a too-small output buffer (SCCG_E_NOMEM) and
-  tokens beyond the reference (:223-229, SCCG_E_RANGE).  The knob is read once per process, so the
+  stay exact: round trips against the target FASTA, a too-small output buffer (SCCG_E_NOMEM, also
+  below the decoded length itself), a far larger one, and tokens beyond the reference (:223-229,
+  SCCG_E_RANGE).  The knob is read once per process, so the
   checks run in a child process.
 * sccg_profile with a family mask brackets only those families (bench.py's timed region).
 """
@@ -61,6 +62,15 @@ for prof, rl, tl, seed in (("hg", 200_000, 201_000, 3), ("hg", 1_000_000, 1_003_
             out["nomem"] = 0
         except sccg.SccgError as e:
             out["nomem"] = e.rc
+        # a capacity below the decoded length D itself: the speculative fill's clamp is what keeps
+        # its writes inside the buffer (ADVICE r4)
+        try:
+            run(rfa, rec, len(tfa) // 3)
+            out["nomem_below_d"] = 0
+        except sccg.SccgError as e:
+            out["nomem_below_d"] = e.rc
+        # a far larger capacity than the record can need: the non-speculative path, still exact
+        out["big_cap"] = run(rfa, rec, need + (160 << 20)) == tfa
 rfa = b">r\n" + b"ACGT" * 50 + b"\n"
 for rec in (b"\n,\n(0,20)(500,30)", b">h\n\n(3,2)\n(0,20)(500,30)", b"\n,\nAC(190,20)"):
     try:
@@ -73,14 +83,20 @@ print(json.dumps(out))
 """
 
 
-def test_fill_after_readback_round_trips_and_errors():
-    env = dict(os.environ, SCCG_DC_SPEC="0")
+@pytest.mark.parametrize("spec", ["0", None], ids=["fill_after_readback", "speculative_fill"])
+def test_fill_round_trips_and_errors(spec):
+    env = dict(os.environ)
+    env.pop("SCCG_DC_SPEC", None)
+    if spec is not None:
+        env["SCCG_DC_SPEC"] = spec
     p = subprocess.run([sys.executable, "-c", f"HERE = {HERE!r}\n" + CHILD], env=env, capture_output=True, text=True,
                        timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads(p.stdout.strip().splitlines()[-1])
     assert d["round_trips"] == [True, True, True], d
     assert d["nomem"] == sccg.ERR_CODES["SCCG_E_NOMEM"], d
+    assert d["nomem_below_d"] == sccg.ERR_CODES["SCCG_E_NOMEM"], d
+    assert d["big_cap"] is True, d
     assert d["range"] == [sccg.ERR_CODES["SCCG_E_RANGE"]] * 3, d
 
 
@@ -96,5 +112,12 @@ def test_profile_family_mask(ctx):
     ctx.profile(False)
     assert set(only) <= {"walk"}, only
     assert "walk" in every and len(every) > 1, every
+    # family 0 alone (its mask is 1, which sccg_profile(ctx, 1) reads as "every family")
+    first = sccg.load_library().sccg_profile_name(0).decode()
+    ctx.profile(True, families=[first])
+    ctx.compress(rfa, tfa)
+    zero = ctx.profile_get()
+    ctx.profile(False)
+    assert set(zero) == {first}, zero
     with pytest.raises(ValueError):
         ctx.profile(True, families=["no_such_family"])

@@ -213,3 +213,111 @@ def test_genome_failing_rank_gloo_world2(tmp_path):
         tgt = (root / "tgt" / f"{n}.fa").read_bytes()
         ref = (root / "ref" / f"{n}.fa").read_bytes()
         assert (root / "out" / n / "compressed_genome.txt").read_bytes() == _FakeCtx().compress(ref, tgt)
+
+
+class _FakeFilesCtx(_FakeCtx):
+    """Also stands in for sccg_compress_files (rank 0's path in genome.run_job)."""
+
+    def compress_files(self, ref_path, tgt_path, out_path):
+        ref = open(ref_path, "rb").read()
+        tgt = open(tgt_path, "rb").read()
+        with open(out_path, "wb") as f:
+            f.write(self.compress(ref, tgt))
+
+
+def _run_job_worker(rank, world, port, q, root, out_name, cost):
+    import torch
+    import torch.distributed as dist
+    import genome
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names = ["chrA", "chrB", "chrC", "chrD", "chrE"]
+        rc, summary = genome.run_job(names, os.path.join(root, "ref"), os.path.join(root, "tgt"),
+                                     os.path.join(root, out_name), _FakeFilesCtx, rank, world, torch.device("cpu"),
+                                     contexts=2, run_7z=False, err_hip=2, cost=cost)
+        q.put((rank, rc, None if summary is None else {n: v["rc"] for n, v in summary["per_chrom"].items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _make_pairs(root):
+    for d in ("ref", "tgt"):
+        (root / d).mkdir()
+    for i, n in enumerate(["chrA", "chrB", "chrC", "chrD", "chrE"]):
+        (root / "ref" / f"{n}.fa").write_bytes(b">r\nACGT" * (i + 1))
+        (root / "tgt" / f"{n}.fa").write_bytes(b">t\nTTGCA" * (5 - i) * 3)
+
+
+def _spawn(fn, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=fn, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=120) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("cost", [None, {"chrE": 1000.0, "chrA": 1.0}])
+def test_genome_run_job_gloo_world2(tmp_path, cost):
+    """genome.py's job as main() runs it: rank 0 writes its own pairs through compress_files, rank 1's
+    texts come over the gather and are written by rank 0 -- every pair once, byte for byte, rc 0;
+    sharding by a measured cost (T2T-like pairs) instead of target size changes only who does what."""
+    import genome
+    _make_pairs(tmp_path)
+    res = _spawn(_run_job_worker, 2, str(tmp_path), "out", cost)
+    rc0, st0 = res[0]
+    assert res[1] == [0, None]
+    assert rc0 == 0 and sorted(st0) == ["chrA", "chrB", "chrC", "chrD", "chrE"] and set(st0.values()) == {0}
+    for n in st0:
+        ref = (tmp_path / "ref" / f"{n}.fa").read_bytes()
+        tgt = (tmp_path / "tgt" / f"{n}.fa").read_bytes()
+        assert (tmp_path / "out" / n / "compressed_genome.txt").read_bytes() == _FakeCtx().compress(ref, tgt)
+    if cost:   # the costly pair sits alone on its rank
+        sizes = [os.path.getsize(tmp_path / "tgt" / f"{n}.fa") for n in sorted(st0)]
+        w = [cost.get(n, s) for n, s in zip(sorted(st0), sizes)]
+        assert [4] in multigpu.lpt_shard(w, 2)
+    assert genome.SCCG_E_OUT != genome.SCCG_E_IO
+
+
+def test_genome_unwritable_out_dir_fails_job(tmp_path):
+    """rank 0's files path with an output folder it cannot create -- every pair is reported
+    failed (SCCG_E_OUT) and the job's rc is 1, instead of the worker thread dying silently."""
+    import genome
+    _make_pairs(tmp_path)
+    blocker = tmp_path / "out"
+    blocker.write_bytes(b"a file where the output folder should be")
+    em = genome.Emitter(str(blocker), False)
+    names = ["chrA", "chrB", "chrC"]
+    stats = genome.compress_shard_files(names, str(tmp_path / "ref"), str(tmp_path / "tgt"), _FakeFilesCtx, em, 2,
+                                        contexts=2)
+    assert {n: v["rc"] for n, v in stats.items()} == {n: genome.SCCG_E_OUT for n in names}
+    assert em.wait() == 1
+
+
+def test_genome_worker_closes_context_on_error(tmp_path):
+    """A context whose compress_files raises something unexpected: the pair fails, the context is
+    still closed, the other pairs go on."""
+    import genome
+    _make_pairs(tmp_path)
+    closed = []
+
+    class Boom(_FakeFilesCtx):
+        def compress_files(self, ref_path, tgt_path, out_path):
+            if "chrB" in ref_path:
+                raise ValueError("boom")
+            super().compress_files(ref_path, tgt_path, out_path)
+
+        def close(self):
+            closed.append(1)
+
+    em = genome.Emitter(str(tmp_path / "out"), False)
+    stats = genome.compress_shard_files(["chrA", "chrB", "chrC"], str(tmp_path / "ref"), str(tmp_path / "tgt"), Boom, em,
+                                        2, contexts=1)
+    assert stats["chrB"]["rc"] != 0 and stats["chrA"]["rc"] == 0 and stats["chrC"]["rc"] == 0
+    assert closed == [1] and em.wait() == 1
