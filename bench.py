@@ -638,7 +638,11 @@ def main() -> None:
     ap.add_argument("--t2t-steps", type=int, default=2)
     ap.add_argument("--no-prof", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--no-k21", action="store_true", help="skip the configs[1] leg (chr1 at k = 21)")
+    ap.add_argument("--only-steps", action="store_true",
+                    help="the timed steps and the line only (traces): no per-pair costs, decompress, k=21, e2e, T2T")
     args = ap.parse_args()
+    if args.only_steps:
+        args.no_decomp = args.no_e2e = args.no_t2t = args.no_k21 = args.no_prof = args.no_cpu_baseline = True
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))   # before HIP initialises
 
@@ -711,7 +715,8 @@ def main() -> None:
         lanes[0].ctx.profile(False)
 
     # ---- per-pair standalone costs (untimed) and the N-GPU makespans they predict (N = 1 lines)
-    hg_cost = standalone_costs(lanes[0], pairs, order) if world == 1 else {}
+    hg_cost = standalone_costs(lanes[0], pairs, order) if world == 1 and not args.only_steps else {}
+    hg_sizes = {n: pairs[n][3] for n in hg_cost}   # (the pairs leave HBM before the T2T-like leg)
 
     # ---- per-rank totals (all ranks' target bases make up the whole job)
     tot = {"target_bases": sum(results[n][1]["target_bases"] for n in order),
@@ -905,7 +910,7 @@ def main() -> None:
             "end_to_end_genome": e2e_genome,
             "t2t_genome": t2t,
             "chr1_k21": k21,
-            "predicted_multi_gpu": {"hg_genome": predicted_makespans(hg_cost, {n: pairs[n][3] for n in hg_cost}, ms_step)
+            "predicted_multi_gpu": {"hg_genome": predicted_makespans(hg_cost, hg_sizes, ms_step)
                                     if hg_cost else None,
                                     "t2t_genome": (t2t or {}).get("predicted"),
                                     "model": "bench.predicted_makespans: per-pair standalone ms, LPT over N GPUs, "

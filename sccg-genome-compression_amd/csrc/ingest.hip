@@ -216,11 +216,12 @@ __device__ __forceinline__ void stage_lane(uint8_t* __restrict__ st, const uint3
 struct StripMasks {
     uint64_t known, unknown, fk, par;
     int32_t last;   // status of the last line start in range: -1 none, 0 drop, 1 keep
+    uint64_t lower, nn;   // RUNS: bytes 'a'..'z' and bytes 'N' / 'n' (the two run lines' predicates)
 };
 
 __device__ __forceinline__ uint64_t below64(int k) { return k >= 64 ? ~0ull : (1ull << k) - 1ull; }
 
-template <IngestMode MODE>
+template <IngestMode MODE, bool RUNS = false>
 __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t (&w)[SNW], uint8_t prev, int64_t off,
                                                   int64_t n, int64_t h, int64_t he, const uint8_t* __restrict__ lbytes) {
     // Byte classes.  Every byte that matters (whitespace, '\n', '>', '(', N / n) is outside
@@ -244,12 +245,27 @@ __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t 
         sph[h] = x;
     }
     const uint64_t sp = ((uint64_t)sph[1] << 32) | sph[0];
+    // RUNS: lowercase bytes in byte order -- an unflagged byte (A C G T a c g t) is lowercase iff its
+    // bit 5 is set (a word's four bits gathered by one multiply); flagged bytes are set below
+    uint64_t lo = 0, nn = 0;
+    if (RUNS) {
+#pragma unroll
+        for (int q = 0; q < SNW; q++) {
+            const uint32_t t = (w[q] >> 5) & 0x01010101u;
+            lo |= (uint64_t)(((t * 0x01020408u) >> 24) & 0xfu) << (4 * q);
+        }
+    }
     uint64_t ws = 0, nl = 0, gt = 0, drop = 0, par = 0;
     for (uint64_t m = sp; m; m &= m - 1) {
         const int j = __builtin_ctzll(m);
         const int i = (j & 32) + 4 * (j & 7) + ((j >> 3) & 3);
         const uint32_t c = lbytes[i];
         const uint64_t bit = 1ull << i;
+        if (RUNS) {
+            lo &= ~bit;
+            if (c >= 'a' && c <= 'z') lo |= bit;
+            if (c == 'N' || c == 'n') nn |= bit;
+        }
         if (c == ' ' || (c >= 9 && c <= 13)) ws |= bit;   // isspace
         if (MODE == INGEST_REF) {
             if (c == '\n') nl |= bit;
@@ -261,7 +277,7 @@ __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t 
     const uint64_t fk = ~drop;
     const int64_t lim = n - off;
     const uint64_t valid = lim >= 64 ? ~0ull : (lim > 0 ? (1ull << lim) - 1ull : 0ull);
-    StripMasks r{0, 0, fk, par, -1};
+    StripMasks r{0, 0, fk, par, -1, lo, nn};
     if (MODE == INGEST_TGT) {
         const int64_t lo = h - off < 0 ? 0 : (h - off > 64 ? 64 : h - off);
         const int64_t hi = he - off < 0 ? 0 : (he - off > 64 ? 64 : he - off);
@@ -324,7 +340,7 @@ __device__ __forceinline__ void load_lane64(const uint8_t* __restrict__ buf, int
 
 // A wave's tile: its words, the byte before it (lane 0's 'prev'), the masks, and each lane's prior
 // line status inside the wave (-1: no line start in the lanes before it).
-template <IngestMode MODE>
+template <IngestMode MODE, bool RUNS = false>
 __device__ __forceinline__ StripMasks strip_tile(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n, int64_t h,
                                                  int64_t he, int64_t off, uint32_t (&w)[SNW], int32_t& prior,
                                                  uint64_t& lsm, uint4* tin) {
@@ -344,7 +360,7 @@ __device__ __forceinline__ StripMasks strip_tile(FilterMode fm, const uint8_t* _
         const uint32_t up = (uint32_t)__shfl_up((int)w[SNW - 1], 1, 64) >> 24;
         prev = lane ? (uint8_t)up : ((off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n');
     }
-    const StripMasks r = strip_masks<MODE>(fm, w, prev, off, n, h, he, reinterpret_cast<const uint8_t*>(tin + 4 * lane));
+    const StripMasks r = strip_masks<MODE, RUNS>(fm, w, prev, off, n, h, he, reinterpret_cast<const uint8_t*>(tin + 4 * lane));
     wave_sync();   // (k_strip_write stages its output in tin next)
     prior = -1;
     lsm = 0;
@@ -514,14 +530,31 @@ __global__ void k_strip_scan_apply(int64_t ntiles, const int64_t* __restrict__ t
     }
 }
 
-template <IngestMode MODE>
+// Run events of a lane's kept bytes (RUNS: the target strip emits both run lines' boundaries,
+// compression.cpp:341-368 lowercase and :527-555 N, instead of two more passes over T).  For a
+// predicate mask p (byte order) and the kept bytes K, the predicate of "the previous kept byte" at
+// every position is p on K filled forward over the dropped bytes D (newlines) -- one carry trick:
+// a D run that starts right after a kept 1 is the set of D bits the +s carry clears.  A run starts
+// at a kept byte whose predicate holds and whose previous kept byte's does not, and ends (exclusive)
+// at a kept byte where it is the other way round.  cin: the previous kept byte's predicate.
+__device__ __forceinline__ void run_events(uint64_t p, uint64_t K, uint32_t cin, uint64_t& st, uint64_t& en) {
+    const uint64_t D = ~K;
+    const uint64_t x = p & K;
+    const uint64_t sd = ((x << 1) | cin) & D;
+    const uint64_t g = x | (D & ~(D + sd));
+    const uint64_t prev = (g << 1) | cin;
+    st = K & g & ~prev;
+    en = K & ~g & prev;
+}
+
+template <IngestMode MODE, bool RUNS>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n,
                                                             const int64_t* __restrict__ hdr,
                                                             const int64_t* __restrict__ toff,
                                                             const int64_t* __restrict__ toff2,
                                                             const int32_t* __restrict__ tcarry,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
-                                                            int32_t* __restrict__ flags) {
+                                                            int32_t* __restrict__ flags, RunSlots rsl) {
     __shared__ uint4 stage_all4[WPB][(STAGE_WORDS + 3) / 4];   // (also the coalesced load's transpose)
     __shared__ uint32_t tab[16];
     if (threadIdx.x < 16) tab[threadIdx.x] = compact_sel(threadIdx.x);
@@ -536,12 +569,56 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
     uint32_t w[SNW];
     int32_t prior;
     uint64_t lsm;
-    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm, stage_all4[wave_in_block()]);
+    const StripMasks r = strip_tile<MODE, RUNS>(fm, buf, n, h, he, off, w, prior, lsm, stage_all4[wave_in_block()]);
     if (MODE == INGEST_REF && prior < 0) prior = tcarry[tile];
     const uint64_t keep = r.known | (prior == 1 ? r.unknown : 0ull), fkeep = keep & r.fk;
     const uint32_t c = (uint32_t)__popcll(keep) | ((uint32_t)__popcll(fkeep) << 16);
     const uint32_t incl = wave_incl_add<uint32_t>(c), tot = lane_val(incl, 63);
     const uint32_t ex = incl - c;
+    if (RUNS) {
+        // the previous kept byte's predicates: the nearest earlier lane with a kept byte; the wave's
+        // first such lane takes its own first byte's (no event there -- the tile boundary is settled
+        // by k_runs_tiles from the tile's first/last predicates)
+        const bool has = keep != 0;
+        const int fb = has ? __builtin_ctzll(keep) : 0, lb = has ? 63 - __builtin_clzll(keep) : 0;
+        const uint32_t first2 = (uint32_t)((r.lower >> fb) & 1u) | ((uint32_t)((r.nn >> fb) & 1u) << 1);
+        const uint32_t last2 = (uint32_t)((r.lower >> lb) & 1u) | ((uint32_t)((r.nn >> lb) & 1u) << 1);
+        const uint64_t hm = __ballot(has);
+        const uint64_t before = hm & below64(lane);
+        const int src = before ? 63 - __builtin_clzll(before) : 0;
+        const uint32_t pl = (uint32_t)__shfl((int)last2, src, 64);
+        const uint32_t cin = before ? pl : first2;
+        uint64_t sl = 0, el = 0, sn = 0, en = 0;
+        if (has) {
+            run_events(r.lower, keep, cin & 1u, sl, el);
+            run_events(r.nn, keep, cin >> 1, sn, en);
+        }
+        const uint64_t cc = (uint64_t)__popcll(sl) | ((uint64_t)__popcll(el) << 16) | ((uint64_t)__popcll(sn) << 32) |
+                            ((uint64_t)__popcll(en) << 48);
+        const uint64_t ci = wave_incl_add<uint64_t>(cc), ct = __shfl(ci, 63, 64);
+        const uint64_t cx = ci - cc;
+        const int fl = hm ? first_lane(hm) : 0, ll = hm ? 63 - __builtin_clzll(hm) : 0;
+        const uint32_t tf = (uint32_t)__shfl((int)first2, fl, 64), tl = (uint32_t)__shfl((int)last2, ll, 64);
+        if (lane == 0) {
+            rsl.rc[tile] = ct;
+            rsl.rf[tile] = (hm ? 1 : 0) | (int32_t)(tf << 1) | (int32_t)(tl << 3);
+        }
+        if ((sl | el | sn | en) != 0) {   // (rare: a lane holds ~0.1 run boundaries)
+            const int64_t o0 = toff[tile] + (int64_t)(ex & 0xffff);
+            int32_t* const dst[4] = {rsl.sl, rsl.el, rsl.sn, rsl.en};
+            const uint64_t ev[4] = {sl, el, sn, en};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t at = (uint32_t)(cx >> (16 * q)) & 0xffffu;
+                for (uint64_t m = ev[q]; m; m &= m - 1) {
+                    const int b = __builtin_ctzll(m);
+                    if (at < RUN_SLOT) dst[q][(size_t)tile * RUN_SLOT + at] = (int32_t)(o0 + __popcll(keep & below64(b)));
+                    else atomicOr(rsl.ovf, 1);
+                    at++;
+                }
+            }
+        }
+    }
     if (flags && __ballot((keep & r.par) != 0) && lane == 0) atomicOr(flags, 1);
     if (out) {   // (null: only the filtered copy is wanted -- the reconstruction needs R' alone)
         stage_lane<false>(s1, tab, w, keep, (int)(ex & 0xffff));
@@ -630,6 +707,73 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_runs_write(const uint8_t* __rest
     put_positions(el, off, re_l, toff_l[blockIdx.x] - (open_l ? 1 : 0) + (xe & 0xffff));
     put_positions(sn, off, rs_n, toff_n[blockIdx.x] + (xs >> 16));
     put_positions(en, off, re_n, toff_n[blockIdx.x] - (open_n ? 1 : 0) + (xe >> 16));
+}
+
+// ---- the run arrays from the target strip's per-tile event slots (RUNS)
+// per tile: its event counts plus the tile-boundary event (its first kept byte against the previous
+// kept byte: the last kept byte of the nearest earlier tile that has one; none at the stream start)
+constexpr int RUNS_LOOKBACK = 64;   // tiles without a kept byte crossed looking for it (more: ovf, fallback)
+__global__ void k_runs_tiles(int64_t ntiles, const uint64_t* __restrict__ rc, const int32_t* __restrict__ rf,
+                             int64_t* __restrict__ cs, int64_t* __restrict__ ce, int32_t* __restrict__ bev,
+                             int32_t* __restrict__ ovf) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t f = rf[t];
+        const uint64_t c = rc[t];
+        int32_t b = 0;
+        if (f & 1) {
+            uint32_t prev = 0;
+            int64_t q = t - 1;
+            for (; q >= 0 && t - q <= RUNS_LOOKBACK; q--) {
+                const int32_t g = rf[q];
+                if (g & 1) { prev = (uint32_t)(g >> 3) & 3u; break; }
+            }
+            if (q >= 0 && t - q > RUNS_LOOKBACK) atomicOr(ovf, 2);
+            const uint32_t first = (uint32_t)(f >> 1) & 3u;
+#pragma unroll
+            for (int p = 0; p < 2; p++) {
+                const uint32_t fp = (first >> p) & 1u, pp = (prev >> p) & 1u;
+                if (fp && !pp) b |= 1 << (2 * p);
+                if (!fp && pp) b |= 2 << (2 * p);
+            }
+        }
+        bev[t] = b;
+        cs[t] = (int64_t)((c & 0xffff) + (b & 1)) | ((int64_t)(((c >> 32) & 0xffff) + ((b >> 2) & 1)) << 32);
+        ce[t] = (int64_t)(((c >> 16) & 0xffff) + ((b >> 1) & 1)) | ((int64_t)((c >> 48) + ((b >> 3) & 1)) << 32);
+    }
+}
+
+// per tile: its boundary event, then its slot events, at the scanned offsets (ends inclusive)
+__global__ void k_runs_copy(int64_t ntiles, const int64_t* __restrict__ toff, const uint64_t* __restrict__ rc,
+                            const int32_t* __restrict__ bev, const int64_t* __restrict__ cs, const int64_t* __restrict__ ce,
+                            RunSlots rsl, int32_t* __restrict__ rs_l, int32_t* __restrict__ re_l,
+                            int32_t* __restrict__ rs_n, int32_t* __restrict__ re_n) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = rc[t];
+        const int32_t b = bev[t];
+        const int32_t t0 = (int32_t)toff[t];
+        const size_t sb = (size_t)t * RUN_SLOT;
+        int32_t* const dst[4] = {rs_l, re_l, rs_n, re_n};
+        const int32_t* const src[4] = {rsl.sl, rsl.el, rsl.sn, rsl.en};
+        const int64_t base[4] = {cs[t] & 0xffffffff, ce[t] & 0xffffffff, cs[t] >> 32, ce[t] >> 32};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int end = q & 1;   // ends are stored inclusive: the exclusive end - 1
+            int64_t at = base[q];
+            if ((b >> q) & 1) dst[q][at++] = t0 - end;
+            const int nq = (int)((c >> (16 * q)) & 0xffff);
+            for (int k = 0; k < nq && k < RUN_SLOT; k++) dst[q][at++] = src[q][sb + k] - end;
+        }
+    }
+}
+
+// counts; a run still open at the end ends at |T| - 1
+__global__ void k_runs_fin(const int64_t* __restrict__ tot, const int64_t* __restrict__ d_nT, int32_t* __restrict__ re_l,
+                           int32_t* __restrict__ re_n, int64_t* __restrict__ d_nruns) {
+    const int64_t sl = tot[0] & 0xffffffff, sn = tot[0] >> 32, el = tot[1] & 0xffffffff, en = tot[1] >> 32;
+    if (sl > el) re_l[sl - 1] = (int32_t)(*d_nT - 1);
+    if (sn > en) re_n[sn - 1] = (int32_t)(*d_nT - 1);
+    d_nruns[0] = sl;
+    d_nruns[1] = sn;
 }
 
 // text of one run: "d," | "(d,len)" | final singleton "d" (compression.cpp:351-366)
@@ -731,7 +875,7 @@ int launch_find_header(const uint8_t* buf, int64_t n, int64_t* d_sc, hipStream_t
 
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,
                        int64_t* d_len, int32_t* d_flags, const IngestScratch& sc, hipStream_t s, FilterMode fmode,
-                       uint8_t* out2, int64_t* d_len2) {
+                       uint8_t* out2, int64_t* d_len2, const RunSlots* runs) {
     if (n <= 0) {
         SCCG_HIP(hipMemsetAsync(d_len, 0, sizeof(int64_t), s));
         if (d_len2) SCCG_HIP(hipMemsetAsync(d_len2, 0, sizeof(int64_t), s));
@@ -755,12 +899,16 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     hipLaunchKernelGGL(k_strip_scan_apply, dim3(grid_for(ntiles, 256)), dim3(256), 0, s, ntiles, sc.tile_a, sc.tile_b,
                        sc.tile_fa, sc.tile_fb, sc.tile_last, btot, sc.tile_off, sc.tile_off2, sc.tile_carry, d_len,
                        d_len2);
-    if (mode == INGEST_TGT)
-        PROF_LAUNCH(PROF_STRIP, s, k_strip_write<INGEST_TGT>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
+    const RunSlots rsl = runs ? *runs : RunSlots{};
+    if (mode == INGEST_TGT && runs)
+        PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_TGT, true>), dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl);
+    else if (mode == INGEST_TGT)
+        PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_TGT, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl);
     else
-        PROF_LAUNCH(PROF_STRIP, s, k_strip_write<INGEST_REF>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags);
+        PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_REF, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl);
     SCCG_HIP(hipGetLastError());
     return 0;
 }
@@ -778,6 +926,20 @@ int launch_runs2(const uint8_t* in, int64_t n, int32_t* rs_l, int32_t* re_l, int
     if (rc) return rc;
     PROF_LAUNCH(PROF_RUNS, s, k_runs_write, dim3((unsigned)ntiles), dim3(SCCG_BLOCK), 0, s, in, n,
                 (const int64_t*)d_cnt_l, (const int64_t*)d_cnt_n, rs_l, re_l, rs_n, re_n);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_runs_from_strip(const RunSlots& rs, int64_t ntiles, const int64_t* toff, const int64_t* d_nT, int32_t* rs_l,
+                           int32_t* re_l, int32_t* rs_n, int32_t* re_n, int64_t* d_nruns, int64_t* cs, int64_t* ce,
+                           int32_t* bev, int64_t* d_tot, int64_t* d_partial, hipStream_t s) {
+    const unsigned g = grid_for(ntiles, 256) > 4096 ? 4096 : grid_for(ntiles, 256);
+    hipLaunchKernelGGL(k_runs_tiles, dim3(g), dim3(256), 0, s, ntiles, (const uint64_t*)rs.rc, (const int32_t*)rs.rf, cs, ce,
+                       bev, rs.ovf);
+    if (const int rc = dev_excl_sum2(cs, cs, d_tot, ce, ce, d_tot + 1, ntiles, d_partial, s)) return rc;
+    PROF_LAUNCH(PROF_RUNS, s, k_runs_copy, dim3(g), dim3(256), 0, s, ntiles, toff, (const uint64_t*)rs.rc, (const int32_t*)bev,
+                (const int64_t*)cs, (const int64_t*)ce, rs, rs_l, re_l, rs_n, re_n);
+    hipLaunchKernelGGL(k_runs_fin, dim3(1), dim3(1), 0, s, (const int64_t*)d_tot, d_nT, re_l, re_n, d_nruns);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

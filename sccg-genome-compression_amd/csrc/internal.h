@@ -93,10 +93,30 @@ int launch_first_match(const uint8_t* buf, int64_t n, const int64_t* from_slot, 
 // d_flags (optional) gets bit0 when a kept byte is '('.  With out2, the same pass also writes the
 // kept bytes through the byte filter + case map `fmode` (N erase of compression.cpp:556-557 /
 // decompression.cpp:108-110) into out2, *d_len2 = their count.
+// Run events the target's strip emits (its write pass, RUNS): per 4 KiB FASTA tile up to RUN_SLOT
+// lowercase-run starts / exclusive ends and N-run starts / exclusive ends (output positions), the
+// tile's counts (rc: 4 x 16 bits) and first / last kept byte predicates (rf: bit 0 has a kept byte,
+// bits 1-2 first (lower, N), bits 3-4 last); ovf is set when a tile held more events than its slots.
+constexpr int RUN_SLOT = 32;
+struct RunSlots {
+    int32_t* sl = nullptr;
+    int32_t* el = nullptr;
+    int32_t* sn = nullptr;
+    int32_t* en = nullptr;
+    uint64_t* rc = nullptr;
+    int32_t* rf = nullptr;
+    int32_t* ovf = nullptr;
+};
+// both run lines' run arrays (as launch_runs2) from a RUNS strip's slots: d_nruns[0..1] = counts,
+// *d_ovf nonzero: a tile overflowed its slots (the caller runs launch_runs2 instead); cs, ce, bev:
+// ntiles scratch each; d_nT: |T| on the device
+int launch_runs_from_strip(const RunSlots& rs, int64_t ntiles, const int64_t* toff, const int64_t* d_nT, int32_t* rs_l,
+                           int32_t* re_l, int32_t* rs_n, int32_t* re_n, int64_t* d_nruns, int64_t* cs, int64_t* ce,
+                           int32_t* bev, int64_t* d_tot, int64_t* d_partial, hipStream_t s);
 int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header,
                        uint8_t* out, int64_t* d_len, int32_t* d_flags, const IngestScratch& sc,
                        hipStream_t s, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
-                       int64_t* d_len2 = nullptr);
+                       int64_t* d_len2 = nullptr, const RunSlots* runs = nullptr);
 // maximal runs of lowercase bytes (rs_l/re_l) and of N/n bytes (rs_n/re_n), start/end inclusive,
 // in one pass; d_nruns[0..1] = their counts
 int launch_runs2(const uint8_t* s_in, int64_t n, int32_t* rs_l, int32_t* re_l, int32_t* rs_n, int32_t* re_n,
@@ -157,6 +177,8 @@ void global_prepare_reset();   // forget a preparation that will not be used
 // global_prepare on the same ws/R' only extends those positions once T' exists.  |R'| is read on
 // the device from d_nRp (no host round trip); nRp_bound >= |R'| sizes the workspace and the anchor
 // table (ws must hold walk_workspace_bytes(nRp_bound, tn, ...)).
+// the workspace at ws is freed (sccg_ctx::get, sccg_ctx_destroy): forget its anchor-table generations
+void walk_forget_workspace(const void* ws);
 int global_sweep_early(const uint8_t* Rp, int64_t nRp_bound, const int64_t* d_nRp, const uint8_t* tgt_fa, int64_t tn,
                        const int64_t* d_hdr, int k, int m, int chunk, void* ws, size_t ws_bytes, hipStream_t s);
 // Where the record text goes, when the caller learns it only during the walk: resolve() is called

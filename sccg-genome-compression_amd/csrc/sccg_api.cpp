@@ -56,6 +56,8 @@ enum Slot {
     B_TILE2_A, B_TILE2_B, B_TILE2_FA, B_TILE2_FB, B_TILE2_LAST, B_TILE2_OFF, B_TILE2_OFF2, B_TILE2_CARRY, B_TILE2_BSUM,
     // fused reconstruction: token table, tokens per record block and their prefix
     B_D_TOK, B_D_BTOK,
+    // the target strip's run-event slots (RunSlots) and the run arrays' per-tile scratch
+    B_RSLOT, B_RTILE,
     B_COUNT
 };
 
@@ -170,7 +172,7 @@ struct sccg_ctx {
     void* get(int slot, size_t bytes) {
         bytes = (bytes + DPAD + 255) & ~(size_t)255;
         if (cap[slot] >= bytes) return buf[slot];
-        if (buf[slot]) (void)hipFree(buf[slot]);
+        if (buf[slot]) { walk_forget_workspace(buf[slot]); (void)hipFree(buf[slot]); }
         buf[slot] = nullptr;
         cap[slot] = 0;
         void* p = nullptr;
@@ -239,7 +241,7 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->side);
     (void)hipStreamSynchronize(ctx->side2);
     for (int i = 0; i < B_COUNT; i++)
-        if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
+        if (ctx->buf[i]) { walk_forget_workspace(ctx->buf[i]); (void)hipFree(ctx->buf[i]); }
     (void)hipEventDestroy(ctx->ev_fork);
     (void)hipEventDestroy(ctx->ev_fork2);
     (void)hipEventDestroy(ctx->ev_join);
@@ -304,7 +306,7 @@ int d2h_i64(sccg_ctx* ctx, const int64_t* d, int64_t* h, int n, hipStream_t s = 
 // (set 1: the second scratch set, so two strips can run at once; s: stream, default the context's)
 int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const int64_t* d_hdr, uint8_t* out,
           int64_t* d_len, int32_t* d_flags, int64_t* h_len, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
-          int set = 0, hipStream_t s = nullptr) {
+          int set = 0, hipStream_t s = nullptr, const RunSlots* runs = nullptr) {
     const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE + 1;
     const int o = set ? B_TILE2_A - B_TILE_A : 0;
     static_assert(B_TILE_BSUM - B_TILE_A == B_TILE2_BSUM - B_TILE2_A, "scratch sets line up");
@@ -321,15 +323,47 @@ int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const in
     sc.tile_a = ta; sc.tile_b = tb; sc.tile_fa = tfa; sc.tile_fb = tfb; sc.tile_last = tl; sc.tile_off = to;
     sc.tile_off2 = to2; sc.tile_carry = tc; sc.block_sums = bs; sc.scalars = nullptr;
     TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, s ? s : ctx->stream, fmode, out2,
-                           out2 ? d_len + 1 : nullptr));
+                           out2 ? d_len + 1 : nullptr, runs));
     return h_len ? d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1, s) : 0;   // h_len null: the caller reads d_len later
 }
 
+// The target strip's run-event slots (RunSlots) for a FASTA of fa_len bytes, or null (no memory: the
+// run lines then take their own passes over T).  The compaction's per-tile scratch comes along.
+struct StripRuns {
+    RunSlots rs;
+    int64_t ntiles = 0;
+    int64_t* cs = nullptr;
+    int64_t* ce = nullptr;
+    int32_t* bev = nullptr;
+};
+bool strip_runs(sccg_ctx* ctx, int64_t fa_len, StripRuns* out) {
+    const int64_t nt = (fa_len + STRIP_TILE - 1) / STRIP_TILE + 1;
+    const size_t slots = (size_t)nt * RUN_SLOT;
+    uint8_t* a = reinterpret_cast<uint8_t*>(ctx->get(B_RSLOT, 4 * slots * 4 + (size_t)nt * 12 + 64));
+    uint8_t* b = reinterpret_cast<uint8_t*>(ctx->get(B_RTILE, (size_t)nt * 20 + 64));
+    if (!a || !b) return false;
+    RunSlots& r = out->rs;
+    r.sl = reinterpret_cast<int32_t*>(a);
+    r.el = r.sl + slots;
+    r.sn = r.el + slots;
+    r.en = r.sn + slots;
+    r.rc = reinterpret_cast<uint64_t*>(r.en + slots);
+    r.rf = reinterpret_cast<int32_t*>(r.rc + nt);
+    r.ovf = r.rf + nt;
+    out->ntiles = (fa_len + STRIP_TILE - 1) / STRIP_TILE;   // the tiles the strip writes
+    out->cs = reinterpret_cast<int64_t*>(b);
+    out->ce = out->cs + nt;
+    out->bev = reinterpret_cast<int32_t*>(out->ce + nt);
+    return true;
+}
+
 // Both run lines of the stripped target (compression.cpp:341-368 lowercase, :495-522 N) in two
-// syncs: run extraction for both predicates, one read of both run counts, run text for both, one
-// read of both text lengths.  The lowercase line goes to out_lower, the N line to out_n.
+// syncs: the run arrays (from the target strip's event slots when it emitted them, else run
+// extraction over T for both predicates), one read of both run counts, run text for both, one read
+// of both text lengths.  The lowercase line goes to out_lower, the N line to out_n.
 int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower, uint8_t** out_n, int64_t* d_sc,
-              int64_t* h_lens, hipStream_t s) {
+              int64_t* h_lens, hipStream_t s, const StripRuns* sr = nullptr, const int64_t* toff = nullptr,
+              const int64_t* d_n = nullptr) {
     const int64_t maxruns = n / 2 + 2;
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE + 1;
     const int64_t ntmp = maxruns > ntiles ? maxruns : ntiles;
@@ -339,10 +373,21 @@ int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower,
     GET(int32_t, rs_n, B_RUN_SN, maxruns);
     GET(int32_t, re_n, B_RUN_EN, maxruns);
     GET(int64_t, tmp_n, B_TMP64N, ntmp);
-    GET(int64_t, part, B_PARTIAL, scan_partials_needed(ntmp) + 16);
-    TRY(launch_runs2(s_in, n, rs_l, re_l, rs_n, re_n, d_sc, tmp_l, tmp_n, part, s));
-    int64_t nruns[2];
-    TRY(d2h_i64(ctx, d_sc, nruns, 2, s));
+    const int64_t npart = ntmp > (sr ? sr->ntiles : 0) ? ntmp : sr->ntiles;
+    GET(int64_t, part, B_PARTIAL, 2 * scan_partials_needed(npart) + 16);
+    int64_t nruns[3] = {0, 0, 1};
+    if (sr) {   // the strip's events; d_sc[4..5] the totals, d_sc[6] <- the overflow flag
+        TRY(launch_runs_from_strip(sr->rs, sr->ntiles, toff, d_n, rs_l, re_l, rs_n, re_n, d_sc, sr->cs, sr->ce, sr->bev,
+                                   d_sc + 4, part, s));
+        int32_t ovf = 0;
+        const RbItem it[2] = {{d_sc, nruns, 16}, {sr->rs.ovf, &ovf, 4}};
+        TRY(dev_readback(it, 2, s));
+        nruns[2] = ovf;
+    }
+    if (nruns[2]) {   // no slots, or a tile overflowed them: run extraction over T
+        TRY(launch_runs2(s_in, n, rs_l, re_l, rs_n, re_n, d_sc, tmp_l, tmp_n, part, s));
+        TRY(d2h_i64(ctx, d_sc, nruns, 2, s));
+    }
     TRY(launch_run_text(rs_l, re_l, nruns[0], n, out_lower, d_sc + 2, tmp_l, part, s));
     GET(uint8_t, nline, B_NLINE, 24 * nruns[1] + 16);   // <= 23 text bytes per run
     *out_n = nline;
@@ -437,7 +482,12 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         TRY(launch_find_header(tfa, tn, sc, s));
     }
     HIPTRY(hipEventRecord(ctx->ev_hdr, s));
-    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp));
+    // the target strip also emits both run lines' boundaries (RunSlots): no extra passes over T
+    StripRuns sruns;
+    const bool have_runs = strip_runs(ctx, tn, &sruns);
+    if (have_runs) HIPTRY(hipMemsetAsync(sruns.rs.ovf, 0, sizeof(int32_t), s));
+    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp, 0, nullptr,
+              have_runs ? &sruns.rs : nullptr));
     // ---- header + lowercase line (compression.cpp:337-368) and the N line: side2, driven by the
     //      context's host worker (its launches wait on run counts).  They need only T, so they are
     //      queued right behind the target's strip -- ahead of the local pass and the walk, which
@@ -470,7 +520,8 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
             TRY(dev_put_bytes(out + hl, "\n", 1, s3));
         }
         // both run lines now (the N line is kept aside until the mode is known)
-        TRY(run_lines(ctx, T, h4[2], out + (hh ? hl + 1 : 0), &nline, sc + 10, rl_len, s3));
+        TRY(run_lines(ctx, T, h4[2], out + (hh ? hl + 1 : 0), &nline, sc + 10, rl_len, s3, have_runs ? &sruns : nullptr,
+                      reinterpret_cast<const int64_t*>(ctx->buf[B_TILE_OFF]), sc + 2));
         HIPTRY(hipEventRecord(ctx->ev_lines, s3));
         return 0;
     });

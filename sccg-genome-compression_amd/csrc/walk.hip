@@ -21,6 +21,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -174,6 +176,7 @@ struct WalkPtrs {
                           // [5] frozen count, [6] frozen-scan first hit, [9] void round, [11] carry count,
                           // [12] trapped triggers of the round end, [13] frozen fills of the round end
     int32_t* trig;        // the round end's trapped triggers (RESPEC_MAX_TRIGGERS)
+    int32_t* tflag;       // per chunk: round in which it was a trapped trigger (k_round_pending)
     int32_t unguessed_spec;   // SCCG_UNGUESSED_SPEC: k_round_pending speculates chunks left without a trajectory
     int32_t* fa_j;        // the round end's frozen fills: chunks fa_j+1 .. fa_l literal with P fa_p (scal[13])
     int32_t* fa_l;
@@ -246,9 +249,6 @@ static_assert(LEAD % (4 * LBW) == 0, "the lead is whole lanes' stretches");
 __device__ __forceinline__ uint32_t wf_h1(uint32_t key) { return slot_hash(key, WFBITS); }
 __device__ __forceinline__ uint32_t wf_h2(uint32_t key) { return (key * 0x85EBCA77u) >> (32 - WFBITS); }
 __device__ __forceinline__ uint32_t wf_h3(uint32_t key) { return (key * 0xC2B2AE3Du + 0x27D4EB2Fu) >> (32 - WFBITS); }
-#ifndef WALK_GLDS
-#define WALK_GLDS 0
-#endif
 typedef __attribute__((address_space(1))) void GVoid;
 typedef __attribute__((address_space(3))) void LVoid;
 struct WalkLds {
@@ -313,109 +313,84 @@ __device__ __forceinline__ int first_diff(const uint32_t (&r)[N], const uint32_t
 }
 __device__ __forceinline__ int first_diff32(const uint32_t (&r)[8], const uint32_t (&t)[8]) { return first_diff<8>(r, t); }
 
+// 4 bytes at byte offset off of an LDS byte array: two dword reads and an alignbyte.  Lane l of a
+// wave reads offsets off0 + 4l: consecutive dwords, conflict-free (a lane stride of 32 bytes put 16
+// lanes on each of two banks per lane group: 8x the LDS cycles, and the walk's LDS was 64 % conflict
+// cycles).
+__device__ __forceinline__ uint32_t lds4(const uint8_t* lds, int32_t off) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (off >> 2);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(off & 3));
+}
+
+// first differing byte of R-copy[ra..] and T-copy[tb..] within [0, n) (n when none); whole wave,
+// 1 KiB per pass, lane l holding the bytes at 4l + 256i of the pass (i < LCE_NI)
+constexpr int LCE_NI = 4;
+__device__ __forceinline__ int32_t lds_first_diff(const uint8_t* rbuf, int32_t ra, const uint8_t* tbuf, int32_t tb, int32_t n) {
+    const int lane = lane_id();
+    for (int32_t base = 0; base < n; base += 256 * LCE_NI) {
+        uint32_t x[LCE_NI];
+#pragma unroll
+        for (int i = 0; i < LCE_NI; i++) {
+            const int32_t pos = base + 256 * i + 4 * lane;
+            const int32_t lim = n - pos;   // bytes of this word inside the range
+            x[i] = 0;
+            if (lim > 0) {
+                x[i] = lds4(rbuf, ra + pos) ^ lds4(tbuf, tb + pos);
+                if (lim < 4) x[i] &= (1u << (8 * lim)) - 1u;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < LCE_NI; i++) {
+            const unsigned long long m = __ballot(x[i] != 0);
+            if (m) {
+                const int l = first_lane(m);
+                return base + 256 * i + 4 * l + (__builtin_ctz(lane_val(x[i], l)) >> 3);
+            }
+        }
+    }
+    return n;
+}
+
 // longest common extension of R[a..] and T[b..], at most maxlen bytes (extend_alignment,
-// compression.cpp:27-34); whole wave.  First from the LDS copy when both starts lie in it (2 KiB
-// per pass); then from HBM, LBV bytes per round trip (lanes 0-3 load the LEAD bytes before the
-// stretch compared), every HBM step leaving its bytes in the copy.
-__device__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a, int32_t b, int32_t maxlen) {
+// compression.cpp:27-34); whole wave.  First from the LDS copy when both starts lie in it; then from
+// HBM, LBV bytes of each per round trip, loaded coalesced (16 bytes per lane and KiB, from 16-byte
+// aligned bases at most 15 bytes before the LEAD bytes kept ahead of the stretch) into the copy and
+// compared from there.  (Lanes loading their own 32-byte stretches took 18 dword loads per lane and
+// step, each touching 16 cache lines: with ~5 walk waves per SIMD the round trips queued to ~10 us.)
+__device__ __forceinline__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a, int32_t b, int32_t maxlen) {
     const int lane = lane_id();
     if (maxlen <= 0) return 0;
     int32_t off = 0;
     if (a >= B.rb0 && b >= B.tb0 && a < B.rb0 + LBV && b < B.tb0 + LBV) {
         int32_t avail = B.rb0 + LBV - a < B.tb0 + LBV - b ? B.rb0 + LBV - a : B.tb0 + LBV - b;
         if (avail > maxlen) avail = maxlen;
-        for (int32_t base = 0; base < avail; base += 2048) {
-            const int32_t my = base + 32 * lane;
-            int32_t e = INT32_MAX;
-            if (my < avail) {
-                uint32_t r[8], t[8];
-                loadw_lds<8>(L.rbuf, a - B.rb0 + my, r);
-                loadw_lds<8>(L.tbuf, b - B.tb0 + my, t);
-                int pos = first_diff32(r, t);
-                if (avail - my < 32 && pos >= avail - my) pos = avail - my == maxlen - my ? avail - my : 32;
-                if (pos < 32) e = my + pos;
-            }
-            const unsigned long long sm = __ballot(e != INT32_MAX);
-            if (sm) {
-                const int32_t m = lane_val(e, first_lane(sm));
-                return m < maxlen ? m : maxlen;
-            }
-        }
-        if (avail >= maxlen) return maxlen;
+        const int32_t e = lds_first_diff(L.rbuf, a - B.rb0, L.tbuf, b - B.tb0, avail);
+        if (e < avail || avail >= maxlen) return e;
         off = avail;
     }
     while (off < maxlen) {
         const int32_t lead = (a + off >= LEAD && b + off >= LEAD) ? LEAD : 0;
-#if WALK_GLDS
-        // LDS-DMA: the copy's bytes go straight to LDS (no staging registers), from 16-byte aligned
-        // bases at most 15 bytes before the lead; then compared from LDS like the copy above
-        {
-            const int32_t sa = (a + off - lead) & ~15, sb = (b + off - lead) & ~15;
-            wave_sync();   // the copy's previous readers are done
-#pragma unroll
-            for (int i = 0; i < LBV / 1024; i++) {
-                __builtin_amdgcn_global_load_lds((GVoid*)(A.R + sa + 1024 * i + 16 * lane), (LVoid*)(L.rbuf + 1024 * i), 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((GVoid*)(A.T + sb + 1024 * i + 16 * lane), (LVoid*)(L.tbuf + 1024 * i), 16, 0, 0);
-            }
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the copy has landed
-            wave_sync();
-            B.rb0 = sa;
-            B.tb0 = sb;
-            const int32_t ra = a + off - sa, tb = b + off - sb;
-            int32_t avail = LBV - (ra > tb ? ra : tb);
-            if (avail > maxlen - off) avail = maxlen - off;
-            for (int32_t base = 0; base < avail; base += 2048) {
-                const int32_t my = base + 32 * lane;
-                int32_t e = INT32_MAX;
-                if (my < avail) {
-                    uint32_t r[8], t[8];
-                    loadw_lds<8>(L.rbuf, ra + my, r);
-                    loadw_lds<8>(L.tbuf, tb + my, t);
-                    int pos = first_diff32(r, t);
-                    if (avail - my < 32 && pos > avail - my) pos = avail - my;
-                    if (pos < 32 && my + pos < avail) e = off + my + pos;
-                }
-                const unsigned long long sm = __ballot(e != INT32_MAX);
-                if (sm) {
-                    const int32_t m = lane_val(e, first_lane(sm));
-                    return m < maxlen ? m : maxlen;
-                }
-            }
-            off += avail;
-            continue;
-        }
-#endif
-        const int32_t sa = a + off - lead, sb = b + off - lead;
-        uint32_t r[LBW], t[LBW];
-        loadw<LBW>(A.R + sa + 4 * LBW * lane, r);
-        loadw<LBW>(A.T + sb + 4 * LBW * lane, t);
+        const int32_t sa = (a + off - lead) & ~15, sb = (b + off - lead) & ~15;
+        static_assert(LBV == 2048, "two KiB of each per step");
+        const uint4* gr = reinterpret_cast<const uint4*>(A.R + sa) + lane;
+        const uint4* gt = reinterpret_cast<const uint4*>(A.T + sb) + lane;
+        const uint4 r0 = gr[0], r1 = gr[64], t0 = gt[0], t1 = gt[64];
         wave_sync();   // the copy's previous readers are done
         {
-            uint4* dr = reinterpret_cast<uint4*>(L.rbuf) + (LBW / 4) * lane;
-            uint4* dt = reinterpret_cast<uint4*>(L.tbuf) + (LBW / 4) * lane;
-#pragma unroll
-            for (int i = 0; i < LBW / 4; i++) {
-                dr[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
-                dt[i] = make_uint4(t[4 * i], t[4 * i + 1], t[4 * i + 2], t[4 * i + 3]);
-            }
+            uint4* dr = reinterpret_cast<uint4*>(L.rbuf) + lane;
+            uint4* dt = reinterpret_cast<uint4*>(L.tbuf) + lane;
+            dr[0] = r0; dr[64] = r1;
+            dt[0] = t0; dt[64] = t1;
         }
         wave_sync();
         B.rb0 = sa;
         B.tb0 = sb;
-        const int32_t rel = 4 * LBW * lane - lead;   // this lane's bytes, from a + off
-        int32_t e = INT32_MAX;
-        if (rel >= 0 && rel < maxlen - off) {   // (LEAD is whole lanes' stretches: no lane straddles a + off)
-            int pos = first_diff<LBW>(r, t);
-            const int32_t lim = maxlen - off - rel;
-            if (lim < 4 * LBW && pos > lim) pos = lim;
-            if (pos < 4 * LBW) e = off + rel + pos;
-        }
-        const unsigned long long sm = __ballot(e != INT32_MAX);
-        if (sm) {
-            const int32_t m = lane_val(e, first_lane(sm));
-            return m < maxlen ? m : maxlen;
-        }
-        off += LBV - lead;
+        const int32_t ra = a + off - sa, tb = b + off - sb;
+        int32_t avail = LBV - (ra > tb ? ra : tb);
+        if (avail > maxlen - off) avail = maxlen - off;
+        const int32_t e = lds_first_diff(L.rbuf, ra, L.tbuf, tb, avail);
+        if (e < avail) return off + e;
+        off += avail;
     }
     return maxlen;
 }
@@ -1106,6 +1081,35 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
     }
 }
 
+// The round's frozen list in chunk order (k_commit appends in atomic order): which chunks the blind
+// frozen batch (FROZEN_FIRST) and the later batches take, and so the round's fills and the next
+// pending list, no longer depend on which block committed first -- the rounds are the same on every
+// run.  One block, bitonic sort in LDS; a list longer than FSORT_CAP stays as it is (exact either way).
+constexpr int FSORT_CAP = 4096;
+__global__ __launch_bounds__(1024) void k_flist_sort(WalkPtrs A) {
+    if (A.scal[9]) return;
+    __shared__ int32_t sb[FSORT_CAP];
+    const int nf = A.scal[5];
+    if (nf <= 1 || nf > FSORT_CAP) return;
+    int np = 2;
+    while (np < nf) np <<= 1;
+    for (int i = (int)threadIdx.x; i < np; i += (int)blockDim.x) sb[i] = i < nf ? A.flist[i] : INT32_MAX;
+    __syncthreads();
+    for (int k = 2; k <= np; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = (int)threadIdx.x; i < np; i += (int)blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const int32_t a = sb[i], b = sb[ixj];
+                    if ((a > b) == ((i & k) == 0)) { sb[i] = b; sb[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = (int)threadIdx.x; i < nf; i += (int)blockDim.x) A.flist[i] = sb[i];
+}
+
 // Frozen chunks (committed fix-ups that ended in a long literal run with P unchanged up to their
 // chunk end; k_commit lists them): for each of the first FROZEN_MAX, the first position after its
 // exit whose k-mer key occurs in its window of P, over the whole rest of the target (grid.y picks
@@ -1194,6 +1198,7 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
         A.lround[j] = 1;
         A.seedq[j] = 0;
         A.trapped[j] = 0;
+        A.tflag[j] = 0;
         A.hintY[j] = -1;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1337,8 +1342,8 @@ __global__ __launch_bounds__(256) void k_round_pending(WalkPtrs A) {
     A.lround[j] = next;
     A.plist[atomicAdd(&A.scal[0], 1)] = j;
     if (j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round) {
-        const int t = atomicAdd(&A.scal[12], 1);
-        if (t < RESPEC_MAX_TRIGGERS) A.trig[t] = j;
+        A.tflag[j] = A.round;   // (k_round_respec takes the first RESPEC_MAX_TRIGGERS in chunk order)
+        atomicAdd(&A.scal[12], 1);
     }
 }
 
@@ -1348,10 +1353,33 @@ __global__ __launch_bounds__(RESPEC_T) void k_round_respec(WalkPtrs A) {
     const int ntrig = A.scal[12];
     if (!ntrig) return;
     const int32_t next = A.round + 1;
-    const int nt = ntrig < RESPEC_MAX_TRIGGERS ? ntrig : RESPEC_MAX_TRIGGERS;
+    __shared__ int32_t trig[RESPEC_MAX_TRIGGERS];
+    __shared__ int32_t wsum[RESPEC_T / 64 + 1];
+    // the round's triggers in chunk order (the first RESPEC_MAX_TRIGGERS): thread t takes a contiguous
+    // share of the chunks, a block scan of the shares' counts places them -- the same set every run
+    {
+        const int32_t per = (A.C + RESPEC_T - 1) / RESPEC_T, c0 = (int32_t)threadIdx.x * per;
+        int cnt = 0;
+        for (int32_t q = c0; q < c0 + per && q < A.C; q++) cnt += A.tflag[q] == A.round;
+        const int incl = wave_incl_add<int>(cnt);
+        const int w = (int)(threadIdx.x >> 6), lane = lane_id();
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int run = 0;
+            for (int i = 0; i < RESPEC_T / 64; i++) { const int x = wsum[i]; wsum[i] = run; run += x; }
+            wsum[RESPEC_T / 64] = run;
+        }
+        __syncthreads();
+        int at = wsum[w] + incl - cnt;
+        for (int32_t q = c0; q < c0 + per && q < A.C && at < RESPEC_MAX_TRIGGERS; q++)
+            if (A.tflag[q] == A.round) trig[at++] = q;
+        __syncthreads();
+    }
+    const int nt = wsum[RESPEC_T / 64] < RESPEC_MAX_TRIGGERS ? wsum[RESPEC_T / 64] : RESPEC_MAX_TRIGGERS;
     const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6), lane = lane_id();
     for (int t = w; t < nt; t += nw) {
-        const int32_t j = A.trig[t], P = A.snapP[j];
+        const int32_t j = trig[t], P = A.snapP[j];
         for (int32_t q0 = j + 1; q0 <= j + RESPEC_AHEAD && q0 < A.C; q0 += 64) {
             const int32_t q = q0 + lane;
             // every chunk after a pending one is unconfirmed, so replacing its trajectory by another
@@ -1798,7 +1826,19 @@ __device__ __forceinline__ bool code32(const uint8_t* s, uint64_t& code) {
     return bad == 0;
 }
 
-__device__ __forceinline__ uint32_t anchor_tag(uint64_t key, uint32_t gen) { return (uint32_t)key ^ gen; }
+// A slot holds gen:16 | tag:16 | position:32 and is written with a 64-bit atomicMax: the call's
+// generation beats every older one (stale slots never need clearing), and among one call's samples
+// that share a slot the winner no longer depends on which wave stores last -- the anchor votes, and
+// with them the speculation and the walk's round counts, are the same on every run.
+__device__ __forceinline__ uint64_t anchor_slot(const WalkPtrs& A, uint64_t key, uint32_t pos) {
+    return ((uint64_t)(A.agen & 0xffffu) << 48) | ((uint64_t)(uint32_t)(key & 0xffffu) << 32) | pos;
+}
+__device__ __forceinline__ bool anchor_hit(const WalkPtrs& A, uint64_t key, uint64_t v) {
+    return (v >> 32) == (anchor_slot(A, key, 0) >> 32) && (uint32_t)v != A_MULTI;
+}
+__device__ __forceinline__ void anchor_put(const WalkPtrs& A, uint64_t key, uint32_t pos) {
+    atomicMax((unsigned long long*)&A.atab[key >> (64 - A.abits)], (unsigned long long)anchor_slot(A, key, pos));
+}
 
 // pass 1 (mark = false): store every sample; pass 2 (mark = true): flag repeated 32-mers
 template <bool MARK>
@@ -1809,13 +1849,11 @@ __global__ void k_anchor_build(WalkPtrs A) {
         uint64_t code;
         if (!code32<true>(A.R + p, code)) continue;
         const uint64_t key = mix64(code);
-        const uint32_t tag = anchor_tag(key, A.agen);
-        uint64_t* slot = &A.atab[key >> (64 - A.abits)];
         if (!MARK) {
-            *slot = ((uint64_t)tag << 32) | (uint32_t)p;
-        } else {
-            const uint64_t v = *slot;
-            if ((uint32_t)(v >> 32) == tag && (uint32_t)v != (uint32_t)p) *slot = ((uint64_t)tag << 32) | A_MULTI;
+            anchor_put(A, key, (uint32_t)p);
+        } else {   // (MULTI is the largest position: the mark is an atomicMax too)
+            const uint64_t v = A.atab[key >> (64 - A.abits)];
+            if ((v >> 32) == (anchor_slot(A, key, 0) >> 32) && (uint32_t)v != (uint32_t)p) anchor_put(A, key, A_MULTI);
         }
     }
 }
@@ -1835,7 +1873,7 @@ __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0) {
         if (y + ANCHOR_K <= A.nT && code32<false>(A.T + y, code)) {
             const uint64_t key = mix64(code);
             const uint64_t v = A.atab[key >> (64 - A.abits)];
-            if ((uint32_t)(v >> 32) == anchor_tag(key, A.agen) && (uint32_t)v != A_MULTI) dg[b] = (int32_t)(uint32_t)v - y;
+            if (anchor_hit(A, key, v)) dg[b] = (int32_t)(uint32_t)v - y;
         }
     }
     int32_t g = INVALID, first = INVALID;
@@ -2084,7 +2122,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
                               }
                               if (acc && bad) continue;
                               const uint64_t key = mix64(code);
-                              A.atab[key >> (64 - A.abits)] = ((uint64_t)anchor_tag(key, A.agen) << 32) | (uint32_t)p;
+                              anchor_put(A, key, (uint32_t)p);
                           }
                       });
     }
@@ -2181,7 +2219,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
                           }
                           if (acc && bad) continue;
                           const uint64_t key = mix64(code);
-                          A.atab[key >> (64 - A.abits)] = ((uint64_t)anchor_tag(key, A.agen) << 32) | (uint32_t)p;
+                          anchor_put(A, key, (uint32_t)p);
                       }
                   });
 }
@@ -2639,6 +2677,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);
     A.trig = c.take<int32_t>(RESPEC_MAX_TRIGGERS);
+    A.tflag = c.take<int32_t>(C);
     A.fa_j = c.take<int32_t>(FROZEN_MAX); A.fa_l = c.take<int32_t>(FROZEN_MAX); A.fa_p = c.take<int32_t>(FROZEN_MAX);
     A.hintY = c.take<int32_t>(C); A.hintP = c.take<int32_t>(C);
     A.skip_hints = env_int("SCCG_SKIP_HINTS", 1);
@@ -2872,14 +2911,32 @@ unsigned first_sweep_grid(const WalkPtrs& A) {
 
 // the anchor table's generation for this call (a fresh workspace is cleared once; afterwards every
 // call's generation retires old slots)
+// Generations increase per workspace (slots are written with atomicMax, anchor_slot), so a table
+// region that held nothing but anchor slots since it was last cleared needs no clearing: stale slots
+// carry older generations.  The table is the workspace's first buffer (carve), sized by the call's
+// |R'|; the bytes past a call's table belong to its other buffers, so `clean` -- the slots that hold
+// only anchor slots -- shrinks to each call's table, and a larger table, a new workspace or the
+// 16-bit generation wrapping clears it once.  (The genome job takes its pairs largest first: one
+// clear per lane and step.)
+struct AnchorSeen { const uint64_t* tab; size_t clean; uint32_t gen; };
+std::mutex g_anchor_mu;
+std::map<const void*, AnchorSeen> g_anchor_seen;
+
 int anchor_generation(WalkPtrs& A, const void* ws, hipStream_t s) {
-    static thread_local const void* ws_seen = nullptr;
-    static thread_local uint32_t gen = 0;
-    if (ws != ws_seen) {
-        SCCG_HIP(hipMemsetAsync(A.atab, 0, ((size_t)1 << A.abits) * sizeof(uint64_t), s));
-        ws_seen = ws;
+    const size_t n = (size_t)1 << A.abits;
+    uint32_t g;
+    bool clear;
+    {
+        std::lock_guard<std::mutex> lk(g_anchor_mu);
+        AnchorSeen& e = g_anchor_seen[ws];
+        clear = e.tab != A.atab || n > e.clean || e.gen >= 0xffffu;
+        if (clear) e.gen = 0;
+        e.tab = A.atab;
+        e.clean = n;
+        g = ++e.gen;
     }
-    A.agen = 0x9E3779B9u * ++gen;
+    if (clear) SCCG_HIP(hipMemsetAsync(A.atab, 0, n * sizeof(uint64_t), s));
+    A.agen = g;
     return 0;
 }
 
@@ -3073,6 +3130,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         if (dev_nlist) RC(launch_carry(A, s));
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
+        hipLaunchKernelGGL(k_flist_sort, dim3(1), dim3(1024), 0, s, A);
         if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, fbase_cap), dim3(FZ_T), 0, s, A, 0);
         SCCG_HIP(hipGetLastError());
         RC(launch_round_end(A, 0, fbase_cap, s));
@@ -3314,6 +3372,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                     // (pn2 == 0) ones are handled after the batch's one sync.
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(gl, 256) > 4096 ? 4096 : grid_for(gl, 256)), dim3(256), 0, s, A,
                                        (const int32_t*)A.plist, gl, dev ? (const int32_t*)A.scal : (const int32_t*)nullptr);
+                    hipLaunchKernelGGL(k_flist_sort, dim3(1), dim3(1024), 0, s, A);
                     if (b + 1 < batch) {   // a whole round; the last one's end is queued below
                         hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, FROZEN_FIRST), dim3(FZ_T), 0, s, A, 0);
                         RC(launch_round_end(A, 0, FROZEN_FIRST, s));
@@ -3374,6 +3433,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                     RC(dev_set_i32(A.scal + 5, 1, {0}, s));   // frozen list of the resumed chunks
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(nr, 256) > 4096 ? 4096 : grid_for(nr, 256)), dim3(256), 0, s, A,
                                        (const int32_t*)A.rlist, nr, (const int32_t*)nullptr);
+                    hipLaunchKernelGGL(k_flist_sort, dim3(1), dim3(1024), 0, s, A);
                     SCCG_HIP(hipGetLastError());
                 }
                 {
@@ -3648,4 +3708,10 @@ int global_match_and_emit(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int
     rt.on = true;
     return match_and_emit_impl(Rp, nRp, Tp, nTp, k, m, FF_CHUNK, ws, ws_bytes, out, out_len, res, s, abs_p, late_out,
                                keep_flat, &rt);
+}
+
+// a workspace buffer is about to be freed: its anchor table's generations are gone with it
+void walk_forget_workspace(const void* ws) {
+    std::lock_guard<std::mutex> lk(g_anchor_mu);
+    g_anchor_seen.erase(ws);
 }

@@ -380,3 +380,59 @@ def test_frozen_chains_vs_oracle(ctx, seed):
     st = ctx.stats()
     assert st["walk_chains"] >= 1
     assert got == oraclelib.compress(rfa, tfa)
+
+
+def _layout_fasta(rng, seq: str, case: str) -> bytes:
+    """A target FASTA with an awkward byte layout around the run boundaries the strip emits."""
+    if case == "crlf_ragged":   # CRLF, line widths 1..120, blank lines
+        out, i = [">t crlf\r\n"], 0
+        while i < len(seq):
+            w = rng.randint(1, 120)
+            out.append(seq[i:i + w] + "\r\n" + ("\r\n" if rng.random() < 0.05 else ""))
+            i += w
+        return "".join(out).encode()
+    if case == "whitespace_gulfs":   # stretches of blank lines longer than 64 strip tiles inside runs
+        gulf = "\n" * (70 * 4096 + 13)
+        cut = [len(seq) // 5, len(seq) // 2, 4 * len(seq) // 5]
+        parts, prev = [], 0
+        for c in cut:
+            parts.append(seq[prev:c])
+            prev = c
+        parts.append(seq[prev:])
+        return (">t gulfs\n" + gulf.join(fuzzgen.to_fasta(p, None, 60).decode() for p in parts)).encode()
+    if case == "tile_edges":   # newlines and run boundaries at strip-tile (4 KiB) edges, a long header
+        hdr = ">" + "h" * 5000 + "\n"
+        body = fuzzgen.to_fasta(seq, None, 4095).decode()   # lines of 4095 + '\n' = one tile each
+        return (hdr + body).encode()
+    if case == "no_final_newline":
+        return fuzzgen.to_fasta(seq, ">t", 61, trailing_newline=False)
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("case", ["crlf_ragged", "whitespace_gulfs", "tile_edges", "no_final_newline"])
+@pytest.mark.parametrize("seed", range(2))
+def test_strip_run_events_vs_oracle(ctx, case, seed):
+    """The target strip emits both run lines' boundaries (lowercase, compression.cpp:341-368; N,
+    :527-555) per 4 KiB tile; runs that cross tiles, dropped bytes (CR, LF, blank-line gulfs wider
+    than the tile look-back, a header longer than a tile) and runs open at the target's end must
+    give the oracle's lines byte for byte (the record text holds both)."""
+    rng = random.Random(1300 + seed)
+    ref = _rand(rng, 400_000).decode()
+    tgt = list(ref[:200_000] + _rand(rng, 2000).decode() + ref[200_000:])
+    i = 0
+    while i < len(tgt):   # soft-masked runs and N runs of every length, some across tile edges
+        ln = rng.choice([1, 2, 3, 50, 700, 4096, 9000])
+        kind = rng.random()
+        for q in range(i, min(len(tgt), i + ln)):
+            if kind < 0.35:
+                tgt[q] = tgt[q].lower()
+            elif kind < 0.45:
+                tgt[q] = "N" if rng.random() < 0.9 else "n"
+        i += ln + rng.choice([0, 1, 5, 300, 3000])
+    for q in range(len(tgt) - 777, len(tgt)):   # a lowercase run open at the end
+        tgt[q] = tgt[q].lower()
+    rfa = fuzzgen.to_fasta(ref)
+    tfa = _layout_fasta(rng, "".join(tgt), case)
+    want = oraclelib.compress(rfa, tfa)
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert (rc, got) == (0, want)
