@@ -52,10 +52,6 @@ METRIC = "target bases compressed/sec at 1/2/4/8 GPUs; bit-exact record stream v
 MANIFEST = os.path.join(REPO, "tests", "golden", "genome_manifest.json")
 DOMINANT = "walk"   # the step's dominant kernel family (k_walk: ~35 % of the kernel time)
 CPU_BASELINE_N1 = os.path.join(REPO, "profiles", "cpu_baseline.json")   # the N = 1 line's measurement
-# GPU_MAX_HW_QUEUES for the run: 0 keeps the environment's (HIP's default, 4).  Measured on the
-# genome bench (profiles/r03_ab.txt): 2 contexts with 4 queues 24.1-24.5 ms per step, with 8 queues
-# 28.0-28.3 ms, 3 contexts with 8-12 queues 26.0-31.3 ms, 1 context 29.8-29.9 ms.
-HW_QUEUES_DEFAULT = 0
 
 
 def log(*a):
@@ -546,8 +542,9 @@ def t2t_genome(pool: LanePool, jobs: list, world: int, rank: int, dev, steps: in
     ms = dt / steps * 1e3
     worst = max(per, key=lambda n: per[n]["rounds"]) if per else None
     stable = all(len(set(p["rounds_per_timed_step"])) <= 1 for p in per.values())
-    return {"workload": "BASELINE configs[4] shape: T2T-like profile (tandem arrays, 1e-2 SNPs, >100-bp deletions "
-                        "every ~100 kb) on the 24 hg18/hg19 UCSC length pairs, seed = chromosome index",
+    return {"workload": "BASELINE configs[4] shape, synthetic: T2T-like profile (tandem arrays, 1e-2 SNPs, >100-bp "
+                        "deletions every ~100 kb) at the hg18/hg19 chromosome lengths (not CHM13/GRCh38 lengths: no "
+                        "T2T data offline), 24 pairs, seed = chromosome index",
             "target_bases": nT, "ms": ms, "bases_per_s": nT / (ms * 1e-3), "steps": steps,
             "pinned_checked": len(checked), "pinned_mismatch": bad,
             "max_rounds": per[worst]["rounds"] if worst else None, "max_rounds_chrom": worst,
@@ -624,8 +621,6 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--contexts", type=int, default=2, help="library contexts (host threads) per GPU")
-    ap.add_argument("--hw-queues", type=int, default=HW_QUEUES_DEFAULT,
-                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--workload", choices=["genome", "chr1"], default="genome",
                     help="genome: BASELINE configs[2] (default); chr1: one chr1-sized pair per rank (configs[1] shape)")
     ap.add_argument("--names", default="", help="comma-separated subset of chromosomes (diagnostics)")
@@ -643,8 +638,6 @@ def main() -> None:
     args = ap.parse_args()
     if args.only_steps:
         args.no_decomp = args.no_e2e = args.no_t2t = args.no_k21 = args.no_prof = args.no_cpu_baseline = True
-    if args.hw_queues > 0:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))   # before HIP initialises
 
     import torch
     import torch.distributed as dist

@@ -138,7 +138,13 @@ struct SegStat {
     int32_t last_p;
     int32_t pad;
 };
-// segments [seg0, seg_end) of one pass (pass 2 only touches segments pass 1 left without a match)
+// SegStat.pass of a segment the local pass proved class 0 without walking it (its records are not
+// computed: launch_local_proven computes them when the pair stays local)
+constexpr int32_t PASS_PROVEN = -1;
+int launch_local_proven(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t iters, uint32_t* recs,
+                        SegStat* stat, hipStream_t s);
+// segments [seg0, seg_end) of one pass (pass 2 only touches segments pass 1 left without a match;
+// pass 3: pass 1 of the PASS_PROVEN segments)
 int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t seg0,
                       int64_t seg_end, uint32_t* recs, SegStat* stat, hipStream_t s);
 // switch FSM (compression.cpp:395-473) over segments [seg0, seg_end) from counter state *state
@@ -147,8 +153,11 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
 // (|R|, |T| read from device memory, so no host sync precedes it; nseg_max bounds the grid):
 // ctl = {unused 0, early-exit bound INT32_MAX, switch segment INT32_MAX (= none), 0} on
 // entry; cls: per-segment classes tagged with gen (never cleared: zero-filled once, gen >= 1)
+// prv / list / cnt (the windowed switch scan's proofs, walk list and its length; null: the single
+// pass over every segment): prv is generation-tagged like cls
 int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
-                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s);
+                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s,
+                     int32_t* prv = nullptr, int32_t* list = nullptr, int32_t* cnt = nullptr);
 // record text for local mode (delta-encoded, compression.cpp:406-415 + :222-304) + leftover
 // (abs_p: "(p," with absolute p instead, the text before delta_encode)
 int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_t* recs,

@@ -128,10 +128,136 @@ __device__ __forceinline__ void seg_words_load(SegWords& W, int64_t seg, const u
     }
 }
 
+// Both segments into LDS, uppercased (compression.cpp:369-370, :386-389); base is a multiple of 1000,
+// so the dword loads are aligned; bytes past a segment end read as 0.  Returns "the target segment
+// holds a byte other than 'N'" (compression.cpp:419), wave-uniform.
+__device__ __forceinline__ bool seg_load(SegLds& L, int64_t seg, int upper, const uint8_t* __restrict__ R, int64_t nR,
+                                         const uint8_t* __restrict__ T, int64_t nT, const SegWords* pre) {
+    const int lane = lane_id();
+    const int64_t base = seg * SEG_L;
+    const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
+    const int nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
+    bool non_n = false;
+    const uint32_t* R4 = reinterpret_cast<const uint32_t*>(R + base);
+    const uint32_t* T4 = reinterpret_cast<const uint32_t*>(T + base);
+    uint32_t* r4 = reinterpret_cast<uint32_t*>(L.r);
+    uint32_t* t4 = reinterpret_cast<uint32_t*>(L.t);
+#pragma unroll
+    for (int j = 0; j < SEGB / 256; j++) {
+        const int i = lane + 64 * j, b0 = 4 * i;
+        uint32_t rw, tw;
+        if (pre) { rw = pre->r[j]; tw = pre->t[j]; }
+        else { rw = b0 < nr ? R4[i] : 0u; tw = b0 < nt ? T4[i] : 0u; }
+        if (nr - b0 < 4) rw &= nr - b0 <= 0 ? 0u : (1u << (8 * (nr - b0))) - 1u;
+        if (nt - b0 < 4) tw &= nt - b0 <= 0 ? 0u : (1u << (8 * (nt - b0))) - 1u;
+        if (upper) { rw = upper4(rw); tw = upper4(tw); }
+        r4[i] = rw;
+        t4[i] = tw;
+#pragma unroll
+        for (int q = 0; q < 4; q++) non_n |= (b0 + q < nt && (uint8_t)(tw >> (8 * q)) != 'N');
+    }
+    non_n = __ballot(non_n) != 0;
+    wave_sync();
+    return non_n;
+}
+
+// Class-0 proof of a segment pair in LDS (the switch scan's common case, compression.cpp:400-416):
+// the k = 14 pass succeeds with at most half of the target literal, without hashing or walking.  A
+// target position whose k-mer occurs in the reference segment has a candidate, so the walk never
+// visits it as a literal step (literal bases are positions without a candidate, plus at most the
+// K - 1 after the last k-mer start); and one such position makes the pass find a match.  Positions
+// "with a candidate" are shown on a few diagonals d: T[i..i+K) == R[i+d..i+d+K).  The diagonals
+// come from 8 sampled target k-mers looked up among the reference segment's k-mer keys.  A segment
+// the proof cannot settle takes the walk as before; the proof only ever answers "class 0".
+constexpr int PROOF_SAMPLES = 8, PROOF_DIAGS = 4;
+__device__ __forceinline__ bool seg_prove(const uint8_t* Lr, const uint8_t* Lt, int nr, int nt) {
+    constexpr int K = 14;
+    constexpr uint32_t MASK = (1u << (2 * K)) - 1u, KM = (1u << K) - 1u;
+    const int lane = lane_id();
+    const int lastr = nr - K, lastk = nt - K;
+    if (lastr < 0 || lastk < 0) return false;
+    // reference keys of positions 16 lane .. 16 lane + 15 (invalid: 0xffffffff)
+    uint32_t rk[16];
+    {
+        const int p0 = 16 * lane;
+        uint64_t code = 0;
+        uint32_t bad = ~0u;
+        if (p0 <= lastr) keys16<K>(&Lr[p0], code, bad);
+#pragma unroll
+        for (int st = 0; st < 16; st++)
+            rk[st] = (p0 + st <= lastr && !((bad >> st) & KM)) ? (uint32_t)(code >> (2 * st)) & MASK : 0xffffffffu;
+    }
+    // sampled target k-mers: lane j < PROOF_SAMPLES holds the key at y_j = j * lastk / PROOF_SAMPLES
+    uint32_t tk = 0xfffffffeu;
+    const int yl = lane < PROOF_SAMPLES ? (int)((int64_t)lane * lastk / PROOF_SAMPLES) : 0;
+    if (lane < PROOF_SAMPLES) {
+        uint32_t w[4], bad;
+        uint64_t code;
+        loadw<4>(&Lt[yl], w);
+        pack_codes<4>(w, code, bad);
+        if (!(bad & KM)) tk = (uint32_t)code & MASK;
+    }
+    int32_t dg[PROOF_DIAGS];
+    int nd = 0;
+    for (int j = 0; j < PROOF_SAMPLES && nd < PROOF_DIAGS; j++) {
+        const uint32_t kj = lane_val(tk, j);
+        if (kj == 0xfffffffeu) continue;
+        uint32_t m = 0;
+#pragma unroll
+        for (int st = 0; st < 16; st++) m |= (uint32_t)(rk[st] == kj) << st;
+        const unsigned long long b = __ballot(m != 0);
+        if (!b) continue;
+        const int fl = first_lane(b);
+        const int32_t d = 16 * fl + __builtin_ctz(lane_val(m, fl)) - lane_val(yl, j);
+        bool dup = false;
+        for (int q = 0; q < nd; q++) dup |= dg[q] == d;
+        if (!dup) dg[nd++] = d;
+    }
+    if (!nd) return false;
+    // positions 16 lane .. +15 covered on some diagonal: 14 equal bytes from i (and from i + d)
+    const int i0 = 16 * lane;
+    uint32_t tw[8];
+    {
+        const uint32_t* t4 = reinterpret_cast<const uint32_t*>(Lt) + 4 * lane;
+#pragma unroll
+        for (int q = 0; q < 8; q++) tw[q] = lane < 63 || q < 4 ? t4[q] : 0u;
+    }
+    uint32_t cov = 0;
+    for (int q = 0; q < nd; q++) {
+        const int32_t d = dg[q];
+        int ra = i0 + d;   // R bytes ra .. ra + 31 (a lane whose stretch leaves the buffer proves nothing)
+        const bool inside = ra >= 0 && ra <= SEGB - 36;
+        ra = inside ? ra : 0;
+        uint32_t rw[8];
+        loadw<8>(&Lr[ra], rw);
+        uint32_t e = 0;
+#pragma unroll
+        for (int w = 0; w < 8; w++) e |= ((~nz_bytes(tw[w] ^ rw[w])) & 0xfu) << (4 * w);
+        uint32_t c = e & (e >> 1);
+        c &= c >> 2;
+        c &= c >> 4;
+        c &= c >> 6;   // bit i: bytes i .. i + 13 equal
+        // valid starts: i <= lastk, 0 <= i + d <= lastr, and the R bytes read really were R[i + d ...]
+        uint32_t v = 0xffffu;
+        const int tv = lastk - i0 + 1;                 // i0 + st <= lastk
+        v &= tv <= 0 ? 0u : (tv >= 16 ? 0xffffu : (1u << tv) - 1u);
+        const int rv = lastr - (i0 + d) + 1;           // i0 + d + st <= lastr
+        v &= rv <= 0 ? 0u : (rv >= 16 ? 0xffffu : (1u << rv) - 1u);
+        if (!inside) v = 0;
+        cov |= c & v;
+    }
+    const int tv = lastk - i0 + 1;
+    const uint32_t tvm = tv <= 0 ? 0u : (tv >= 16 ? 0xffffu : (1u << tv) - 1u);
+    const int unc = wave_sum((int)__popc(tvm & ~cov));
+    const bool any = __ballot(cov != 0) != 0;
+    return any && 2 * (unc + (nt - 1 - lastk)) <= nt;
+}
+
 template <int K, bool DBG>
 __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pass, int non_n_prev, int upper,
                                                  const uint8_t* __restrict__ R, int64_t nR, const uint8_t* __restrict__ T,
-                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr) {
+                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr,
+                                                 int loaded = -1) {
     const int lane = lane_id();
     const int64_t base = seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
@@ -142,31 +268,8 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
         if (DBG) { const uint64_t t = wall_clock64(); tph[i] += t - tq; tq = t; }
     };
 
-    // ---- load both segments, uppercased (compression.cpp:369-370, :386-389); base is a multiple
-    //      of 1000, so the dword loads are aligned; bytes past the segment end read as 0
-    bool non_n = false;
-    {
-        const uint32_t* R4 = reinterpret_cast<const uint32_t*>(R + base);
-        const uint32_t* T4 = reinterpret_cast<const uint32_t*>(T + base);
-        uint32_t* r4 = reinterpret_cast<uint32_t*>(L.r);
-        uint32_t* t4 = reinterpret_cast<uint32_t*>(L.t);
-#pragma unroll
-        for (int j = 0; j < SEGB / 256; j++) {
-            const int i = lane + 64 * j, b0 = 4 * i;
-            uint32_t rw, tw;
-            if (pre) { rw = pre->r[j]; tw = pre->t[j]; }
-            else { rw = b0 < nr ? R4[i] : 0u; tw = b0 < nt ? T4[i] : 0u; }
-            if (nr - b0 < 4) rw &= nr - b0 <= 0 ? 0u : (1u << (8 * (nr - b0))) - 1u;
-            if (nt - b0 < 4) tw &= nt - b0 <= 0 ? 0u : (1u << (8 * (nt - b0))) - 1u;
-            if (upper) { rw = upper4(rw); tw = upper4(tw); }
-            r4[i] = rw;
-            t4[i] = tw;
-#pragma unroll
-            for (int q = 0; q < 4; q++) non_n |= (b0 + q < nt && (uint8_t)(tw >> (8 * q)) != 'N');
-        }
-    }
-    non_n = __ballot(non_n) != 0;
-    wave_sync();
+    // ---- both segments in LDS (loaded >= 0: already there, `loaded` = its non-N flag)
+    const bool non_n = loaded >= 0 ? loaded != 0 : seg_load(L, seg, upper, R, nR, T, nT, pre);
     tick(0);
 
     // ---- H: every k-mer of the reference segment (compression.cpp:41-47), counting-sorted by
@@ -395,8 +498,9 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
     const int64_t G = (int64_t)gridDim.x * WPB;
     for (int64_t seg = seg0 + (int64_t)blockIdx.x * WPB + w; seg < seg_end; seg += G) {
         if (pass == 2 && stat[seg].pass != 0) continue;
-        const SegStat st = local_segment<K, DBG>(lds_all[w], seg, pass, pass == 2 ? stat[seg].non_n : 0, upper, R, nR, T,
-                                                 nT, recs);
+        if (pass == 3 && stat[seg].pass != PASS_PROVEN) continue;   // (a proof means the k pass succeeds)
+        const SegStat st = local_segment<K, DBG>(lds_all[w], seg, pass == 3 ? 1 : pass, pass == 2 ? stat[seg].non_n : 0,
+                                                 upper, R, nR, T, nT, recs);
         if (lane_id() == 0) stat[seg] = st;
         wave_sync();   // the next segment reuses this wave's LDS
     }
@@ -433,30 +537,49 @@ __device__ __forceinline__ int32_t seg_count(int64_t nR, int64_t nT) {
 #ifndef LOCAL_WAVES_PER_EU
 #define LOCAL_WAVES_PER_EU 4   // the LDS allows 4 waves/SIMD (4 blocks of SegLds x 4); VGPRs must fit 128
 #endif
+// list (optional): walk only list[0 .. *cnt) (increasing segment order), the segments the windowed
+// pass could not settle by proof (k_local_prove / k_local_list); null: every segment.
 template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_all(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
                                                           const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
                                                           uint32_t* __restrict__ recs, SegStat* __restrict__ stat,
-                                                          int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl) {
+                                                          int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl,
+                                                          int prove, const int32_t* __restrict__ list,
+                                                          const int32_t* __restrict__ cnt) {
     __shared__ SegLds lds_all[WPB];
     const int64_t nR = *dnR, nT = *dnT;
     const int32_t nseg = seg_count(nR, nT);
     const int w = wave_in_block(), lane = lane_id();
     SegLds& L = lds_all[w];
     const int32_t G = (int32_t)gridDim.x * WPB;
+    const int32_t nitem = list ? *cnt : nseg;
+    auto item = [&](int32_t i) { return list ? uni(list[i]) : i; };
     SegWords cur, nxt;
-    int32_t seg = (int32_t)blockIdx.x * WPB + w;
-    if (seg < nseg) seg_words_load(cur, seg, R, nR, T, nT);
-    for (; seg < nseg; seg += G) {
+    int32_t it = (int32_t)blockIdx.x * WPB + w;
+    if (it < nitem) seg_words_load(cur, item(it), R, nR, T, nT);
+    for (; it < nitem; it += G) {
+        const int32_t seg = item(it);
         if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
-        if (seg + G < nseg) seg_words_load(nxt, seg + G, R, nR, T, nT);   // in flight during this segment
-        SegStat st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, &cur);
-        if (!st.pass) {
-            wave_sync();
-            st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs);
+        if (it + G < nitem) seg_words_load(nxt, item(it + G), R, nR, T, nT);   // in flight during this segment
+        const bool non_n = seg_load(L, seg, 1, R, nR, T, nT, &cur);
+        SegStat st;
+        int c;
+        const int64_t base = (int64_t)seg * SEG_L;
+        const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L), nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
+        if (prove && seg_prove(L.r, L.t, nr, nt)) {
+            // class 0 without its records: a pair that stays local computes them later (PASS_PROVEN)
+            st = SegStat{0, 0, 0, PASS_PROVEN, (int)non_n, -1, -1, nt};
+            c = 0;
+            if (DBG && lane == 0) atomicAdd(&g_local_dbg[15], 1ull);
+        } else {
+            st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, nullptr, (int)non_n);
+            if (!st.pass) {
+                wave_sync();
+                st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs);
+            }
+            c = seg_class(st);
         }
         if (lane == 0) stat[seg] = st;
-        const int c = seg_class(st);
         if (lane == 0) __hip_atomic_store(&cls[seg], (gen << 2) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // classes of seg-4 .. seg+4 (lane i holds seg-4+i; -1 = not published in this call)
         const int32_t idx = seg - 4 + lane;
@@ -479,6 +602,113 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
         wave_sync();   // the next segment reuses this wave's LDS
         cur = nxt;
     }
+}
+
+// ---- the windowed switch scan.  The first switch (compression.cpp:462-473) is the first class-2
+// segment whose 4 predecessors are class 1 or 2, so a segment proved class 0 (seg_prove) breaks
+// every window it lies in, and a segment that is not proved matters only inside a run of >= 5
+// unproved segments.  Per window of segments: k_local_prove proves every segment it can (one wave
+// per segment pair, no hashing, no walk) and publishes class 0; k_local_list lists, in segment
+// order, the unproved segments that lie in such a run; k_local_all walks only those.  A window
+// past an earlier window's switch returns at once.  Every segment's SegStat says PASS_PROVEN
+// ("records not computed") unless it was walked: a pair that stays local computes them afterwards
+// (launch_local_proven).  k_switch_final then finds the exact first switch as before (a segment
+// never walked and never proved is published as no class, which no switch window holds).
+struct ProveLds {
+    uint8_t r[SEGB];
+    uint8_t t[SEGB];
+};
+__global__ __launch_bounds__(SCCG_BLOCK) void k_local_prove(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
+                                                            const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
+                                                            int32_t w0, int32_t w1, SegStat* __restrict__ stat,
+                                                            int32_t* __restrict__ cls, int32_t* __restrict__ prv, int32_t gen,
+                                                            const int32_t* __restrict__ ctl) {
+    __shared__ ProveLds lds_all[WPB];
+    const int64_t nR = *dnR, nT = *dnT;
+    const int32_t nseg = seg_count(nR, nT);
+    const int32_t end = w1 < nseg ? w1 : nseg;
+    if (w0 >= end || w0 > __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    const int w = wave_in_block(), lane = lane_id();
+    ProveLds& L = lds_all[w];
+    const int32_t G = (int32_t)gridDim.x * WPB;
+    for (int32_t seg = w0 + (int32_t)blockIdx.x * WPB + w; seg < end; seg += G) {
+        const int64_t base = (int64_t)seg * SEG_L;
+        const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L), nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
+        const uint32_t* R4 = reinterpret_cast<const uint32_t*>(R + base);
+        const uint32_t* T4 = reinterpret_cast<const uint32_t*>(T + base);
+        uint32_t* r4 = reinterpret_cast<uint32_t*>(L.r);
+        uint32_t* t4 = reinterpret_cast<uint32_t*>(L.t);
+        bool non_n = false;
+        uint32_t rw[SEGB / 256], tw[SEGB / 256];
+#pragma unroll
+        for (int j = 0; j < SEGB / 256; j++) {   // (all loads first)
+            const int i = lane + 64 * j, b0 = 4 * i;
+            rw[j] = b0 < nr ? R4[i] : 0u;
+            tw[j] = b0 < nt ? T4[i] : 0u;
+        }
+        wave_sync();   // (the previous segment's readers are done)
+#pragma unroll
+        for (int j = 0; j < SEGB / 256; j++) {
+            const int i = lane + 64 * j, b0 = 4 * i;
+            if (nr - b0 < 4) rw[j] &= nr - b0 <= 0 ? 0u : (1u << (8 * (nr - b0))) - 1u;
+            if (nt - b0 < 4) tw[j] &= nt - b0 <= 0 ? 0u : (1u << (8 * (nt - b0))) - 1u;
+            r4[i] = upper4(rw[j]);
+            t4[i] = upper4(tw[j]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) non_n |= (b0 + q < nt && (uint8_t)(t4[i] >> (8 * q)) != 'N');
+        }
+        non_n = __ballot(non_n) != 0;
+        wave_sync();
+        const bool ok = seg_prove(L.r, L.t, nr, nt);
+        if (lane == 0) {
+            stat[seg] = SegStat{0, 0, 0, PASS_PROVEN, (int)non_n, -1, -1, nt};
+            prv[seg] = ok ? gen : 0;
+            if (ok) __hip_atomic_store(&cls[seg], gen << 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// One block: the window's segments that must be walked -- not proved, and inside a run of >= 5
+// segments none of which is proved (segments past the window count as not proved) -- in order.
+constexpr int LIST_T = 1024;
+__global__ __launch_bounds__(LIST_T) void k_local_list(const int64_t* __restrict__ dnR, const int64_t* __restrict__ dnT,
+                                                       int32_t w0, int32_t w1, const int32_t* __restrict__ prv, int32_t gen,
+                                                       int32_t* __restrict__ list, int32_t* __restrict__ cnt,
+                                                       const int32_t* __restrict__ ctl) {
+    __shared__ int32_t wsum[LIST_T / 64 + 1];
+    const int32_t nseg = seg_count(*dnR, *dnT);
+    const int32_t end = w1 < nseg ? w1 : nseg;
+    const bool live = w0 < end && w0 <= __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t n = live ? end - w0 : 0;
+    const int32_t per = (n + LIST_T - 1) / LIST_T;
+    const int32_t s0 = w0 + (int32_t)threadIdx.x * per, s1 = s0 + per < end ? s0 + per : end;
+    auto unproved = [&](int32_t q) -> bool {   // (q past the window: its proof has not run yet)
+        return q >= 0 && q < nseg && (q >= end || prv[q] != gen);
+    };
+    // need(s): s unproved and some run [a, a + 4] with a <= s <= a + 4 fully unproved
+    int c = 0;
+    auto need = [&](int32_t sgm) -> bool {
+        if (!unproved(sgm)) return false;
+        int back = 0, fwd = 0;
+        for (int32_t q = sgm - 1; q >= sgm - 4 && unproved(q); q--) back++;
+        for (int32_t q = sgm + 1; q <= sgm + 4 && unproved(q); q++) fwd++;
+        return back + fwd + 1 >= 5;
+    };
+    for (int32_t q = s0; q < s1; q++) c += need(q);
+    const int incl = wave_incl_add(c);
+    const int w = wave_in_block(), lane = lane_id();
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int i = 0; i < LIST_T / 64; i++) { const int t = wsum[i]; wsum[i] = acc; acc += t; }
+        wsum[LIST_T / 64] = acc;
+    }
+    __syncthreads();
+    int at = wsum[w] + incl - c;
+    for (int32_t q = s0; q < s1; q++)
+        if (need(q)) list[at++] = q;
+    if (threadIdx.x == 0) *cnt = wsum[LIST_T / 64];
 }
 
 __global__ void k_switch_final(const int32_t* __restrict__ cls, int32_t gen, const int64_t* __restrict__ dnR,
@@ -651,8 +881,24 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
     return 0;
 }
 
+constexpr int64_t LOCAL_WIN0 = 16384;
+// SCCG_LOCAL_PROVE=0: every segment walks (A/B runs and tests of the proof)
+int local_prove() {
+    static const int v = [] { const char* e = getenv("SCCG_LOCAL_PROVE"); return e ? atoi(e) != 0 : 1; }();
+    return v;
+}
+
+int launch_local_proven(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t iters, uint32_t* recs,
+                        SegStat* stat, hipStream_t s) {
+    if (!local_prove() || iters <= 0) return 0;
+    // (an unproved segment the windowed scan never walked may fail the k pass: the k2 pass follows)
+    const int rc = launch_local_pass(14, 3, 1, R, nR, T, nT, 0, iters, recs, stat, s);
+    return rc ? rc : launch_local_pass(10, 2, 1, R, nR, T, nT, 0, iters, recs, stat, s);
+}
+
 int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
-                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s) {
+                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s, int32_t* prv,
+                     int32_t* list, int32_t* cnt) {
     if (nseg_max <= 0) return 0;
     // resident capacity: the grid drains the counter, extra blocks would only find it exhausted
     static const unsigned cap = [] {
@@ -678,18 +924,32 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
         const unsigned long long z[16] = {};
         SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl);
+                    gen, ctl, local_prove(), (const int32_t*)nullptr, (const int32_t*)nullptr);
         unsigned long long d[16];
         SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
         SCCG_HIP(hipStreamSynchronize(s));
         const double n = d[5] ? (double)d[5] : 1.0;
+        fprintf(stderr, "[local all] %llu segments proved class 0 without a walk\n", d[15]);
         fprintf(stderr, "[local all] %llu segment passes, per pass (us): load %.2f keys %.2f insert %.2f hits %.2f walk %.2f"
                 " | max %.2f (seg %llu, %llu matches: load %.2f keys %.2f insert %.2f hits %.2f walk %.2f)\n", d[5],
                 d[0] / n / 100, d[1] / n / 100, d[2] / n / 100, d[3] / n / 100, d[4] / n / 100, d[6] / 100.0, d[13], d[14],
                 d[8] / 100.0, d[9] / 100.0, d[10] / 100.0, d[11] / 100.0, d[12] / 100.0);
+    } else if (local_prove() && prv && list && cnt) {
+        // windows of 16 Ki, 48 Ki, 144 Ki ... segments: the switch of an hg-like pair lies in the first
+        // (chr1 at segment 10,980); later windows then return at once
+        for (int64_t w0 = 0, wsz = LOCAL_WIN0; w0 < nseg_max; w0 += wsz, wsz *= 3) {
+            const int64_t w1 = w0 + wsz < nseg_max ? w0 + wsz : nseg_max;
+            const unsigned gp = grid_for(w1 - w0, WPB) > 8192 ? 8192 : grid_for(w1 - w0, WPB);
+            PROF_LAUNCH(PROF_LOCAL14, s, k_local_prove, dim3(gp), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, (int32_t)w0,
+                        (int32_t)w1, stat, cls, prv, gen, (const int32_t*)ctl);
+            hipLaunchKernelGGL(k_local_list, dim3(1), dim3(LIST_T), 0, s, d_nR, d_nT, (int32_t)w0, (int32_t)w1,
+                               (const int32_t*)prv, gen, list, cnt, (const int32_t*)ctl);
+            PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat,
+                        cls, gen, ctl, 0, (const int32_t*)list, (const int32_t*)cnt);
+        }
     } else {
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl);
+                    gen, ctl, 0, (const int32_t*)nullptr, (const int32_t*)nullptr);
     }
     if (nseg_max > 4) {
         const unsigned gs = grid_for(nseg_max - 4, 256) > 2048 ? 2048 : grid_for(nseg_max - 4, 256);

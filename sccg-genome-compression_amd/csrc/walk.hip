@@ -186,6 +186,8 @@ struct WalkPtrs {
     int32_t skip_hints;   // SCCG_SKIP_HINTS (default on)
     uint64_t* atab;
     uint32_t agen;            // anchor tag generation (one per call)
+    int32_t adet;             // anchor slots written with atomicMax (SCCG_ANCHOR_DET, default off)
+    int32_t lsort;            // frozen / carry lists sorted into chunk order (SCCG_LIST_SORT, default on)
     int32_t round;            // walk round of the launch (kernel argument copy)
     int32_t abits;
     const int64_t* dnR;       // early sweep: |R'| in device memory (nR is then only a bound)
@@ -313,39 +315,116 @@ __device__ __forceinline__ int first_diff(const uint32_t (&r)[N], const uint32_t
 }
 __device__ __forceinline__ int first_diff32(const uint32_t (&r)[8], const uint32_t (&t)[8]) { return first_diff<8>(r, t); }
 
-// 4 bytes at byte offset off of an LDS byte array: two dword reads and an alignbyte.  Lane l of a
-// wave reads offsets off0 + 4l: consecutive dwords, conflict-free (a lane stride of 32 bytes put 16
-// lanes on each of two banks per lane group: 8x the LDS cycles, and the walk's LDS was 64 % conflict
-// cycles).
-__device__ __forceinline__ uint32_t lds4(const uint8_t* lds, int32_t off) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (off >> 2);
-    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(off & 3));
+// WALK_LCE_V (build option, A/B): 0 = lanes compare their own 32-byte stretches (the HBM step's
+// loads compared straight from registers); 1 = coalesced 16-byte lanes through the LDS copy.
+#ifndef WALK_LCE_V
+#define WALK_LCE_V 0
+#endif
+#if WALK_LCE_V == 0
+// longest common extension of R[a..] and T[b..], at most maxlen bytes (extend_alignment,
+// compression.cpp:27-34); whole wave.  First from the LDS copy when both starts lie in it (2 KiB
+// per pass); then from HBM, LBV bytes per round trip (lanes 0-3 load the LEAD bytes before the
+// stretch compared), every HBM step leaving its bytes in the copy.
+__device__ __forceinline__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a, int32_t b, int32_t maxlen) {
+    const int lane = lane_id();
+    if (maxlen <= 0) return 0;
+    int32_t off = 0;
+    if (a >= B.rb0 && b >= B.tb0 && a < B.rb0 + LBV && b < B.tb0 + LBV) {
+        int32_t avail = B.rb0 + LBV - a < B.tb0 + LBV - b ? B.rb0 + LBV - a : B.tb0 + LBV - b;
+        if (avail > maxlen) avail = maxlen;
+        for (int32_t base = 0; base < avail; base += 2048) {
+            const int32_t my = base + 32 * lane;
+            int32_t e = INT32_MAX;
+            if (my < avail) {
+                uint32_t r[8], t[8];
+                loadw_lds<8>(L.rbuf, a - B.rb0 + my, r);
+                loadw_lds<8>(L.tbuf, b - B.tb0 + my, t);
+                int pos = first_diff32(r, t);
+                if (avail - my < 32 && pos >= avail - my) pos = avail - my == maxlen - my ? avail - my : 32;
+                if (pos < 32) e = my + pos;
+            }
+            const unsigned long long sm = __ballot(e != INT32_MAX);
+            if (sm) {
+                const int32_t m = lane_val(e, first_lane(sm));
+                return m < maxlen ? m : maxlen;
+            }
+        }
+        if (avail >= maxlen) return maxlen;
+        off = avail;
+    }
+    while (off < maxlen) {
+        const int32_t lead = (a + off >= LEAD && b + off >= LEAD) ? LEAD : 0;
+        const int32_t sa = a + off - lead, sb = b + off - lead;
+        uint32_t r[LBW], t[LBW];
+        loadw<LBW>(A.R + sa + 4 * LBW * lane, r);
+        loadw<LBW>(A.T + sb + 4 * LBW * lane, t);
+        wave_sync();   // the copy's previous readers are done
+        {
+            uint4* dr = reinterpret_cast<uint4*>(L.rbuf) + (LBW / 4) * lane;
+            uint4* dt = reinterpret_cast<uint4*>(L.tbuf) + (LBW / 4) * lane;
+#pragma unroll
+            for (int i = 0; i < LBW / 4; i++) {
+                dr[i] = make_uint4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+                dt[i] = make_uint4(t[4 * i], t[4 * i + 1], t[4 * i + 2], t[4 * i + 3]);
+            }
+        }
+        wave_sync();
+        B.rb0 = sa;
+        B.tb0 = sb;
+        const int32_t rel = 4 * LBW * lane - lead;   // this lane's bytes, from a + off
+        int32_t e = INT32_MAX;
+        if (rel >= 0 && rel < maxlen - off) {   // (LEAD is whole lanes' stretches: no lane straddles a + off)
+            int pos = first_diff<LBW>(r, t);
+            const int32_t lim = maxlen - off - rel;
+            if (lim < 4 * LBW && pos > lim) pos = lim;
+            if (pos < 4 * LBW) e = off + rel + pos;
+        }
+        const unsigned long long sm = __ballot(e != INT32_MAX);
+        if (sm) {
+            const int32_t m = lane_val(e, first_lane(sm));
+            return m < maxlen ? m : maxlen;
+        }
+        off += LBV - lead;
+    }
+    return maxlen;
+}
+
+#else
+// 16 bytes at byte offset off + 16 lane of an LDS byte array (off lane-uniform): three 8-byte reads
+// from the 8-byte aligned base below and one alignment for the whole wave (lane stride 16 bytes:
+// ds_read_b64 spreads a lane group over all 64 banks but for one pair -- a 32-byte lane stride,
+// as before, put 16 lanes on two banks).  The walk is VALU-bound (~500 VALU per match step on
+// chr1): 16 bytes per lane and pass cost about half the instructions of 4-byte reads.
+__device__ __forceinline__ void lds16(const uint8_t* lds, int32_t off, uint32_t (&o)[4]) {
+    const int32_t a = off + 16 * lane_id();
+    const uint2* p = reinterpret_cast<const uint2*>(lds + (a & ~7));
+    const uint2 v0 = p[0], v1 = p[1], v2 = p[2];
+    const uint32_t sh = (uint32_t)(off & 3);
+    uint32_t w[5];
+    if (off & 4) { w[0] = v0.y; w[1] = v1.x; w[2] = v1.y; w[3] = v2.x; w[4] = v2.y; }
+    else { w[0] = v0.x; w[1] = v0.y; w[2] = v1.x; w[3] = v1.y; w[4] = v2.x; }
+#pragma unroll
+    for (int i = 0; i < 4; i++) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
 
 // first differing byte of R-copy[ra..] and T-copy[tb..] within [0, n) (n when none); whole wave,
-// 1 KiB per pass, lane l holding the bytes at 4l + 256i of the pass (i < LCE_NI)
-constexpr int LCE_NI = 4;
+// 1 KiB per pass, lane l holding the 16 bytes at 16 l of the pass
 __device__ __forceinline__ int32_t lds_first_diff(const uint8_t* rbuf, int32_t ra, const uint8_t* tbuf, int32_t tb, int32_t n) {
     const int lane = lane_id();
-    for (int32_t base = 0; base < n; base += 256 * LCE_NI) {
-        uint32_t x[LCE_NI];
-#pragma unroll
-        for (int i = 0; i < LCE_NI; i++) {
-            const int32_t pos = base + 256 * i + 4 * lane;
-            const int32_t lim = n - pos;   // bytes of this word inside the range
-            x[i] = 0;
-            if (lim > 0) {
-                x[i] = lds4(rbuf, ra + pos) ^ lds4(tbuf, tb + pos);
-                if (lim < 4) x[i] &= (1u << (8 * lim)) - 1u;
-            }
+    for (int32_t base = 0; base < n; base += 1024) {
+        const int32_t lim = n - base - 16 * lane;   // bytes of this lane's 16 inside the range
+        int e = 16;
+        if (lim > 0) {
+            uint32_t r[4], t[4];
+            lds16(rbuf, ra + base, r);
+            lds16(tbuf, tb + base, t);
+            e = first_diff<4>(r, t);
+            if (e >= lim) e = 16;
         }
-#pragma unroll
-        for (int i = 0; i < LCE_NI; i++) {
-            const unsigned long long m = __ballot(x[i] != 0);
-            if (m) {
-                const int l = first_lane(m);
-                return base + 256 * i + 4 * l + (__builtin_ctz(lane_val(x[i], l)) >> 3);
-            }
+        const unsigned long long m = __ballot(e < 16);
+        if (m) {
+            const int l = first_lane(m);
+            return base + 16 * l + lane_val(e, l);
         }
     }
     return n;
@@ -394,6 +473,8 @@ __device__ __forceinline__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPo
     }
     return maxlen;
 }
+
+#endif   // WALK_LCE_V
 
 // the same from HBM only (no copy kept; 2 KiB per round trip)
 __device__ int32_t wave_lce_hbm(const uint8_t* __restrict__ R, int32_t a, const uint8_t* __restrict__ T, int32_t b,
@@ -1086,14 +1167,14 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
 // pending list, no longer depend on which block committed first -- the rounds are the same on every
 // run.  One block, bitonic sort in LDS; a list longer than FSORT_CAP stays as it is (exact either way).
 constexpr int FSORT_CAP = 4096;
-__global__ __launch_bounds__(1024) void k_flist_sort(WalkPtrs A) {
-    if (A.scal[9]) return;
+__global__ __launch_bounds__(1024) void k_list_sort(WalkPtrs A, int32_t* __restrict__ list, const int32_t* __restrict__ count) {
+    if (A.scal[9] || !A.lsort) return;
     __shared__ int32_t sb[FSORT_CAP];
-    const int nf = A.scal[5];
+    const int nf = *count;
     if (nf <= 1 || nf > FSORT_CAP) return;
     int np = 2;
     while (np < nf) np <<= 1;
-    for (int i = (int)threadIdx.x; i < np; i += (int)blockDim.x) sb[i] = i < nf ? A.flist[i] : INT32_MAX;
+    for (int i = (int)threadIdx.x; i < np; i += (int)blockDim.x) sb[i] = i < nf ? list[i] : INT32_MAX;
     __syncthreads();
     for (int k = 2; k <= np; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
@@ -1107,7 +1188,7 @@ __global__ __launch_bounds__(1024) void k_flist_sort(WalkPtrs A) {
             __syncthreads();
         }
     }
-    for (int i = (int)threadIdx.x; i < nf; i += (int)blockDim.x) A.flist[i] = sb[i];
+    for (int i = (int)threadIdx.x; i < nf; i += (int)blockDim.x) list[i] = sb[i];
 }
 
 // Frozen chunks (committed fix-ups that ended in a long literal run with P unchanged up to their
@@ -1837,7 +1918,8 @@ __device__ __forceinline__ bool anchor_hit(const WalkPtrs& A, uint64_t key, uint
     return (v >> 32) == (anchor_slot(A, key, 0) >> 32) && (uint32_t)v != A_MULTI;
 }
 __device__ __forceinline__ void anchor_put(const WalkPtrs& A, uint64_t key, uint32_t pos) {
-    atomicMax((unsigned long long*)&A.atab[key >> (64 - A.abits)], (unsigned long long)anchor_slot(A, key, pos));
+    if (A.adet) atomicMax((unsigned long long*)&A.atab[key >> (64 - A.abits)], (unsigned long long)anchor_slot(A, key, pos));
+    else A.atab[key >> (64 - A.abits)] = anchor_slot(A, key, pos);   // (SCCG_ANCHOR_DET=0: last writer wins)
 }
 
 // pass 1 (mark = false): store every sample; pass 2 (mark = true): flag repeated 32-mers
@@ -2717,6 +2799,9 @@ WalkKernel walk_kernel(const WalkPtrs& A) { return A.dbg ? k_walk<true, false> :
 // (chunks past that stay pending for the next round, as without carrying)
 constexpr int CARRY_GRID = 256;
 int launch_carry(const WalkPtrs& A, hipStream_t s) {
+    // the carry candidates in chunk order: which ones the CARRY_GRID waves take when there are more
+    // is then the same on every run
+    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(1024), 0, s, A, A.clist, (const int32_t*)(A.scal + 11));
     PROF_LAUNCH(PROF_WALK_CARRY, s, (A.dbg ? k_walk<true, true> : k_walk<false, true>), dim3(CARRY_GRID), dim3(64 * WWPB), 0, s, A,
                 (const int32_t*)A.clist, 0, (const int32_t*)(A.scal + 11));
     SCCG_HIP(hipGetLastError());
@@ -2972,6 +3057,11 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
         return e ? atoi(e) : STALE_BUDGET_DEFAULT;
     }();
     A.stale_budget = sb;
+    // (SCCG_ANCHOR_DET=1: atomicMax slots -- the same votes on every run, but the genome bench's
+    // sweep took +1.2 ms per step for the read-modify-writes, and the rounds still vary with the
+    // chains' timing-dependent generations; off by default)
+    A.adet = env_int("SCCG_ANCHOR_DET", 0);
+    A.lsort = env_int("SCCG_LIST_SORT", 1);
     static const int32_t ug = getenv("SCCG_UNGUESSED_SPEC") != nullptr;
     A.unguessed_spec = ug;
     return A;
@@ -3130,7 +3220,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         if (dev_nlist) RC(launch_carry(A, s));
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
-        hipLaunchKernelGGL(k_flist_sort, dim3(1), dim3(1024), 0, s, A);
+        hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(1024), 0, s, A, A.flist, (const int32_t*)(A.scal + 5));
         if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, fbase_cap), dim3(FZ_T), 0, s, A, 0);
         SCCG_HIP(hipGetLastError());
         RC(launch_round_end(A, 0, fbase_cap, s));
@@ -3372,7 +3462,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                     // (pn2 == 0) ones are handled after the batch's one sync.
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(gl, 256) > 4096 ? 4096 : grid_for(gl, 256)), dim3(256), 0, s, A,
                                        (const int32_t*)A.plist, gl, dev ? (const int32_t*)A.scal : (const int32_t*)nullptr);
-                    hipLaunchKernelGGL(k_flist_sort, dim3(1), dim3(1024), 0, s, A);
+                    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(1024), 0, s, A, A.flist, (const int32_t*)(A.scal + 5));
                     if (b + 1 < batch) {   // a whole round; the last one's end is queued below
                         hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, FROZEN_FIRST), dim3(FZ_T), 0, s, A, 0);
                         RC(launch_round_end(A, 0, FROZEN_FIRST, s));
@@ -3433,7 +3523,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                     RC(dev_set_i32(A.scal + 5, 1, {0}, s));   // frozen list of the resumed chunks
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(nr, 256) > 4096 ? 4096 : grid_for(nr, 256)), dim3(256), 0, s, A,
                                        (const int32_t*)A.rlist, nr, (const int32_t*)nullptr);
-                    hipLaunchKernelGGL(k_flist_sort, dim3(1), dim3(1024), 0, s, A);
+                    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(1024), 0, s, A, A.flist, (const int32_t*)(A.scal + 5));
                     SCCG_HIP(hipGetLastError());
                 }
                 {

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build a variant of libsccg.so with extra compiler flags on every source:
-#   variants/build_flags.sh <name> <flags...>   -> variants/<name>/libsccg.so
+#   sccg-genome-compression_amd/tools/ab/build_flags.sh <name> <flags...>   -> variants/<name>/libsccg.so
 set -eo pipefail
 NAME=$1; shift
 PKG=sccg-genome-compression_amd

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build a variant of libsccg.so for A/B runs: variants/build_variant.sh <name> [walk.hip source] [extra hipcc flags...]
+# Build a variant of libsccg.so for A/B runs: sccg-genome-compression_amd/tools/ab/build_variant.sh <name> [walk.hip source] [extra hipcc flags...]
 # (objects other than walk.hip are the in-tree ones; output variants/<name>/libsccg.so)
 set -eo pipefail
 NAME=$1; SRC=${2:-sccg-genome-compression_amd/csrc/walk.hip}; shift 2 || shift $#

@@ -154,7 +154,7 @@ def test_chr1_roundtrip(ctx):
     assert ctx.reconstruct(rec, rfa) == tfa
 
 
-def _switch_case(seed: int, nseg: int = 2400):
+def _switch_case(seed: int, nseg: int = 2400, plant_at: int | None = None):
     """Segment-kind patterns for the local->global switch (compression.cpp:462-473): identical
     segments (good), unrelated random ones (failed or mostly literal), half-copied ones (matched
     but > 50 % literal), all-N ones (failed, all N: resets the counter) and poly-A ones (failed,
@@ -172,7 +172,7 @@ def _switch_case(seed: int, nseg: int = 2400):
         n = int(rng.integers(1, 4))   # bursts too short to switch on their own ...
         kinds[i:i + n] = rng.choice([1, 2, 3, 4], size=min(n, max(0, nseg - i)))
         i += n
-    plant = [None, 4, 5, 9, 63, 64, 65, 1000, 4095, nseg - 1][seed % 10]
+    plant = [None, 4, 5, 9, 63, 64, 65, 1000, 4095, nseg - 1][seed % 10] if plant_at is None else plant_at
     if plant is not None and plant < nseg:
         kinds[max(0, plant - 4):plant + 1] = rng.choice([1, 2, 4], size=min(plant + 1, 5))   # ... but this one
         kinds[plant] = 4
@@ -436,3 +436,41 @@ def test_strip_run_events_vs_oracle(ctx, case, seed):
     want = oraclelib.compress(rfa, tfa)
     got, rc = _gpu_compress(ctx, rfa, tfa)
     assert (rc, got) == (0, want)
+
+
+def test_walk_rounds_deterministic(ctx, monkeypatch):
+    """With deterministic anchor slots (SCCG_ANCHOR_DET=1: atomicMax) and the frozen / carry lists and
+    trapped triggers in chunk order, a T2T-like pair (frozen and trapped stretches, many rounds) takes
+    the same number of rounds and chains in every call, in this context and in a fresh one, and the
+    record equals the oracle's."""
+    monkeypatch.setenv("SCCG_ANCHOR_DET", "1")
+    rfa, tfa = synthlib.synth_pair("t2t", 12_000_000, 12_000_000, 91)
+    got, rounds = None, set()
+    for _ in range(3):
+        rec = ctx.compress(rfa, tfa)
+        st = ctx.stats()
+        rounds.add((st["walk_rounds"], st["walk_chains"]))
+        got = got or rec
+        assert rec == got
+    with sccg.Context(0) as c2:
+        assert c2.compress(rfa, tfa) == got
+        st = c2.stats()
+        rounds.add((st["walk_rounds"], st["walk_chains"]))
+    assert len(rounds) == 1, rounds
+    assert got == oraclelib.compress(rfa, tfa)
+
+
+@pytest.mark.parametrize("plant", [16382, 16386, 16900, None])
+def test_switch_across_scan_windows_vs_oracle(ctx, plant):
+    """The windowed switch scan (16 Ki segments, then 48 Ki, ...): a switch window wholly inside the
+    first window, one straddling its end, one in the second window, and a pair that stays local
+    (every proved segment's records computed afterwards) -- against the oracle's state machine."""
+    rfa, tfa = _switch_case(700 + (plant or 0) % 97, nseg=17000, plant_at=plant)
+    want = oraclelib.compress(rfa, tfa)
+    mode_global, sw = oraclelib.last_mode()
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert rc == 0
+    st = ctx.stats()
+    assert bool(st["mode_global"]) == mode_global
+    assert st["switch_segment"] == (sw if mode_global else -1)
+    assert got == want
