@@ -537,30 +537,27 @@ __device__ __forceinline__ int32_t seg_count(int64_t nR, int64_t nT) {
 #ifndef LOCAL_WAVES_PER_EU
 #define LOCAL_WAVES_PER_EU 4   // the LDS allows 4 waves/SIMD (4 blocks of SegLds x 4); VGPRs must fit 128
 #endif
-// list (optional): walk only list[0 .. *cnt) (increasing segment order), the segments the windowed
-// pass could not settle by proof (k_local_prove / k_local_list); null: every segment.
+// prove: each segment is first tried by the class-0 proof (seg_prove); a proved segment publishes
+// class 0 without its records (PASS_PROVEN: a pair that stays local computes them afterwards,
+// launch_local_proven) -- only the switch scan of a pair that goes global skips its walk.
 template <bool DBG>
 __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_all(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
                                                           const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
                                                           uint32_t* __restrict__ recs, SegStat* __restrict__ stat,
                                                           int32_t* __restrict__ cls, int32_t gen, int32_t* __restrict__ ctl,
-                                                          int prove, const int32_t* __restrict__ list,
-                                                          const int32_t* __restrict__ cnt) {
+                                                          int prove) {
     __shared__ SegLds lds_all[WPB];
     const int64_t nR = *dnR, nT = *dnT;
     const int32_t nseg = seg_count(nR, nT);
     const int w = wave_in_block(), lane = lane_id();
     SegLds& L = lds_all[w];
     const int32_t G = (int32_t)gridDim.x * WPB;
-    const int32_t nitem = list ? *cnt : nseg;
-    auto item = [&](int32_t i) { return list ? uni(list[i]) : i; };
     SegWords cur, nxt;
-    int32_t it = (int32_t)blockIdx.x * WPB + w;
-    if (it < nitem) seg_words_load(cur, item(it), R, nR, T, nT);
-    for (; it < nitem; it += G) {
-        const int32_t seg = item(it);
+    int32_t seg = (int32_t)blockIdx.x * WPB + w;
+    if (seg < nseg) seg_words_load(cur, seg, R, nR, T, nT);
+    for (; seg < nseg; seg += G) {
         if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
-        if (it + G < nitem) seg_words_load(nxt, item(it + G), R, nR, T, nT);   // in flight during this segment
+        if (seg + G < nseg) seg_words_load(nxt, seg + G, R, nR, T, nT);   // in flight during this segment
         const bool non_n = seg_load(L, seg, 1, R, nR, T, nT, &cur);
         SegStat st;
         int c;
@@ -602,113 +599,6 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
         wave_sync();   // the next segment reuses this wave's LDS
         cur = nxt;
     }
-}
-
-// ---- the windowed switch scan.  The first switch (compression.cpp:462-473) is the first class-2
-// segment whose 4 predecessors are class 1 or 2, so a segment proved class 0 (seg_prove) breaks
-// every window it lies in, and a segment that is not proved matters only inside a run of >= 5
-// unproved segments.  Per window of segments: k_local_prove proves every segment it can (one wave
-// per segment pair, no hashing, no walk) and publishes class 0; k_local_list lists, in segment
-// order, the unproved segments that lie in such a run; k_local_all walks only those.  A window
-// past an earlier window's switch returns at once.  Every segment's SegStat says PASS_PROVEN
-// ("records not computed") unless it was walked: a pair that stays local computes them afterwards
-// (launch_local_proven).  k_switch_final then finds the exact first switch as before (a segment
-// never walked and never proved is published as no class, which no switch window holds).
-struct ProveLds {
-    uint8_t r[SEGB];
-    uint8_t t[SEGB];
-};
-__global__ __launch_bounds__(SCCG_BLOCK) void k_local_prove(const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR,
-                                                            const uint8_t* __restrict__ T, const int64_t* __restrict__ dnT,
-                                                            int32_t w0, int32_t w1, SegStat* __restrict__ stat,
-                                                            int32_t* __restrict__ cls, int32_t* __restrict__ prv, int32_t gen,
-                                                            const int32_t* __restrict__ ctl) {
-    __shared__ ProveLds lds_all[WPB];
-    const int64_t nR = *dnR, nT = *dnT;
-    const int32_t nseg = seg_count(nR, nT);
-    const int32_t end = w1 < nseg ? w1 : nseg;
-    if (w0 >= end || w0 > __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    const int w = wave_in_block(), lane = lane_id();
-    ProveLds& L = lds_all[w];
-    const int32_t G = (int32_t)gridDim.x * WPB;
-    for (int32_t seg = w0 + (int32_t)blockIdx.x * WPB + w; seg < end; seg += G) {
-        const int64_t base = (int64_t)seg * SEG_L;
-        const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L), nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
-        const uint32_t* R4 = reinterpret_cast<const uint32_t*>(R + base);
-        const uint32_t* T4 = reinterpret_cast<const uint32_t*>(T + base);
-        uint32_t* r4 = reinterpret_cast<uint32_t*>(L.r);
-        uint32_t* t4 = reinterpret_cast<uint32_t*>(L.t);
-        bool non_n = false;
-        uint32_t rw[SEGB / 256], tw[SEGB / 256];
-#pragma unroll
-        for (int j = 0; j < SEGB / 256; j++) {   // (all loads first)
-            const int i = lane + 64 * j, b0 = 4 * i;
-            rw[j] = b0 < nr ? R4[i] : 0u;
-            tw[j] = b0 < nt ? T4[i] : 0u;
-        }
-        wave_sync();   // (the previous segment's readers are done)
-#pragma unroll
-        for (int j = 0; j < SEGB / 256; j++) {
-            const int i = lane + 64 * j, b0 = 4 * i;
-            if (nr - b0 < 4) rw[j] &= nr - b0 <= 0 ? 0u : (1u << (8 * (nr - b0))) - 1u;
-            if (nt - b0 < 4) tw[j] &= nt - b0 <= 0 ? 0u : (1u << (8 * (nt - b0))) - 1u;
-            r4[i] = upper4(rw[j]);
-            t4[i] = upper4(tw[j]);
-#pragma unroll
-            for (int q = 0; q < 4; q++) non_n |= (b0 + q < nt && (uint8_t)(t4[i] >> (8 * q)) != 'N');
-        }
-        non_n = __ballot(non_n) != 0;
-        wave_sync();
-        const bool ok = seg_prove(L.r, L.t, nr, nt);
-        if (lane == 0) {
-            stat[seg] = SegStat{0, 0, 0, PASS_PROVEN, (int)non_n, -1, -1, nt};
-            prv[seg] = ok ? gen : 0;
-            if (ok) __hip_atomic_store(&cls[seg], gen << 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// One block: the window's segments that must be walked -- not proved, and inside a run of >= 5
-// segments none of which is proved (segments past the window count as not proved) -- in order.
-constexpr int LIST_T = 1024;
-__global__ __launch_bounds__(LIST_T) void k_local_list(const int64_t* __restrict__ dnR, const int64_t* __restrict__ dnT,
-                                                       int32_t w0, int32_t w1, const int32_t* __restrict__ prv, int32_t gen,
-                                                       int32_t* __restrict__ list, int32_t* __restrict__ cnt,
-                                                       const int32_t* __restrict__ ctl) {
-    __shared__ int32_t wsum[LIST_T / 64 + 1];
-    const int32_t nseg = seg_count(*dnR, *dnT);
-    const int32_t end = w1 < nseg ? w1 : nseg;
-    const bool live = w0 < end && w0 <= __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int32_t n = live ? end - w0 : 0;
-    const int32_t per = (n + LIST_T - 1) / LIST_T;
-    const int32_t s0 = w0 + (int32_t)threadIdx.x * per, s1 = s0 + per < end ? s0 + per : end;
-    auto unproved = [&](int32_t q) -> bool {   // (q past the window: its proof has not run yet)
-        return q >= 0 && q < nseg && (q >= end || prv[q] != gen);
-    };
-    // need(s): s unproved and some run [a, a + 4] with a <= s <= a + 4 fully unproved
-    int c = 0;
-    auto need = [&](int32_t sgm) -> bool {
-        if (!unproved(sgm)) return false;
-        int back = 0, fwd = 0;
-        for (int32_t q = sgm - 1; q >= sgm - 4 && unproved(q); q--) back++;
-        for (int32_t q = sgm + 1; q <= sgm + 4 && unproved(q); q++) fwd++;
-        return back + fwd + 1 >= 5;
-    };
-    for (int32_t q = s0; q < s1; q++) c += need(q);
-    const int incl = wave_incl_add(c);
-    const int w = wave_in_block(), lane = lane_id();
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int i = 0; i < LIST_T / 64; i++) { const int t = wsum[i]; wsum[i] = acc; acc += t; }
-        wsum[LIST_T / 64] = acc;
-    }
-    __syncthreads();
-    int at = wsum[w] + incl - c;
-    for (int32_t q = s0; q < s1; q++)
-        if (need(q)) list[at++] = q;
-    if (threadIdx.x == 0) *cnt = wsum[LIST_T / 64];
 }
 
 __global__ void k_switch_final(const int32_t* __restrict__ cls, int32_t gen, const int64_t* __restrict__ dnR,
@@ -881,7 +771,6 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
     return 0;
 }
 
-constexpr int64_t LOCAL_WIN0 = 16384;
 // SCCG_LOCAL_PROVE=0: every segment walks (A/B runs and tests of the proof)
 int local_prove() {
     static const int v = [] { const char* e = getenv("SCCG_LOCAL_PROVE"); return e ? atoi(e) != 0 : 1; }();
@@ -897,8 +786,7 @@ int launch_local_proven(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t 
 }
 
 int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
-                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s, int32_t* prv,
-                     int32_t* list, int32_t* cnt) {
+                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s) {
     if (nseg_max <= 0) return 0;
     // resident capacity: the grid drains the counter, extra blocks would only find it exhausted
     static const unsigned cap = [] {
@@ -924,7 +812,7 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
         const unsigned long long z[16] = {};
         SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_local_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl, local_prove(), (const int32_t*)nullptr, (const int32_t*)nullptr);
+                    gen, ctl, local_prove());
         unsigned long long d[16];
         SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_local_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
         SCCG_HIP(hipStreamSynchronize(s));
@@ -934,22 +822,9 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
                 " | max %.2f (seg %llu, %llu matches: load %.2f keys %.2f insert %.2f hits %.2f walk %.2f)\n", d[5],
                 d[0] / n / 100, d[1] / n / 100, d[2] / n / 100, d[3] / n / 100, d[4] / n / 100, d[6] / 100.0, d[13], d[14],
                 d[8] / 100.0, d[9] / 100.0, d[10] / 100.0, d[11] / 100.0, d[12] / 100.0);
-    } else if (local_prove() && prv && list && cnt) {
-        // windows of 16 Ki, 48 Ki, 144 Ki ... segments: the switch of an hg-like pair lies in the first
-        // (chr1 at segment 10,980); later windows then return at once
-        for (int64_t w0 = 0, wsz = LOCAL_WIN0; w0 < nseg_max; w0 += wsz, wsz *= 3) {
-            const int64_t w1 = w0 + wsz < nseg_max ? w0 + wsz : nseg_max;
-            const unsigned gp = grid_for(w1 - w0, WPB) > 8192 ? 8192 : grid_for(w1 - w0, WPB);
-            PROF_LAUNCH(PROF_LOCAL14, s, k_local_prove, dim3(gp), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, (int32_t)w0,
-                        (int32_t)w1, stat, cls, prv, gen, (const int32_t*)ctl);
-            hipLaunchKernelGGL(k_local_list, dim3(1), dim3(LIST_T), 0, s, d_nR, d_nT, (int32_t)w0, (int32_t)w1,
-                               (const int32_t*)prv, gen, list, cnt, (const int32_t*)ctl);
-            PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat,
-                        cls, gen, ctl, 0, (const int32_t*)list, (const int32_t*)cnt);
-        }
     } else {
         PROF_LAUNCH(PROF_LOCAL14, s, k_local_all<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, R, d_nR, T, d_nT, recs, stat, cls,
-                    gen, ctl, 0, (const int32_t*)nullptr, (const int32_t*)nullptr);
+                    gen, ctl, local_prove());
     }
     if (nseg_max > 4) {
         const unsigned gs = grid_for(nseg_max - 4, 256) > 2048 ? 2048 : grid_for(nseg_max - 4, 256);

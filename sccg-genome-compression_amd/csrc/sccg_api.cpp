@@ -58,8 +58,6 @@ enum Slot {
     B_D_TOK, B_D_BTOK,
     // the target strip's run-event slots (RunSlots) and the run arrays' per-tile scratch
     B_RSLOT, B_RTILE,
-    // the local pass's walk list (windowed switch scan)
-    B_SEGLIST, B_SEGPRV,
     B_COUNT
 };
 
@@ -156,8 +154,6 @@ struct sccg_ctx {
     void* cls_buf = nullptr;   // local segment classes: buffer the generation tags refer to
     size_t cls_cap = 0;
     int32_t cls_gen = 0;
-    void* prv_buf = nullptr;   // the proofs' buffer (zeroed with cls_buf)
-    size_t prv_cap = 0;
 
     int fail(int rc, const char* fmt, ...) {
         char tmp[512];
@@ -562,10 +558,6 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     GET(uint32_t, recs, B_RECS, (iters_max > 0 ? iters_max : 1) * SEG_REC_CAP);
     GET(SegStat, stat, B_STAT, iters_max > 0 ? iters_max : 1);
     GET(int32_t, cls, B_SEGCLS, iters_max > 0 ? iters_max : 1);
-    // the windowed switch scan: proofs (generation-tagged like cls, in a buffer of their own: a stale
-    // class word must never read as a proof), the walk list and its length
-    GET(int32_t, prv, B_SEGPRV, iters_max > 0 ? iters_max : 1);
-    GET(int32_t, seglist, B_SEGLIST, (iters_max > 0 ? iters_max : 1) + 16);
     int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
     // Where the local pass goes.  It fills every CU while it runs (LDS and VGPRs), but only the final
     // record text needs it; the global walk (side stream) is the critical path of a switching pair.
@@ -581,20 +573,16 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
             HIPTRY(hipStreamWaitEvent(s, ctx->ev_fork2, 0));
         }
         if (iters_max > 0 && !force_global) {
-        if (cls != ctx->cls_buf || ctx->cap[B_SEGCLS] != ctx->cls_cap || prv != ctx->prv_buf ||
-            ctx->cap[B_SEGPRV] != ctx->prv_cap || ctx->cls_gen >= (1 << 28)) {
-            // new buffers (or tags about to wrap): zero them once, so no stale tag can match
+        if (cls != ctx->cls_buf || ctx->cap[B_SEGCLS] != ctx->cls_cap || ctx->cls_gen >= (1 << 28)) {
+            // a new buffer (or tags about to wrap): zero it once, so no stale tag can match
             HIPTRY(hipMemsetAsync(cls, 0, ctx->cap[B_SEGCLS], s));
-            HIPTRY(hipMemsetAsync(prv, 0, ctx->cap[B_SEGPRV], s));
             ctx->cls_buf = cls;
             ctx->cls_cap = ctx->cap[B_SEGCLS];
-            ctx->prv_buf = prv;
-            ctx->prv_cap = ctx->cap[B_SEGPRV];
             ctx->cls_gen = 0;
         }
         const int32_t gen = ++ctx->cls_gen;
         // one launch over every segment; segments past a detected switch are never started
-        TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, s, prv, seglist + 1, seglist));
+        TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, s));
         }
         return 0;
     };
@@ -1390,8 +1378,14 @@ int sccg_walk_range_device(sccg_ctx* ctx, const void* d_ref, size_t nr, const vo
     memset(out, 0, sizeof *out);
     HIPTRY(hipSetDevice(ctx->device));
     global_prepare_reset();   // buffers shared with compress: never reuse its preparation
-    return walk_range_dev(ctx, (const uint8_t*)d_ref, (int64_t)nr, (const uint8_t*)d_tgt, (int64_t)nt, k, m, x0, P0, x_end,
-                          out, exit_state, stream ? (hipStream_t)stream : ctx->stream);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    // the walk reads up to 4 KiB past both sequences (whole-wave compares, prefetches): it runs on
+    // context copies with that slack, not on the caller's buffers
+    GET(uint8_t, R, B_RP, nr + 64);
+    GET(uint8_t, T, B_TP, nt + 64);
+    if (nr) HIPTRY(hipMemcpyAsync(R, d_ref, nr, hipMemcpyDeviceToDevice, s));
+    if (nt) HIPTRY(hipMemcpyAsync(T, d_tgt, nt, hipMemcpyDeviceToDevice, s));
+    return walk_range_dev(ctx, R, (int64_t)nr, T, (int64_t)nt, k, m, x0, P0, x_end, out, exit_state, s);
 }
 
 int sccg_walk_range(sccg_ctx* ctx, const uint8_t* sr, size_t nr, const uint8_t* st, size_t nt, int k, int m, int64_t x0,

@@ -2040,9 +2040,14 @@ __device__ __forceinline__ void sweep_kmers_w(const uint8_t* __restrict__ R, int
                 for (int i = 0; i < 8; i++) { uint32_t d; swar_codes(gw[i], d); bad |= nz_bytes(d) << (4 * i); }
             }
             uint32_t m16 = 0;   // built high position first: shifts by one, no per-bit constants
+            if (!acc) {   // (the usual block: every byte A/C/G/T, every k-mer pure -- no per-position test)
 #pragma unroll
-            for (int st = 15; st >= 0; st--)
-                m16 = (m16 << 1) | (uint32_t)pred((uint32_t)(code >> (2 * st)) & MASK, ((bad >> st) & KM) == 0);
+                for (int st = 15; st >= 0; st--) m16 = (m16 << 1) | (uint32_t)pred((uint32_t)(code >> (2 * st)) & MASK, true);
+            } else {
+#pragma unroll
+                for (int st = 15; st >= 0; st--)
+                    m16 = (m16 << 1) | (uint32_t)pred((uint32_t)(code >> (2 * st)) & MASK, ((bad >> st) & KM) == 0);
+            }
             hits |= (uint64_t)m16 << (16 * g);
         }
         if (p0 + FC_PER_T > npos) hits &= npos - p0 >= 64 ? ~0ull : ((1ull << (npos - p0)) - 1);

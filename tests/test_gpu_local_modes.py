@@ -1,0 +1,64 @@
+"""The local pass with and without its class-0 proof, against the oracle (GPU).
+
+SCCG_LOCAL_PROVE selects how the local controller of compression.cpp:372-481 finds the first
+switch (:462-473): 1 (the default) proves each segment class 0 before walking it, and walks it only
+when the proof fails; a proved segment has no records yet, so a pair that stays local computes
+them afterwards.  0 walks every segment.  The knob is read once per process: each mode runs in a
+child, and the parent compares record bytes, mode and switch segment with the oracle's.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import oraclelib
+from test_gpu_parity import _switch_case
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+pytestmark = pytest.mark.gpu
+
+# (seed, nseg, plant): planted switch windows near the start, deep, at the last segment, and
+# pairs that stay local
+CASES = [(0, 2400, None), (1, 2400, 4), (3, 2400, 9), (7, 2400, 1000), (9, 2400, 2399), (700, 17000, 16386),
+         (701, 17000, None)]
+
+CHILD = r"""
+import hashlib, json, sys
+sys.path.insert(0, HERE)
+import torch
+torch.zeros(1, device=torch.device("cuda", 0))   # torch's HIP runtime before the library context
+from pkg import sccg
+from test_gpu_parity import _switch_case
+out = []
+with sccg.Context(0) as ctx:
+    for seed, nseg, plant in CASES:
+        rfa, tfa = _switch_case(seed, nseg=nseg, plant_at=plant)
+        rec = ctx.compress(rfa, tfa)
+        st = ctx.stats()
+        out.append([hashlib.sha256(rec).hexdigest(), int(st["mode_global"]), int(st["switch_segment"])])
+print(json.dumps(out))
+"""
+
+
+@pytest.fixture(scope="module")
+def want():
+    res = []
+    for seed, nseg, plant in CASES:
+        rfa, tfa = _switch_case(seed, nseg=nseg, plant_at=plant)
+        rec = oraclelib.compress(rfa, tfa)
+        mode_global, sw = oraclelib.last_mode()
+        res.append([hashlib.sha256(rec).hexdigest(), int(mode_global), sw if mode_global else -1])
+    return res
+
+
+@pytest.mark.parametrize("mode", ["0", "1"], ids=["walk_every_segment", "prove_first"])
+def test_local_modes_vs_oracle(want, mode):
+    env = dict(os.environ, SCCG_LOCAL_PROVE=mode)
+    p = subprocess.run([sys.executable, "-c", f"HERE = {HERE!r}\nCASES = {CASES!r}\n" + CHILD], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    got = json.loads(p.stdout.strip().splitlines()[-1])
+    assert got == want

@@ -461,10 +461,11 @@ def test_walk_rounds_deterministic(ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("plant", [16382, 16386, 16900, None])
-def test_switch_across_scan_windows_vs_oracle(ctx, plant):
-    """The windowed switch scan (16 Ki segments, then 48 Ki, ...): a switch window wholly inside the
-    first window, one straddling its end, one in the second window, and a pair that stays local
-    (every proved segment's records computed afterwards) -- against the oracle's state machine."""
+def test_switch_deep_vs_oracle(ctx, plant):
+    """Deep switch windows in a 17,000-segment pair (more segments than the pass has waves in
+    flight: segments past a found switch are skipped, earlier ones finish) and a pair that stays
+    local (every proved segment's records computed afterwards) -- against the oracle's state
+    machine."""
     rfa, tfa = _switch_case(700 + (plant or 0) % 97, nseg=17000, plant_at=plant)
     want = oraclelib.compress(rfa, tfa)
     mode_global, sw = oraclelib.last_mode()
