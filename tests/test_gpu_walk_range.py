@@ -17,10 +17,10 @@ import socket
 import pytest
 import torch.multiprocessing as mp
 
+from pkg import sccg  # (puts the package directory on sys.path first)
 import multigpu
 import oraclelib
 import synthlib
-from pkg import sccg
 
 pytestmark = pytest.mark.gpu
 
