@@ -75,14 +75,14 @@ def survey_alg_bytes(nT: int, nR: int, nRp: int, out: int) -> float:
 
 def design_alg_bytes(tfa: int, rfa: int, nT: int, nR: int, nRp: int, out: int, mode_global: bool) -> float:
     """What this design must move at least, per pair: both FASTA texts read once
-    and their stripped + N-erased copies written (ingest, compression.cpp:181-220, :523-557), T read
-    once for the run lines (:341-368, :527-555), R' read once by the first-step sweep (the exact
-    ungated first step, :64-161 with pme == -1), the walk's 0.5 B per target base,
-    and the record text written.  The local pass (compression.cpp:372-481) is counted only for the
-    segments of a pair that stays local (both segment strings once)."""
+    and their stripped + N-erased copies written (ingest, compression.cpp:181-220, :523-557; the run
+    lines' boundaries, :341-368 and :527-555, come out of the target's strip, so T is not read
+    again for them), R' read once by the first-step sweep (the exact ungated first step, :64-161
+    with pme == -1), the walk's 0.5 B per target base, and the record text written.
+    The local pass (compression.cpp:372-481) is counted only for the segments of a pair that stays
+    local (both segment strings once)."""
     ingest = tfa + rfa + 2.0 * (nT + nR)
-    runs = float(nT)
-    b = ingest + runs + out
+    b = ingest + out
     if mode_global:
         b += nRp + walk_alg_bytes(nT)
     else:
@@ -96,8 +96,8 @@ def kernel_alg_bytes(kernel: str, tot: dict) -> float | None:
         return walk_alg_bytes(tot["target_bases"])
     if kernel == "fasta_strip":          # read the FASTA, write the stripped and the N-erased copies
         return tot["tgt_fa"] + tot["ref_fa"] + 2.0 * (tot["target_bases"] + tot["reference_bases"])
-    if kernel == "run_extract":          # T once
-        return float(tot["target_bases"])
+    if kernel == "run_extract":          # the strip's per-tile run-event counts and flags (12 B per 4 KiB
+        return 12.0 * tot["target_bases"] / 4096.0   # tile; the events themselves are a few bytes per run)
     if kernel == "first_sweep_anchors":  # R' once + one 8-byte anchor slot per 32 reference bases
         return tot["walk_reference_bases"] * (1.0 + 8.0 / 32.0)
     if kernel == "local_segments":       # both segment strings (up to the switch, bounded by all of them)
