@@ -84,13 +84,17 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_reduce(ScanArrays a, int64_
 #define SCCG_SB_T 1024
 #endif
 constexpr int SB_T = SCCG_SB_T, PART_PER = 4;
-template <class Op>
-__global__ __launch_bounds__(SB_T) void k_partials_scan(ScanArrays a, int64_t nb) {
+// A short scan (the usual case: a few dozen tile partials, or a few thousand elements) runs in one
+// wave or a 256-thread block instead: a 1024-thread block needs a CU with 16 free wave slots, and
+// beside another grid (the reconstruction's reference strip) it waited for one -- 72 us of the chr1
+// reconstruction's critical path for a 19-element scan (gpurun_out/r05q/dprof).
+template <class Op, int T = SB_T>
+__global__ __launch_bounds__(T) void k_partials_scan(ScanArrays a, int64_t nb) {
     __shared__ int64_t tmp[17];
     int64_t* __restrict__ partial = a.partial[blockIdx.y];
     int64_t* total = a.total[blockIdx.y];
     int64_t carry = Op::id();
-    for (int64_t base = 0; base < nb; base += SB_T * PART_PER) {
+    for (int64_t base = 0; base < nb; base += T * PART_PER) {
         const int64_t i0 = base + (int64_t)threadIdx.x * PART_PER;
         int64_t v[PART_PER], acc = Op::id();
 #pragma unroll
@@ -137,13 +141,13 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tile_scan(ScanArrays a, int64_t 
 // consecutive elements, reduced 16 at a time (the 16 loads issued together), then re-read
 // (L2-hot) for the prefixes
 constexpr int SMALL_PER = 16, SMALL_MAX = 16384;   // (<= 64 elements per thread at 256 threads)
-template <class Op>
-__global__ __launch_bounds__(SB_T) void k_small_scan(ScanArrays a, int64_t n) {
+template <class Op, int T = SB_T>
+__global__ __launch_bounds__(T) void k_small_scan(ScanArrays a, int64_t n) {
     __shared__ int64_t tmp[17];
     const int64_t* __restrict__ in = a.in[blockIdx.y];
     int64_t* __restrict__ out = a.out[blockIdx.y];
     int64_t* total = a.total[blockIdx.y];
-    const int64_t per = (n + SB_T - 1) / SB_T, base = (int64_t)threadIdx.x * per;
+    const int64_t per = (n + T - 1) / T, base = (int64_t)threadIdx.x * per;
     int64_t acc = Op::id();
     for (int64_t g = 0; g < per; g += SMALL_PER) {
         int64_t v[SMALL_PER];
@@ -177,6 +181,16 @@ int scan_impl(const ScanArrays& a, int m, int64_t n, hipStream_t s) {
             }
         return 0;
     }
+    if (n <= 64 * SMALL_PER) {
+        hipLaunchKernelGGL((k_small_scan<Op, 64>), dim3(1, m), dim3(64), 0, s, a, n);
+        SCCG_HIP(hipGetLastError());
+        return 0;
+    }
+    if (n <= 256 * SMALL_PER) {
+        hipLaunchKernelGGL((k_small_scan<Op, 256>), dim3(1, m), dim3(256), 0, s, a, n);
+        SCCG_HIP(hipGetLastError());
+        return 0;
+    }
     if (n <= SMALL_MAX) {
         hipLaunchKernelGGL(k_small_scan<Op>, dim3(1, m), dim3(SB_T), 0, s, a, n);
         SCCG_HIP(hipGetLastError());
@@ -184,7 +198,9 @@ int scan_impl(const ScanArrays& a, int m, int64_t n, hipStream_t s) {
     }
     const int64_t nb = (n + TILE - 1) / TILE;
     hipLaunchKernelGGL(k_tile_reduce<Op>, dim3((unsigned)nb, m), dim3(SCCG_BLOCK), 0, s, a, n);
-    hipLaunchKernelGGL(k_partials_scan<Op>, dim3(1, m), dim3(SB_T), 0, s, a, nb);
+    if (nb <= 64 * PART_PER) hipLaunchKernelGGL((k_partials_scan<Op, 64>), dim3(1, m), dim3(64), 0, s, a, nb);
+    else if (nb <= 256 * PART_PER) hipLaunchKernelGGL((k_partials_scan<Op, 256>), dim3(1, m), dim3(256), 0, s, a, nb);
+    else hipLaunchKernelGGL(k_partials_scan<Op>, dim3(1, m), dim3(SB_T), 0, s, a, nb);
     hipLaunchKernelGGL(k_tile_scan<Op>, dim3((unsigned)nb, m), dim3(SCCG_BLOCK), 0, s, a, n);
     SCCG_HIP(hipGetLastError());
     return 0;

@@ -74,8 +74,11 @@ int walk_chunk(int64_t target_bytes) {
         return c >= 1024 && c <= (1 << 20) ? c : 0;
     }();
     if (env) return env;
-    const int64_t c = (target_bytes / WALK_CHUNKS_TARGET) & ~int64_t(4095);
-    return (int)(c < WALK_CHUNK_MIN ? WALK_CHUNK_MIN : c > WALK_CHUNK_MAX ? WALK_CHUNK_MAX : c);
+    // (tuning runs: SCCG_WALK_CHUNKS_TARGET / SCCG_WALK_CHUNK_MAX move the size rule)
+    static const int64_t target = [] { const char* e = getenv("SCCG_WALK_CHUNKS_TARGET"); const int64_t v = e ? atoll(e) : 0; return v >= 256 ? v : WALK_CHUNKS_TARGET; }();
+    static const int64_t cmax = [] { const char* e = getenv("SCCG_WALK_CHUNK_MAX"); const int64_t v = e ? atoll(e) : 0; return v >= WALK_CHUNK_MIN && v <= (1 << 20) ? v : (int64_t)WALK_CHUNK_MAX; }();
+    const int64_t c = (target_bytes / target) & ~int64_t(4095);
+    return (int)(c < WALK_CHUNK_MIN ? WALK_CHUNK_MIN : c > cmax ? cmax : c);
 }
 constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide compares, tails)
 

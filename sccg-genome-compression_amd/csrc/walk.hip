@@ -187,7 +187,8 @@ struct WalkPtrs {
     uint64_t* atab;
     uint32_t agen;            // anchor tag generation (one per call)
     int32_t adet;             // anchor slots written with atomicMax (SCCG_ANCHOR_DET, default off)
-    int32_t lsort;            // frozen / carry lists sorted into chunk order (SCCG_LIST_SORT, default on)
+    uint32_t* fbits;          // the round's frozen / carry lists as chunk bitmaps (k_list_sort puts the
+    uint32_t* cbits;          //   lists into chunk order from them and clears them)
     int32_t round;            // walk round of the launch (kernel argument copy)
     int32_t abits;
     const int64_t* dnR;       // early sweep: |R'| in device memory (nR is then only a bound)
@@ -1073,6 +1074,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         if (lane == 0) {
             const int32_t at = atomicAdd(&A.scal[11], 1);
             if (at < A.C) A.clist[at] = j1;
+            atomicOr(&A.cbits[j1 >> 5], 1u << (j1 & 31));
         }
         return;
     } else {
@@ -1158,37 +1160,47 @@ __global__ void k_commit(WalkPtrs A, const int32_t* __restrict__ list, int32_t n
         A.usedX[j] = A.snapX[j];
         A.usedP[j] = A.snapP[j];
         A.seedq[j] = 0;   // a fix-up (with a converged suffix) is a walk from its entry
-        if (A.frozen[j]) A.flist[atomicAdd(&A.scal[5], 1)] = j;
+        if (A.frozen[j]) {
+            A.flist[atomicAdd(&A.scal[5], 1)] = j;
+            atomicOr(&A.fbits[j >> 5], 1u << (j & 31));
+        }
     }
 }
 
-// The round's frozen list in chunk order (k_commit appends in atomic order): which chunks the blind
-// frozen batch (FROZEN_FIRST) and the later batches take, and so the round's fills and the next
-// pending list, no longer depend on which block committed first -- the rounds are the same on every
-// run.  One block, bitonic sort in LDS; a list longer than FSORT_CAP stays as it is (exact either way).
-constexpr int FSORT_CAP = 4096;
-__global__ __launch_bounds__(1024) void k_list_sort(WalkPtrs A, int32_t* __restrict__ list, const int32_t* __restrict__ count) {
-    if (A.scal[9] || !A.lsort) return;
-    __shared__ int32_t sb[FSORT_CAP];
-    const int nf = *count;
-    if (nf <= 1 || nf > FSORT_CAP) return;
-    int np = 2;
-    while (np < nf) np <<= 1;
-    for (int i = (int)threadIdx.x; i < np; i += (int)blockDim.x) sb[i] = i < nf ? list[i] : INT32_MAX;
+// The round's frozen list and carry list in chunk order (k_commit and k_walk append in atomic
+// order, and mark each entry in a chunk bitmap): which chunks the blind frozen batch (FROZEN_FIRST)
+// and the later batches take, which chunks the CARRY_GRID carry waves take, and so the round's
+// fills and the next pending list, no longer depend on which wave appended first -- the rounds are
+// the same on every run, however long the lists.  One block: the bitmap's words in contiguous
+// shares per thread, a block scan of their popcounts, the list rewritten in chunk order, the words
+// cleared for the next round.
+constexpr int LS_T = 256;   // (a block this small starts beside the other context's walk grid)
+__global__ __launch_bounds__(LS_T) void k_list_sort(WalkPtrs A, int32_t* __restrict__ list, const int32_t* __restrict__ count,
+                                                    uint32_t* __restrict__ bits) {
+    if (A.scal[9]) return;
+    __shared__ int32_t wsum[LS_T / 64 + 1];
+    if (*count <= 0) return;   // (nothing appended: no bit set)
+    const int32_t nw = (A.C + 31) >> 5;
+    const int32_t per = (nw + LS_T - 1) / LS_T, w0 = (int32_t)threadIdx.x * per;
+    const int32_t w1 = w0 + per < nw ? w0 + per : nw;
+    int c = 0;
+    for (int32_t w = w0; w < w1; w++) c += __popc(bits[w]);
+    const int incl = wave_incl_add<int>(c);
+    const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    for (int k = 2; k <= np; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = (int)threadIdx.x; i < np; i += (int)blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const int32_t a = sb[i], b = sb[ixj];
-                    if ((a > b) == ((i & k) == 0)) { sb[i] = b; sb[ixj] = a; }
-                }
-            }
-            __syncthreads();
-        }
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int i = 0; i < LS_T / 64; i++) { const int x = wsum[i]; wsum[i] = run; run += x; }
     }
-    for (int i = (int)threadIdx.x; i < nf; i += (int)blockDim.x) list[i] = sb[i];
+    __syncthreads();
+    int at = wsum[wv] + incl - c;
+    for (int32_t w = w0; w < w1; w++) {
+        uint32_t b = bits[w];
+        if (!b) continue;
+        bits[w] = 0;
+        for (; b; b &= b - 1) list[at++] = (w << 5) + __ffs((int)b) - 1;
+    }
 }
 
 // Frozen chunks (committed fix-ups that ended in a long literal run with P unchanged up to their
@@ -1281,6 +1293,17 @@ __global__ void k_walk_init(WalkPtrs A, int32_t startX, int32_t startP) {
         A.trapped[j] = 0;
         A.tflag[j] = 0;
         A.hintY[j] = -1;
+        // (round numbers restart at 1 every call: a previous call's "walked in round r, exit
+        // changed" must not reach k_commit's predecessor test -- the workspace is reused, and
+        // stale values made the rounds vary from call to call)
+        A.walked[j] = 0;
+        A.changed[j] = 0;
+        A.conv[j] = 0;
+        A.frozen[j] = 0;
+    }
+    for (int32_t w = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); w <= A.C / 32; w += (int32_t)(gridDim.x * blockDim.x)) {
+        A.fbits[w] = 0;
+        A.cbits[w] = 0;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.scal[0] = 0; A.scal[1] = 0; A.scal[2] = startX; A.scal[3] = startP;
@@ -2761,6 +2784,7 @@ WalkPtrs carve(void* ws, size_t ws_bytes, const uint8_t* R, int64_t nR, const ui
     A.seedq = c.take<int32_t>(C);
     A.trapped = c.take<int32_t>(C);
     A.frozen = c.take<int32_t>(C); A.flist = c.take<int32_t>(C);
+    A.fbits = c.take<uint32_t>(C / 32 + 1); A.cbits = c.take<uint32_t>(C / 32 + 1);
     A.fy = c.take<int32_t>(FROZEN_MAX);
     A.scal = c.take<int32_t>(16);
     A.trig = c.take<int32_t>(RESPEC_MAX_TRIGGERS);
@@ -2806,7 +2830,7 @@ constexpr int CARRY_GRID = 256;
 int launch_carry(const WalkPtrs& A, hipStream_t s) {
     // the carry candidates in chunk order: which ones the CARRY_GRID waves take when there are more
     // is then the same on every run
-    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(1024), 0, s, A, A.clist, (const int32_t*)(A.scal + 11));
+    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(LS_T), 0, s, A, A.clist, (const int32_t*)(A.scal + 11), A.cbits);
     PROF_LAUNCH(PROF_WALK_CARRY, s, (A.dbg ? k_walk<true, true> : k_walk<false, true>), dim3(CARRY_GRID), dim3(64 * WWPB), 0, s, A,
                 (const int32_t*)A.clist, 0, (const int32_t*)(A.scal + 11));
     SCCG_HIP(hipGetLastError());
@@ -3066,7 +3090,6 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
     // sweep took +1.2 ms per step for the read-modify-writes, and the rounds still vary with the
     // chains' timing-dependent generations; off by default)
     A.adet = env_int("SCCG_ANCHOR_DET", 0);
-    A.lsort = env_int("SCCG_LIST_SORT", 1);
     static const int32_t ug = getenv("SCCG_UNGUESSED_SPEC") != nullptr;
     A.unguessed_spec = ug;
     return A;
@@ -3225,7 +3248,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         if (dev_nlist) RC(launch_carry(A, s));
         hipLaunchKernelGGL(k_commit, dim3(grid_for(A.C, 256) > 4096 ? 4096 : grid_for(A.C, 256)), dim3(256), 0, s, A,
                            (const int32_t*)A.plist, A.C, nd);
-        hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(1024), 0, s, A, A.flist, (const int32_t*)(A.scal + 5));
+        hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(LS_T), 0, s, A, A.flist, (const int32_t*)(A.scal + 5), A.fbits);
         if (fbase_cap > 0) hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, fbase_cap), dim3(FZ_T), 0, s, A, 0);
         SCCG_HIP(hipGetLastError());
         RC(launch_round_end(A, 0, fbase_cap, s));
@@ -3467,7 +3490,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                     // (pn2 == 0) ones are handled after the batch's one sync.
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(gl, 256) > 4096 ? 4096 : grid_for(gl, 256)), dim3(256), 0, s, A,
                                        (const int32_t*)A.plist, gl, dev ? (const int32_t*)A.scal : (const int32_t*)nullptr);
-                    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(1024), 0, s, A, A.flist, (const int32_t*)(A.scal + 5));
+                    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(LS_T), 0, s, A, A.flist, (const int32_t*)(A.scal + 5), A.fbits);
                     if (b + 1 < batch) {   // a whole round; the last one's end is queued below
                         hipLaunchKernelGGL(k_frozen_scan, dim3(FZ_GRID, FROZEN_FIRST), dim3(FZ_T), 0, s, A, 0);
                         RC(launch_round_end(A, 0, FROZEN_FIRST, s));
@@ -3528,7 +3551,7 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                     RC(dev_set_i32(A.scal + 5, 1, {0}, s));   // frozen list of the resumed chunks
                     hipLaunchKernelGGL(k_commit, dim3(grid_for(nr, 256) > 4096 ? 4096 : grid_for(nr, 256)), dim3(256), 0, s, A,
                                        (const int32_t*)A.rlist, nr, (const int32_t*)nullptr);
-                    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(1024), 0, s, A, A.flist, (const int32_t*)(A.scal + 5));
+                    hipLaunchKernelGGL(k_list_sort, dim3(1), dim3(LS_T), 0, s, A, A.flist, (const int32_t*)(A.scal + 5), A.fbits);
                     SCCG_HIP(hipGetLastError());
                 }
                 {
@@ -3540,6 +3563,10 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                 RC(dev_readback(&rs_item, 1, s));
             }
             nlist = rs[0];
+            static const bool round_log = getenv("SCCG_ROUND_LOG") != nullptr;   // (determinism diagnostics)
+            if (round_log)
+                fprintf(stderr, "[round] %lld pending %d esc %d frozen %d chains %lld\n", (long long)round, rs[0], rs[1], rs[5],
+                        (long long)res->chains);
             if (dbg) {
                 SCCG_HIP(hipStreamSynchronize(s));
                 static thread_local auto tprev = std::chrono::steady_clock::now();
