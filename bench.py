@@ -98,8 +98,8 @@ def kernel_alg_bytes(kernel: str, tot: dict) -> float | None:
         return tot["tgt_fa"] + tot["ref_fa"] + 2.0 * (tot["target_bases"] + tot["reference_bases"])
     if kernel == "run_extract":          # the strip's per-tile run-event counts and flags (12 B per 4 KiB
         return 12.0 * tot["target_bases"] / 4096.0   # tile; the events themselves are a few bytes per run)
-    if kernel == "first_sweep_anchors":  # R' once + one 8-byte anchor slot per 32 reference bases
-        return tot["walk_reference_bases"] * (1.0 + 8.0 / 32.0)
+    if kernel == "first_sweep_anchors":  # R' once + one 8-byte anchor slot per 64 reference bases
+        return tot["walk_reference_bases"] * (1.0 + 8.0 / 64.0)
     if kernel == "local_segments":       # both segment strings (up to the switch, bounded by all of them)
         return 2.0 * min(tot["target_bases"], tot["reference_bases"])
     return None

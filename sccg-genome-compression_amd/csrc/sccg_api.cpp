@@ -1086,17 +1086,17 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     }
     HIPTRY(hipEventRecord(ctx->ev_fork2, s));
     HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
-    // the run lines' three launches go first (the host issues launches one at a time) on side2;
-    // the record line's chain, the longer one on genome records (chr1: ~20 us), stays on the main
-    // stream, so the join below waits for an event that has usually fired already (a wait for one
-    // that fires later cost ~13 us in a trace)
+    // The record line's chain (main stream) is the critical one -- its token blocks share the GPU
+    // with the reference strip, ~0.1 ms on chr1 (gpurun_out/r05t/dprof) -- so it is issued first
+    // (the host issues launches one at a time); the run lines' parses follow on side2 and are
+    // joined before the N check.
     DcRuns lr{}, nr{};
     lr.start = ls; lr.len = ll; lr.cum = lc;
     nr.start = ns; nr.len = nlr; nr.cum = nc;
-    TRY(dc_parse_runs2(lower, nlower, &lr, sc + 14, nline, nnl, &nr, sc + 16, lp, flag, dlt, part, d_err, ctx->side2));
-    HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
     TRY(dc_decode_prepare(enc, nenc, lp2, contrib, dlt2, doff, dsum, sc + 9, ctx->ev_rstrip, part2, d_err, sc + 12,
                           s, fused ? &tk : nullptr));
+    TRY(dc_parse_runs2(lower, nlower, &lr, sc + 14, nline, nnl, &nr, sc + 16, lp, flag, dlt, part, d_err, ctx->side2));
+    HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
     // The usual call queues the token fill right behind the N check, before the host knows the
     // decoded length D, into a buffer of the output's capacity (D <= nres < out_cap whenever the

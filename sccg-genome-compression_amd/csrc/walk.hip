@@ -47,7 +47,11 @@ constexpr int ANCHOR_K = 32;
 constexpr int KEY_K = 15;
 constexpr int KMAX = 32;              // largest k the walk takes
 constexpr int KB_COUNT = 32;          // kb: the first k bytes of T' at [0, k), their count at [32, 36)
-constexpr int ANCHOR_STEP_DEFAULT = 32;   // reference sample stride (SCCG_ANCHOR_STEP for tuning runs)
+// Reference sample stride (SCCG_ANCHOR_STEP for tuning runs).  Round 5: 64 instead of 32 -- half the
+// table's scattered 8-byte writes (the early sweep's dominant cost: genome bench 4.0-4.4 -> 2.0 ms
+// of sweep per step, gpurun_out/r05r) and no loss in the walk's speculation (hg genome walk and
+// rounds unchanged; a 256-position vote window still holds ~4 samples of an aligned stretch).
+constexpr int ANCHOR_STEP_DEFAULT = 64;
 constexpr int ANCHOR_LOAD_DEFAULT = 1;    // table slots per sample, rounded up to a power of two (SCCG_ANCHOR_LOAD):
                                           // a 64 MiB table for chr1 stays in the MALL (4 slots/sample: 256 MiB, sweep +40 %)
 #ifndef ANCHOR_PROBE_BATCHES
@@ -1464,7 +1468,10 @@ __global__ __launch_bounds__(RESPEC_T) void k_round_respec(WalkPtrs A) {
     {
         const int32_t per = (A.C + RESPEC_T - 1) / RESPEC_T, c0 = (int32_t)threadIdx.x * per;
         int cnt = 0;
-        for (int32_t q = c0; q < c0 + per && q < A.C; q++) cnt += A.tflag[q] == A.round;
+        // (a trigger must still be pending: a later frozen batch of the same round may have filled it,
+        // and a stale trigger's run would overlap an earlier trigger's -- two waves writing different
+        // guesses into the same chunks made the rounds vary from run to run)
+        for (int32_t q = c0; q < c0 + per && q < A.C; q++) cnt += A.tflag[q] == A.round && A.lround[q] == next;
         const int incl = wave_incl_add<int>(cnt);
         const int w = (int)(threadIdx.x >> 6), lane = lane_id();
         if (lane == 63) wsum[w] = incl;
@@ -1477,7 +1484,7 @@ __global__ __launch_bounds__(RESPEC_T) void k_round_respec(WalkPtrs A) {
         __syncthreads();
         int at = wsum[w] + incl - cnt;
         for (int32_t q = c0; q < c0 + per && q < A.C && at < RESPEC_MAX_TRIGGERS; q++)
-            if (A.tflag[q] == A.round) trig[at++] = q;
+            if (A.tflag[q] == A.round && A.lround[q] == next) trig[at++] = q;
         __syncthreads();
     }
     const int nt = wsum[RESPEC_T / 64] < RESPEC_MAX_TRIGGERS ? wsum[RESPEC_T / 64] : RESPEC_MAX_TRIGGERS;
@@ -2201,8 +2208,9 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_presence(WalkPtrs A, int32_t x0,
 // The usual first step: does the target's first k-mer (x0) occur in R' at all, and the candidate
 // statistics if so.  One key, no tables: a plain compare per reference position, so this sweep
 // runs at streaming speed; k_presence (the general batch search) runs only when it finds nothing.
-// ANCH: the same pass also stores the anchor samples (every 32nd position, astep == 32) -- their
-// 2-bit codes are the words the sweep already packed, so the anchor index costs no extra read of R'.
+// ANCH: the same pass also stores the anchor samples (every 32nd or 64th position, astep 32 / 64)
+// -- their 2-bit codes are the words the sweep already packed, so the anchor index costs no extra
+// read of R'.
 template <bool ANCH>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
     __shared__ CandBest wbest[SCCG_BLOCK / 64];
@@ -2219,10 +2227,11 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_key0(WalkPtrs A, int32_t x0) {
                       },
                       [&](int64_t p0, const uint32_t (&cw)[20], const uint32_t (&dw)[20], uint32_t acc) {
                           if (!ANCH) return;
+                          const int nh = A.astep == 32 ? 2 : 1;   // (samples at p0 and p0 + 32, or p0 only)
 #pragma unroll
                           for (int h = 0; h < 2; h++) {
                               const int64_t p = p0 + 32 * h;
-                              if (p + ANCHOR_K > A.nR) break;
+                              if (h >= nh || p + ANCHOR_K > A.nR) break;
                               uint64_t code = 0;
                               uint32_t bad = 0;
 #pragma unroll
@@ -2316,10 +2325,11 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_sweep_early(WalkPtrs A) {
                   },
                   [&](int64_t p0, const uint32_t (&cw)[20], const uint32_t (&dw)[20], uint32_t acc) {
                       if (!ANCH) return;
+                      const int nh = A.astep == 32 ? 2 : 1;   // (samples at p0 and p0 + 32, or p0 only)
 #pragma unroll
                       for (int h = 0; h < 2; h++) {
                           const int64_t p = p0 + 32 * h;
-                          if (p + ANCHOR_K > nR) break;
+                          if (h >= nh || p + ANCHOR_K > nR) break;
                           uint64_t code = 0;
                           uint32_t bad = 0;
 #pragma unroll
@@ -3062,7 +3072,7 @@ int queue_prepare(WalkPtrs& A, const void* ws, hipStream_t s) {
     RC(anchor_generation(A, ws, s));
     // the usual first step: x0 = 0's own k-mer (statistics land in fc[4..11]); with the default
     // sample stride the same sweep stores the anchor samples
-    const bool fused = A.astep == 32;
+    const bool fused = A.astep == 32 || A.astep == 64;
     if (fused) PROF_LAUNCH(PROF_ANCHOR, s, k_key0<true>, dim3(gsweep), dim3(SCCG_BLOCK), 0, s, A, 0);
     else hipLaunchKernelGGL(k_key0<false>, dim3(gsweep), dim3(SCCG_BLOCK), 0, s, A, 0);
     hipLaunchKernelGGL(k_cand_reduce, dim3(1), dim3(1024), 0, s, A, (int)gsweep, 0);
@@ -3114,7 +3124,7 @@ int global_sweep_early(const uint8_t* Rp, int64_t nRp, const int64_t* d_nRp, con
     RC(set_u64(A.fc + 12, {0, 0}, s));
     hipLaunchKernelGGL(k_first_kmer, dim3(1), dim3(SCCG_BLOCK), 0, s, tgt_fa, tn, d_hdr, k, (int64_t)1 << 20, A.kb);
     const unsigned g = first_sweep_grid(A);
-    if (A.astep == 32) {
+    if (A.astep == 32 || A.astep == 64) {
         PROF_LAUNCH(PROF_ANCHOR, s, k_sweep_early<true>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
     } else {
         hipLaunchKernelGGL(k_sweep_early<false>, dim3(g), dim3(SCCG_BLOCK), 0, s, A);
@@ -3564,9 +3574,22 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
             }
             nlist = rs[0];
             static const bool round_log = getenv("SCCG_ROUND_LOG") != nullptr;   // (determinism diagnostics)
-            if (round_log)
-                fprintf(stderr, "[round] %lld pending %d esc %d frozen %d chains %lld\n", (long long)round, rs[0], rs[1], rs[5],
-                        (long long)res->chains);
+            if (round_log) {
+                // (with SCCG_ROUND_LOG=2 also a digest of the chunk states, to find where two runs part)
+                uint64_t hsh = 0;
+                if (getenv("SCCG_ROUND_LOG")[0] == '2') {
+                    std::vector<int32_t> v(C);
+                    const int32_t* arrs[6] = {A.exitX, A.exitP, A.usedX, A.usedP, A.cur, A.plist};
+                    for (int a = 0; a < 6; a++) {
+                        const size_t nn = a == 5 ? (size_t)(rs[0] > 0 ? rs[0] : 0) : C;
+                        SCCG_HIP(hipMemcpy(v.data(), arrs[a], nn * 4, hipMemcpyDeviceToHost));
+                        if (a == 5) std::sort(v.begin(), v.begin() + nn);
+                        for (size_t i = 0; i < nn; i++) hsh = (hsh ^ (uint32_t)v[i]) * 0x100000001b3ull + a;
+                    }
+                }
+                fprintf(stderr, "[round] %lld pending %d esc %d frozen %d chains %lld digest %016llx\n", (long long)round, rs[0], rs[1],
+                        rs[5], (long long)res->chains, (unsigned long long)hsh);
+            }
             if (dbg) {
                 SCCG_HIP(hipStreamSynchronize(s));
                 static thread_local auto tprev = std::chrono::steady_clock::now();
