@@ -19,7 +19,8 @@ from collections import defaultdict
 
 FAMILY = {  # kernel symbol fragment -> bench.py / sccg_profile family name
     "k_walk<false, true>": "walk_carry", "k_walk<true, true>": "walk_carry", "k_walk(": "walk", "k_walk<": "walk", "k_local_all": "local_segments", "k_local_pass<14>": "local_pass_k14", "k_local_pass<10>": "local_pass_k10",
-    "k_strip_write": "fasta_strip", "k_filter_write": "n_filter", "k_runs_write": "run_extract",
+    "k_strip_write": "fasta_strip", "k_filter_write": "n_filter", "k_runs_write": "run_extract", "k_runs_copy": "run_extract",
+    "k_sweep_early<true>": "first_sweep_anchors",
     "k_run_textwrite": "run_text", "k_seg_textwrite": "local_emit", "k_anchor_build": "anchor_build", "k_key0<true>": "first_sweep_anchors", "k_chunk_text<true>": "match_emit",
     "k_presence": "presence_scan", "k_fullc": "fullc_scan", "k_match_textwrite": "match_emit",
     "k_tok_fill": "dc_decode", "k_format": "dc_format",
