@@ -1734,18 +1734,25 @@ __global__ __launch_bounds__(64) void k_chain_step(WalkPtrs A) {
     bool gen_end = false;
     int64_t hits = 0;         // band hits of this generation
     int64_t visited = 0;      // of which the step visited
-    // skip the leading blocks without hits and without a cut (their hit counts read at once, 8 per
-    // lane, instead of one dependent pair of loads per block)
-    int bstart = CH_GRID;
+    // Only the blocks with hits or a cut do anything below: their hit counts and cuts are read at
+    // once (coalesced, 64 blocks per load) into LDS with a bitmap of them in block order, and the
+    // loop visits those blocks alone -- one dependent pair of loads per block of the scan grid
+    // (512) was most of a generation's ~0.2 ms on the T2T-like pairs.
     static_assert(CH_GRID % 64 == 0, "blocks per lane");
+    __shared__ int32_t s_nh[CH_GRID], s_tr[CH_GRID];
+#pragma unroll
     for (int i = 0; i < CH_GRID / 64; i++) {
-        const int b = lane * (CH_GRID / 64) + i;
-        if ((A.chh_n[b] > 0 || A.chh_tr[b] != INT32_MAX) && b < bstart) bstart = b;
+        const int b = 64 * i + lane;
+        s_nh[b] = A.chh_n[b];
+        s_tr[b] = A.chh_tr[b];
     }
-    bstart = wave_min(bstart);
-    if (bstart > 0 && lane == 0) A.chs[11] = 0;   // (what block 0, without hits or a cut, does below)
-    for (int b = bstart; b < CH_GRID && !gen_end && !reason; b++) {
-        const int32_t nh = A.chh_n[b], tr = A.chh_tr[b];
+    wave_sync();
+    if (s_nh[0] == 0 && s_tr[0] == INT32_MAX && lane == 0) A.chs[11] = 0;   // (what block 0, without hits or a cut, does below)
+    for (int i = 0; i < CH_GRID / 64 && !gen_end && !reason; i++)
+    for (uint64_t bm = __ballot(s_nh[64 * i + lane] > 0 || s_tr[64 * i + lane] != INT32_MAX); bm && !gen_end && !reason;
+         bm &= bm - 1) {
+        const int b = 64 * i + __ffsll((long long)bm) - 1;
+        const int32_t nh = s_nh[b], tr = s_tr[b];
         hits += nh;
         const int32_t* hy = A.chh_y + (size_t)b * CH_HCAP;
         const uint32_t* hk = A.chh_k + (size_t)b * CH_HCAP;
