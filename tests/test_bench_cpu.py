@@ -96,8 +96,8 @@ def test_job_models_say_what_they_count():
     import bench
     nT, nR, nRp, out, tfa, rfa = 249_250_621, 247_249_719, 225_000_000, 6_700_000, 254_000_000, 252_000_000
     d = bench.design_alg_bytes(tfa, rfa, nT, nR, nRp, out, True)
-    assert d == tfa + rfa + 2 * (nT + nR) + nT + out + nRp + 0.5 * nT
+    assert d == tfa + rfa + 2 * (nT + nR) + out + nRp + 0.5 * nT   # (run lines: out of the strip, no T re-read)
     d_local = bench.design_alg_bytes(tfa, rfa, nT, nR, nRp, out, False)
-    assert d_local == tfa + rfa + 2 * (nT + nR) + nT + out + 2 * min(nT, nR)
+    assert d_local == tfa + rfa + 2 * (nT + nR) + out + 2 * min(nT, nR)
     s = bench.survey_alg_bytes(nT, nR, nRp, out)
     assert s == 1.25 * (nT + nR) + 0.25 * nR + 4 * nRp + 0.5 * nT + out
