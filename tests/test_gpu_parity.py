@@ -154,12 +154,13 @@ def test_chr1_roundtrip(ctx):
     assert ctx.reconstruct(rec, rfa) == tfa
 
 
-def _switch_case(seed: int, nseg: int = 2400, plant_at: int | None = None):
+def _switch_case(seed: int, nseg: int = 2400, plant_at: int | None = None, gap=None):
     """Segment-kind patterns for the local->global switch (compression.cpp:462-473): identical
     segments (good), unrelated random ones (failed or mostly literal), half-copied ones (matched
     but > 50 % literal), all-N ones (failed, all N: resets the counter) and poly-A ones (failed,
     not N), in bursts of 1-3, with a planted 5-burst ending in a failure at a seed-dependent
-    segment (or none)."""
+    segment (or none).  gap = (start, length, kinds): a long run of segments drawn from `kinds`
+    (e.g. only half-copied ones, or all-N: unproved segments that never switch)."""
     import numpy as np
     rng = np.random.default_rng(seed)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
@@ -172,6 +173,9 @@ def _switch_case(seed: int, nseg: int = 2400, plant_at: int | None = None):
         n = int(rng.integers(1, 4))   # bursts too short to switch on their own ...
         kinds[i:i + n] = rng.choice([1, 2, 3, 4], size=min(n, max(0, nseg - i)))
         i += n
+    if gap is not None:
+        g0, gl, gk = gap
+        kinds[g0:g0 + gl] = rng.choice(list(gk), size=len(kinds[g0:g0 + gl]))
     plant = [None, 4, 5, 9, 63, 64, 65, 1000, 4095, nseg - 1][seed % 10] if plant_at is None else plant_at
     if plant is not None and plant < nseg:
         kinds[max(0, plant - 4):plant + 1] = rng.choice([1, 2, 4], size=min(plant + 1, 5))   # ... but this one
