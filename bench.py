@@ -847,7 +847,7 @@ def main() -> None:
                 am = prof_all[k][0] / prof_all[k][1]
                 e = {"alg_bytes_per_launch": ab, "avg_launch_ms": am, "achieved_GBps": ab / (am * 1e-3) / 1e9,
                      "frac": ab / (am * 1e-3) / 1e9 / HBM_PEAK_GBS}
-                pmc = load_pmc({"first_sweep_anchors": "k_sweep_early"}.get(k, k))
+                pmc = load_pmc(k) or load_pmc({"first_sweep_anchors": "k_sweep_early"}.get(k, k))   # (family, or round-4 kernel name)
                 if pmc:
                     e["traffic_per_launch"] = pmc["hbm_bytes_per_launch"]
                 kroof[k] = e
