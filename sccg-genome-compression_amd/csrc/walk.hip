@@ -123,6 +123,7 @@ constexpr int FF_CHUNK = 8192;
 // for its whole span (T2T-like 100 Mb pair: ~73 us per generation, 40 generations)
 constexpr int64_t CH_FF_SPAN = SCCG_CH_FF_SPAN;
 constexpr int CH_MAX_GENS = 4096;      // generations per chain
+constexpr int MARCH_ROUNDS = 4;        // rounds settling <= 2 chunks each before a march chain
 constexpr int64_t CH_DENSE_HITS = 32768;  // band hits of one generation that switch the chain to find-first generations
 constexpr int CH_DENSE_N = 32;         // hand back to the chunk rounds when CH_DENSE_N matches
 constexpr int32_t CH_DENSE_SPAN = 8192;   // fall within this many target bases (the walk is aligned again)
@@ -223,6 +224,7 @@ struct WalkPtrs {
     int32_t* chm_p;
     int32_t* chm_l;
     int32_t chm_cap;
+    int32_t ch_settled;       // this chain starts only from a settled frozen chunk (march chains, host-set)
     int32_t* chh_y;           // CH_GRID x CH_HCAP band hits (position, key), in position order per block
     uint32_t* chh_k;
     int32_t* chh_n;           // per block: hits recorded, first position not covered (INT32_MAX: none)
@@ -1541,8 +1543,16 @@ __global__ void k_chain_init(WalkPtrs A) {
     if (A.scal[9]) return;
     const int lane = lane_id();
     const int nf = A.scal[5];
+    // settled: only a frozen chunk before the first pending one (every chunk up to it was walked
+    // from its predecessor's final exit), so the chain walks the sequential walk itself
+    int32_t pmin = INT32_MAX;
+    if (A.ch_settled) {
+        const int np = A.scal[0];
+        for (int i = lane; i < np; i += 64) { const int32_t q = A.plist[i]; pmin = q < pmin ? q : pmin; }
+        pmin = wave_min(pmin);
+    }
     int32_t jm = INT32_MAX;
-    for (int f = lane; f < nf; f += 64) { const int32_t j = A.flist[f]; jm = j < jm ? j : jm; }
+    for (int f = lane; f < nf; f += 64) { const int32_t j = A.flist[f]; jm = j < jm && j < pmin ? j : jm; }
     jm = wave_min(jm);
     if (lane) return;
     if (jm == INT32_MAX) { A.chs[0] = 0; A.chs[5] = 0; return; }
@@ -3477,6 +3487,10 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
         const bool dbg = getenv("SCCG_DEBUG") != nullptr;
         static const bool chains_env = getenv("SCCG_NO_CHAINS") == nullptr;   // (A/B and tests)
         bool chains_on = chains_env && !range;   // off for the rest of the call after a trapped chain
+        static const bool march_chains = [] { const char* e = getenv("SCCG_MARCH_CHAINS"); return e ? atoi(e) != 0 : true; }();
+        int march = 0;
+        int32_t prev_pend = -1;
+        A.ch_settled = 0;
         // with the device first step, rounds 1 and 2 went out before the first readback
         const int64_t round0 = pre_round ? 2 : 1;
         // Rounds queued blind (SCCG_ROUND_BATCH, from round ROUND_BATCH_FROM on): once the first rounds
@@ -3543,8 +3557,19 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
             // 10): synthetic chr22 2.3 / 1.7 / 1.7 ms, 20 Mb T2T-like pair 5.5 / 5.7 / 5.7 ms, 100 Mb
             // T2T-like pair 14.0 / 14.4-17.6 / 12.4 ms (23 ms without chains).
             static const int chain_round = [] { const char* e = getenv("SCCG_CHAIN_ROUND"); const int v = e ? atoi(e) : 10; return v >= 2 ? v : 10; }();
-            const bool chain_now = chains_on && rs[5] > 0 && (round == 1 || round >= chain_round);
+            // A march: chains are off (a trapped hand-back) and the rounds settle one or two chunks each
+            // -- the frontier chunk ends frozen, its frozen scan finds the next hit a chunk on, and the
+            // chunks behind it keep re-walking from entries that are not final.  A chain from the
+            // frontier (the settled frozen chunk) walks those hits on the device instead.
+            if (!chains_on && rs[0] > 0 && prev_pend >= 0 && rs[0] <= prev_pend && prev_pend - rs[0] <= 2) march++;
+            else march = 0;
+            prev_pend = rs[0];
+            const bool march_chain = march_chains && chains_env && !range && !chains_on && march >= MARCH_ROUNDS && rs[5] > 0;
+            const bool chain_now = (chains_on && rs[5] > 0 && (round == 1 || round >= chain_round)) || march_chain;
             if (chain_now) {
+                A.ch_settled = march_chain ? 1 : 0;
+                static const bool march_reset = [] { const char* e = getenv("SCCG_MARCH_RESET"); return e ? atoi(e) != 0 : false; }();
+                if (march_chain && march_reset) march = 0;
                 // a frozen chain: walk it on over the rest of the target, then the pending list again
                 int gens = 0;
                 bool trapped = false;
