@@ -3564,7 +3564,8 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
             if (!chains_on && rs[0] > 0 && prev_pend >= 0 && rs[0] <= prev_pend && prev_pend - rs[0] <= 2) march++;
             else march = 0;
             prev_pend = rs[0];
-            const bool march_chain = march_chains && chains_env && !range && !chains_on && march >= MARCH_ROUNDS && rs[5] > 0;
+            static const int march_rounds = [] { const char* e = getenv("SCCG_MARCH_ROUNDS"); const int v = e ? atoi(e) : MARCH_ROUNDS; return v >= 1 ? v : MARCH_ROUNDS; }();
+            const bool march_chain = march_chains && chains_env && !range && !chains_on && march >= march_rounds && rs[5] > 0;
             const bool chain_now = (chains_on && rs[5] > 0 && (round == 1 || round >= chain_round)) || march_chain;
             if (chain_now) {
                 A.ch_settled = march_chain ? 1 : 0;
