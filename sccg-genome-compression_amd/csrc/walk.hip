@@ -1451,10 +1451,12 @@ __global__ __launch_bounds__(256) void k_round_pending(WalkPtrs A) {
     A.kind[j] = KIND_FIX;
     A.lround[j] = next;
     A.plist[atomicAdd(&A.scal[0], 1)] = j;
-    if (j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round) {
-        A.tflag[j] = A.round;   // (k_round_respec takes the first RESPEC_MAX_TRIGGERS in chunk order)
-        atomicAdd(&A.scal[12], 1);
-    }
+    // (k_round_respec takes the first RESPEC_MAX_TRIGGERS in chunk order; a chunk that was a trigger
+    // in an earlier pending pass of this round -- before a chain filled its predecessor -- and is
+    // not one now is cleared)
+    const bool trig = j > 0 && A.trapped[j - 1] && A.walked[j - 1] == A.round;
+    A.tflag[j] = trig ? A.round : -1;
+    if (trig) atomicAdd(&A.scal[12], 1);
 }
 
 // re-speculate the still-speculative chunks after each trapped trigger (see TRAP_P)
