@@ -21,9 +21,25 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--window-ms", type=float, required=True)
+    ap.add_argument("--windows", type=int, default=0,
+                    help="also the busy fraction of this many consecutive windows back from the last kernel "
+                         "(the last one usually holds the run's tail, not a step)")
     a = ap.parse_args()
     rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in csv.DictReader(open(a.csv))]
     t1 = max(e for _, e, _ in rows)
+    if a.windows:
+        merged: list[list[int]] = []
+        for s, e, _ in sorted(rows):
+            if merged and s <= merged[-1][1]:
+                merged[-1][1] = max(merged[-1][1], e)
+            else:
+                merged.append([s, e])
+        w = int(a.window_ms * 1e6)
+        fr = []
+        for k in range(a.windows):
+            hi, lo = t1 - k * w, t1 - (k + 1) * w
+            fr.append(sum(min(e, hi) - max(s, lo) for s, e in merged if e > lo and s < hi) / w)
+        print("busy per window (last first): " + " ".join(f"{f:.3f}" for f in fr))
     t0 = t1 - int(a.window_ms * 1e6)
     rows = [(max(s, t0), e, n) for s, e, n in rows if e > t0]
     ev = sorted([(s, 1, i) for i, (s, _, _) in enumerate(rows)] + [(e, -1, i) for i, (_, e, _) in enumerate(rows)])
