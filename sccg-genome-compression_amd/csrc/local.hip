@@ -572,7 +572,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
             st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, nullptr, (int)non_n);
             if (!st.pass) {
                 wave_sync();
-                st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs);
+                // (the segment strings are still in LDS: the k pass only reads them)
+                st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs, nullptr, 1);
             }
             c = seg_class(st);
         }
