@@ -571,6 +571,9 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
         } else {
             st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, nullptr, (int)non_n);
             if (!st.pass) {
+                // a switch found meanwhile at or before this segment: its class is never read (no
+                // window past the first switch counts), so the k2 pass is skipped and nothing published
+                if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
                 wave_sync();
                 // (the segment strings are still in LDS: the k pass only reads them)
                 st = local_segment<10, DBG>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs, nullptr, 1);
