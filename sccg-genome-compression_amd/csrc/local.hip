@@ -569,6 +569,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
             c = 0;
             if (DBG && lane == 0) atomicAdd(&g_local_dbg[15], 1ull);
         } else {
+            // (unproved: re-read the bound before the k pass as well -- a switch found during the proof)
+            if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
             st = local_segment<14, DBG>(L, seg, 1, 0, 1, R, nR, T, nT, recs, nullptr, (int)non_n);
             if (!st.pass) {
                 // a switch found meanwhile at or before this segment: its class is never read (no
