@@ -149,6 +149,24 @@ def timed_region(step, steps: int, warmup: int, world: int, sync=lambda: None, d
     return dt
 
 
+def make_step(pool, order: list, job, results: dict, gather=None):
+    """One step: every pair of this rank's shard compressed on its lanes (pool.run), then -- N > 1 --
+    the per-chromosome record streams queued to rank 0 (multigpu.StreamGather: point-to-point,
+    unpadded, behind the lanes' streams).  The step reads nothing back from the device and never
+    waits for it; timed_region's final device sync is the only synchronisation.  The gather's plan
+    (the stream lengths, an all_gather_object) is made in the first, untimed call."""
+
+    def step() -> None:
+        pool.run(order, job)
+        if gather is not None:
+            parts = {n: results[n][0] for n in order}
+            if gather.plan_lengths is None:
+                pool.sync()
+                gather.plan(parts, parts[order[0]].device if order else None)
+            gather.step(parts, after=[ln.stream for ln in pool.lanes])
+    return step
+
+
 def gather_streams(results: dict, order: list, world: int, device) -> dict | None:
     """Every rank's per-chromosome record streams on rank 0 (multigpu.gather_records: one size
     all-gather + one gather to rank 0); None on the other ranks."""
@@ -523,7 +541,7 @@ def t2t_genome(pool: LanePool, jobs: list, world: int, rank: int, dev, steps: in
     per = {n: {"rounds": results[n][1]["walk_rounds"], "rounds_per_timed_step": [r[n] for r in timed_rounds],
                "chains": results[n][1]["walk_chains"], "matches": results[n][1]["n_matches"],
                "mode": "global" if results[n][1]["mode_global"] else "local", "ms_alone": cost[n],
-               "target_bases": results[n][1]["target_bases"]}
+               "switch_segment": results[n][1]["switch_segment"], "target_bases": results[n][1]["target_bases"]}
            for n in order}
     nT = sum(results[n][1]["target_bases"] for n in order)
     if world > 1:
@@ -680,17 +698,10 @@ def main() -> None:
     order = sorted(pairs, key=lambda n: -pairs[n][3])   # largest first onto the first free lane
     results: dict = {}      # name -> (device tensor of its record text, stats)
     job = device_job(pairs, results, dev)
-    gathered: list = [None]
+    gather = multigpu.StreamGather() if world > 1 else None
+    step = make_step(pool, order, job, results, gather)
 
-    def step() -> None:
-        pool.run(order, job)
-        pool.sync()
-        if world > 1:
-            # per-chromosome record streams -> rank 0 over RCCL (multigpu.gather_records): one size
-            # all-gather, then one gather of each rank's packed streams; only rank 0 receives
-            gathered[0] = multigpu.gather_records({n: results[n][0] for n in order}, device=dev)
-
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1 if world > 1 else 0)):   # (N > 1: the gather's plan is made here)
         step()
     # HIP events inside the timed region bracket the dominant kernel's launches only (k_walk; events
     # around every family cost ~1 ms of a ~23 ms step); one more, untimed step brackets every family
@@ -729,7 +740,12 @@ def main() -> None:
     # ---- parity: every chromosome's record stream against the reference's pinned sha256
     parity = None
     if not args.no_check:
-        streams = gathered[0] if world > 1 else gather_streams(results, order, 1, dev)
+        torch.cuda.synchronize()
+        if world > 1:
+            got = gather.result()
+            streams = {n: t.cpu().numpy().tobytes() for n, t in got.items()} if got is not None else None
+        else:
+            streams = gather_streams(results, order, 1, dev)
         if rank == 0:
             pins = load_manifest() if args.workload == "genome" else {}
             parity = check_pins(streams, pins)
@@ -870,6 +886,7 @@ def main() -> None:
             cpu = cpu_baseline_pointer()
         per = {n: {"mode": "global" if results[n][1]["mode_global"] else "local",
                    "rounds": results[n][1]["walk_rounds"], "matches": results[n][1]["n_matches"],
+                   "switch_segment": results[n][1]["switch_segment"],
                    "record_bytes": int(results[n][0].numel())} for n in order}
         wl = ("hg19-vs-hg18 whole genome: 24 chromosome pairs at UCSC lengths (BASELINE configs[2])"
               if args.workload == "genome" else "hg19-vs-hg18 chr1-sized pair per GPU (BASELINE configs[1] shape)")

@@ -71,7 +71,10 @@ typedef struct {
 
 typedef struct {
     int mode_global;          /* 1 when the local loop switched (compression.cpp:462-473) */
-    int64_t switch_segment;   /* segment index of the switch, -1 if it stayed local */
+    int64_t switch_segment;   /* last segment of a switch window (compression.cpp:417-473), -1 if it
+                                 stayed local: the reference's switch segment (the first window)
+                                 with SCCG_OPT_EXACT_SWITCH, otherwise the first window the mode
+                                 probe found (>= it; the record file is the same either way) */
     int64_t target_bases;     /* |T| after whitespace strip (compression.cpp:218) */
     int64_t reference_bases;  /* |R| */
     int64_t n_matches;        /* (p,l) tokens on the record line */
@@ -87,6 +90,15 @@ int sccg_ctx_create(int device, sccg_ctx** out);
 void sccg_ctx_destroy(sccg_ctx* ctx);
 const char* sccg_last_error(const sccg_ctx* ctx);
 int sccg_last_stats(const sccg_ctx* ctx, sccg_stats* out);
+
+/* Context options (sccg_ctx_set_option; SCCG_E_INVALID for an unknown option):
+ *   SCCG_OPT_EXACT_SWITCH  0 (default): the local/global mode is decided from ANY switch window
+ *                          (a few probed runs of segments first), which is enough for the record
+ *                          file (compression.cpp:462-473 truncates it and the global pass
+ *                          regenerates it); 1: the in-order pass finds the first window, so
+ *                          sccg_stats.switch_segment is the reference's switch segment. */
+#define SCCG_OPT_EXACT_SWITCH 1
+int sccg_ctx_set_option(sccg_ctx* ctx, int option, int64_t value);
 
 /* Whole-file compression up to (excluding) 7z: returns the exact bytes of
  * <out>/compressed_genome.txt for the given reference/target FASTA file contents. */

@@ -26,6 +26,8 @@ constexpr int SEGB = 1024;        // LDS bytes per segment string (1000 + zero p
 constexpr int NBB = 9;            // 512 k-mer buckets
 constexpr int NB = 1 << NBB;
 constexpr int MANY = 4;           // more candidates than this: extend one per lane
+constexpr int32_t PASS_ABORTED = -2;   // a walk stopped at its step budget (switch probe only)
+constexpr int32_t PASS_NEED_K2 = -3;   // a proved segment whose k pass found no match (launch_local_proven)
 
 struct SegLds {
     uint8_t r[SEGB];
@@ -257,7 +259,7 @@ template <int K, bool DBG>
 __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pass, int non_n_prev, int upper,
                                                  const uint8_t* __restrict__ R, int64_t nR, const uint8_t* __restrict__ T,
                                                  int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr,
-                                                 int loaded = -1) {
+                                                 int loaded = -1, int budget = INT32_MAX) {
     const int lane = lane_id();
     const int64_t base = seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
@@ -327,7 +329,9 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     const int lastk = nt - K;
     uint32_t* out = recs + seg * SEG_REC_CAP;
     int idx = 0, pme = -1, nrec = 0, nmatch = 0, lit = 0, firstp = -1, lastp = -1;
+    bool aborted = false;
     for (;;) {
+        if (nmatch >= budget) { aborted = true; break; }   // (the switch probe's step budget)
         // next target position >= idx with a candidate (and its key)
         int nxt = -1;
         uint32_t key = 0;
@@ -479,7 +483,7 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     s.nrec = nrec;
     s.nmatch = nmatch;
     s.lit = lit;
-    s.pass = nmatch ? pass : 0;
+    s.pass = aborted ? PASS_ABORTED : nmatch ? pass : 0;
     s.non_n = pass == 1 ? (int)non_n : non_n_prev;
     s.first_p = firstp;
     s.last_p = lastp;
@@ -499,8 +503,10 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_local_pass(int pass, int upper, 
     for (int64_t seg = seg0 + (int64_t)blockIdx.x * WPB + w; seg < seg_end; seg += G) {
         if (pass == 2 && stat[seg].pass != 0) continue;
         if (pass == 3 && stat[seg].pass != PASS_PROVEN) continue;   // (a proof means the k pass succeeds)
-        const SegStat st = local_segment<K, DBG>(lds_all[w], seg, pass == 3 ? 1 : pass, pass == 2 ? stat[seg].non_n : 0,
-                                                 upper, R, nR, T, nT, recs);
+        if (pass == 4 && stat[seg].pass != PASS_NEED_K2) continue;
+        SegStat st = local_segment<K, DBG>(lds_all[w], seg, pass == 3 ? 1 : pass == 4 ? 2 : pass,
+                                           pass == 2 || pass == 4 ? stat[seg].non_n : 0, upper, R, nR, T, nT, recs);
+        if (pass == 3 && st.pass == 0) st.pass = PASS_NEED_K2;   // (never, if the proof holds)
         if (lane_id() == 0) stat[seg] = st;
         wave_sync();   // the next segment reuses this wave's LDS
     }
@@ -554,6 +560,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
     const int32_t G = (int32_t)gridDim.x * WPB;
     SegWords cur, nxt;
     int32_t seg = (int32_t)blockIdx.x * WPB + w;
+    // (a probe window already decided the mode: ctl[1] = -1, nothing to start)
+    if (uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0) return;
     if (seg < nseg) seg_words_load(cur, seg, R, nR, T, nT);
     for (; seg < nseg; seg += G) {
         if (seg > uni(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
@@ -604,6 +612,85 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
             __hip_atomic_fetch_min(&ctl[1], hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         wave_sync();   // the next segment reuses this wave's LDS
         cur = nxt;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Switch probe (round 6; the default unless the caller asks for the exact switch segment).  The
+// machine switches iff SOME window of 5 class-1/2 segments ends in a class-2 segment (the counter is
+// a run length reset by class 0/3, and a window at e makes it switch at e unless it did before), and
+// a switching pair's record file does not depend on where it switched (compression.cpp:462-473 -- the
+// file is truncated and the global pass regenerates it, :484-574).  So one complete window anywhere
+// decides the mode.  Drifted hg/T2T pairs are full of them past their first switch (segment pairs
+// that no longer overlap fail both passes or match by chance: classes 1 and 2), so PROBE_RUNS runs of
+// PROBE_RUN consecutive segments spread over the pair are classified first, one wave per segment,
+// and a window inside any run lowers the in-order pass's bound below every segment (ctl[1] = -1:
+// k_local_all starts nothing) and records its end in ctl[2].  No window: the in-order pass runs as
+// before (the probed segments' classes, records and stats are the ones it recomputes).
+// ---------------------------------------------------------------------------------------------
+constexpr int PROBE_RUN = 8, PROBE_RUNS = 16, PROBE_MIN_SEGS = 4 * PROBE_RUN * PROBE_RUNS;
+// SCCG_DEBUG: per probed segment {start, after load+prove, after k, after k2, end} (wall clock) and its class
+__device__ unsigned long long g_probe_dbg[PROBE_RUNS * PROBE_RUN][6];
+// A segment's walk stops after `budget` matches (repeat-rich drifted segments take hundreds of short
+// chance matches, ~0.5 ms for one wave, and the probe is as slow as its slowest segment): its class
+// is then unknown (-1, no window holds it) and nothing is published for it.
+template <bool DBG>
+__global__ __launch_bounds__(64 * PROBE_RUN) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_probe(
+    const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR, const uint8_t* __restrict__ T,
+    const int64_t* __restrict__ dnT, uint32_t* __restrict__ recs, SegStat* __restrict__ stat, int32_t* __restrict__ cls,
+    int32_t gen, int32_t* __restrict__ ctl, int prove, int budget) {
+    unsigned long long tk[5] = {DBG ? (unsigned long long)wall_clock64() : 0ull, 0, 0, 0, 0};
+    __shared__ SegLds lds_all[PROBE_RUN];
+    __shared__ int32_t rc[PROBE_RUN];
+    const int64_t nR = *dnR, nT = *dnT;
+    const int32_t nseg = seg_count(nR, nT);
+    if (nseg < PROBE_MIN_SEGS) return;   // (block-uniform) small pairs: the in-order pass is cheap
+    const int w = wave_in_block(), lane = lane_id();
+    // run j starts at (j + 1)(nseg - RUN) / RUNS: the last run ends at the last segment
+    const int32_t a = (int32_t)((int64_t)(blockIdx.x + 1) * (nseg - PROBE_RUN) / PROBE_RUNS);
+    const int32_t seg = a + w;
+    SegLds& L = lds_all[w];
+    const bool non_n = seg_load(L, seg, 1, R, nR, T, nT, nullptr);
+    const int64_t base = (int64_t)seg * SEG_L;
+    const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L), nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
+    SegStat st;
+    int c;
+    const bool proved = prove && seg_prove(L.r, L.t, nr, nt);
+    if (DBG) tk[1] = tk[2] = tk[3] = wall_clock64();
+    if (proved) {   // exactly as k_local_all
+        st = SegStat{0, 0, 0, PASS_PROVEN, (int)non_n, -1, -1, nt};
+        c = 0;
+    } else {
+        st = local_segment<14, false>(L, seg, 1, 0, 1, R, nR, T, nT, recs, nullptr, (int)non_n, budget);
+        if (DBG) tk[2] = tk[3] = wall_clock64();
+        if (!st.pass) {
+            wave_sync();
+            st = local_segment<10, false>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs, nullptr, 1, budget);
+            if (DBG) tk[3] = wall_clock64();
+        }
+        c = st.pass == PASS_ABORTED ? -1 : seg_class(st);
+    }
+    if (DBG && lane == 0) {
+        tk[4] = wall_clock64();
+        unsigned long long* d = g_probe_dbg[blockIdx.x * PROBE_RUN + w];
+        for (int i = 0; i < 5; i++) d[i] = tk[i];
+        d[5] = (unsigned long long)(c + 1) | ((unsigned long long)st.nmatch << 8) | ((unsigned long long)seg << 32);
+    }
+    if (lane == 0 && c < 0) rc[w] = c;
+    if (lane == 0 && c >= 0) {
+        stat[seg] = st;
+        __hip_atomic_store(&cls[seg], (gen << 2) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rc[w] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t hit = INT32_MAX;
+        for (int e = PROBE_RUN - 1; e >= 4; e--)
+            if (rc[e] == 2 && mism(rc[e - 1]) && mism(rc[e - 2]) && mism(rc[e - 3]) && mism(rc[e - 4])) hit = a + e;
+        if (hit != INT32_MAX) {
+            __hip_atomic_fetch_min(&ctl[2], hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_min(&ctl[1], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -786,14 +873,44 @@ int local_prove() {
 int launch_local_proven(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t nT, int64_t iters, uint32_t* recs,
                         SegStat* stat, hipStream_t s) {
     if (!local_prove() || iters <= 0) return 0;
-    // (an unproved segment the windowed scan never walked may fail the k pass: the k2 pass follows)
+    // The k pass over the proved segments (pass 3), then k2 only over a proved segment whose k pass
+    // found no match (pass 4, PASS_NEED_K2; the proof says there is none) -- not over the segments
+    // k_local_all already took through both passes.
     const int rc = launch_local_pass(14, 3, 1, R, nR, T, nT, 0, iters, recs, stat, s);
-    return rc ? rc : launch_local_pass(10, 2, 1, R, nR, T, nT, 0, iters, recs, stat, s);
+    return rc ? rc : launch_local_pass(10, 4, 1, R, nR, T, nT, 0, iters, recs, stat, s);
 }
 
 int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
-                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s) {
+                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, bool exact_switch,
+                     hipStream_t s) {
     if (nseg_max <= 0) return 0;
+    // the switch probe (any window decides the mode); the exact first switch needs the in-order pass
+    static const bool probe_on = [] { const char* e = getenv("SCCG_SWITCH_PROBE"); return e && atoi(e) != 0; }();
+    static const int budget = [] { const char* e = getenv("SCCG_PROBE_BUDGET"); const int v = e ? atoi(e) : 0; return v > 0 ? v : 32; }();
+    static const bool pdbg = getenv("SCCG_DEBUG") != nullptr;
+    if (probe_on && !exact_switch && nseg_max >= PROBE_MIN_SEGS) {
+        if (!pdbg) {
+            PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<false>, dim3(PROBE_RUNS), dim3(64 * PROBE_RUN), 0, s, R, d_nR, T, d_nT,
+                        recs, stat, cls, gen, ctl, local_prove(), budget);
+        } else {
+            const unsigned long long z[PROBE_RUNS * PROBE_RUN][6] = {};
+            SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_probe_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
+            PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<true>, dim3(PROBE_RUNS), dim3(64 * PROBE_RUN), 0, s, R, d_nR, T, d_nT,
+                        recs, stat, cls, gen, ctl, local_prove(), budget);
+            unsigned long long d[PROBE_RUNS * PROBE_RUN][6];
+            SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_probe_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
+            SCCG_HIP(hipStreamSynchronize(s));
+            unsigned long long t0 = ~0ull;
+            for (auto& x : d) if (x[0] && x[0] < t0) t0 = x[0];
+            for (int i = 0; i < PROBE_RUNS * PROBE_RUN; i++) {
+                const auto& x = d[i];
+                if (!x[0]) continue;
+                fprintf(stderr, "[probe] seg %llu class %d matches %llu: start %.1f prove %.1f k %.1f k2 %.1f end %.1f us\n",
+                        x[5] >> 32, (int)(x[5] & 0xff) - 1, (x[5] >> 8) & 0xffffff, (x[0] - t0) / 100.0, (x[1] - x[0]) / 100.0,
+                        (x[2] - x[1]) / 100.0, (x[3] - x[2]) / 100.0, (x[4] - x[0]) / 100.0);
+            }
+        }
+    }
     // resident capacity: the grid drains the counter, extra blocks would only find it exhausted
     static const unsigned cap = [] {
         int dev = 0, cus = 256, per = 4;

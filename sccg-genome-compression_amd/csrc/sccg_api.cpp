@@ -60,6 +60,8 @@ enum Slot {
     B_RSLOT, B_RTILE,
     B_COUNT
 };
+// (the slot numbers tests/test_gpu_oom.py passes in SCCG_TEST_OOM)
+static_assert(B_RSLOT == 62 && B_D_DEC == 43 && B_COUNT <= 64, "SCCG_TEST_OOM slot numbers moved");
 
 // Target bases per speculative walk chunk.  Larger chunks mean fewer convergence checks per base,
 // smaller ones more chunks in flight: chr1-sized targets (~7.7k chunks of 32 Ki) measured fastest at
@@ -81,6 +83,27 @@ int walk_chunk(int64_t target_bytes) {
     return (int)(c < WALK_CHUNK_MIN ? WALK_CHUNK_MIN : c > cmax ? cmax : c);
 }
 constexpr int DPAD = 4096;   // readable slack after every byte buffer (wide compares, tails)
+
+// SCCG_TEST_OOM: comma-separated slot numbers whose allocation is forced to fail (tests only)
+bool oom_slot(int slot) {
+    static const uint64_t mask = [] {
+        uint64_t m = 0;
+        const char* e = getenv("SCCG_TEST_OOM");
+        while (e && *e) {
+            char* end = nullptr;
+            const long v = strtol(e, &end, 10);
+            if (end == e) break;
+            if (v >= 0 && v < 64) m |= 1ull << v;
+            e = *end ? end + 1 : end;
+        }
+        return m;
+    }();
+    // each listed slot fails once per process (its first allocation), so a caller's fallback that
+    // allocates the same slot later still succeeds
+    static std::atomic<uint64_t> failed{0};
+    if (slot < 0 || slot >= 64 || !((mask >> slot) & 1)) return false;
+    return !((failed.fetch_or(1ull << slot) >> slot) & 1);
+}
 
 }  // namespace
 
@@ -157,6 +180,7 @@ struct sccg_ctx {
     void* cls_buf = nullptr;   // local segment classes: buffer the generation tags refer to
     size_t cls_cap = 0;
     int32_t cls_gen = 0;
+    bool exact_switch = false;   // SCCG_OPT_EXACT_SWITCH: stats report the reference's first switch
 
     int fail(int rc, const char* fmt, ...) {
         char tmp[512];
@@ -179,7 +203,15 @@ struct sccg_ctx {
         buf[slot] = nullptr;
         cap[slot] = 0;
         void* p = nullptr;
-        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        // SCCG_TEST_OOM=<slot>[,<slot>...]: those slots ask for 2^62 bytes, so hipMalloc really
+        // fails there (tests of the optional-allocation fallbacks)
+        if (oom_slot(slot)) bytes = (size_t)1 << 62;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            // HIP keeps the failure as its last error: clear it, or the next launch check after a
+            // caller's fallback would report this out-of-memory
+            (void)hipGetLastError();
+            return nullptr;
+        }
         buf[slot] = p;
         cap[slot] = bytes;
         return p;
@@ -269,6 +301,14 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
 }
 
 const char* sccg_last_error(const sccg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int sccg_ctx_set_option(sccg_ctx* ctx, int option, int64_t value) {
+    if (!ctx) return SCCG_E_INVALID;
+    switch (option) {
+        case SCCG_OPT_EXACT_SWITCH: ctx->exact_switch = value != 0; return SCCG_OK;
+        default: return SCCG_E_INVALID;
+    }
+}
 
 int sccg_last_stats(const sccg_ctx* ctx, sccg_stats* out) {
     if (!ctx || !out) return SCCG_E_INVALID;
@@ -585,7 +625,7 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         }
         const int32_t gen = ++ctx->cls_gen;
         // one launch over every segment; segments past a detected switch are never started
-        TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, s));
+        TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, ctx->exact_switch, s));
         }
         return 0;
     };

@@ -1557,7 +1557,7 @@ __global__ void k_chain_init(WalkPtrs A) {
     for (int f = lane; f < nf; f += 64) { const int32_t j = A.flist[f]; jm = j < jm && j < pmin ? j : jm; }
     jm = wave_min(jm);
     if (lane) return;
-    if (jm == INT32_MAX) { A.chs[0] = 0; A.chs[5] = 0; return; }
+    if (jm == INT32_MAX) { A.chs[0] = 0; A.chs[4] = -1; A.chs[5] = 0; return; }   // (chs[4] -1: none started)
     const int32_t x0 = A.exitX[jm], P0 = A.exitP[jm];
     A.chs[0] = 1; A.chs[1] = x0; A.chs[2] = P0; A.chs[3] = 0; A.chs[4] = jm; A.chs[5] = 0;
     A.chs[8] = 0; A.chs[9] = x0; A.chs[10] = P0; A.chs[11] = 0; A.chs[12] = 0; A.chs[13] = INT32_MAX;
@@ -1956,12 +1956,15 @@ __device__ __forceinline__ bool code32(const uint8_t* s, uint64_t& code) {
     return bad == 0;
 }
 
-// A slot holds gen:16 | tag:16 | position:32 and is written with a 64-bit atomicMax: the call's
-// generation beats every older one (stale slots never need clearing), and among one call's samples
-// that share a slot the winner no longer depends on which wave stores last -- the anchor votes, and
-// with them the speculation and the walk's round counts, are the same on every run.
+// A slot holds gen:12 | tag:20 | position:32 (the tag: the key's low 20 bits; the slot index is
+// its top bits).  A slot is a hit only for the call's generation, so stale slots never need
+// clearing (anchor_generation clears the table when the generation wraps).  Samples that share a
+// slot: the last plain store wins by default; SCCG_ANCHOR_DET=1 stores with a 64-bit atomicMax, so
+// the winner -- and with it the anchor votes, the speculation and the round counts -- no longer
+// depends on which wave stores last.
+constexpr uint32_t ANCHOR_GEN_MASK = 0xfffu;
 __device__ __forceinline__ uint64_t anchor_slot(const WalkPtrs& A, uint64_t key, uint32_t pos) {
-    return ((uint64_t)(A.agen & 0xffffu) << 48) | ((uint64_t)(uint32_t)(key & 0xffffu) << 32) | pos;
+    return ((uint64_t)(A.agen & ANCHOR_GEN_MASK) << 52) | ((uint64_t)(uint32_t)(key & 0xfffffu) << 32) | pos;
 }
 __device__ __forceinline__ bool anchor_hit(const WalkPtrs& A, uint64_t key, uint64_t v) {
     return (v >> 32) == (anchor_slot(A, key, 0) >> 32) && (uint32_t)v != A_MULTI;
@@ -2911,11 +2914,13 @@ int h2d_sync(void* dst, const void* src, size_t bytes, hipStream_t s) {
 // The frozen chain from the earliest frozen chunk committed in this round (k_chain_*): generations
 // are queued CH_GENS_PER_SYNC at a time (a finished chain turns the rest into no-ops), then the
 // covered chunks are filled.  *gens: generations run; *trapped: it handed back as a trapped
-// (match-rich) chain.
-int run_chain(WalkPtrs& A, hipStream_t s, int* gens, bool* trapped) {
+// (match-rich) chain; *started: false when no frozen chunk qualified (a settled-only march chain
+// with no frozen chunk before the first pending one) -- nothing was walked or filled.
+int run_chain(WalkPtrs& A, hipStream_t s, int* gens, bool* trapped, bool* started) {
     hipLaunchKernelGGL(k_chain_init, dim3(1), dim3(64), 0, s, A);
     SCCG_HIP(hipGetLastError());
-    int32_t st[2] = {0, 0};
+    int32_t st[5] = {0, 0, 0, 0, 0};
+    *started = true;
     for (int it = 0;; it++) {
         for (int g = 0; g < CH_GENS_PER_SYNC; g++) {
             hipLaunchKernelGGL(k_chain_scan, dim3(CH_GRID), dim3(1024), 0, s, A);
@@ -2925,6 +2930,12 @@ int run_chain(WalkPtrs& A, hipStream_t s, int* gens, bool* trapped) {
         const RbItem it0{A.chs, st, (int)sizeof st};
         const int rc = dev_readback(&it0, 1, s);
         if (rc) return rc;
+        if (!st[0] && st[4] < 0) {   // no chain started (chs[4] = -1 from k_chain_init)
+            *started = false;
+            *gens = 0;
+            *trapped = false;
+            return 0;
+        }
         if (!st[0]) break;
         if (it > CH_MAX_GENS / CH_GENS_PER_SYNC + 1) return SCCG_E_INTERNAL;   // k_chain_step caps the generations
     }
@@ -3054,12 +3065,13 @@ unsigned first_sweep_grid(const WalkPtrs& A) {
 
 // the anchor table's generation for this call (a fresh workspace is cleared once; afterwards every
 // call's generation retires old slots)
-// Generations increase per workspace (slots are written with atomicMax, anchor_slot), so a table
-// region that held nothing but anchor slots since it was last cleared needs no clearing: stale slots
-// carry older generations.  The table is the workspace's first buffer (carve), sized by the call's
-// |R'|; the bytes past a call's table belong to its other buffers, so `clean` -- the slots that hold
-// only anchor slots -- shrinks to each call's table, and a larger table, a new workspace or the
-// 16-bit generation wrapping clears it once.  (The genome job takes its pairs largest first: one
+// Generations increase per workspace and a slot counts only for the call's own generation
+// (anchor_hit), so a table region that held nothing but anchor slots since it was last cleared
+// needs no clearing: stale slots carry older generations (skipping the clear relies on that
+// generation match, not on the store order).  The table is the workspace's first buffer (carve),
+// sized by the call's |R'|; the bytes past a call's table belong to its other buffers, so `clean`
+// -- the slots that hold only anchor slots -- shrinks to each call's table, and a larger table, a
+// new workspace or the 12-bit generation wrapping clears it once.  (The genome job takes its pairs largest first: one
 // clear per lane and step.)
 struct AnchorSeen { const uint64_t* tab; size_t clean; uint32_t gen; };
 std::mutex g_anchor_mu;
@@ -3072,7 +3084,7 @@ int anchor_generation(WalkPtrs& A, const void* ws, hipStream_t s) {
     {
         std::lock_guard<std::mutex> lk(g_anchor_mu);
         AnchorSeen& e = g_anchor_seen[ws];
-        clear = e.tab != A.atab || n > e.clean || e.gen >= 0xffffu;
+        clear = e.tab != A.atab || n > e.clean || e.gen >= ANCHOR_GEN_MASK;
         if (clear) e.gen = 0;
         e.tab = A.atab;
         e.clean = n;
@@ -3575,14 +3587,24 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                 if (march_chain && march_reset) march = 0;
                 // a frozen chain: walk it on over the rest of the target, then the pending list again
                 int gens = 0;
-                bool trapped = false;
-                RC(run_chain(A, s, &gens, &trapped));
+                bool trapped = false, started = true;
+                RC(run_chain(A, s, &gens, &trapped, &started));
                 static const bool keep_chains = getenv("SCCG_KEEP_CHAINS") != nullptr;   // (A/B)
                 if (trapped && !keep_chains) chains_on = false;   // a trapped walk: the rounds' re-speculation resolves it
-                RC(frozen_batch(0, 0, false));
-                RC(dev_readback(&rs_item, 1, s));
-                spec_text = false;   // the chain rewrote chunks after the round's text was queued
-                res->chains++;
+                if (started) {
+                    RC(frozen_batch(0, 0, false));
+                    RC(dev_readback(&rs_item, 1, s));
+                    spec_text = false;   // the chain rewrote chunks after the round's text was queued
+                    res->chains++;
+                } else {
+                    //  a march chain with no settled frozen chunk: nothing ran, so the round
+                    // takes the frozen batches past the blind one as usual and the march restarts
+                    march = 0;
+                    if (rs[5] > FROZEN_FIRST) {
+                        for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, true));
+                        RC(dev_readback(&rs_item, 1, s));
+                    }
+                }
             } else if (rs[5] > FROZEN_FIRST) {   // more frozen chunks than the blind batch covered
                 for (int fb = FROZEN_FIRST; fb < rs[5]; fb += FROZEN_MAX) RC(frozen_batch(fb, FROZEN_MAX, true));
                 RC(dev_readback(&rs_item, 1, s));

@@ -249,6 +249,20 @@ def collect(names: list[str], parts: dict, stats: dict, em: Emitter | None, dev,
     return all_stats
 
 
+def cost_weights(names: list, sizes: list, cost: dict) -> list:
+    """LPT weights in one unit: a pair the cost file lists weighs its measured cost; a pair it does
+    not list weighs its target size scaled by the median cost per byte of the listed pairs (a bare
+    byte count next to costs of ~10 ms would put that pair alone on a rank)."""
+    per_byte = sorted(cost[n] / s for n, s in zip(names, sizes) if n in cost and s > 0)
+    scale = per_byte[len(per_byte) // 2] if per_byte else 1.0
+    return [float(cost[n]) if n in cost else s * scale for n, s in zip(names, sizes)]
+
+
+def load_cost(path: str) -> dict:
+    with open(path) as f:
+        return json.load(f)
+
+
 def run_job(names: list[str], ref_dir: str, tgt_dir: str, out_dir: str, make_ctx, rank: int, world: int, dev,
             contexts: int = 2, run_7z: bool = True, seven_zip: str = "7z", err_hip: int | None = None,
             cost: dict | None = None) -> tuple[int, dict | None]:
@@ -263,7 +277,7 @@ def run_job(names: list[str], ref_dir: str, tgt_dir: str, out_dir: str, make_ctx
         err_hip = sccg.ERR_CODES["SCCG_E_HIP"]
     sizes = [os.path.getsize(os.path.join(tgt_dir, n + ".fa")) if os.path.exists(os.path.join(tgt_dir, n + ".fa"))
              else 0 for n in names]
-    weights = [cost.get(n, s) for n, s in zip(names, sizes)] if cost else sizes
+    weights = cost_weights(names, sizes, cost) if cost else sizes
     mine = [names[i] for i in multigpu.lpt_shard(weights, world)[rank]]
     em = Emitter(out_dir, run_7z, seven_zip) if rank == 0 else None
     t0 = time.perf_counter()
@@ -311,7 +325,7 @@ def main(argv=None) -> int:
         names = [n for n in names if n in keep]
     rc, summary = run_job(names, args.ref_dir, args.tgt_dir, args.out, lambda: sccg.Context(local), rank, world, dev,
                           contexts=args.contexts, run_7z=not args.no_7z,
-                          cost=json.load(open(args.cost)) if args.cost else None)
+                          cost=load_cost(args.cost) if args.cost else None)
     if rank == 0:
         print(json.dumps(summary))
     if world > 1:

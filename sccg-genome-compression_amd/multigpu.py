@@ -71,6 +71,85 @@ def gather_to_root(buf: torch.Tensor, n: int, group=None) -> list[torch.Tensor] 
     return [parts[r][: sizes_h[r]] for r in range(world)]
 
 
+class StreamGather:
+    """The per-step gather of every rank's per-chromosome record streams to rank 0 with no host
+    synchronisation inside the step and no padding (the genome job's only exchange,
+    compression.cpp:584-610: one record file per pair).
+
+    A stream's length is a function of its pair's inputs, so the lengths are exchanged once, in
+    plan() (outside the timed region: one all_gather_object of {name: length}), and rank 0
+    preallocates one receive tensor per remote stream of exactly that length.  step() then posts,
+    in one batch_isend_irecv, one send per stream on the other ranks and the matching receives on
+    rank 0 (RCCL point-to-point over xGMI on GPUs, gloo on CPU; both sides post in name order, so
+    messages between two ranks match in order).  The only per-step check is on the host, against
+    lengths the host already holds (the library returns each length synchronously): a stream whose
+    length differs from the plan raises instead of being truncated.  Nothing is read back from the
+    device, and the sends/receives are ordered behind the lanes' streams by stream waits
+    (`after`), not by host syncs."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.plan_lengths: list[dict[str, int]] | None = None
+        self.recv: dict[str, torch.Tensor] = {}
+        self.local: dict[str, torch.Tensor] = {}
+
+    def _peer(self, r: int) -> int:
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
+
+    def plan(self, parts: dict[str, torch.Tensor], device: torch.device) -> None:
+        """Exchange the per-stream lengths (outside the timed region) and allocate rank 0's
+        receive tensors."""
+        mine = {n: int(t.numel()) for n, t in parts.items()}
+        got: list = [None] * self.world
+        dist.all_gather_object(got, mine, group=self.group)
+        self.plan_lengths = got
+        if self.rank == 0:
+            self.recv = {n: torch.empty(ln, dtype=torch.uint8, device=device)
+                         for r in range(1, self.world) for n, ln in sorted(got[r].items())}
+
+    def step(self, parts: dict[str, torch.Tensor], after=()) -> None:
+        """Queue this step's gather.  `after`: CUDA streams the record tensors were written on
+        (the current stream waits for them; nothing waits on the host)."""
+        if self.plan_lengths is None:
+            raise RuntimeError("StreamGather.step before plan()")
+        mine = self.plan_lengths[self.rank]
+        if set(parts) != set(mine):
+            raise RuntimeError("StreamGather: the rank's chromosomes differ from the plan")
+        for n, t in parts.items():
+            if int(t.numel()) != mine[n]:
+                raise RuntimeError(f"StreamGather: record stream {n} is {t.numel()} bytes, the plan has {mine[n]}: "
+                                   "re-plan before the timed region")
+        if torch.cuda.is_available():
+            cur = torch.cuda.current_stream()
+            for s in after:
+                cur.wait_stream(s)
+        self.local = dict(parts)
+        ops = []
+        if self.rank == 0:
+            for r in range(1, self.world):
+                for n in sorted(self.plan_lengths[r]):
+                    if self.recv[n].numel():
+                        ops.append(dist.P2POp(dist.irecv, self.recv[n], self._peer(r), self.group))
+        else:
+            for n in sorted(mine):
+                if parts[n].numel():
+                    ops.append(dist.P2POp(dist.isend, parts[n].reshape(-1), self._peer(0), self.group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()   # (RCCL: the current stream waits; gloo: the host, on CPU tensors)
+
+    def result(self) -> dict[str, torch.Tensor] | None:
+        """Rank 0: {name: record stream tensor} of every rank (after the step's work has run);
+        None elsewhere."""
+        if self.rank != 0:
+            return None
+        out = dict(self.local)
+        out.update(self.recv)
+        return out
+
+
 def pack_records(parts: dict[str, bytes | torch.Tensor], device: torch.device) -> torch.Tensor:
     """One uint8 buffer: int64 header [n_names, len(names blob), len(blob_i)...], the NUL-joined
     names, then the blobs in name order."""

@@ -18,6 +18,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "sccg.h")
 
 SCCG_OK = 0
 SCCG_E_DELTA_STOI = 4
+OPT_EXACT_SWITCH = 1   # sccg_ctx_set_option (include/sccg.h)
 ERRORS = {1: "SCCG_E_INVALID", 2: "SCCG_E_HIP", 3: "SCCG_E_NOMEM", 4: "SCCG_E_DELTA_STOI",
           5: "SCCG_E_FORMAT", 6: "SCCG_E_RANGE", 7: "SCCG_E_PARSE", 8: "SCCG_E_UNSUPPORTED",
           9: "SCCG_E_INTERNAL", 10: "SCCG_E_OPEN_REF", 11: "SCCG_E_OPEN_TGT", 12: "SCCG_E_WRITE"}
@@ -101,6 +102,7 @@ def load_library():
     lib.sccg_last_error.argtypes = [vp]
     lib.sccg_last_error.restype = ctypes.c_char_p
     lib.sccg_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    lib.sccg_ctx_set_option.argtypes = [vp, ctypes.c_int, i64]
     lib.sccg_compress.argtypes = [vp, c, sz, c, sz, ctypes.POINTER(Buf)]
     lib.sccg_compress_device.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
     if hasattr(lib, "sccg_params_default"):   # (absent from builds older than the overrides: A/B runs)
@@ -166,6 +168,17 @@ class Context:
 
     def _err(self, rc: int):
         raise SccgError(rc, self.lib.sccg_last_error(self.ptr).decode(errors="replace"))
+
+    def set_option(self, option: int, value: int) -> None:
+        """sccg_ctx_set_option (include/sccg.h), e.g. OPT_EXACT_SWITCH."""
+        rc = self.lib.sccg_ctx_set_option(self.ptr, option, value)
+        if rc:
+            self._err(rc)
+
+    def exact_switch(self, on: bool = True) -> None:
+        """stats()['switch_segment'] = the reference's first switch (the in-order local pass)
+        instead of any switch window (the default mode probe); the record bytes are the same."""
+        self.set_option(OPT_EXACT_SWITCH, int(on))
 
     def stats(self) -> dict:
         st = Stats()

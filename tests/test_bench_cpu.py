@@ -90,6 +90,113 @@ def test_bench_distributed_pieces_gloo_world2():
     assert ptr is not None and ptr["value"] > 0 and "N = 1" in ptr["measured_in"]
 
 
+class _FakeLane:
+    stream = None
+
+
+class _FakePool:
+    """bench.LanePool's interface: run(order, job) does every pair on some lane."""
+
+    def __init__(self, n_lanes=2):
+        self.lanes = [_FakeLane() for _ in range(n_lanes)]
+
+    def run(self, order, job):
+        for i, n in enumerate(order):
+            job(self.lanes[i % len(self.lanes)], n)
+
+    def sync(self):
+        pass
+
+
+def _step_worker(rank, world, port, q):
+    """bench.make_step -- the step main() times -- with a fake compress job, gloo world 2."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        import multigpu
+        names = multigpu.CHROMS
+        mine = [names[i] for i in multigpu.lpt_shard(multigpu.HG19, world)[rank]]
+        order = sorted(mine, key=lambda n: -multigpu.HG19[names.index(n)])
+        results = {}
+
+        def job(lane, name):   # the fake compress: the pair's record stream into results
+            results[name] = (torch.frombuffer(bytearray(_fake_stream(name)), dtype=torch.uint8), {})
+
+        gather = multigpu.StreamGather()
+        step = bench.make_step(_FakePool(), order, job, results, gather)
+        # host synchronisation inside the timed steps: device reads and host-side collectives
+        syncs = []
+        watch = {"item": torch.Tensor, "tolist": torch.Tensor, "cpu": torch.Tensor, "numpy": torch.Tensor}
+        saved = {k: getattr(c, k) for k, c in watch.items()}
+        saved_sync, saved_ago, saved_ag = torch.cuda.synchronize, dist.all_gather_object, dist.all_gather
+        counting = [False]
+
+        def wrap(name, f):
+            def g(*a, **k):
+                if counting[0]:
+                    syncs.append(name)
+                return f(*a, **k)
+            return g
+        for k, c in watch.items():
+            setattr(c, k, wrap(k, saved[k]))
+        torch.cuda.synchronize = wrap("cuda.synchronize", saved_sync)
+        dist.all_gather_object = wrap("all_gather_object", saved_ago)
+        dist.all_gather = wrap("all_gather", saved_ag)
+        try:
+            step()   # warm-up: the gather's plan (outside the timed region in bench.main)
+
+            def counted_step():
+                counting[0] = True
+                step()
+                counting[0] = False
+            dt = bench.timed_region(counted_step, 3, 0, world)
+        finally:
+            for k, c in watch.items():
+                setattr(c, k, saved[k])
+            torch.cuda.synchronize, dist.all_gather_object, dist.all_gather = saved_sync, saved_ago, saved_ag
+        got = gather.result()
+        streams = {n: bytes(t.numpy().tobytes()) for n, t in got.items()} if got is not None else None
+        # a record stream whose length left the plan is refused, not truncated
+        results[order[0]] = (torch.zeros(3, dtype=torch.uint8), {})
+        try:
+            gather.step({n: results[n][0] for n in order})
+            refused = False
+        except RuntimeError:
+            refused = True
+        q.put((rank, {"dt": dt, "syncs": syncs, "streams": streams, "refused": refused,
+                      "recv_bytes": sum(int(t.numel()) for t in gather.recv.values())}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_step_gather_no_host_sync_gloo_world2():
+    """bench.make_step at N = 2 (gloo): rank 0 ends up with every chromosome's stream, the step
+    reads nothing back and runs no host-side collective (timed_region's barrier + MAX are outside it),
+    rank 0 receives exactly the other rank's bytes (no padding to the largest), and a stream whose
+    length left the plan is refused."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_step_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import multigpu
+    r0, r1 = res[0], res[1]
+    assert r0["streams"] == {n: _fake_stream(n) for n in multigpu.CHROMS}
+    assert r1["streams"] is None
+    assert r0["syncs"] == [] and r1["syncs"] == [], (r0["syncs"], r1["syncs"])
+    rank1 = [multigpu.CHROMS[i] for i in multigpu.lpt_shard(multigpu.HG19, 2)[1]]
+    assert r0["recv_bytes"] == sum(len(_fake_stream(n)) for n in rank1)
+    assert r0["refused"] and r1["refused"]
+
+
 def test_job_models_say_what_they_count():
     """roofline_job's design model (what this design moves: byte copies, no k-mer index) and
     SURVEY §8(d)'s model (2-bit packing, a 4|R'| CSR index this design never builds)."""

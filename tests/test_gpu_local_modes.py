@@ -45,6 +45,7 @@ from pkg import sccg
 from test_gpu_parity import _switch_case
 out = []
 with sccg.Context(0) as ctx:
+    ctx.exact_switch(EXACT)
     for seed, nseg, plant, gap in CASES:
         rfa, tfa = _switch_case(seed, nseg=nseg, plant_at=plant, gap=gap)
         rec = ctx.compress(rfa, tfa)
@@ -65,11 +66,16 @@ def want():
     return res
 
 
-@pytest.mark.parametrize("mode", ["0", "1"], ids=["walk_every_segment", "prove_first"])
-def test_local_modes_vs_oracle(want, mode):
+@pytest.mark.parametrize("mode,exact", [("0", True), ("1", True), ("1", False)],
+                         ids=["walk_every_segment", "prove_first", "prove_first_probe"])
+def test_local_modes_vs_oracle(want, mode, exact):
     env = dict(os.environ, SCCG_LOCAL_PROVE=mode)
-    p = subprocess.run([sys.executable, "-c", f"HERE = {HERE!r}\nCASES = {CASES!r}\n" + CHILD], env=env,
-                       capture_output=True, text=True, timeout=300)
+    p = subprocess.run([sys.executable, "-c", f"HERE = {HERE!r}\nCASES = {CASES!r}\nEXACT = {exact!r}\n" + CHILD],
+                       env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     got = json.loads(p.stdout.strip().splitlines()[-1])
-    assert got == want
+    if exact:
+        assert got == want
+    else:   # the mode probe: same bytes and mode, a switch window at or after the first
+        assert [g[:2] for g in got] == [w[:2] for w in want]
+        assert all(g[2] == w[2] if w[2] < 0 else g[2] >= w[2] for g, w in zip(got, want))

@@ -154,7 +154,7 @@ def test_chr1_roundtrip(ctx):
     assert ctx.reconstruct(rec, rfa) == tfa
 
 
-def _switch_case(seed: int, nseg: int = 2400, plant_at: int | None = None, gap=None):
+def _switch_case(seed: int, nseg: int = 2400, plant_at=None, gap=None):
     """Segment-kind patterns for the local->global switch (compression.cpp:462-473): identical
     segments (good), unrelated random ones (failed or mostly literal), half-copied ones (matched
     but > 50 % literal), all-N ones (failed, all N: resets the counter) and poly-A ones (failed,
@@ -177,9 +177,10 @@ def _switch_case(seed: int, nseg: int = 2400, plant_at: int | None = None, gap=N
         g0, gl, gk = gap
         kinds[g0:g0 + gl] = rng.choice(list(gk), size=len(kinds[g0:g0 + gl]))
     plant = [None, 4, 5, 9, 63, 64, 65, 1000, 4095, nseg - 1][seed % 10] if plant_at is None else plant_at
-    if plant is not None and plant < nseg:
-        kinds[max(0, plant - 4):plant + 1] = rng.choice([1, 2, 4], size=min(plant + 1, 5))   # ... but this one
-        kinds[plant] = 4
+    for p in (plant if isinstance(plant, (list, tuple)) else [plant]):   # (several windows: a list)
+        if p is not None and p < nseg:
+            kinds[max(0, p - 4):p + 1] = rng.choice([1, 2, 4], size=min(p + 1, 5))   # ... but this one
+            kinds[p] = 4
     for s, k in enumerate(kinds):
         seg = slice(s * 1000, (s + 1) * 1000)
         if k == 1:
@@ -194,18 +195,76 @@ def _switch_case(seed: int, nseg: int = 2400, plant_at: int | None = None, gap=N
     return fa(b"r", r), fa(b"t", t)
 
 
+class _exact:
+    """The context in SCCG_OPT_EXACT_SWITCH mode for one test (stats report the first switch)."""
+
+    def __init__(self, ctx, on=True):
+        self.ctx, self.on = ctx, on
+
+    def __enter__(self):
+        self.ctx.exact_switch(self.on)
+
+    def __exit__(self, *a):
+        self.ctx.exact_switch(False)
+
+
+def _probe_runs(nseg: int) -> list[range]:
+    """The segment runs local.hip's k_local_probe classifies (PROBE_RUN 8, PROBE_RUNS 16; pairs
+    of at least 512 segments)."""
+    if nseg < 512:
+        return []
+    return [range(a, a + 8) for a in ((j + 1) * (nseg - 8) // 16 for j in range(16))]
+
+
+@pytest.mark.parametrize("exact", [True, False], ids=["exact", "probe"])
 @pytest.mark.parametrize("seed", range(20))
-def test_switch_window_vs_oracle(ctx, seed):
-    """The fused local kernel's switch detection against the oracle's state machine."""
+def test_switch_window_vs_oracle(ctx, seed, exact):
+    """The fused local kernel's switch detection against the oracle's state machine: the exact
+    first switch in SCCG_OPT_EXACT_SWITCH mode; the default mode's probe reports a switch window
+    at or after it (the record bytes and the mode are the same)."""
     rfa, tfa = _switch_case(seed)
     want = oraclelib.compress(rfa, tfa)
     mode_global, sw = oraclelib.last_mode()
-    got, rc = _gpu_compress(ctx, rfa, tfa)
+    with _exact(ctx, exact):
+        got, rc = _gpu_compress(ctx, rfa, tfa)
+        st = ctx.stats()
     assert rc == 0
-    st = ctx.stats()
     assert bool(st["mode_global"]) == mode_global
-    assert st["switch_segment"] == (sw if mode_global else -1)
+    if exact or not mode_global:
+        assert st["switch_segment"] == (sw if mode_global else -1)
+    else:
+        assert st["switch_segment"] >= sw
     assert got == want
+
+
+# (nseg, planted windows): a first window the probe does not see and a later one inside probe run
+# 0 / 9 / 15 (the last segments), a window only inside a probe run, and windows straddling a run's
+# first segment (its 5 segments are not all inside the run: the probe must not count it)
+PROBE_CASES = [(2400, [40, 155]), (2400, [300, 1350]), (2400, [40, 2399]), (2400, [1353]), (2400, [2396]),
+               (2400, [150]), (17000, [3000, 16996]), (17000, [10000])]
+
+
+@pytest.mark.parametrize("nseg,plants", PROBE_CASES)
+def test_switch_probe_vs_oracle(ctx, nseg, plants):
+    """The mode probe (local.hip k_local_probe): a window inside a probed run decides the mode at
+    once, and the record file equals the reference's wherever the first switch lies
+    (compression.cpp:462-473 truncates the file, :484-574 regenerates it); with
+    SCCG_OPT_EXACT_SWITCH the first switch is reported."""
+    rfa, tfa = _switch_case(900 + nseg % 7 + plants[0], nseg=nseg, plant_at=plants)
+    want = oraclelib.compress(rfa, tfa)
+    mode_global, sw = oraclelib.last_mode()
+    assert mode_global
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    st = ctx.stats()
+    assert rc == 0 and got == want
+    assert st["mode_global"] == 1 and st["switch_segment"] >= sw
+    in_run = [r for r in _probe_runs(nseg) if st["switch_segment"] in r]
+    if st["switch_segment"] != sw:   # a later window: the probe's, inside one of its runs
+        assert in_run and st["switch_segment"] - 4 >= in_run[0].start
+    with _exact(ctx):
+        got2, rc2 = _gpu_compress(ctx, rfa, tfa)
+        st2 = ctx.stats()
+    assert rc2 == 0 and got2 == want and st2["switch_segment"] == sw
 
 
 @pytest.mark.parametrize("seed", range(16, 64))
@@ -473,9 +532,12 @@ def test_switch_deep_vs_oracle(ctx, plant):
     rfa, tfa = _switch_case(700 + (plant or 0) % 97, nseg=17000, plant_at=plant)
     want = oraclelib.compress(rfa, tfa)
     mode_global, sw = oraclelib.last_mode()
-    got, rc = _gpu_compress(ctx, rfa, tfa)
+    with _exact(ctx):
+        got, rc = _gpu_compress(ctx, rfa, tfa)
+        st = ctx.stats()
     assert rc == 0
-    st = ctx.stats()
     assert bool(st["mode_global"]) == mode_global
     assert st["switch_segment"] == (sw if mode_global else -1)
     assert got == want
+    got2, rc2 = _gpu_compress(ctx, rfa, tfa)   # default mode: the same bytes
+    assert rc2 == 0 and got2 == want and ctx.stats()["mode_global"] == int(mode_global)

@@ -321,3 +321,15 @@ def test_genome_worker_closes_context_on_error(tmp_path):
                                         2, contexts=1)
     assert stats["chrB"]["rc"] != 0 and stats["chrA"]["rc"] == 0 and stats["chrC"]["rc"] == 0
     assert closed == [1] and em.wait() == 1
+
+
+def test_cost_weights_one_unit():
+    """genome.py --cost: pairs missing from the cost file are weighed in the file's unit (median
+    cost per target byte), not in bytes next to milliseconds."""
+    import genome
+    names, sizes = ["a", "b", "c", "d"], [100_000_000, 200_000_000, 50_000_000, 150_000_000]
+    w = genome.cost_weights(names, sizes, {"a": 10.0, "b": 30.0, "c": 5.0})
+    assert w[:3] == [10.0, 30.0, 5.0]
+    assert w[3] == pytest.approx(150_000_000 * 1e-7)   # median of 1e-7, 1.5e-7, 1e-7 ms per byte
+    parts = multigpu.lpt_shard(w, 2)   # 30 | 15 + 10 + 5 (in bytes, "d" would sit alone on a rank)
+    assert sorted(sum(w[i] for i in p) for p in parts) == [30.0, 30.0]
