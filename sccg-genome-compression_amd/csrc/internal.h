@@ -155,7 +155,15 @@ int launch_local_pass(int k, int pass, int upper, const uint8_t* R, int64_t nR, 
 // entry; cls: per-segment classes tagged with gen (never cleared: zero-filled once, gen >= 1).
 // Each segment is first tried by the class-0 proof (seg_prove; SCCG_LOCAL_PROVE=0 walks every one).
 int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
-                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, bool exact_switch, hipStream_t s);
+                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s);
+// The switch-window probe (local.hip k_local_probe): classes of PROBE_PAIRS segments in runs spread
+// over the pair into pout[0 .. PROBE_PAIRS) (-1 unknown) and their segment indices into
+// pout[PROBE_PAIRS ..); local_probe_window finds the first window among them on the host (-1: none).
+constexpr int PROBE_PAIRS = 128;
+int local_probe_applies(int64_t nseg_max);
+int launch_local_probe(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int32_t* pout,
+                       hipStream_t s);
+int local_probe_window(const int32_t* pout);
 // record text for local mode (delta-encoded, compression.cpp:406-415 + :222-304) + leftover
 // (abs_p: "(p," with absolute p instead, the text before delta_encode)
 int launch_local_emit(const uint8_t* T, int64_t nT, int64_t iters, const uint32_t* recs,

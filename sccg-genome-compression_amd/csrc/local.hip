@@ -26,7 +26,6 @@ constexpr int SEGB = 1024;        // LDS bytes per segment string (1000 + zero p
 constexpr int NBB = 9;            // 512 k-mer buckets
 constexpr int NB = 1 << NBB;
 constexpr int MANY = 4;           // more candidates than this: extend one per lane
-constexpr int32_t PASS_ABORTED = -2;   // a walk stopped at its step budget (switch probe only)
 constexpr int32_t PASS_NEED_K2 = -3;   // a proved segment whose k pass found no match (launch_local_proven)
 
 struct SegLds {
@@ -255,27 +254,13 @@ __device__ __forceinline__ bool seg_prove(const uint8_t* Lr, const uint8_t* Lt, 
     return any && 2 * (unc + (nt - 1 - lastk)) <= nt;
 }
 
-template <int K, bool DBG>
-__device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pass, int non_n_prev, int upper,
-                                                 const uint8_t* __restrict__ R, int64_t nR, const uint8_t* __restrict__ T,
-                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr,
-                                                 int loaded = -1, int budget = INT32_MAX) {
+// H of compression.cpp:41-47 for one segment: every K-mer of the reference segment in LDS,
+// counting-sorted by bucket (lane l owns starts 16l..16l+15); L.bstart[b] .. L.bstart[b+1] hold
+// bucket b's keys (L.skey) and positions (L.spos).
+template <int K>
+__device__ __forceinline__ void seg_table(SegLds& L, int nr) {
     const int lane = lane_id();
-    const int64_t base = seg * SEG_L;
-    const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
-    const int nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
     constexpr uint32_t MASK = (1u << (2 * K)) - 1u, KM = (1u << K) - 1u;
-    uint64_t tq = DBG ? wall_clock64() : 0, tph[5] = {0, 0, 0, 0, 0};
-    auto tick = [&](int i) {
-        if (DBG) { const uint64_t t = wall_clock64(); tph[i] += t - tq; tq = t; }
-    };
-
-    // ---- both segments in LDS (loaded >= 0: already there, `loaded` = its non-N flag)
-    const bool non_n = loaded >= 0 ? loaded != 0 : seg_load(L, seg, upper, R, nR, T, nT, pre);
-    tick(0);
-
-    // ---- H: every k-mer of the reference segment (compression.cpp:41-47), counting-sorted by
-    //      bucket; lane l owns starts 16l..16l+15
     const int lastr = nr - K;
     uint32_t* cnt = L.skey;   // bucket counters live where the keys go later
     for (int i = lane; i < NB; i += 64) cnt[i] = 0;
@@ -318,6 +303,58 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
         }
     }
     wave_sync();
+}
+
+// Hit positions of the target segment: y in [0, nt - K] whose K-mer occurs among the reference
+// segment's (compression.cpp:77 H.find succeeds); the table is seg_table<K>'s.  Pure keys only
+// (the caller has excluded segments holding bytes outside ACGT).  Counts up to at least `cap`.
+template <int K>
+__device__ __forceinline__ int seg_hits(const SegLds& L, int nr, int nt) {
+    const int lane = lane_id();
+    constexpr uint32_t MASK = (1u << (2 * K)) - 1u;
+    const int lastk = nt - K;
+    if (nr < K || lastk < 0) return 0;
+    const int p0 = lane * 16;
+    uint64_t code = 0;
+    uint32_t bad = 0;
+    if (p0 <= lastk) keys16<K>(&L.t[p0], code, bad);
+    int h = 0;
+#pragma unroll
+    for (int st = 0; st < 16; st++) {
+        if (p0 + st <= lastk) {
+            const uint32_t key = (uint32_t)(code >> (2 * st)) & MASK;
+            const uint32_t b = slot_hash(key, NBB);
+            const int e1 = (int)L.bstart[b + 1];
+            bool hit = false;
+            for (int e = (int)L.bstart[b]; e < e1 && !hit; e++) hit = L.skey[e] == key;
+            h += hit;
+        }
+    }
+    return wave_sum(h);
+}
+
+template <int K, bool DBG>
+__device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pass, int non_n_prev, int upper,
+                                                 const uint8_t* __restrict__ R, int64_t nR, const uint8_t* __restrict__ T,
+                                                 int64_t nT, uint32_t* __restrict__ recs, const SegWords* pre = nullptr,
+                                                 int loaded = -1) {
+    const int lane = lane_id();
+    const int64_t base = seg * SEG_L;
+    const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L);
+    const int nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
+    constexpr uint32_t MASK = (1u << (2 * K)) - 1u, KM = (1u << K) - 1u;
+    uint64_t tq = DBG ? wall_clock64() : 0, tph[5] = {0, 0, 0, 0, 0};
+    auto tick = [&](int i) {
+        if (DBG) { const uint64_t t = wall_clock64(); tph[i] += t - tq; tq = t; }
+    };
+
+    // ---- both segments in LDS (loaded >= 0: already there, `loaded` = its non-N flag)
+    const bool non_n = loaded >= 0 ? loaded != 0 : seg_load(L, seg, upper, R, nR, T, nT, pre);
+    tick(0);
+
+    seg_table<K>(L, nr);
+    const int lastr = nr - K;
+    wave_sync();
     tick(1);
     tick(2);
     tick(3);
@@ -329,9 +366,7 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     const int lastk = nt - K;
     uint32_t* out = recs + seg * SEG_REC_CAP;
     int idx = 0, pme = -1, nrec = 0, nmatch = 0, lit = 0, firstp = -1, lastp = -1;
-    bool aborted = false;
     for (;;) {
-        if (nmatch >= budget) { aborted = true; break; }   // (the switch probe's step budget)
         // next target position >= idx with a candidate (and its key)
         int nxt = -1;
         uint32_t key = 0;
@@ -483,7 +518,7 @@ __device__ __forceinline__ SegStat local_segment(SegLds& L, int64_t seg, int pas
     s.nrec = nrec;
     s.nmatch = nmatch;
     s.lit = lit;
-    s.pass = aborted ? PASS_ABORTED : nmatch ? pass : 0;
+    s.pass = nmatch ? pass : 0;
     s.non_n = pass == 1 ? (int)non_n : non_n_prev;
     s.first_p = firstp;
     s.last_p = lastp;
@@ -616,82 +651,101 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
 }
 
 // ---------------------------------------------------------------------------------------------
-// Switch probe (round 6; the default unless the caller asks for the exact switch segment).  The
-// machine switches iff SOME window of 5 class-1/2 segments ends in a class-2 segment (the counter is
-// a run length reset by class 0/3, and a window at e makes it switch at e unless it did before), and
-// a switching pair's record file does not depend on where it switched (compression.cpp:462-473 -- the
-// file is truncated and the global pass regenerates it, :484-574).  So one complete window anywhere
-// decides the mode.  Drifted hg/T2T pairs are full of them past their first switch (segment pairs
-// that no longer overlap fail both passes or match by chance: classes 1 and 2), so PROBE_RUNS runs of
-// PROBE_RUN consecutive segments spread over the pair are classified first, one wave per segment,
-// and a window inside any run lowers the in-order pass's bound below every segment (ctl[1] = -1:
-// k_local_all starts nothing) and records its end in ctl[2].  No window: the in-order pass runs as
-// before (the probed segments' classes, records and stats are the ones it recomputes).
+// Switch probe (round 6; the default unless the caller asks for the exact switch segment,
+// SCCG_OPT_EXACT_SWITCH).  The machine switches iff SOME window of 5 class-1/2 segments ends in a
+// class-2 segment (the counter is a run length reset by class 0/3, and a window at e makes it switch
+// at e unless it did before), and a switching pair's record file does not depend on where it
+// switched (compression.cpp:462-473 -- the file is truncated and the global pass regenerates it,
+// :484-574).  So one complete window anywhere decides the mode.  Drifted hg/T2T pairs are full of
+// them past their first switch (segment pairs that no longer overlap fail both passes or match by
+// chance: classes 1 and 2), so PROBE_RUNS runs of PROBE_RUN consecutive segments spread over the pair
+// are classified first, one wave per segment, from their k2 hit counts alone (below).  The host reads
+// the 128 classes back behind the walk's first rounds (sccg_api.cpp decide_probe): a window among
+// them decides the pair global and the in-order pass (k_local_all) is never launched; otherwise it
+// runs as before.
 // ---------------------------------------------------------------------------------------------
 constexpr int PROBE_RUN = 8, PROBE_RUNS = 16, PROBE_MIN_SEGS = 4 * PROBE_RUN * PROBE_RUNS;
-// SCCG_DEBUG: per probed segment {start, after load+prove, after k, after k2, end} (wall clock) and its class
+static_assert(PROBE_RUN * PROBE_RUNS == PROBE_PAIRS, "internal.h's probe size");
+// run r starts at (r + 1) nseg / (RUNS + 1): spread over the pair, clear of its last segments
+// (telomere gaps)
+__device__ __forceinline__ int32_t probe_run_start(int32_t r, int32_t nseg) {
+    return (int32_t)((int64_t)(r + 1) * nseg / (PROBE_RUNS + 1)) - PROBE_RUN / 2;
+}
+// bytes of w (the first `valid` of its 4) outside A, C, G, T (uppercased)
+__device__ __forceinline__ bool non_acgt4(uint32_t w, int valid) {
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t b = (w >> (8 * q)) & 0xffu;
+        bad |= q < valid && b != 'A' && b != 'C' && b != 'G' && b != 'T';
+    }
+    return bad;
+}
+// SCCG_DEBUG: per probed segment {start, after the load, -, -, end} (wall clock), its class and k2 hits
 __device__ unsigned long long g_probe_dbg[PROBE_RUNS * PROBE_RUN][6];
-// A segment's walk stops after `budget` matches (repeat-rich drifted segments take hundreds of short
-// chance matches, ~0.5 ms for one wave, and the probe is as slow as its slowest segment): its class
-// is then unknown (-1, no window holds it) and nothing is published for it.
+// One wave per workgroup: beside the other pairs' walks and strips, which fill most CUs' registers,
+// a 9 KiB / one-wave group finds a slot at once (an 8-wave group of a whole run, 74 KiB of LDS and
+// two waves' registers on every SIMD, waited ~0.5 ms for a CU to drain).  Each wave writes its
+// segment's class (or -1) and index to pout; the host looks for windows (local_probe_window).
 template <bool DBG>
-__global__ __launch_bounds__(64 * PROBE_RUN) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_probe(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_probe(
     const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR, const uint8_t* __restrict__ T,
-    const int64_t* __restrict__ dnT, uint32_t* __restrict__ recs, SegStat* __restrict__ stat, int32_t* __restrict__ cls,
-    int32_t gen, int32_t* __restrict__ ctl, int prove, int budget) {
+    const int64_t* __restrict__ dnT, int32_t* __restrict__ pout) {
     unsigned long long tk[5] = {DBG ? (unsigned long long)wall_clock64() : 0ull, 0, 0, 0, 0};
-    __shared__ SegLds lds_all[PROBE_RUN];
-    __shared__ int32_t rc[PROBE_RUN];
+    __shared__ SegLds L;
     const int64_t nR = *dnR, nT = *dnT;
     const int32_t nseg = seg_count(nR, nT);
-    if (nseg < PROBE_MIN_SEGS) return;   // (block-uniform) small pairs: the in-order pass is cheap
-    const int w = wave_in_block(), lane = lane_id();
-    // run j starts at (j + 1)(nseg - RUN) / RUNS: the last run ends at the last segment
-    const int32_t a = (int32_t)((int64_t)(blockIdx.x + 1) * (nseg - PROBE_RUN) / PROBE_RUNS);
-    const int32_t seg = a + w;
-    SegLds& L = lds_all[w];
-    const bool non_n = seg_load(L, seg, 1, R, nR, T, nT, nullptr);
+    const int lane = lane_id();
+    if (nseg < PROBE_MIN_SEGS) {   // (uniform) small pairs: the in-order pass is cheap
+        if (lane == 0) { pout[blockIdx.x] = -1; pout[PROBE_RUNS * PROBE_RUN + blockIdx.x] = -1; }
+        return;
+    }
+    const int32_t r = (int32_t)blockIdx.x / PROBE_RUN, w = (int32_t)blockIdx.x % PROBE_RUN;
+    const int32_t seg = probe_run_start(r, nseg) + w;
+    (void)seg_load(L, seg, 1, R, nR, T, nT, nullptr);
+    if (DBG) tk[1] = wall_clock64();
     const int64_t base = (int64_t)seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L), nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
-    SegStat st;
-    int c;
-    const bool proved = prove && seg_prove(L.r, L.t, nr, nt);
-    if (DBG) tk[1] = tk[2] = tk[3] = wall_clock64();
-    if (proved) {   // exactly as k_local_all
-        st = SegStat{0, 0, 0, PASS_PROVEN, (int)non_n, -1, -1, nt};
-        c = 0;
-    } else {
-        st = local_segment<14, false>(L, seg, 1, 0, 1, R, nR, T, nT, recs, nullptr, (int)non_n, budget);
-        if (DBG) tk[2] = tk[3] = wall_clock64();
-        if (!st.pass) {
-            wave_sync();
-            st = local_segment<10, false>(L, seg, 2, st.non_n, 1, R, nR, T, nT, recs, nullptr, 1, budget);
-            if (DBG) tk[3] = wall_clock64();
+    // A segment pair holding any byte outside ACGT is left unknown: an all-N reference segment puts
+    // its ~1000 identical k-mers into one LDS bucket, which every target lane hashing there scans in
+    // full on each probe step (such pairs -- assembly gaps, telomeres -- took 0.2-0.8 ms per pass
+    // beside the genome's other kernels).  The in-order pass classifies them when it has to.
+    bool exotic = false;
+    {
+        const uint32_t* r4 = reinterpret_cast<const uint32_t*>(L.r);
+        const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.t);
+#pragma unroll
+        for (int j = 0; j < SEGB / 256; j++) {
+            const int i = lane + 64 * j, b0 = 4 * i;
+            exotic = exotic || non_acgt4(r4[i], nr - b0) || non_acgt4(t4[i], nt - b0);
         }
-        c = st.pass == PASS_ABORTED ? -1 : seg_class(st);
+        exotic = __ballot(exotic) != 0;
     }
+    // The k2 hit positions decide the class of a segment pair with few of them.  Every match a pass
+    // takes (compression.cpp:64-161, local: no gate) starts at a hit position, a match of length l
+    // covers l - k + 1 hit positions of its diagonal, and a k-mer hit's first 10 bases are a k2 hit:
+    // so either pass matches at most 14 h10 bases.  h10 = 0: neither pass finds a match (class 2 --
+    // non-N: the pair is pure ACGT); 28 h10 < nt: whichever pass succeeds leaves more than half of
+    // the segment literal (class 1, :417-421).  More hits: unknown (such a pair is usually aligned,
+    // class 0, and no window holds it either way).  tests/test_local_proof_cpu.py checks the rule
+    // against the oracle's passes.
+    int c = -1, h10 = 0;
+    if (!exotic) {
+        seg_table<10>(L, nr);
+        h10 = seg_hits<10>(L, nr, nt);
+        if (h10 == 0) c = 2;
+        else if (28 * h10 < nt) c = 1;
+    }
+    if (DBG) tk[2] = tk[3] = wall_clock64();
     if (DBG && lane == 0) {
         tk[4] = wall_clock64();
-        unsigned long long* d = g_probe_dbg[blockIdx.x * PROBE_RUN + w];
+        unsigned long long* d = g_probe_dbg[blockIdx.x];
         for (int i = 0; i < 5; i++) d[i] = tk[i];
-        d[5] = (unsigned long long)(c + 1) | ((unsigned long long)st.nmatch << 8) | ((unsigned long long)seg << 32);
+        d[5] = (unsigned long long)(c + 1) | ((unsigned long long)h10 << 8) | ((unsigned long long)seg << 32);
     }
-    if (lane == 0 && c < 0) rc[w] = c;
-    if (lane == 0 && c >= 0) {
-        stat[seg] = st;
-        __hip_atomic_store(&cls[seg], (gen << 2) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rc[w] = c;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t hit = INT32_MAX;
-        for (int e = PROBE_RUN - 1; e >= 4; e--)
-            if (rc[e] == 2 && mism(rc[e - 1]) && mism(rc[e - 2]) && mism(rc[e - 3]) && mism(rc[e - 4])) hit = a + e;
-        if (hit != INT32_MAX) {
-            __hip_atomic_fetch_min(&ctl[2], hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_min(&ctl[1], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    // (nothing else is written: a window makes the pair global, and without one the in-order pass
+    // computes every segment's records, statistics and class itself)
+    if (lane == 0) { pout[blockIdx.x] = c; pout[PROBE_RUNS * PROBE_RUN + blockIdx.x] = seg; }
 }
 
 __global__ void k_switch_final(const int32_t* __restrict__ cls, int32_t gen, const int64_t* __restrict__ dnR,
@@ -880,37 +934,55 @@ int launch_local_proven(const uint8_t* R, int64_t nR, const uint8_t* T, int64_t 
     return rc ? rc : launch_local_pass(10, 4, 1, R, nR, T, nT, 0, iters, recs, stat, s);
 }
 
-int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
-                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, bool exact_switch,
-                     hipStream_t s) {
-    if (nseg_max <= 0) return 0;
-    // the switch probe (any window decides the mode); the exact first switch needs the in-order pass
-    static const bool probe_on = [] { const char* e = getenv("SCCG_SWITCH_PROBE"); return e && atoi(e) != 0; }();
-    static const int budget = [] { const char* e = getenv("SCCG_PROBE_BUDGET"); const int v = e ? atoi(e) : 0; return v > 0 ? v : 32; }();
-    static const bool pdbg = getenv("SCCG_DEBUG") != nullptr;
-    if (probe_on && !exact_switch && nseg_max >= PROBE_MIN_SEGS) {
-        if (!pdbg) {
-            PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<false>, dim3(PROBE_RUNS), dim3(64 * PROBE_RUN), 0, s, R, d_nR, T, d_nT,
-                        recs, stat, cls, gen, ctl, local_prove(), budget);
-        } else {
-            const unsigned long long z[PROBE_RUNS * PROBE_RUN][6] = {};
-            SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_probe_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
-            PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<true>, dim3(PROBE_RUNS), dim3(64 * PROBE_RUN), 0, s, R, d_nR, T, d_nT,
-                        recs, stat, cls, gen, ctl, local_prove(), budget);
-            unsigned long long d[PROBE_RUNS * PROBE_RUN][6];
-            SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_probe_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
-            SCCG_HIP(hipStreamSynchronize(s));
-            unsigned long long t0 = ~0ull;
-            for (auto& x : d) if (x[0] && x[0] < t0) t0 = x[0];
-            for (int i = 0; i < PROBE_RUNS * PROBE_RUN; i++) {
-                const auto& x = d[i];
-                if (!x[0]) continue;
-                fprintf(stderr, "[probe] seg %llu class %d matches %llu: start %.1f prove %.1f k %.1f k2 %.1f end %.1f us\n",
-                        x[5] >> 32, (int)(x[5] & 0xff) - 1, (x[5] >> 8) & 0xffffff, (x[0] - t0) / 100.0, (x[1] - x[0]) / 100.0,
-                        (x[2] - x[1]) / 100.0, (x[3] - x[2]) / 100.0, (x[4] - x[0]) / 100.0);
-            }
+int local_probe_applies(int64_t nseg_max) {
+    static const bool probe_on = [] { const char* e = getenv("SCCG_SWITCH_PROBE"); return !e || atoi(e) != 0; }();
+    return probe_on && nseg_max >= PROBE_MIN_SEGS;
+}
+
+int local_probe_window(const int32_t* pout) {
+    int32_t best = -1;
+    for (int r = 0; r < PROBE_RUNS; r++) {
+        const int32_t* c = pout + r * PROBE_RUN;
+        for (int i = 4; i < PROBE_RUN; i++) {
+            const bool m4 = (c[i - 1] == 1 || c[i - 1] == 2) && (c[i - 2] == 1 || c[i - 2] == 2) &&
+                            (c[i - 3] == 1 || c[i - 3] == 2) && (c[i - 4] == 1 || c[i - 4] == 2);
+            const int32_t e = pout[PROBE_RUNS * PROBE_RUN + r * PROBE_RUN + i];
+            if (c[i] == 2 && m4 && e >= 4 && (best < 0 || e < best)) best = e;
         }
     }
+    return best;
+}
+
+int launch_local_probe(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int32_t* pout,
+                       hipStream_t s) {
+    static const bool pdbg = getenv("SCCG_DEBUG") != nullptr;
+    constexpr int NP = PROBE_RUNS * PROBE_RUN;
+    if (!pdbg) {
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<false>, dim3(NP), dim3(64), 0, s, R, d_nR, T, d_nT, pout);
+    } else {
+        const unsigned long long z[NP][6] = {};
+        SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_probe_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<true>, dim3(NP), dim3(64), 0, s, R, d_nR, T, d_nT, pout);
+        unsigned long long d[NP][6];
+        SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_probe_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
+        SCCG_HIP(hipStreamSynchronize(s));
+        unsigned long long t0 = ~0ull;
+        for (auto& x : d) if (x[0] && x[0] < t0) t0 = x[0];
+        for (int i = 0; i < NP; i++) {
+            const auto& x = d[i];
+            if (!x[0]) continue;
+            fprintf(stderr, "[probe] seg %llu class %d k2 hits %llu: start %.1f load %.1f end %.1f us\n",
+                    x[5] >> 32, (int)(x[5] & 0xff) - 1, (x[5] >> 8) & 0xffffff, (x[0] - t0) / 100.0, (x[1] - x[0]) / 100.0,
+                    (x[4] - x[0]) / 100.0);
+        }
+    }
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int64_t nseg_max,
+                     uint32_t* recs, SegStat* stat, int32_t* cls, int32_t gen, int32_t* ctl, hipStream_t s) {
+    if (nseg_max <= 0) return 0;
     // resident capacity: the grid drains the counter, extra blocks would only find it exhausted
     static const unsigned cap = [] {
         int dev = 0, cus = 256, per = 4;

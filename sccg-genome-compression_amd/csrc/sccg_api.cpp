@@ -165,8 +165,9 @@ struct sccg_ctx {
     hipStream_t side = nullptr;       // walk preparation, overlapping the local pass
     hipStream_t side2 = nullptr;      // header + run lines, overlapping the local pass
     hipEvent_t ev_fork = nullptr, ev_fork2 = nullptr, ev_join = nullptr, ev_lines = nullptr, ev_rstrip = nullptr, ev_hdr = nullptr, ev_tstrip = nullptr,
-               ev_local = nullptr;
+               ev_local = nullptr, ev_probe = nullptr;
     int64_t* h_switch = nullptr;      // pinned: the local pass's switch word, copied behind the pass
+    int32_t* h_probe = nullptr;       // pinned: the switch probe's classes and segments (2 PROBE_PAIRS)
     std::string err;
     sccg_stats stats{};
     void* buf[B_COUNT] = {};
@@ -259,6 +260,8 @@ int sccg_ctx_create(int device, sccg_ctx** out) {
         hipEventCreateWithFlags(&c->ev_rstrip, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_hdr, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_local, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_probe, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c->h_probe), 2 * PROBE_PAIRS * sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&c->h_switch), 64, hipHostMallocDefault) != hipSuccess) {
         delete c;
         return SCCG_E_HIP;
@@ -285,6 +288,8 @@ void sccg_ctx_destroy(sccg_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_rstrip);
     (void)hipEventDestroy(ctx->ev_hdr);
     (void)hipEventDestroy(ctx->ev_local);
+    if (ctx->ev_probe) (void)hipEventDestroy(ctx->ev_probe);
+    if (ctx->h_probe) (void)hipHostFree(ctx->h_probe);
     if (ctx->h_switch) (void)hipHostFree(ctx->h_switch);
     for (int i = 0; i < 16; i++) {
         if (ctx->stage[i]) (void)hipHostFree(ctx->stage[i]);
@@ -600,7 +605,9 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     const int64_t iters_max = ((rn < tn ? rn : tn) + SEG_L - 1) / SEG_L;   // FASTA lengths bound the sequences'
     GET(uint32_t, recs, B_RECS, (iters_max > 0 ? iters_max : 1) * SEG_REC_CAP);
     GET(SegStat, stat, B_STAT, iters_max > 0 ? iters_max : 1);
-    GET(int32_t, cls, B_SEGCLS, iters_max > 0 ? iters_max : 1);
+    // (the switch probe's output after the classes: 2 PROBE_PAIRS words)
+    GET(int32_t, cls, B_SEGCLS, (iters_max > 0 ? iters_max : 1) + 2 * PROBE_PAIRS);
+    int32_t* probe_out = cls + (iters_max > 0 ? iters_max : 1);
     int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
     // Where the local pass goes.  It fills every CU while it runs (LDS and VGPRs), but only the final
     // record text needs it; the global walk (side stream) is the critical path of a switching pair.
@@ -608,14 +615,13 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     //   first-step statistics);  2: behind walk round 1 (SCCG_LOCAL_ORDER, tuning runs)
     static const int local_order = [] { const char* e = getenv("SCCG_LOCAL_ORDER"); const int v = e ? atoi(e) : 0; return v >= 0 && v <= 2 ? v : 0; }();
     bool local_launched = false;
-    auto launch_local = [&](hipStream_t after) -> int {
-        if (local_launched) return 0;
-        local_launched = true;
-        if (after) {
-            HIPTRY(hipEventRecord(ctx->ev_fork2, after));
-            HIPTRY(hipStreamWaitEvent(s, ctx->ev_fork2, 0));
-        }
-        if (iters_max > 0 && !force_global) {
+    // The switch probe (default; not with SCCG_OPT_EXACT_SWITCH): a few runs of segments spread over
+    // the pair are classified first (local.hip k_local_probe); one complete switch window among them
+    // decides the pair global (a switching pair's record file does not depend on where it switched,
+    // compression.cpp:462-473, :484-574), so the in-order pass is launched only when they hold none.
+    // The host reads the probe's 1 KiB back behind the walk's first rounds (decide_probe).
+    bool probe_pending = false;
+    auto launch_inorder = [&]() -> int {
         if (cls != ctx->cls_buf || ctx->cap[B_SEGCLS] != ctx->cls_cap || ctx->cls_gen >= (1 << 28)) {
             // a new buffer (or tags about to wrap): zero it once, so no stale tag can match
             HIPTRY(hipMemsetAsync(cls, 0, ctx->cap[B_SEGCLS], s));
@@ -625,7 +631,25 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         }
         const int32_t gen = ++ctx->cls_gen;
         // one launch over every segment; segments past a detected switch are never started
-        TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, ctx->exact_switch, s));
+        TRY(launch_local_all(R, sc + 7, T, sc + 2, iters_max, recs, stat, cls, gen, ctl, s));
+        return 0;
+    };
+    auto launch_local = [&](hipStream_t after) -> int {
+        if (local_launched) return 0;
+        local_launched = true;
+        if (after) {
+            HIPTRY(hipEventRecord(ctx->ev_fork2, after));
+            HIPTRY(hipStreamWaitEvent(s, ctx->ev_fork2, 0));
+        }
+        if (iters_max > 0 && !force_global) {
+            if (!ctx->exact_switch && local_probe_applies(iters_max)) {
+                TRY(launch_local_probe(R, sc + 7, T, sc + 2, probe_out, s));
+                HIPTRY(hipMemcpyAsync(ctx->h_probe, probe_out, 2 * PROBE_PAIRS * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+                HIPTRY(hipEventRecord(ctx->ev_probe, s));
+                probe_pending = true;
+            } else {
+                TRY(launch_inorder());
+            }
         }
         return 0;
     };
@@ -668,7 +692,28 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
 
     // ---- the switch point (compression.cpp:417-481), read once the local pass is done
     bool sw_known = iters <= 0 || force_global;
+    auto local_tail = [&]() -> int {   // the switch word behind the local pass, and its event
+        if (iters > 0 && !force_global) HIPTRY(hipMemcpyAsync(ctx->h_switch, sc + 21, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPTRY(hipEventRecord(ctx->ev_local, s));
+        return 0;
+    };
+    // the probe's verdict: a window decides the mode (no in-order pass at all), none queues the pass
+    auto decide_probe = [&]() -> int {
+        if (!probe_pending) return 0;
+        probe_pending = false;
+        HIPTRY(hipEventSynchronize(ctx->ev_probe));
+        const int32_t w = local_probe_window(ctx->h_probe);
+        if (w >= 0) {
+            sw = w;
+            sw_known = true;
+            HIPTRY(hipEventRecord(ctx->ev_local, s));
+            return 0;
+        }
+        TRY(launch_inorder());
+        return local_tail();
+    };
     auto read_switch = [&]() -> int {
+        TRY(decide_probe());
         if (sw_known) return 0;
         HIPTRY(hipEventSynchronize(ctx->ev_local));
         const int64_t h_sw = *ctx->h_switch;   // ctl[2] | ctl[3] << 32
@@ -676,16 +721,11 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         sw_known = true;
         return 0;
     };
-    auto local_tail = [&]() -> int {   // the switch word behind the local pass, and its event
-        if (iters > 0 && !force_global) HIPTRY(hipMemcpyAsync(ctx->h_switch, sc + 21, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIPTRY(hipEventRecord(ctx->ev_local, s));
-        return 0;
-    };
-    if (local_launched) TRY(local_tail());
+    if (local_launched && !probe_pending) TRY(local_tail());
     auto ensure_local = [&](hipStream_t after) -> int {   // (order 2 when the walk never queued round 1)
         if (local_launched) return 0;
         TRY(launch_local(after));
-        return local_tail();
+        return probe_pending ? 0 : local_tail();
     };
 
     // ---- global (compression.cpp:484-574), speculatively: the walk runs on the side stream right
@@ -721,11 +761,17 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
                },
                [&]() -> int {
                    if (force_global || !local_launched) return 0;
+                   if (decide_probe()) return 0;   // (the resolve step reports the error)
                    if (!sw_known && hipEventQuery(ctx->ev_local) != hipSuccess) return 0;   // pass still running
                    if (read_switch()) return 0;   // the resolve step reports the error
                    return sw < 0;
                },
-               [&](hipStream_t st) -> int { return local_order == 2 ? ensure_local(st) : 0; }};
+               [&](hipStream_t st) -> int {
+                   // (the probe's verdict once the walk's first rounds are queued: the in-order pass,
+                   // when needed, then runs beside them)
+                   TRY(local_order == 2 ? ensure_local(st) : 0);
+                   return decide_probe();
+               }};
         const EmitTarget target{&Late::call, &late, &Late::abandon, &Late::round1};
         const int rc = global_match_and_emit(Rp, np[1], Tp, np[0], kg, mg, walk_chunk(tn), ws, wsb, nullptr, &g_rlen, &wr,
                                              s2, paren, &target, /*keep_flat=*/false);

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Build a variant of libsccg.so with extra compiler flags on every source:
-#   sccg-genome-compression_amd/tools/ab/build_flags.sh <name> <flags...>   -> variants/<name>/libsccg.so
+#   sccg-genome-compression_amd/tools/ab/build_flags.sh <name> <flags...>   -> abvar/<name>/libsccg.so
 set -eo pipefail
 NAME=$1; shift
 PKG=sccg-genome-compression_amd
-OUT=variants/$NAME
+OUT=abvar/$NAME
 mkdir -p $OUT/obj
 for f in $PKG/csrc/*.hip $PKG/csrc/*.cpp; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" -c $f -o $OUT/obj/$(basename $f).o &

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Build a variant of libsccg.so for A/B runs: sccg-genome-compression_amd/tools/ab/build_variant.sh <name> [walk.hip source] [extra hipcc flags...]
-# (objects other than walk.hip are the in-tree ones; output variants/<name>/libsccg.so)
+# (objects other than walk.hip are the in-tree ones; output abvar/<name>/libsccg.so)
 set -eo pipefail
 NAME=$1; SRC=${2:-sccg-genome-compression_amd/csrc/walk.hip}; shift 2 || shift $#
 PKG=sccg-genome-compression_amd
-OUT=variants/$NAME
+OUT=abvar/$NAME
 mkdir -p $OUT
 cp "$SRC" $PKG/csrc/_variant_walk.hip
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" -c $PKG/csrc/_variant_walk.hip -o $OUT/walk.o

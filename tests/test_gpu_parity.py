@@ -209,11 +209,11 @@ class _exact:
 
 
 def _probe_runs(nseg: int) -> list[range]:
-    """The segment runs local.hip's k_local_probe classifies (PROBE_RUN 8, PROBE_RUNS 16; pairs
-    of at least 512 segments)."""
+    """The segment runs local.hip's k_local_probe classifies (PROBE_RUN 8, PROBE_RUNS 16, run r
+    from (r + 1) nseg / 17 - 4; pairs of at least 512 segments)."""
     if nseg < 512:
         return []
-    return [range(a, a + 8) for a in ((j + 1) * (nseg - 8) // 16 for j in range(16))]
+    return [range(a, a + 8) for a in ((j + 1) * nseg // 17 - 4 for j in range(16))]
 
 
 @pytest.mark.parametrize("exact", [True, False], ids=["exact", "probe"])
@@ -238,10 +238,11 @@ def test_switch_window_vs_oracle(ctx, seed, exact):
 
 
 # (nseg, planted windows): a first window the probe does not see and a later one inside probe run
-# 0 / 9 / 15 (the last segments), a window only inside a probe run, and windows straddling a run's
-# first segment (its 5 segments are not all inside the run: the probe must not count it)
-PROBE_CASES = [(2400, [40, 155]), (2400, [300, 1350]), (2400, [40, 2399]), (2400, [1353]), (2400, [2396]),
-               (2400, [150]), (17000, [3000, 16996]), (17000, [10000])]
+# 0 / 8 / 15, a window only inside a probe run, windows straddling a run's first or last segment
+# (its 5 segments are not all inside the run: the probe must not count it) and one at the last
+# segment (no run covers the pair's end)
+PROBE_CASES = [(2400, [40, 143]), (2400, [300, 1272]), (2400, [40, 2260]), (2400, [1274]), (2400, [2399]),
+               (2400, [138]), (17000, [3000, 16003]), (17000, [10000])]
 
 
 @pytest.mark.parametrize("nseg,plants", PROBE_CASES)

@@ -125,3 +125,48 @@ def test_class0_proof_is_sound(seed):
             proved += 1
             assert oracle_class(r, t) == 0, (kind, r, t)
     assert proved > 30   # (the aligned-like cases are proved: the proof is not vacuous)
+
+
+def full_class(r: bytes, t: bytes) -> int:
+    """The reference's segment class with both passes (compression.cpp:400-460): k = 14, then
+    k2 = 10 when the first finds no match."""
+    non_n = any(c != ord("N") for c in t)
+    for k in (14, 10):
+        recs = oraclelib.match(r, t, k, 0, False, 0)
+        if any(kind for kind, _, _, _ in recs):
+            lit = sum(l for kind, _, l, _ in recs if not kind)
+            return 1 if (2 * lit > len(t) and non_n) else 0
+    return 2 if non_n else 3
+
+
+def hits10(r: bytes, t: bytes) -> int:
+    """Mirror of seg_hits<10>: target positions whose 10-mer occurs among the reference's."""
+    ks = {r[p:p + 10] for p in range(len(r) - 9)}
+    return sum(1 for y in range(len(t) - 9) if t[y:y + 10] in ks)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_probe_hit_count_rule(seed):
+    """k_local_probe's class from the k2 hit count (pure ACGT segment pairs): no hit position means
+    neither pass matches (class 2); fewer than nt / 28 means any match the passes take leaves more
+    than half of the segment literal (class 1) -- each match of length l covers l - k + 1 hit
+    positions and every 14-mer hit is a 10-mer hit, so at most 14 h10 bases match."""
+    fired = 0
+    rng = random.Random(900 + seed)
+    extra = []
+    for _ in range(60):   # sparse chance hits: unrelated segments with planted 10-40 base copies
+        r = bytes(rng.choice(b"ACGT") for _ in range(1000))
+        t = bytearray(rng.choice(b"ACGT") for _ in range(rng.choice([1000, 1000, 400, 37])))
+        for _ in range(rng.randint(0, 3)):
+            ln = rng.randint(10, 40)
+            a, b = rng.randint(0, 1000 - ln), rng.randint(0, max(0, len(t) - ln))
+            t[b:b + ln] = r[a:a + ln]
+        extra.append(("planted", r, bytes(t)))
+    for kind, r, t in list(cases(7000 + seed, 200)) + extra:
+        if not (set(r) <= set(b"ACGT") and set(t) <= set(b"ACGT")) or not t:
+            continue
+        h = hits10(r, t)
+        if h == 0 or 28 * h < len(t):
+            fired += 1
+            assert full_class(r, t) == (2 if h == 0 else 1), (kind, h, r, t)
+    assert fired > 40
