@@ -159,7 +159,10 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
 // The switch-window probe (local.hip k_local_probe): classes of PROBE_PAIRS segments in runs spread
 // over the pair into pout[0 .. PROBE_PAIRS) (-1 unknown) and their segment indices into
 // pout[PROBE_PAIRS ..); local_probe_window finds the first window among them on the host (-1: none).
-constexpr int PROBE_PAIRS = 128;
+#ifndef SCCG_PROBE_RUNS
+#define SCCG_PROBE_RUNS 16
+#endif
+constexpr int PROBE_PAIRS = SCCG_PROBE_RUNS * 8;
 int local_probe_applies(int64_t nseg_max);
 int launch_local_probe(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int32_t* pout,
                        hipStream_t s);

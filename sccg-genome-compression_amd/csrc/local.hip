@@ -664,7 +664,7 @@ __global__ __launch_bounds__(SCCG_BLOCK) __attribute__((amdgpu_waves_per_eu(LOCA
 // them decides the pair global and the in-order pass (k_local_all) is never launched; otherwise it
 // runs as before.
 // ---------------------------------------------------------------------------------------------
-constexpr int PROBE_RUN = 8, PROBE_RUNS = 16, PROBE_MIN_SEGS = 4 * PROBE_RUN * PROBE_RUNS;
+constexpr int PROBE_RUN = 8, PROBE_RUNS = SCCG_PROBE_RUNS, PROBE_MIN_SEGS = 512;
 static_assert(PROBE_RUN * PROBE_RUNS == PROBE_PAIRS, "internal.h's probe size");
 // run r starts at (r + 1) nseg / (RUNS + 1): spread over the pair, clear of its last segments
 // (telomere gaps)

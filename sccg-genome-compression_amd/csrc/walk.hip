@@ -323,9 +323,11 @@ __device__ __forceinline__ int first_diff(const uint32_t (&r)[N], const uint32_t
 __device__ __forceinline__ int first_diff32(const uint32_t (&r)[8], const uint32_t (&t)[8]) { return first_diff<8>(r, t); }
 
 // WALK_LCE_V (build option, A/B): 0 = lanes compare their own 32-byte stretches (the HBM step's
-// loads compared straight from registers); 1 = coalesced 16-byte lanes through the LDS copy.
+// loads compared straight from registers); 1 = coalesced 16-byte lanes through the LDS copy (the
+// default since round 6: LDS bank-conflict cycles 65 -> 56 % of the LDS-active cycles, genome bench
+// 151.6-162.1 -> 166.4-172.8 Gbase/s interleaved on one box, gpurun_out/r06n, profiles/r06/).
 #ifndef WALK_LCE_V
-#define WALK_LCE_V 0
+#define WALK_LCE_V 1
 #endif
 #if WALK_LCE_V == 0
 // longest common extension of R[a..] and T[b..], at most maxlen bytes (extend_alignment,
