@@ -231,6 +231,7 @@ struct WalkPtrs {
     int32_t* chh_tr;
     uint64_t* dbg;            // SCCG_DEBUG: per chunk DBG_SLOTS counters (k_walk<K, true>)
     int32_t dbg_phases;       // SCCG_DEBUG_PHASES: also per-phase clocks
+    int32_t dbg_round;        // SCCG_DEBUG_ROUND: keep the per-chunk counters of that round only (-1: the last)
 };
 
 // chunk j's target range [lo, hi)
@@ -745,13 +746,28 @@ __device__ int32_t wide_scan_ring(const WalkPtrs& A, WalkLds& L, BufPos& B, cons
 // the chunk walk (one wave per chunk)
 // ---------------------------------------------------------------------------------------------
 __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0);   // anchors, below
+__device__ __forceinline__ int32_t anchor_diag_f(int32_t nT, const uint8_t* __restrict__ T, const uint64_t* __restrict__ atab, int32_t abits,
+                                 uint32_t agen, int32_t y0);
+#define ANCHOR_DIAG_KC(y) anchor_diag_f(KC->nT, KC->T, KC->atab, KC->abits, KC->agen, (y))
+
+// The kernel's argument segment, laundered: a field read through it is loaded (s_load) where the
+// code reads it, instead of being hoisted to the kernel entry and kept in SGPRs.  k_walk reads its
+// cold fields (per-chunk state read before the walk loop or written after it) this way: kept live
+// across the loop, ~80 SGPRs of them spilled into VGPR lanes (v_writelane / v_readlane).
+typedef const __attribute__((address_space(4))) WalkPtrs* KArgPtr;
+__device__ __forceinline__ KArgPtr kargs() {
+    KArgPtr p = (KArgPtr)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(p));
+    return p;
+}
+#define KC (kargs())
 
 constexpr int DBG_SLOTS = 16;   // ticks, matches, batches, wides, windows, cands, ext bases, t_win, t_find, t_cand, t_tail
 #ifndef WALK_WAVES_PER_EU
 #define WALK_WAVES_PER_EU 5
 #endif
 // nlist_dev (optional): the list length from device memory (a round queued before the host knows it)
-// CARRY: the carry launch of a round (list = A.clist): each listed chunk is walked from its
+// CARRY: the carry launch of a round (list = KC->clist): each listed chunk is walked from its
 // predecessor's staged exit and committed here, and the walk carries on while the rule allows.
 template <bool DBG, bool CARRY>
 __global__ __launch_bounds__(64 * WWPB) __attribute__((amdgpu_waves_per_eu(WALK_WAVES_PER_EU)))
@@ -762,11 +778,11 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     if (nlist_dev) nlist = *nlist_dev;
     if (CARRY && nlist > A.C) nlist = A.C;
     // the round's frozen list starts empty (also when nothing is listed: a round queued blind)
-    if (!CARRY && blockIdx.x == 0 && threadIdx.x == 0 && !A.scal[9]) A.scal[5] = 0;
-    if (li >= nlist || A.scal[9]) return;
+    if (!CARRY && blockIdx.x == 0 && threadIdx.x == 0 && !KC->scal[9]) KC->scal[5] = 0;
+    if (li >= nlist || KC->scal[9]) return;
     WalkLds& L = lds_all[w];
     int32_t j = uni(list[li]);   // (j, lo_j, hi_j ... change when the walk carries on, below)
-    const int32_t kind = CARRY ? KIND_FIX : uni(A.kind[j]);
+    const int32_t kind = CARRY ? KIND_FIX : uni(KC->kind[j]);
     int32_t lo_j = chunk_lo(A, j);
     int32_t hi_j = chunk_hi(A, j);
     const int32_t lastk = A.nT - A.k;
@@ -774,52 +790,52 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     int32_t x, P, n = 0, q = 0, ob, cb = -1, cc = 0;
     bool first_spec = false;
     if (CARRY) {   // entry: the predecessor's staged exit (k_commit has not run yet)
-        cb = uni(A.cur[j]);
+        cb = uni(KC->cur[j]);
         ob = 1 - cb;
-        cc = uni(A.cnt[cb][j]);
-        x = uni(A.newX[j - 1]);
-        P = uni(A.newP[j - 1]);
+        cc = uni(KC->cnt[cb][j]);
+        x = uni(KC->newX[j - 1]);
+        P = uni(KC->newP[j - 1]);
     } else if (kind == KIND_SPEC) {
-        ob = uni(A.cur[j]);
+        ob = uni(KC->cur[j]);
         x = lo_j;
         // a chunk's first speculation (round 1, or the round after a frozen-first round 1 that
         // walked chunk 0 alone): guess from the anchors, re-seed a stuck guess
-        first_spec = uni(A.usedX[j]) == NEVER;
+        first_spec = uni(KC->usedX[j]) == NEVER;
         if (first_spec) {   // first guess: the anchor vote at the chunk start (anchor_diag)
-            int32_t d = anchor_diag(A, lo_j);
+            int32_t d = ANCHOR_DIAG_KC(lo_j);
             // no vote there (an indel, N run or diverged copy under the 128 probes): vote further
             // into the chunk.  A chunk left without a guess costs a whole serial re-walk next round
             // and delays its successor's settlement by one more round.
             for (int i = 1; d == INVALID && i <= ANCHOR_RETRIES && lo_j + i * ANCHOR_RETRY_STEP < hi_j; i++)
-                d = uni(anchor_diag(A, lo_j + i * ANCHOR_RETRY_STEP));
+                d = uni(ANCHOR_DIAG_KC(lo_j + i * ANCHOR_RETRY_STEP));
             P = INVALID;
             if (d != INVALID) {
                 int64_t gp = (int64_t)lo_j - 1 + d;
                 P = (int32_t)(gp < 0 ? 0 : (gp > A.nR - 1 ? A.nR - 1 : gp));
             }
             P = uni(P);
-            if (lane == 0) A.guess[j] = P;
+            if (lane == 0) KC->guess[j] = P;
         } else {
-            P = uni(A.guess[j]);   // re-speculation (k_round_respec)
+            P = uni(KC->guess[j]);   // re-speculation (k_round_respec)
         }
-        if (lane == 0) { A.usedX[j] = lo_j; A.usedP[j] = P; }
+        if (lane == 0) { KC->usedX[j] = lo_j; KC->usedP[j] = P; }
     } else if (kind == KIND_FIX) {   // result is committed (or discarded) by k_commit
-        cb = uni(A.cur[j]);
+        cb = uni(KC->cur[j]);
         ob = 1 - cb;
-        cc = uni(A.cnt[cb][j]);
-        x = uni(A.snapX[j]);
-        P = uni(A.snapP[j]);
+        cc = uni(KC->cnt[cb][j]);
+        x = uni(KC->snapX[j]);
+        P = uni(KC->snapP[j]);
     } else {   // resume after an escalation was resolved on the host
-        cb = uni(A.cur[j]);
+        cb = uni(KC->cur[j]);
         ob = 1 - cb;
-        cc = uni(A.cnt[cb][j]);
-        x = uni(A.escX[j]);
-        P = uni(A.escP[j]);
-        n = uni(A.escN[j]);
-        q = uni(A.escQ[j]);
+        cc = uni(KC->cnt[cb][j]);
+        x = uni(KC->escX[j]);
+        P = uni(KC->escP[j]);
+        n = uni(KC->escN[j]);
+        q = uni(KC->escQ[j]);
     }
     if (!CARRY) {
-        if (lane == 0) A.status[j] = ST_OK;
+        if (lane == 0) KC->status[j] = ST_OK;
     }
     int32_t x_entry = x, P_entry = P;
     const uint64_t dbg_t0 = DBG ? wall_clock64() : 0;
@@ -832,24 +848,20 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         if (DBG && phases) { const uint64_t t = wall_clock64(); dbg_c[slot] += t - tq; tq = t; }
     };
     if (P == INVALID) {   // speculative chunk without an anchor: nothing to offer
-        if (lane == 0) { A.cnt[ob][j] = 0; A.exitX[j] = INVALID; A.exitP[j] = INVALID; }
+        if (lane == 0) { KC->cnt[ob][j] = 0; KC->exitX[j] = INVALID; KC->exitP[j] = INVALID; }
         return;
     }
     // The trajectory buffers: the main walk keeps their addresses; the carry walk (whose chunk
     // changes) forms them where they are used -- loop-carried, they cost it registers it spills.
     const size_t cap = (size_t)A.cap;
-    int32_t* const ot0 = CARRY ? nullptr : A.bt[ob] + (size_t)j * cap;
-    int32_t* const op0 = CARRY ? nullptr : A.bp[ob] + (size_t)j * cap;
-    int32_t* const ol0 = CARRY ? nullptr : A.bl[ob] + (size_t)j * cap;
-    const int32_t* const ct0 = CARRY || cb < 0 ? nullptr : A.bt[cb] + (size_t)j * cap;
-    const int32_t* const cp0 = CARRY || cb < 0 ? nullptr : A.bp[cb] + (size_t)j * cap;
-    const int32_t* const cl0 = CARRY || cb < 0 ? nullptr : A.bl[cb] + (size_t)j * cap;
-#define W_OT (CARRY ? A.bt[ob] + (size_t)j * cap : ot0)
-#define W_OP (CARRY ? A.bp[ob] + (size_t)j * cap : op0)
-#define W_OL (CARRY ? A.bl[ob] + (size_t)j * cap : ol0)
-#define W_CT (CARRY ? A.bt[cb] + (size_t)j * cap : ct0)
-#define W_CP (CARRY ? A.bp[cb] + (size_t)j * cap : cp0)
-#define W_CL (CARRY ? A.bl[cb] + (size_t)j * cap : cl0)
+    // (formed where they are used -- every 64 matches -- from the argument segment: kept in
+    // registers across the walk loop, these pointers and the other cold fields spilled SGPRs)
+#define W_OT (KC->bt[ob] + (size_t)j * cap)
+#define W_OP (KC->bp[ob] + (size_t)j * cap)
+#define W_OL (KC->bl[ob] + (size_t)j * cap)
+#define W_CT (KC->bt[cb] + (size_t)j * cap)
+#define W_CP (KC->bp[cb] + (size_t)j * cap)
+#define W_CL (KC->bl[cb] + (size_t)j * cap)
 
     RegWin W;
     W.P = INVALID;
@@ -862,13 +874,13 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     // literal (the scan covered every position from the frozen chunk's exit on), so the walk
     // starts there -- the trajectory and exit are those of the walk from x
     if (!CARRY && kind == KIND_FIX && A.skip_hints) {
-        const int32_t hy = uni(A.hintY[j]);
-        if (hy > x && hy < scan_end && uni(A.hintP[j]) == P) x = hy;
+        const int32_t hy = uni(KC->hintY[j]);
+        if (hy > x && hy < scan_end && uni(KC->hintP[j]) == P) x = hy;
     }
     // stale entry (predecessor re-walked in this round): converge within the budget or give up
-    const bool stale = !CARRY && A.stale_budget > 0 && kind == KIND_FIX && j > 0 && A.lround[j - 1] == A.round;
+    const bool stale = !CARRY && A.stale_budget > 0 && kind == KIND_FIX && j > 0 && KC->lround[j - 1] == A.round;
     int32_t budget_end = stale && x + A.stale_budget < scan_end ? x + A.stale_budget : scan_end;
-    int32_t old_seedq = cb >= 0 ? uni(A.seedq[j]) : 0;
+    int32_t old_seedq = cb >= 0 ? uni(KC->seedq[j]) : 0;
     int32_t seed_x = x, seedq = 0;
     bool truncated = false;
     // the previous trajectory (fix-ups), 64 entries at a time in registers: lane i holds entry cq0 + i
@@ -928,7 +940,7 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
                 if (first_spec) {   // re-seed a stuck first guess (see RESEED_GAP)
                     if (x - (lme > seed_x ? lme : seed_x) >= RESEED_GAP) {
                         seed_x = x;
-                        const int32_t d = anchor_diag(A, x);
+                        const int32_t d = ANCHOR_DIAG_KC(x);
                         if (d != INVALID) {
                             int64_t np = (int64_t)x - 1 + d;
                             np = np < 0 ? 0 : (np > A.nR - 1 ? A.nR - 1 : np);
@@ -986,11 +998,11 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         if (p == 0) {   // pn2 == 0: the reference falls back to the ungated (pn1, ln1) (:134-138)
             escalated = true;
             if (lane == 0 && !CARRY) {   // (a carried chunk is left as it was: pending next round)
-                if (kind == KIND_SPEC) { A.cnt[ob][j] = 0; A.exitX[j] = INVALID; A.exitP[j] = INVALID; }
+                if (kind == KIND_SPEC) { KC->cnt[ob][j] = 0; KC->exitX[j] = INVALID; KC->exitP[j] = INVALID; }
                 else {
-                    A.status[j] = ST_ESC;
-                    A.escX[j] = y; A.escP[j] = P; A.escN[j] = n; A.escQ[j] = q;
-                    atomicAdd(&A.scal[1], 1);
+                    KC->status[j] = ST_ESC;
+                    KC->escX[j] = y; KC->escP[j] = P; KC->escN[j] = n; KC->escQ[j] = q;
+                    atomicAdd(&KC->scal[1], 1);
                 }
             }
             break;
@@ -1034,55 +1046,55 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     }
     flush_recs();
     if (escalated) return;
-    const int32_t nx = converged ? uni(A.exitX[j]) : x, np = converged ? uni(A.exitP[j]) : P;
+    const int32_t nx = converged ? uni(KC->exitX[j]) : x, np = converged ? uni(KC->exitP[j]) : P;
     const bool frozen_end = !converged && x == hi_j && x - lme >= FROZEN_MIN;
     const bool trapped = !converged && x - x_entry >= A.S / 2 && (P - P_entry < TRAP_P && P_entry - P < TRAP_P);
-    const bool exit_changed = nx != uni(A.exitX[j]) || np != uni(A.exitP[j]);
+    const bool exit_changed = nx != uni(KC->exitX[j]) || np != uni(KC->exitP[j]);
     if (!CARRY) {
-        if (DBG && lane == 0) {
+        if (DBG && lane == 0 && (A.dbg_round < 0 || A.dbg_round == A.round)) {
             tick(9);
-            uint64_t* d = A.dbg + (size_t)j * DBG_SLOTS;
+            uint64_t* d = KC->dbg + (size_t)j * DBG_SLOTS;
             d[0] = wall_clock64() - dbg_t0;
             for (int i = 0; i < 13; i++) d[1 + i] = dbg_c[i];
             d[14] = (uint64_t)A.round;
             d[15] = dbg_t0;   // start (wall clock), for the launch's start spread
         }
         if (lane == 0 && truncated) {   // nothing to commit; the chunk stays pending
-            A.conv[j] = 0;
-            A.changed[j] = 0;
-            A.walked[j] = A.round;
-            A.frozen[j] = 0;
-            A.status[j] = ST_TRUNC;
+            KC->conv[j] = 0;
+            KC->changed[j] = 0;
+            KC->walked[j] = A.round;
+            KC->frozen[j] = 0;
+            KC->status[j] = ST_TRUNC;
             return;
         }
         if (lane == 0) {
-            A.cnt[ob][j] = n;
+            KC->cnt[ob][j] = n;
             if (cb < 0) {   // speculative: the trajectory is the chunk's first, take it as is
-                A.exitX[j] = x; A.exitP[j] = P;
-                A.seedq[j] = seedq;
+                KC->exitX[j] = x; KC->exitP[j] = P;
+                KC->seedq[j] = seedq;
             } else {        // fix-up: staged; k_commit decides
-                A.newX[j] = nx; A.newP[j] = np;
-                A.conv[j] = converged;
-                A.changed[j] = exit_changed;
-                A.walked[j] = A.round;
+                KC->newX[j] = nx; KC->newP[j] = np;
+                KC->conv[j] = converged;
+                KC->changed[j] = exit_changed;
+                KC->walked[j] = A.round;
                 // ended in a long literal run with P frozen at the chunk end: k_frozen_scan territory
-                A.frozen[j] = frozen_end;
-                A.trapped[j] = trapped;
+                KC->frozen[j] = frozen_end;
+                KC->trapped[j] = trapped;
             }
-            A.status[j] = converged ? ST_CONV : ST_DONE;
+            KC->status[j] = converged ? ST_CONV : ST_DONE;
         }
         if (truncated) return;
         // carry on only from a fix-up whose commit is certain (k_commit takes it: its predecessor is
         // not listed, and -- by the rule below -- not carried into either), and not where the
         // frozen scan (frozen end) or the trapped re-speculation (k_round_respec) resolves faster
-        if (kind != KIND_FIX || (j > 0 && uni(A.lround[j - 1]) == A.round)) return;
+        if (kind != KIND_FIX || (j > 0 && uni(KC->lround[j - 1]) == A.round)) return;
         if (converged || !exit_changed || frozen_end || trapped) return;
         const int32_t j1 = j + 1;
-        if (j1 >= A.C || uni(A.lround[j1]) == A.round || (j1 + 1 < A.C && uni(A.lround[j1 + 1]) == A.round)) return;
+        if (j1 >= A.C || uni(KC->lround[j1]) == A.round || (j1 + 1 < A.C && uni(KC->lround[j1 + 1]) == A.round)) return;
         if (lane == 0) {
-            const int32_t at = atomicAdd(&A.scal[11], 1);
-            if (at < A.C) A.clist[at] = j1;
-            atomicOr(&A.cbits[j1 >> 5], 1u << (j1 & 31));
+            const int32_t at = atomicAdd(&KC->scal[11], 1);
+            if (at < A.C) KC->clist[at] = j1;
+            atomicOr(&KC->cbits[j1 >> 5], 1u << (j1 & 31));
         }
         return;
     } else {
@@ -1090,16 +1102,16 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
         // A frozen end is left pending (next round's fix-up hands it to the frozen scan).
         if (frozen_end) return;
         if (lane == 0) {
-            A.cnt[ob][j] = n;
-            A.cur[j] = ob;
-            A.exitX[j] = nx; A.exitP[j] = np;
-            A.usedX[j] = x_entry; A.usedP[j] = P_entry;
-            A.seedq[j] = 0;
-            A.conv[j] = converged;
-            A.changed[j] = exit_changed;
-            A.walked[j] = A.round;
-            A.frozen[j] = 0;
-            A.trapped[j] = trapped;
+            KC->cnt[ob][j] = n;
+            KC->cur[j] = ob;
+            KC->exitX[j] = nx; KC->exitP[j] = np;
+            KC->usedX[j] = x_entry; KC->usedP[j] = P_entry;
+            KC->seedq[j] = 0;
+            KC->conv[j] = converged;
+            KC->changed[j] = exit_changed;
+            KC->walked[j] = A.round;
+            KC->frozen[j] = 0;
+            KC->trapped[j] = trapped;
         }
     }
     // carry into chunk j + 1 when its entry changed and nobody else walks it or depends on it in
@@ -1107,16 +1119,16 @@ void k_walk(WalkPtrs A, const int32_t* __restrict__ list, int32_t nlist, const i
     // its state for the whole round, so that its own commit rule -- and carry -- stay exact)
     if (converged || !exit_changed || frozen_end || trapped) return;
     const int32_t j1 = j + 1;
-    if (j1 >= A.C || uni(A.lround[j1]) == A.round || (j1 + 1 < A.C && uni(A.lround[j1 + 1]) == A.round)) return;
+    if (j1 >= A.C || uni(KC->lround[j1]) == A.round || (j1 + 1 < A.C && uni(KC->lround[j1 + 1]) == A.round)) return;
     j = j1;
     lo_j = chunk_lo(A, j);
     hi_j = chunk_hi(A, j);
     scan_end = hi_j < lastk + 1 ? hi_j : lastk + 1;
     budget_end = scan_end;
-    cb = uni(A.cur[j]);
+    cb = uni(KC->cur[j]);
     ob = 1 - cb;
-    cc = uni(A.cnt[cb][j]);
-    old_seedq = uni(A.seedq[j]);
+    cc = uni(KC->cnt[cb][j]);
+    old_seedq = uni(KC->seedq[j]);
     n = 0;
     q = 0;
     rb_n0 = 0;
@@ -1997,19 +2009,24 @@ __global__ void k_anchor_build(WalkPtrs A) {
 // Whole wave: probe the 256 target positions from y0; each hit on a sampled reference 32-mer
 // votes for its diagonal (reference - target position).  The diagonal with the most votes (>= 2;
 // a lone hit is often a repeat copy), ties to the earliest; else the earliest; INVALID if none.
-__device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0) {
+// (the table's fields as arguments: k_walk passes them from its argument segment, kargs)
+__device__ __forceinline__ int32_t anchor_diag_f(int32_t nT, const uint8_t* __restrict__ T, const uint64_t* __restrict__ atab, int32_t abits,
+                                 uint32_t agen, int32_t y0) {
     const int lane = lane_id();
     constexpr int NB = ANCHOR_PROBE_BATCHES;
+    const uint64_t tag = ((uint64_t)(agen & ANCHOR_GEN_MASK) << 52);
     int32_t dg[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
         const int32_t y = y0 + b * 64 + lane;
         dg[b] = INVALID;
         uint64_t code;
-        if (y + ANCHOR_K <= A.nT && code32<false>(A.T + y, code)) {
+        if (y + ANCHOR_K <= nT && code32<false>(T + y, code)) {
             const uint64_t key = mix64(code);
-            const uint64_t v = A.atab[key >> (64 - A.abits)];
-            if (anchor_hit(A, key, v)) dg[b] = (int32_t)(uint32_t)v - y;
+            const uint64_t v = atab[key >> (64 - abits)];
+            // (anchor_hit: this call's generation and the key's tag, not a repeated 32-mer)
+            if ((v >> 32) == ((tag | ((uint64_t)(uint32_t)(key & 0xfffffu) << 32)) >> 32) && (uint32_t)v != A_MULTI)
+                dg[b] = (int32_t)(uint32_t)v - y;
         }
     }
     int32_t g = INVALID, first = INVALID;
@@ -2033,6 +2050,7 @@ __device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0) {
     }
     return g == INVALID ? first : g;
 }
+__device__ int32_t anchor_diag(const WalkPtrs& A, int32_t y0) { return anchor_diag_f(A.nT, A.T, A.atab, A.abits, A.agen, y0); }
 
 
 // ---------------------------------------------------------------------------------------------
@@ -3124,6 +3142,7 @@ WalkPtrs make_ptrs(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64_t nT
     WalkPtrs A = carve(ws, ws_bytes, Rp, nRp, Tp, nTp, k, m, chunk, used, abits);
     if (!getenv("SCCG_DEBUG")) A.dbg = nullptr;   // per-chunk counters only in diagnostic runs
     A.dbg_phases = getenv("SCCG_DEBUG_PHASES") != nullptr;
+    A.dbg_round = getenv("SCCG_DEBUG_ROUND") ? atoi(getenv("SCCG_DEBUG_ROUND")) : -1;
     static const int32_t sb = [] {
         const char* e = getenv("SCCG_STALE_BUDGET");
         return e ? atoi(e) : STALE_BUDGET_DEFAULT;
@@ -3665,8 +3684,9 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                 SCCG_HIP(hipStreamSynchronize(s));
                 std::vector<uint64_t> tk(C);
                 uint64_t sum[14] = {};
+                const int64_t rep = A.dbg_round > 0 ? A.dbg_round : round;   // (the round whose counters are kept)
                 for (size_t j = 0; j < C; j++) {
-                    const bool mine = d[j * DS + 14] == (uint64_t)round;
+                    const bool mine = d[j * DS + 14] == (uint64_t)rep;
                     tk[j] = mine ? d[j * DS] : 0;
                     if (mine) for (int i = 0; i < 14; i++) sum[i] += d[j * DS + i];
                 }
@@ -3686,10 +3706,10 @@ int match_and_emit_impl(const uint8_t* Rp, int64_t nRp, const uint8_t* Tp, int64
                         (unsigned long long)sum[4], (unsigned long long)sum[5], (unsigned long long)sum[6]);
                 {   // launch spread: when the chunks' waves started and ended, from the first start
                     uint64_t s0 = ~0ull;
-                    for (size_t j = 0; j < C; j++) if (d[j * DS + 14] == (uint64_t)round && d[j * DS + 15] < s0) s0 = d[j * DS + 15];
+                    for (size_t j = 0; j < C; j++) if (d[j * DS + 14] == (uint64_t)rep && d[j * DS + 15] < s0) s0 = d[j * DS + 15];
                     std::vector<uint64_t> st, en;
                     for (size_t j = 0; j < C; j++)
-                        if (d[j * DS + 14] == (uint64_t)round) { st.push_back(d[j * DS + 15] - s0); en.push_back(d[j * DS + 15] - s0 + d[j * DS]); }
+                        if (d[j * DS + 14] == (uint64_t)rep) { st.push_back(d[j * DS + 15] - s0); en.push_back(d[j * DS + 15] - s0 + d[j * DS]); }
                     if (!st.empty()) {
                         std::sort(st.begin(), st.end());
                         std::sort(en.begin(), en.end());
