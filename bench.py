@@ -80,8 +80,10 @@ def design_alg_bytes(tfa: int, rfa: int, nT: int, nR: int, nRp: int, out: int, m
     again for them), R' read once by the first-step sweep (the exact ungated first step, :64-161
     with pme == -1), the walk's 0.5 B per target base, and the record text written.
     The local pass (compression.cpp:372-481) is counted only for the segments of a pair that stays
-    local (both segment strings once)."""
-    ingest = tfa + rfa + 2.0 * (nT + nR)
+    local (both segment strings once).  Round 6: a pair whose mode the switch probe decides writes
+    only the N-erased copies T' and R' (the unfiltered T and R are read only by a local pass; the
+    probe gathers its 128 segments of them from the FASTA), counted as |T| + |R'| (|T'| <= |T|)."""
+    ingest = tfa + rfa + (nT + nRp if mode_global else 2.0 * (nT + nR))
     b = ingest + out
     if mode_global:
         b += nRp + walk_alg_bytes(nT)
@@ -94,8 +96,8 @@ def kernel_alg_bytes(kernel: str, tot: dict) -> float | None:
     """Algorithmic HBM bytes of one STEP of `kernel` summed over the step's pairs."""
     if kernel == "walk":
         return walk_alg_bytes(tot["target_bases"])
-    if kernel == "fasta_strip":          # read the FASTA, write the stripped and the N-erased copies
-        return tot["tgt_fa"] + tot["ref_fa"] + 2.0 * (tot["target_bases"] + tot["reference_bases"])
+    if kernel == "fasta_strip":          # read the FASTA, write the N-erased copies (+ the stripped ones: local pairs)
+        return tot["tgt_fa"] + tot["ref_fa"] + tot.get("strip_out_bytes", 2.0 * (tot["target_bases"] + tot["reference_bases"]))
     if kernel == "run_extract":          # the strip's per-tile run-event counts and flags (12 B per 4 KiB
         return 12.0 * tot["target_bases"] / 4096.0   # tile; the events themselves are a few bytes per run)
     if kernel == "first_sweep_anchors":  # R' once + one 8-byte anchor slot per 64 reference bases
@@ -728,6 +730,9 @@ def main() -> None:
            "walk_reference_bases": sum(results[n][1]["walk_reference_bases"] for n in order),
            "record_bytes": sum(int(results[n][0].numel()) for n in order),
            "tgt_fa": tgt_fa_bytes, "ref_fa": ref_fa_bytes,
+           "strip_out_bytes": sum((results[n][1]["target_bases"] + results[n][1]["walk_reference_bases"])
+                                  if results[n][1]["mode_global"] else
+                                  2 * (results[n][1]["target_bases"] + results[n][1]["reference_bases"]) for n in order),
            "design_bytes": sum(design_alg_bytes(pairs[n][3], pairs[n][1], results[n][1]["target_bases"],
                                                 results[n][1]["reference_bases"], results[n][1]["walk_reference_bases"],
                                                 int(results[n][0].numel()), bool(results[n][1]["mode_global"]))
@@ -872,8 +877,8 @@ def main() -> None:
                     "alg_bytes_per_step": job_tot["design_bytes"],
                     "achieved": job_tot["design_bytes"] / per_s / 1e9,
                     "frac": job_tot["design_bytes"] / per_s / 1e9 / (HBM_PEAK_GBS * world),
-                    "model": "design (DESIGN.md §4, bench.design_alg_bytes): per pair both FASTA read + T, R, T', R' "
-                             "written once (ingest) + T once (run lines) + R' once (first-step sweep) + 0.5 B per "
+                    "model": "design (DESIGN.md §4, bench.design_alg_bytes): per pair both FASTA read + T', R' (+ T, R for a local pair) "
+                             "written once (ingest; run lines from the target strip) + R' once (first-step sweep) + 0.5 B per "
                              "target base (walk, SURVEY §8(d)) + the record text; a pair that stays local: its segments "
                              "once instead of the sweep and walk.  |R'| measured per pair.",
                     "survey_model": {"alg_bytes_per_step": job_tot["survey_bytes"],

@@ -638,6 +638,59 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
 }
 
 // ---------------------------------------------------------------------------------------------
+// Stripped bytes on demand (round 6).  A pair whose mode the switch probe decides (local.hip
+// k_local_probe) never reads the unfiltered stripped copies T and R unless it stays local, so the
+// strips skip writing them (out = null) and the probe's 128 segments of each are materialised here
+// from the FASTA and the write pass's tile offsets: the wave of slot i finds the tile holding
+// stripped byte q0 = seg * SEG_L (the last tile whose output offset is <= q0), re-classifies that
+// tile and the next ones exactly as k_strip_write does, and drops each kept byte that falls in
+// [q0, q0 + SEG_L) into dst[i * SEG_B + (pos - q0)].  seg < 0: nothing (the slot stays unused).
+// ---------------------------------------------------------------------------------------------
+template <IngestMode MODE>
+__global__ __launch_bounds__(64) void k_strip_gather(const uint8_t* __restrict__ buf, int64_t n,
+                                                     const int64_t* __restrict__ hdr, const int64_t* __restrict__ toff,
+                                                     const int32_t* __restrict__ tcarry, const int64_t* __restrict__ d_len,
+                                                     const int32_t* __restrict__ segs, uint8_t* __restrict__ dst) {
+    __shared__ uint4 tin[STRIP_WTILE / 16];
+    const int lane = lane_id();
+    const int32_t seg = segs[blockIdx.x];
+    if (seg < 0) return;
+    const int64_t len = *d_len;
+    const int64_t q0 = (int64_t)seg * SEG_L;
+    const int64_t q1 = q0 + SEG_L < len ? q0 + SEG_L : len;
+    uint8_t* out = dst + (size_t)blockIdx.x * SEG_GATHER_B;
+    if (q0 >= q1) return;
+    const int64_t ntiles = (n + STRIP_WTILE - 1) / STRIP_WTILE;
+    // last tile t with toff[t] <= q0 (toff is nondecreasing; toff[0] = 0)
+    int64_t lo = 0, hi = ntiles - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (toff[mid] <= q0) lo = mid; else hi = mid - 1;
+    }
+    const int64_t h = MODE == INGEST_TGT ? hdr[0] : 0, he = MODE == INGEST_TGT ? hdr[1] : 0;
+    for (int64_t tile = lo; tile < ntiles && toff[tile] < q1; tile++) {
+        const int64_t off = tile * STRIP_WTILE + (int64_t)lane * SL;
+        uint32_t w[SNW];
+        int32_t prior;
+        uint64_t lsm;
+        const StripMasks r = strip_tile<MODE>(FILTER_UPPER, buf, n, h, he, off, w, prior, lsm, tin);
+        int32_t pr = prior;
+        if (MODE == INGEST_REF && pr < 0) pr = tcarry[tile];
+        const uint64_t keep = r.known | (pr == 1 ? r.unknown : 0ull);
+        const uint32_t c = (uint32_t)__popcll(keep);
+        const uint32_t ex = wave_incl_add<uint32_t>(c) - c;
+        int64_t pos = toff[tile] + ex;
+        if (pos < q1 && pos + c > q0) {
+            for (uint64_t m = keep; m; m &= m - 1, pos++) {
+                const int b = __builtin_ctzll(m);
+                if (pos >= q0 && pos < q1) out[pos - q0] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+            }
+        }
+        wave_sync();   // (tin is reused by the next tile)
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // runs of a predicate
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool run_pred(RunPred p, uint8_t c) {
@@ -955,6 +1008,38 @@ int launch_run_text(const int32_t* rs, const int32_t* re, int64_t nruns, int64_t
     int rc = dev_excl_sum(d_tmp, d_tmp, nruns, d_len, d_partial, s);
     if (rc) return rc;
     PROF_LAUNCH(PROF_RUNTEXT, s, k_run_textwrite, dim3(g), dim3(256), 0, s, rs, re, nruns, n, (const int64_t*)d_tmp, out);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_strip_gather(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, const int64_t* toff,
+                        const int32_t* tcarry, const int64_t* d_len, const int32_t* segs, int nslots, uint8_t* dst,
+                        hipStream_t s) {
+    if (n <= 0 || nslots <= 0) return 0;
+    if (mode == INGEST_TGT)
+        hipLaunchKernelGGL(k_strip_gather<INGEST_TGT>, dim3(nslots), dim3(64), 0, s, buf, n, d_header, toff, tcarry, d_len,
+                           segs, dst);
+    else
+        hipLaunchKernelGGL(k_strip_gather<INGEST_REF>, dim3(nslots), dim3(64), 0, s, buf, n, d_header, toff, tcarry, d_len,
+                           segs, dst);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+// the unfiltered stripped copy alone (out), from the tile offsets of an earlier launch_fasta_strip
+// of the same input (its scan results are still in sc): the write pass again, without the filter
+int launch_strip_rewrite(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,
+                         const IngestScratch& sc, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE;
+    const unsigned g = grid_for(ntiles, WPB);
+    const RunSlots rsl{};
+    if (mode == INGEST_TGT)
+        PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_TGT, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, FILTER_UPPER, buf, n,
+                    d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, (uint8_t*)nullptr, (int32_t*)nullptr, rsl);
+    else
+        PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_REF, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, FILTER_UPPER, buf, n,
+                    d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, (uint8_t*)nullptr, (int32_t*)nullptr, rsl);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

@@ -117,6 +117,16 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
                        uint8_t* out, int64_t* d_len, int32_t* d_flags, const IngestScratch& sc,
                        hipStream_t s, FilterMode fmode = FILTER_UPPER, uint8_t* out2 = nullptr,
                        int64_t* d_len2 = nullptr, const RunSlots* runs = nullptr);
+// Stripped bytes [seg * SEG_L, +SEG_L) of the FASTA for each slot i (segs[i] >= 0) into
+// dst[i * SEG_GATHER_B ..] from the tile offsets an earlier launch_fasta_strip of it left in
+// (toff = its scratch tile_off, tcarry = tile_carry; d_len = the stripped length); and the
+// unfiltered copy alone from those offsets (a pair the switch probe leaves local).
+constexpr int SEG_GATHER_B = 1024;
+int launch_strip_gather(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, const int64_t* toff,
+                        const int32_t* tcarry, const int64_t* d_len, const int32_t* segs, int nslots, uint8_t* dst,
+                        hipStream_t s);
+int launch_strip_rewrite(IngestMode mode, const uint8_t* buf, int64_t n, const int64_t* d_header, uint8_t* out,
+                         const IngestScratch& sc, hipStream_t s);
 // maximal runs of lowercase bytes (rs_l/re_l) and of N/n bytes (rs_n/re_n), start/end inclusive,
 // in one pass; d_nruns[0..1] = their counts
 int launch_runs2(const uint8_t* s_in, int64_t n, int32_t* rs_l, int32_t* re_l, int32_t* rs_n, int32_t* re_n,
@@ -164,8 +174,11 @@ int launch_local_all(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, co
 #endif
 constexpr int PROBE_PAIRS = SCCG_PROBE_RUNS * 8;
 int local_probe_applies(int64_t nseg_max);
-int launch_local_probe(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int32_t* pout,
-                       hipStream_t s);
+int launch_probe_segs(const int64_t* d_nR, const int64_t* d_nT, int32_t* segs, hipStream_t s);
+int launch_segment_copy(const uint8_t* src, const int64_t* d_len, const int32_t* segs, int nslots, uint8_t* dst,
+                        hipStream_t s);
+int launch_local_probe(const uint8_t* gR, const int64_t* d_nR, const uint8_t* gT, const int64_t* d_nT, const int32_t* segs,
+                       int32_t* pout, hipStream_t s);
 int local_probe_window(const int32_t* pout);
 // record text for local mode (delta-encoded, compression.cpp:406-415 + :222-304) + leftover
 // (abs_p: "(p," with absolute p instead, the text before delta_encode)

@@ -687,10 +687,39 @@ __device__ unsigned long long g_probe_dbg[PROBE_RUNS * PROBE_RUN][6];
 // a 9 KiB / one-wave group finds a slot at once (an 8-wave group of a whole run, 74 KiB of LDS and
 // two waves' registers on every SIMD, waited ~0.5 ms for a CU to drain).  Each wave writes its
 // segment's class (or -1) and index to pout; the host looks for windows (local_probe_window).
+// The probed segments (slot i = run i / RUN, segment i % RUN of it; -1: none), for the gathers of
+// their stripped bytes (ingest.hip k_strip_gather) and the probe.
+__global__ void k_probe_segs(const int64_t* __restrict__ dnR, const int64_t* __restrict__ dnT, int32_t* __restrict__ segs) {
+    const int32_t nseg = seg_count(*dnR, *dnT);
+    for (int i = (int)threadIdx.x; i < PROBE_RUNS * PROBE_RUN; i += (int)blockDim.x)
+        segs[i] = nseg < PROBE_MIN_SEGS ? -1 : probe_run_start(i / PROBE_RUN, nseg) + i % PROBE_RUN;
+}
+
+// Both segments of slot i from the gathered copies (SEG_GATHER_B bytes per slot; bytes past a
+// segment's end read as 0), uppercased as seg_load does.
+__device__ __forceinline__ void seg_load_gathered(SegLds& L, int slot, int nr, int nt, const uint8_t* __restrict__ gR,
+                                                  const uint8_t* __restrict__ gT) {
+    const int lane = lane_id();
+    const uint32_t* R4 = reinterpret_cast<const uint32_t*>(gR + (size_t)slot * SEG_GATHER_B);
+    const uint32_t* T4 = reinterpret_cast<const uint32_t*>(gT + (size_t)slot * SEG_GATHER_B);
+    uint32_t* r4 = reinterpret_cast<uint32_t*>(L.r);
+    uint32_t* t4 = reinterpret_cast<uint32_t*>(L.t);
+#pragma unroll
+    for (int j = 0; j < SEGB / 256; j++) {
+        const int i = lane + 64 * j, b0 = 4 * i;
+        uint32_t rw = b0 < nr ? R4[i] : 0u, tw = b0 < nt ? T4[i] : 0u;
+        if (nr - b0 < 4) rw &= nr - b0 <= 0 ? 0u : (1u << (8 * (nr - b0))) - 1u;
+        if (nt - b0 < 4) tw &= nt - b0 <= 0 ? 0u : (1u << (8 * (nt - b0))) - 1u;
+        r4[i] = upper4(rw);
+        t4[i] = upper4(tw);
+    }
+    wave_sync();
+}
+
 template <bool DBG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_PER_EU))) void k_local_probe(
-    const uint8_t* __restrict__ R, const int64_t* __restrict__ dnR, const uint8_t* __restrict__ T,
-    const int64_t* __restrict__ dnT, int32_t* __restrict__ pout) {
+    const uint8_t* __restrict__ gR, const int64_t* __restrict__ dnR, const uint8_t* __restrict__ gT,
+    const int64_t* __restrict__ dnT, const int32_t* __restrict__ segs, int32_t* __restrict__ pout) {
     unsigned long long tk[5] = {DBG ? (unsigned long long)wall_clock64() : 0ull, 0, 0, 0, 0};
     __shared__ SegLds L;
     const int64_t nR = *dnR, nT = *dnT;
@@ -700,12 +729,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LOCAL_WAVES_
         if (lane == 0) { pout[blockIdx.x] = -1; pout[PROBE_RUNS * PROBE_RUN + blockIdx.x] = -1; }
         return;
     }
-    const int32_t r = (int32_t)blockIdx.x / PROBE_RUN, w = (int32_t)blockIdx.x % PROBE_RUN;
-    const int32_t seg = probe_run_start(r, nseg) + w;
-    (void)seg_load(L, seg, 1, R, nR, T, nT, nullptr);
-    if (DBG) tk[1] = wall_clock64();
+    const int32_t seg = segs[blockIdx.x];
     const int64_t base = (int64_t)seg * SEG_L;
     const int nr = (int)((nR - base) < SEG_L ? (nR - base) : SEG_L), nt = (int)((nT - base) < SEG_L ? (nT - base) : SEG_L);
+    seg_load_gathered(L, (int)blockIdx.x, nr, nt, gR, gT);
+    if (DBG) tk[1] = wall_clock64();
     // A segment pair holding any byte outside ACGT is left unknown: an all-N reference segment puts
     // its ~1000 identical k-mers into one LDS bucket, which every target lane hashing there scans in
     // full on each probe step (such pairs -- assembly gaps, telomeres -- took 0.2-0.8 ms per pass
@@ -953,16 +981,39 @@ int local_probe_window(const int32_t* pout) {
     return best;
 }
 
-int launch_local_probe(const uint8_t* R, const int64_t* d_nR, const uint8_t* T, const int64_t* d_nT, int32_t* pout,
-                       hipStream_t s) {
+// the probe's segments copied out of a written stripped copy (strips that wrote T / R)
+__global__ void k_segment_copy(const uint8_t* __restrict__ src, const int64_t* __restrict__ d_len,
+                               const int32_t* __restrict__ segs, uint8_t* __restrict__ dst) {
+    const int32_t seg = segs[blockIdx.x];
+    if (seg < 0) return;
+    const int64_t q0 = (int64_t)seg * SEG_L, len = *d_len;
+    for (int i = (int)threadIdx.x; i < SEG_L && q0 + i < len; i += (int)blockDim.x)
+        dst[(size_t)blockIdx.x * SEG_GATHER_B + i] = src[q0 + i];
+}
+
+int launch_segment_copy(const uint8_t* src, const int64_t* d_len, const int32_t* segs, int nslots, uint8_t* dst,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_segment_copy, dim3(nslots), dim3(256), 0, s, src, d_len, segs, dst);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_probe_segs(const int64_t* d_nR, const int64_t* d_nT, int32_t* segs, hipStream_t s) {
+    hipLaunchKernelGGL(k_probe_segs, dim3(1), dim3(PROBE_RUNS * PROBE_RUN), 0, s, d_nR, d_nT, segs);
+    SCCG_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_local_probe(const uint8_t* gR, const int64_t* d_nR, const uint8_t* gT, const int64_t* d_nT, const int32_t* segs,
+                       int32_t* pout, hipStream_t s) {
     static const bool pdbg = getenv("SCCG_DEBUG") != nullptr;
     constexpr int NP = PROBE_RUNS * PROBE_RUN;
     if (!pdbg) {
-        PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<false>, dim3(NP), dim3(64), 0, s, R, d_nR, T, d_nT, pout);
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<false>, dim3(NP), dim3(64), 0, s, gR, d_nR, gT, d_nT, segs, pout);
     } else {
         const unsigned long long z[NP][6] = {};
         SCCG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_probe_dbg), z, sizeof z, 0, hipMemcpyHostToDevice, s));
-        PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<true>, dim3(NP), dim3(64), 0, s, R, d_nR, T, d_nT, pout);
+        PROF_LAUNCH(PROF_LOCAL14, s, k_local_probe<true>, dim3(NP), dim3(64), 0, s, gR, d_nR, gT, d_nT, segs, pout);
         unsigned long long d[NP][6];
         SCCG_HIP(hipMemcpyFromSymbolAsync(d, HIP_SYMBOL(g_probe_dbg), sizeof d, 0, hipMemcpyDeviceToHost, s));
         SCCG_HIP(hipStreamSynchronize(s));

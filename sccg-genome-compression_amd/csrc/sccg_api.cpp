@@ -411,7 +411,7 @@ bool strip_runs(sccg_ctx* ctx, int64_t fa_len, StripRuns* out) {
 // of both text lengths.  The lowercase line goes to out_lower, the N line to out_n.
 int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower, uint8_t** out_n, int64_t* d_sc,
               int64_t* h_lens, hipStream_t s, const StripRuns* sr = nullptr, const int64_t* toff = nullptr,
-              const int64_t* d_n = nullptr) {
+              const int64_t* d_n = nullptr, const std::function<int(hipStream_t)>& need_input = {}) {
     const int64_t maxruns = n / 2 + 2;
     const int64_t ntiles = (n + INGEST_TILE - 1) / INGEST_TILE + 1;
     const int64_t ntmp = maxruns > ntiles ? maxruns : ntiles;
@@ -433,6 +433,7 @@ int run_lines(sccg_ctx* ctx, const uint8_t* s_in, int64_t n, uint8_t* out_lower,
         nruns[2] = ovf;
     }
     if (nruns[2]) {   // no slots, or a tile overflowed them: run extraction over T
+        if (need_input) TRY(need_input(s));   // (T not written by a lean strip: write it now)
         TRY(launch_runs2(s_in, n, rs_l, re_l, rs_n, re_n, d_sc, tmp_l, tmp_n, part, s));
         TRY(d2h_i64(ctx, d_sc, nruns, 2, s));
     }
@@ -501,6 +502,15 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     // by the same ingest pass (the local pass may end up not needing them)
     GET(uint8_t, Tp, B_TP, tn + 64);
     GET(uint8_t, Rp, B_RP, rn + 64);
+    // Lean strips (round 6): the unfiltered stripped copies T and R are read only by the local pass
+    // (and by the run-line fallback when a tile overflows its run-event slots).  When the switch
+    // probe decides the mode (or there is no local pass, local = 0), the strips write only T' and
+    // R'; the probe gathers its segments of T and R from the FASTA (k_strip_gather), and a pair it
+    // leaves local gets T and R from a second write pass (launch_strip_rewrite) before its pass.
+    const int64_t iters_max = ((rn < tn ? rn : tn) + SEG_L - 1) / SEG_L;   // FASTA lengths bound the sequences'
+    static const bool lean_on = [] { const char* e = getenv("SCCG_LEAN_STRIP"); return !e || atoi(e) != 0; }();
+    const bool probe_mode = !force_global && !ctx->exact_switch && iters_max > 0 && local_probe_applies(iters_max);
+    const bool lean_R = lean_on && (probe_mode || force_global);
     int32_t* d_flags = reinterpret_cast<int32_t*>(sc + 32);
     HIPTRY(hipMemsetAsync(d_flags, 0, sizeof(int32_t), s));
     // local pass control {0, early-exit bound, switch segment, 0}: INT32_MAX = none yet
@@ -521,7 +531,8 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         if (const int rc = rdy->ref(rdy->user, &e)) return rc;
         HIPTRY(hipStreamWaitEvent(ctx->side, e, 0));
     }
-    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1, ctx->side));
+    TRY(strip(ctx, INGEST_REF, rfa, rn, nullptr, lean_R ? nullptr : R, sc + 7, nullptr, nullptr, FILTER_DROP_N_UPPER, Rp, 1,
+              ctx->side));
     HIPTRY(hipEventRecord(ctx->ev_rstrip, ctx->side));
     if (rdy) {
         hipEvent_t e = nullptr;
@@ -534,8 +545,20 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     StripRuns sruns;
     const bool have_runs = strip_runs(ctx, tn, &sruns);
     if (have_runs) HIPTRY(hipMemsetAsync(sruns.rs.ovf, 0, sizeof(int32_t), s));
-    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp, 0, nullptr,
-              have_runs ? &sruns.rs : nullptr));
+    const bool lean_T = lean_R && have_runs;   // (without run-event slots the run lines read T)
+    TRY(strip(ctx, INGEST_TGT, tfa, tn, sc, lean_T ? nullptr : T, sc + 2, d_flags, nullptr, FILTER_DROP_N_UPPER, Tp, 0,
+              nullptr, have_runs ? &sruns.rs : nullptr));
+    // T and R written after all (a pair the probe leaves local, or a run-slot overflow), from the
+    // strips' tile offsets (scratch sets 0 and 1); each at most once per stream that needs it
+    auto rewrite = [&](IngestMode mode, hipStream_t st) -> int {
+        const int o = mode == INGEST_REF ? B_TILE2_A - B_TILE_A : 0;
+        IngestScratch isc{};
+        isc.tile_off = reinterpret_cast<int64_t*>(ctx->buf[B_TILE_OFF + o]);
+        isc.tile_off2 = reinterpret_cast<int64_t*>(ctx->buf[B_TILE_OFF2 + o]);
+        isc.tile_carry = reinterpret_cast<int32_t*>(ctx->buf[B_TILE_CARRY + o]);
+        return mode == INGEST_REF ? launch_strip_rewrite(INGEST_REF, rfa, rn, nullptr, R, isc, st)
+                                  : launch_strip_rewrite(INGEST_TGT, tfa, tn, sc, T, isc, st);
+    };
     // ---- header + lowercase line (compression.cpp:337-368) and the N line: side2, driven by the
     //      context's host worker (its launches wait on run counts).  They need only T, so they are
     //      queued right behind the target's strip -- ahead of the local pass and the walk, which
@@ -569,7 +592,9 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
         }
         // both run lines now (the N line is kept aside until the mode is known)
         TRY(run_lines(ctx, T, h4[2], out + (hh ? hl + 1 : 0), &nline, sc + 10, rl_len, s3, have_runs ? &sruns : nullptr,
-                      reinterpret_cast<const int64_t*>(ctx->buf[B_TILE_OFF]), sc + 2));
+                      reinterpret_cast<const int64_t*>(ctx->buf[B_TILE_OFF]), sc + 2,
+                      lean_T ? std::function<int(hipStream_t)>([&](hipStream_t st) { return rewrite(INGEST_TGT, st); })
+                             : std::function<int(hipStream_t)>()));
         HIPTRY(hipEventRecord(ctx->ev_lines, s3));
         return 0;
     });
@@ -602,12 +627,17 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
     hipStream_t s2 = ctx->side;
     HIPTRY(hipEventRecord(ctx->ev_fork, s));
     HIPTRY(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
-    const int64_t iters_max = ((rn < tn ? rn : tn) + SEG_L - 1) / SEG_L;   // FASTA lengths bound the sequences'
     GET(uint32_t, recs, B_RECS, (iters_max > 0 ? iters_max : 1) * SEG_REC_CAP);
     GET(SegStat, stat, B_STAT, iters_max > 0 ? iters_max : 1);
     // (the switch probe's output after the classes: 2 PROBE_PAIRS words)
-    GET(int32_t, cls, B_SEGCLS, (iters_max > 0 ? iters_max : 1) + 2 * PROBE_PAIRS);
-    int32_t* probe_out = cls + (iters_max > 0 ? iters_max : 1);
+    // (after the classes: the switch probe's output (2 PROBE_PAIRS words), its segment list
+    // (PROBE_PAIRS) and the gathered T and R segments (2 PROBE_PAIRS * SEG_GATHER_B bytes))
+    constexpr int64_t PROBE_WORDS = 3 * PROBE_PAIRS + 2 * PROBE_PAIRS * SEG_GATHER_B / 4;
+    GET(int32_t, cls, B_SEGCLS, (iters_max > 0 ? iters_max : 1) + PROBE_WORDS + 64);
+    int32_t* probe_out = cls + (((iters_max > 0 ? iters_max : 1) + 63) & ~int64_t(63));
+    int32_t* probe_segs = probe_out + 2 * PROBE_PAIRS;
+    uint8_t* probe_gT = reinterpret_cast<uint8_t*>(probe_segs + PROBE_PAIRS);
+    uint8_t* probe_gR = probe_gT + PROBE_PAIRS * SEG_GATHER_B;
     int32_t* ctl = reinterpret_cast<int32_t*>(sc + 20);   // {0, bound, switch, 0}
     // Where the local pass goes.  It fills every CU while it runs (LDS and VGPRs), but only the final
     // record text needs it; the global walk (side stream) is the critical path of a switching pair.
@@ -642,8 +672,24 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
             HIPTRY(hipStreamWaitEvent(s, ctx->ev_fork2, 0));
         }
         if (iters_max > 0 && !force_global) {
-            if (!ctx->exact_switch && local_probe_applies(iters_max)) {
-                TRY(launch_local_probe(R, sc + 7, T, sc + 2, probe_out, s));
+            if (probe_mode) {
+                // the probed segments of T and R, from the FASTA when the strips did not write them
+                TRY(launch_probe_segs(sc + 7, sc + 2, probe_segs, s));
+                if (lean_T) {
+                    TRY(launch_strip_gather(INGEST_TGT, tfa, tn, sc, reinterpret_cast<const int64_t*>(ctx->buf[B_TILE_OFF]),
+                                            reinterpret_cast<const int32_t*>(ctx->buf[B_TILE_CARRY]), sc + 2, probe_segs,
+                                            PROBE_PAIRS, probe_gT, s));
+                } else {
+                    TRY(launch_segment_copy(T, sc + 2, probe_segs, PROBE_PAIRS, probe_gT, s));
+                }
+                if (lean_R) {
+                    TRY(launch_strip_gather(INGEST_REF, rfa, rn, nullptr, reinterpret_cast<const int64_t*>(ctx->buf[B_TILE2_OFF]),
+                                            reinterpret_cast<const int32_t*>(ctx->buf[B_TILE2_CARRY]), sc + 7, probe_segs,
+                                            PROBE_PAIRS, probe_gR, s));
+                } else {
+                    TRY(launch_segment_copy(R, sc + 7, probe_segs, PROBE_PAIRS, probe_gR, s));
+                }
+                TRY(launch_local_probe(probe_gR, sc + 7, probe_gT, sc + 2, probe_segs, probe_out, s));
                 HIPTRY(hipMemcpyAsync(ctx->h_probe, probe_out, 2 * PROBE_PAIRS * sizeof(int32_t), hipMemcpyDeviceToHost, s));
                 HIPTRY(hipEventRecord(ctx->ev_probe, s));
                 probe_pending = true;
@@ -709,6 +755,8 @@ int compress_device_impl(sccg_ctx* ctx, const sccg_params& P, const uint8_t* rfa
             HIPTRY(hipEventRecord(ctx->ev_local, s));
             return 0;
         }
+        if (lean_T) TRY(rewrite(INGEST_TGT, s));   // (the local pass reads T and R)
+        if (lean_R) TRY(rewrite(INGEST_REF, s));
         TRY(launch_inorder());
         return local_tail();
     };

@@ -203,7 +203,7 @@ def test_job_models_say_what_they_count():
     import bench
     nT, nR, nRp, out, tfa, rfa = 249_250_621, 247_249_719, 225_000_000, 6_700_000, 254_000_000, 252_000_000
     d = bench.design_alg_bytes(tfa, rfa, nT, nR, nRp, out, True)
-    assert d == tfa + rfa + 2 * (nT + nR) + out + nRp + 0.5 * nT   # (run lines: out of the strip, no T re-read)
+    assert d == tfa + rfa + (nT + nRp) + out + nRp + 0.5 * nT   # (lean strips: T', R' only; run lines from the strip)
     d_local = bench.design_alg_bytes(tfa, rfa, nT, nR, nRp, out, False)
     assert d_local == tfa + rfa + 2 * (nT + nR) + out + 2 * min(nT, nR)
     s = bench.survey_alg_bytes(nT, nR, nRp, out)

@@ -542,3 +542,40 @@ def test_switch_deep_vs_oracle(ctx, plant):
     assert got == want
     got2, rc2 = _gpu_compress(ctx, rfa, tfa)   # default mode: the same bytes
     assert rc2 == 0 and got2 == want and ctx.stats()["mode_global"] == int(mode_global)
+
+
+@pytest.mark.parametrize("kind", ["global", "local", "local0_params"])
+def test_lean_strip_overflow_vs_oracle(ctx, kind):
+    """Lean strips (round 6): a pair of >= 512 segments has its mode decided by the switch probe, so
+    its strips write only T' and R' -- the probe gathers its segments of T and R from the FASTA, a
+    pair that stays local gets T and R from a second write pass, and a tile with more run events
+    than its slots (alternating case: a boundary every base) takes the run-line fallback over T,
+    which writes T first.  Drifted (global), identical (stays local) and local = 0 pairs, each with
+    an overflowing tile and N runs, against the oracle."""
+    rng = random.Random({"global": 7, "local": 8, "local0_params": 9}[kind])
+    ref = list(_rand(rng, 700_000).decode())
+    if kind == "global":   # a 1.5 kb insertion every ~40 kb: segments drift apart
+        tgt = []
+        for i in range(0, len(ref), 40_000):
+            tgt += ref[i:i + 40_000] + list(_rand(rng, 1500).decode())
+    else:
+        tgt = list(ref)
+    for q in range(300_000, 312_000):   # alternating case: a run boundary at every base
+        if q % 2:
+            tgt[q] = tgt[q].lower()
+    for a, ln in ((100_000, 5000), (450_001, 37), (650_000, 1)):
+        for q in range(a, a + ln):
+            tgt[q] = "N"
+    rfa = fuzzgen.to_fasta("".join(ref))
+    tfa = fuzzgen.to_fasta("".join(tgt))
+    if kind == "local0_params":
+        want = oraclelib.compress_params(rfa, tfa, local=0)
+        got = ctx.compress(rfa, tfa, local=0)
+        assert got == want
+        return
+    want = oraclelib.compress(rfa, tfa)
+    mode_global, _ = oraclelib.last_mode()
+    assert mode_global == (kind == "global")
+    got, rc = _gpu_compress(ctx, rfa, tfa)
+    assert (rc, got) == (0, want)
+    assert ctx.stats()["mode_global"] == int(mode_global)
