@@ -483,6 +483,11 @@ def standalone_costs(lane: Lane, pairs: dict, order: list) -> dict:
     plan needs (a T2T-like pair's cost is not proportional to its length)."""
     import torch
     out = {}
+    if order:   # (the lane's buffers sized for the largest pair first: a pair this lane never took in
+        dr, rn, dt_, tn = pairs[order[0]]   # the steps would otherwise pay its reallocations here)
+        lane.ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, lane.out.data_ptr(), lane.cap,
+                                 lane.stream.cuda_stream)
+        lane.stream.synchronize()
     for n in order:
         dr, rn, dt_, tn = pairs[n]
         torch.cuda.synchronize()
@@ -702,6 +707,14 @@ def main() -> None:
     job = device_job(pairs, results, dev)
     gather = multigpu.StreamGather() if world > 1 else None
     step = make_step(pool, order, job, results, gather)
+    # every lane sized for the largest pair once, before any step: the lanes take pairs from a shared
+    # queue, and a lane meeting a larger pair than before in a timed step would grow its buffers there
+    # (hipMalloc, the anchor table's first clear)
+    if order:
+        dr, rn, dt_, tn = pairs[order[0]]
+        for ln in lanes:
+            ln.ctx.compress_device(dr.data_ptr(), rn, dt_.data_ptr(), tn, ln.out.data_ptr(), ln.cap, ln.stream.cuda_stream)
+            ln.stream.synchronize()
 
     for _ in range(max(args.warmup, 1 if world > 1 else 0)):   # (N > 1: the gather's plan is made here)
         step()
