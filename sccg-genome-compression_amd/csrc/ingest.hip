@@ -661,11 +661,21 @@ __global__ __launch_bounds__(64) void k_strip_gather(const uint8_t* __restrict__
     uint8_t* out = dst + (size_t)blockIdx.x * SEG_GATHER_B;
     if (q0 >= q1) return;
     const int64_t ntiles = (n + STRIP_WTILE - 1) / STRIP_WTILE;
-    // last tile t with toff[t] <= q0 (toff is nondecreasing; toff[0] = 0)
-    int64_t lo = 0, hi = ntiles - 1;
+    // last tile t with toff[t] <= q0 (toff is nondecreasing; toff[0] = 0): a 64-way search, one
+    // probe per lane and step (three dependent round trips for a chr1-sized FASTA, not sixteen)
+    int64_t lo = 0, hi = ntiles - 1;   // invariant: toff[lo] <= q0, the answer is in [lo, hi]
     while (lo < hi) {
-        const int64_t mid = (lo + hi + 1) >> 1;
-        if (toff[mid] <= q0) lo = mid; else hi = mid - 1;
+        const int64_t span = hi - lo;
+        const int64_t p = lo + (span * (lane + 1) + 63) / 64;   // lane 63 probes hi
+        const bool le = p <= hi && toff[p] <= q0;
+        const unsigned long long m = __ballot(le);
+        if (!m) { hi = lo + (span + 63) / 64 - 1; if (hi < lo) hi = lo; continue; }
+        const int l = 63 - __builtin_clzll(m);
+        const int64_t pl = lo + (span * (l + 1) + 63) / 64;
+        const int64_t pn = l < 63 ? lo + (span * (l + 2) + 63) / 64 - 1 : hi;
+        lo = pl;
+        hi = pn < hi ? pn : hi;
+        if (hi < lo) hi = lo;
     }
     const int64_t h = MODE == INGEST_TGT ? hdr[0] : 0, he = MODE == INGEST_TGT ? hdr[1] : 0;
     for (int64_t tile = lo; tile < ntiles && toff[tile] < q1; tile++) {
