@@ -446,9 +446,6 @@ __device__ __forceinline__ int32_t lds_first_diff(const uint8_t* rbuf, int32_t r
 // aligned bases at most 15 bytes before the LEAD bytes kept ahead of the stretch) into the copy and
 // compared from there.  (Lanes loading their own 32-byte stretches took 18 dword loads per lane and
 // step, each touching 16 cache lines: with ~5 walk waves per SIMD the round trips queued to ~10 us.)
-#ifndef WALK_LCE_PREFETCH
-#define WALK_LCE_PREFETCH 0
-#endif
 __device__ __forceinline__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPos& B, int32_t a, int32_t b, int32_t maxlen) {
     const int lane = lane_id();
     if (maxlen <= 0) return 0;
@@ -456,42 +453,9 @@ __device__ __forceinline__ int32_t wave_lce(const WalkPtrs& A, WalkLds& L, BufPo
     if (a >= B.rb0 && b >= B.tb0 && a < B.rb0 + LBV && b < B.tb0 + LBV) {
         int32_t avail = B.rb0 + LBV - a < B.tb0 + LBV - b ? B.rb0 + LBV - a : B.tb0 + LBV - b;
         if (avail > maxlen) avail = maxlen;
-#if WALK_LCE_PREFETCH
-        // (WALK_LCE_PREFETCH, A/B) the extension may run past the copy: the next 2 KiB of each are
-        // loaded now, while the copy's part is compared, and dropped if a mismatch comes first
-        if (avail < maxlen && avail >= WALK_LCE_PREFETCH) {
-            const int32_t o2 = avail;
-            const int32_t lead = (a + o2 >= LEAD && b + o2 >= LEAD) ? LEAD : 0;
-            const int32_t sa = (a + o2 - lead) & ~15, sb = (b + o2 - lead) & ~15;
-            const uint4* gr = reinterpret_cast<const uint4*>(A.R + sa) + lane;
-            const uint4* gt = reinterpret_cast<const uint4*>(A.T + sb) + lane;
-            const uint4 r0 = gr[0], r1 = gr[64], t0 = gt[0], t1 = gt[64];
-            const int32_t e = lds_first_diff(L.rbuf, a - B.rb0, L.tbuf, b - B.tb0, avail);
-            if (e < avail) return e;
-            wave_sync();   // the copy's previous readers are done
-            {
-                uint4* dr = reinterpret_cast<uint4*>(L.rbuf) + lane;
-                uint4* dt = reinterpret_cast<uint4*>(L.tbuf) + lane;
-                dr[0] = r0; dr[64] = r1;
-                dt[0] = t0; dt[64] = t1;
-            }
-            wave_sync();
-            B.rb0 = sa;
-            B.tb0 = sb;
-            off = o2;
-            const int32_t ra = a + off - sa, tb = b + off - sb;
-            int32_t av2 = LBV - (ra > tb ? ra : tb);
-            if (av2 > maxlen - off) av2 = maxlen - off;
-            const int32_t e2 = lds_first_diff(L.rbuf, ra, L.tbuf, tb, av2);
-            if (e2 < av2) return off + e2;
-            off += av2;
-        } else
-#endif
-        {
-            const int32_t e = lds_first_diff(L.rbuf, a - B.rb0, L.tbuf, b - B.tb0, avail);
-            if (e < avail || avail >= maxlen) return e;
-            off = avail;
-        }
+        const int32_t e = lds_first_diff(L.rbuf, a - B.rb0, L.tbuf, b - B.tb0, avail);
+        if (e < avail || avail >= maxlen) return e;
+        off = avail;
     }
     while (off < maxlen) {
         const int32_t lead = (a + off >= LEAD && b + off >= LEAD) ? LEAD : 0;
