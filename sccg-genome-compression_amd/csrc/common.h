@@ -144,6 +144,20 @@ __device__ __forceinline__ T wave_incl_add(T v) {
     }
     return v;
 }
+// 32-bit inclusive wave scan on DPP (six v_add_u32_dpp, against ~36 VALU and six ds_bpermute for
+// the shuffle ladder above): row_shr 1/2/4/8 inside each 16-lane row (bound_ctrl: lanes shifted in
+// from outside the row add 0), then row 0's total into row 1 and row 2's into row 3 (row_bcast:15),
+// then rows 0-1's into rows 2-3 (row_bcast:31).  Needs the whole wave active.  Packed counters
+// scan field by field as long as no field's total carries into the next.
+__device__ __forceinline__ uint32_t wave_incl_add_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

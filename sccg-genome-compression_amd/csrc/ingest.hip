@@ -217,11 +217,23 @@ struct StripMasks {
     uint64_t known, unknown, fk, par;
     int32_t last;   // status of the last line start in range: -1 none, 0 drop, 1 keep
     uint64_t lower, nn;   // RUNS: bytes 'a'..'z' and bytes 'N' / 'n' (the two run lines' predicates)
+    uint64_t odd;         // ODD: nonzero when a flagged byte is neither whitespace nor a letter other than N / n
 };
+
+// RUNS: lowercase bytes by bit 5 alone -- exact for letters (and unkept whitespace does not matter)
+__device__ __forceinline__ uint64_t lower_fast(const uint32_t (&w)[SNW]) {
+    uint64_t lo = 0;
+#pragma unroll
+    for (int q = 0; q < SNW; q++) {
+        const uint32_t t = (w[q] >> 5) & 0x01010101u;
+        lo |= (uint64_t)(((t * 0x01020408u) >> 24) & 0xfu) << (4 * q);
+    }
+    return lo;
+}
 
 __device__ __forceinline__ uint64_t below64(int k) { return k >= 64 ? ~0ull : (1ull << k) - 1ull; }
 
-template <IngestMode MODE, bool RUNS = false>
+template <IngestMode MODE, bool RUNS = false, bool ODD = false>
 __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t (&w)[SNW], uint8_t prev, int64_t off,
                                                   int64_t n, int64_t h, int64_t he, const uint8_t* __restrict__ lbytes) {
     // Byte classes.  Every byte that matters (whitespace, '\n', '>', '(', N / n) is outside
@@ -247,15 +259,9 @@ __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t 
     const uint64_t sp = ((uint64_t)sph[1] << 32) | sph[0];
     // RUNS: lowercase bytes in byte order -- an unflagged byte (A C G T a c g t) is lowercase iff its
     // bit 5 is set (a word's four bits gathered by one multiply); flagged bytes are set below
-    uint64_t lo = 0, nn = 0;
-    if (RUNS) {
-#pragma unroll
-        for (int q = 0; q < SNW; q++) {
-            const uint32_t t = (w[q] >> 5) & 0x01010101u;
-            lo |= (uint64_t)(((t * 0x01020408u) >> 24) & 0xfu) << (4 * q);
-        }
-    }
+    uint64_t lo = RUNS ? lower_fast(w) : 0ull, nn = 0;
     uint64_t ws = 0, nl = 0, gt = 0, drop = 0, par = 0;
+    bool odd = false;   // (a lane flag: its compares stay in scalar lane masks)
     for (uint64_t m = sp; m; m &= m - 1) {
         const int j = __builtin_ctzll(m);
         const int i = (j & 32) + 4 * (j & 7) + ((j >> 3) & 3);
@@ -266,7 +272,12 @@ __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t 
             if (c >= 'a' && c <= 'z') lo |= bit;
             if (c == 'N' || c == 'n') nn |= bit;
         }
-        if (c == ' ' || (c >= 9 && c <= 13)) ws |= bit;   // isspace
+        const bool space = c == ' ' || (c >= 9 && c <= 13);
+        if (space) ws |= bit;   // isspace
+        if (ODD) {   // (bitwise, not short-circuit: a branch per flagged byte cost more than the compares)
+            const uint32_t cl = c | 32u;
+            odd |= !(space | (((cl - 'a') < 26u) & (cl != 'n')));
+        }
         if (MODE == INGEST_REF) {
             if (c == '\n') nl |= bit;
             if (c == '>') gt |= bit;
@@ -277,7 +288,7 @@ __device__ __forceinline__ StripMasks strip_masks(FilterMode fm, const uint32_t 
     const uint64_t fk = ~drop;
     const int64_t lim = n - off;
     const uint64_t valid = lim >= 64 ? ~0ull : (lim > 0 ? (1ull << lim) - 1ull : 0ull);
-    StripMasks r{0, 0, fk, par, -1, lo, nn};
+    StripMasks r{0, 0, fk, par, -1, lo, nn, odd ? 1ull : 0ull};
     if (MODE == INGEST_TGT) {
         const int64_t lo = h - off < 0 ? 0 : (h - off > 64 ? 64 : h - off);
         const int64_t hi = he - off < 0 ? 0 : (he - off > 64 ? 64 : he - off);
@@ -340,7 +351,7 @@ __device__ __forceinline__ void load_lane64(const uint8_t* __restrict__ buf, int
 
 // A wave's tile: its words, the byte before it (lane 0's 'prev'), the masks, and each lane's prior
 // line status inside the wave (-1: no line start in the lanes before it).
-template <IngestMode MODE, bool RUNS = false>
+template <IngestMode MODE, bool RUNS = false, bool ODD = false>
 __device__ __forceinline__ StripMasks strip_tile(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n, int64_t h,
                                                  int64_t he, int64_t off, uint32_t (&w)[SNW], int32_t& prior,
                                                  uint64_t& lsm, uint4* tin) {
@@ -360,7 +371,7 @@ __device__ __forceinline__ StripMasks strip_tile(FilterMode fm, const uint8_t* _
         const uint32_t up = (uint32_t)__shfl_up((int)w[SNW - 1], 1, 64) >> 24;
         prev = lane ? (uint8_t)up : ((off > 0 && off - 1 < n) ? buf[off - 1] : (uint8_t)'\n');
     }
-    const StripMasks r = strip_masks<MODE, RUNS>(fm, w, prev, off, n, h, he, reinterpret_cast<const uint8_t*>(tin + 4 * lane));
+    const StripMasks r = strip_masks<MODE, RUNS, ODD>(fm, w, prev, off, n, h, he, reinterpret_cast<const uint8_t*>(tin + 4 * lane));
     wave_sync();   // (k_strip_write stages its output in tin next)
     prior = -1;
     lsm = 0;
@@ -374,11 +385,19 @@ __device__ __forceinline__ StripMasks strip_tile(FilterMode fm, const uint8_t* _
     return r;
 }
 
-template <IngestMode MODE>
+// KC: also the keep-mask cache of the write pass.  kc: per lane the positions of its (at most two)
+// unkept bytes, 7 bits each (64: none), with the tile's line status assumed "keep" where it is
+// still open -- a FASTA line of 32 or more bytes leaves one or two newlines per 64-byte lane.
+// kflag bit 0: the tile is plain -- every byte outside ACGTacgt is whitespace or a letter other
+// than N / n (nothing is filtered, no '(' or '>' is kept, the run predicates follow from the bytes
+// alone) and no lane has more than two unkept bytes; bit 1: some kept byte depends on the line
+// status carried in from earlier tiles.
+template <IngestMode MODE, bool KC>
 __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(FilterMode fm, const uint8_t* __restrict__ buf, int64_t n,
                                                               const int64_t* __restrict__ hdr, int64_t* __restrict__ ta,
                                                               int64_t* __restrict__ tb, int64_t* __restrict__ tfa,
-                                                              int64_t* __restrict__ tfb, int32_t* __restrict__ tlast) {
+                                                              int64_t* __restrict__ tfb, int32_t* __restrict__ tlast,
+                                                              uint16_t* __restrict__ kc, int32_t* __restrict__ kflag) {
     __shared__ uint4 tin_all[WPB][STRIP_WTILE / 16];
     const int64_t tile = (int64_t)blockIdx.x * WPB + wave_in_block();
     if (tile * STRIP_WTILE >= n) return;
@@ -388,13 +407,24 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_summary(FilterMode fm, con
     uint32_t w[SNW];
     int32_t prior;
     uint64_t lsm;
-    const StripMasks r = strip_tile<MODE>(fm, buf, n, h, he, off, w, prior, lsm, tin_all[wave_in_block()]);
+    const StripMasks r = strip_tile<MODE, false, KC>(fm, buf, n, h, he, off, w, prior, lsm, tin_all[wave_in_block()]);
+    if (KC) {
+        const uint64_t hole = ~(r.known | (prior != 0 ? r.unknown : 0ull));
+        const uint32_t h1 = hole ? (uint32_t)__builtin_ctzll(hole) : 64u, h2 = hole ? 63u - (uint32_t)__builtin_clzll(hole) : 64u;
+        kc[tile * 64 + lane] = (uint16_t)(h1 | (h2 << 7));
+        const uint64_t odd = __ballot(r.odd != 0 || __popcll(hole) > 2);
+        const uint64_t sens = __ballot(MODE == INGEST_REF && prior < 0 && r.unknown != 0);
+        if (lane == 0) kflag[tile] = (odd ? 0 : 1) | (sens ? 2 : 0);
+    }
     // a-bytes of a lane with a prior line start in the wave are resolved now
     const uint64_t ra = (uint64_t)__popcll(r.unknown), rb = (uint64_t)__popcll(r.known);
     const uint64_t rfa = (uint64_t)__popcll(r.unknown & r.fk), rfb = (uint64_t)__popcll(r.known & r.fk);
     const uint64_t A = prior < 0 ? ra : 0, B = rb + (prior == 1 ? ra : 0);
     const uint64_t FA = prior < 0 ? rfa : 0, FB = rfb + (prior == 1 ? rfa : 0);
-    const uint64_t tot = wave_sum<uint64_t>(A | (B << 16) | (FA << 32) | (FB << 48));   // <= 4096 each
+    // (each field's total <= 4096: the two 32-bit halves are summed apart)
+    const uint32_t t_ab = lane_val(wave_incl_add_dpp((uint32_t)(A | (B << 16))), 63);
+    const uint32_t t_f = lane_val(wave_incl_add_dpp((uint32_t)(FA | (FB << 16))), 63);
+    const uint64_t tot = (uint64_t)t_ab | ((uint64_t)t_f << 32);
     if (lane == 0) {
         ta[tile] = (int64_t)(tot & 0xffff);
         tb[tile] = (int64_t)((tot >> 16) & 0xffff);
@@ -554,7 +584,8 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
                                                             const int64_t* __restrict__ toff2,
                                                             const int32_t* __restrict__ tcarry,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out2,
-                                                            int32_t* __restrict__ flags, RunSlots rsl) {
+                                                            int32_t* __restrict__ flags, RunSlots rsl,
+                                                            const uint16_t* __restrict__ kc, const int32_t* __restrict__ kflag) {
     __shared__ uint4 stage_all4[WPB][(STAGE_WORDS + 3) / 4];   // (also the coalesced load's transpose)
     __shared__ uint32_t tab[16];
     if (threadIdx.x < 16) tab[threadIdx.x] = compact_sel(threadIdx.x);
@@ -569,11 +600,24 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
     uint32_t w[SNW];
     int32_t prior;
     uint64_t lsm;
-    const StripMasks r = strip_tile<MODE, RUNS>(fm, buf, n, h, he, off, w, prior, lsm, stage_all4[wave_in_block()]);
-    if (MODE == INGEST_REF && prior < 0) prior = tcarry[tile];
+    StripMasks r;
+    // a plain tile (k_strip_summary's kflag) takes its kept bytes from the summary's mask cache
+    // instead of classifying its bytes again, unless they depend on a carried-in line status other
+    // than "keep"
+    const int32_t kf = kc ? uni(kflag[tile]) : 0;
+    if ((kf & 1) && (MODE == INGEST_TGT || !(kf & 2) || uni(tcarry[tile]) == 1)) {
+        load_words<SNW>(buf, n, off, w);
+        const uint32_t code = kc[tile * 64 + lane], h1 = code & 127u, h2 = code >> 7;
+        const uint64_t keep = ~((h1 < 64 ? 1ull << h1 : 0ull) | (h2 < 64 ? 1ull << h2 : 0ull));
+        r = StripMasks{keep, 0ull, ~0ull, 0ull, -1, RUNS ? lower_fast(w) : 0ull, 0ull, 0ull};
+        prior = 1;
+    } else {
+        r = strip_tile<MODE, RUNS>(fm, buf, n, h, he, off, w, prior, lsm, stage_all4[wave_in_block()]);
+        if (MODE == INGEST_REF && prior < 0) prior = tcarry[tile];
+    }
     const uint64_t keep = r.known | (prior == 1 ? r.unknown : 0ull), fkeep = keep & r.fk;
     const uint32_t c = (uint32_t)__popcll(keep) | ((uint32_t)__popcll(fkeep) << 16);
-    const uint32_t incl = wave_incl_add<uint32_t>(c), tot = lane_val(incl, 63);
+    const uint32_t incl = wave_incl_add_dpp(c), tot = lane_val(incl, 63);
     const uint32_t ex = incl - c;
     if (RUNS) {
         // the previous kept byte's predicates: the nearest earlier lane with a kept byte; the wave's
@@ -595,7 +639,10 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_strip_write(FilterMode fm, const
         }
         const uint64_t cc = (uint64_t)__popcll(sl) | ((uint64_t)__popcll(el) << 16) | ((uint64_t)__popcll(sn) << 32) |
                             ((uint64_t)__popcll(en) << 48);
-        const uint64_t ci = wave_incl_add<uint64_t>(cc), ct = __shfl(ci, 63, 64);
+        // (four 16-bit counts, totals <= 4096: the halves scan apart)
+        const uint32_t ci_lo = wave_incl_add_dpp((uint32_t)cc), ci_hi = wave_incl_add_dpp((uint32_t)(cc >> 32));
+        const uint64_t ci = (uint64_t)ci_lo | ((uint64_t)ci_hi << 32);
+        const uint64_t ct = (uint64_t)lane_val(ci_lo, 63) | ((uint64_t)lane_val(ci_hi, 63) << 32);
         const uint64_t cx = ci - cc;
         const int fl = hm ? first_lane(hm) : 0, ll = hm ? 63 - __builtin_clzll(hm) : 0;
         const uint32_t tf = (uint32_t)__shfl((int)first2, fl, 64), tl = (uint32_t)__shfl((int)last2, ll, 64);
@@ -947,12 +994,16 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     if (!out2) fmode = FILTER_UPPER;   // second output unused
     const int64_t ntiles = (n + STRIP_TILE - 1) / STRIP_TILE;
     const unsigned g = grid_for(ntiles, WPB);
-    if (mode == INGEST_TGT)
-        hipLaunchKernelGGL(k_strip_summary<INGEST_TGT>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header, sc.tile_a,
-                           sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last);
-    else
-        hipLaunchKernelGGL(k_strip_summary<INGEST_REF>, dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header, sc.tile_a,
-                           sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last);
+    uint16_t* const kc = sc.keep_cache;
+    int32_t* const kf = sc.keep_flag;
+#define SUMMARY(M, K)                                                                                                   \
+    hipLaunchKernelGGL((k_strip_summary<M, K>), dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header, sc.tile_a,   \
+                       sc.tile_b, sc.tile_fa, sc.tile_fb, sc.tile_last, kc, kf)
+    if (mode == INGEST_TGT && kc) SUMMARY(INGEST_TGT, true);
+    else if (mode == INGEST_TGT) SUMMARY(INGEST_TGT, false);
+    else if (kc) SUMMARY(INGEST_REF, true);
+    else SUMMARY(INGEST_REF, false);
+#undef SUMMARY
     const int64_t nblk = (ntiles + SCAN_B - 1) / SCAN_B;
     if (nblk > SCAN_B) return SCCG_E_UNSUPPORTED;   // > 4 GiB of FASTA
     TileSum* btot = reinterpret_cast<TileSum*>(sc.block_sums);
@@ -965,13 +1016,13 @@ int launch_fasta_strip(IngestMode mode, const uint8_t* buf, int64_t n, const int
     const RunSlots rsl = runs ? *runs : RunSlots{};
     if (mode == INGEST_TGT && runs)
         PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_TGT, true>), dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl);
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl, (const uint16_t*)kc, (const int32_t*)kf);
     else if (mode == INGEST_TGT)
         PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_TGT, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl);
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl, (const uint16_t*)kc, (const int32_t*)kf);
     else
         PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_REF, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, fmode, buf, n, d_header,
-                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl);
+                    sc.tile_off, sc.tile_off2, sc.tile_carry, out, out2, d_flags, rsl, (const uint16_t*)kc, (const int32_t*)kf);
     SCCG_HIP(hipGetLastError());
     return 0;
 }
@@ -1046,10 +1097,12 @@ int launch_strip_rewrite(IngestMode mode, const uint8_t* buf, int64_t n, const i
     const RunSlots rsl{};
     if (mode == INGEST_TGT)
         PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_TGT, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, FILTER_UPPER, buf, n,
-                    d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, (uint8_t*)nullptr, (int32_t*)nullptr, rsl);
+                    d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, (uint8_t*)nullptr, (int32_t*)nullptr, rsl,
+                    (const uint16_t*)nullptr, (const int32_t*)nullptr);
     else
         PROF_LAUNCH(PROF_STRIP, s, (k_strip_write<INGEST_REF, false>), dim3(g), dim3(SCCG_BLOCK), 0, s, FILTER_UPPER, buf, n,
-                    d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, (uint8_t*)nullptr, (int32_t*)nullptr, rsl);
+                    d_header, sc.tile_off, sc.tile_off2, sc.tile_carry, out, (uint8_t*)nullptr, (int32_t*)nullptr, rsl,
+                    (const uint16_t*)nullptr, (const int32_t*)nullptr);
     SCCG_HIP(hipGetLastError());
     return 0;
 }

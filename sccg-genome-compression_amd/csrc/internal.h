@@ -79,6 +79,8 @@ struct IngestScratch {
     int32_t* tile_carry;
     void* block_sums;     // (1024 + 1) x 40 bytes
     int64_t* scalars;     // [0] header start, [1] header end, [2] out len, [3] flags
+    uint16_t* keep_cache = nullptr;   // per tile 64 lanes' unkept-byte codes, or null: the write pass classifies every tile
+    int32_t* keep_flag = nullptr;     // per tile (k_strip_summary)
 };
 
 // Target header: first line starting with '>' (compression.cpp:210); writes [h, he) into

@@ -367,9 +367,17 @@ int strip(sccg_ctx* ctx, IngestMode mode, const uint8_t* fa, int64_t n, const in
     GET(int64_t, to, B_TILE_OFF + o, ntiles);
     GET(int64_t, to2, B_TILE_OFF2 + o, ntiles);
     GET(int32_t, tc, B_TILE_CARRY + o, ntiles);
-    GET(int64_t, bs, B_TILE_BSUM + o, 1025 * 5);
+    // the block sums, then (SCCG_STRIP_KC, default on) the write pass's keep-mask cache: 2 bytes per
+    // 64 FASTA bytes, written by the summary and read back instead of classifying plain tiles again
+    static const bool kc_on = [] { const char* e = getenv("SCCG_STRIP_KC"); return !e || atoi(e) > 0; }();
+    constexpr int64_t KC_AT = 5152;   // (int64s: 1025 x 5 rounded up to 256 bytes)
+    GET(int64_t, bs, B_TILE_BSUM + o, kc_on ? KC_AT + ntiles * 16 + (ntiles + 1) / 2 : 1025 * 5);
     sc.tile_a = ta; sc.tile_b = tb; sc.tile_fa = tfa; sc.tile_fb = tfb; sc.tile_last = tl; sc.tile_off = to;
     sc.tile_off2 = to2; sc.tile_carry = tc; sc.block_sums = bs; sc.scalars = nullptr;
+    if (kc_on) {
+        sc.keep_cache = reinterpret_cast<uint16_t*>(bs + KC_AT);
+        sc.keep_flag = reinterpret_cast<int32_t*>(bs + KC_AT + ntiles * 16);
+    }
     TRY(launch_fasta_strip(mode, fa, n, d_hdr, out, d_len, d_flags, sc, s ? s : ctx->stream, fmode, out2,
                            out2 ? d_len + 1 : nullptr, runs));
     return h_len ? d2h_i64(ctx, d_len, h_len, out2 ? 2 : 1, s) : 0;   // h_len null: the caller reads d_len later
