@@ -465,47 +465,64 @@ __global__ void k_tok_check(const uint8_t* __restrict__ s, int64_t n, const int6
 }
 
 constexpr int WPB = 4;
+// 16 bytes from any byte address: one global_load_dwordx4 (gfx950 runs in unaligned access mode;
+// SCCG_UNALIGNED_LD=0: five dword loads combined with v_alignbyte, as before round 6)
+#ifndef SCCG_UNALIGNED_LD
+#define SCCG_UNALIGNED_LD 1
+#endif
+__device__ __forceinline__ uint4 load16u(const uint8_t* __restrict__ p) {
+    uint4 v;
+    if (SCCG_UNALIGNED_LD) {
+        __builtin_memcpy(&v, p, 16);
+    } else {
+        const uint32_t* sa = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+        const unsigned sh = (unsigned)((uintptr_t)p & 3);
+        uint32_t w[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) w[i] = sa[i];
+        v = make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                       __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh));
+    }
+    return v;
+}
 // dst[0, l) = src[0, l) by one wave: bytes up to dst's next 16-byte boundary and after its last one
-// one per lane, the rest 16 bytes per lane as aligned stores built from five dword loads of the
-// (unaligned) source combined with v_alignbyte.  The source may be read up to 19 bytes past
-// src + l (the reference buffers carry 64 bytes of slack).
+// one per lane, the rest 16 bytes per lane as aligned stores of (unaligned) 16-byte source loads.
+// The source may be read up to 19 bytes past src + l (the reference buffers carry 64 bytes of slack).
 #ifndef WC_DEPTH
 #define WC_DEPTH 2
 #endif
+__device__ __forceinline__ void wave_copy_body(uint4* __restrict__ d, const uint8_t* __restrict__ s0, int64_t nb, int64_t from,
+                                               int lane);
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t l, int lane) {
     const int64_t h = ((16 - ((uintptr_t)dst & 15)) & 15) < l ? ((16 - ((uintptr_t)dst & 15)) & 15) : l;
     const int64_t nb = (l - h) >> 4;
     const int64_t t0 = h + (nb << 4);
     if (lane < h) dst[lane] = src[lane];
     if (lane < l - t0) dst[t0 + lane] = src[t0 + lane];
-    const uint8_t* s0 = src + h;
-    const unsigned sh = (unsigned)((uintptr_t)s0 & 3);
-    const uint32_t* sa = reinterpret_cast<const uint32_t*>((uintptr_t)s0 & ~(uintptr_t)3);
-    uint4* d = reinterpret_cast<uint4*>(dst + h);
+    wave_copy_body(reinterpret_cast<uint4*>(dst + h), src + h, nb, 0, lane);
+}
+
+// 16-byte chunks [from, nb) of d = s0 (d 16-byte aligned)
+__device__ __forceinline__ void wave_copy_body(uint4* __restrict__ d, const uint8_t* __restrict__ s0, int64_t nb, int64_t from,
+                                               int lane) {
     // WC_DEPTH KiB of loads in flight per wave before the stores (one 1 KiB step at a time left the
     // fill bound by the bytes in flight: ~3 TB/s)
-    for (int64_t c0 = lane; c0 < nb; c0 += 64 * WC_DEPTH) {
-        uint32_t w[WC_DEPTH][5];
+    for (int64_t c0 = from + lane; c0 < nb; c0 += 64 * WC_DEPTH) {
+        uint4 v[WC_DEPTH];
 #pragma unroll
         for (int u = 0; u < WC_DEPTH; u++) {
             const int64_t c = c0 + 64 * u;
-            if (c < nb) {
-                const uint32_t* ws = sa + 4 * c;
-#pragma unroll
-                for (int i = 0; i < 5; i++) w[u][i] = ws[i];
-            }
+            if (c < nb) v[u] = load16u(s0 + 16 * c);
         }
 #pragma unroll
         for (int u = 0; u < WC_DEPTH; u++) {
             const int64_t c = c0 + 64 * u;
-            if (c < nb) {
-                uint4 v;
-                v.x = __builtin_amdgcn_alignbyte(w[u][1], w[u][0], sh);
-                v.y = __builtin_amdgcn_alignbyte(w[u][2], w[u][1], sh);
-                v.z = __builtin_amdgcn_alignbyte(w[u][3], w[u][2], sh);
-                v.w = __builtin_amdgcn_alignbyte(w[u][4], w[u][3], sh);
-                d[c] = v;
-            }
+            if (c < nb) d[c] = v[u];
         }
     }
 }
@@ -675,10 +692,10 @@ __global__ __launch_bounds__(SCCG_BLOCK) void k_tok_fill2(const uint8_t* __restr
     if (!tok && contrib == 1 && c != '(' && o < dcap) dec[o] = c;   // literals, a stray ')' included
     unsigned long long tm = __ballot(tok);
     while (tm) {
-        const int j = __ffsll((long long)tm) - 1;
+        const int j = __ffsll((long long)tm) - 1;   // (wave-uniform: the token's fields by readlane)
         tm &= tm - 1;
-        const int64_t pj = __shfl(p, j), oj = __shfl(o, j);
-        int64_t lj = __shfl(contrib, j);
+        const int64_t pj = readlane64(p, j), oj = readlane64(o, j);
+        int64_t lj = readlane64(contrib, j);
         if (lj > dcap - oj) lj = dcap - oj > 0 ? dcap - oj : 0;
         wave_copy(dec + oj, R + pj, lj, lane);
     }
@@ -1064,13 +1081,8 @@ __device__ __forceinline__ void format_out16_at(int64_t o0, int64_t total, const
             }
             uint32_t w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0};
             auto load16 = [&](int64_t at, uint32_t (&w)[4]) {
-                const uint32_t* sw = reinterpret_cast<const uint32_t*>(sdec) + (at >> 2);
-                const uint32_t sh = (uint32_t)(at & 3);
-                uint32_t v[5];
-#pragma unroll
-                for (int qq = 0; qq < 5; qq++) v[qq] = sw[qq];
-#pragma unroll
-                for (int qq = 0; qq < 4; qq++) w[qq] = __builtin_amdgcn_alignbyte(v[qq + 1], v[qq], sh);
+                const uint4 v = load16u(reinterpret_cast<const uint8_t*>(sdec) + at);
+                w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
             };
             if (use1) load16(at1, w1);
             if (use2) load16(at2, w2);
