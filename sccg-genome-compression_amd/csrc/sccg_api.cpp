@@ -1228,17 +1228,26 @@ int reconstruct_impl(sccg_ctx* ctx, const uint8_t* rfa, int64_t rn, const uint8_
     }
     HIPTRY(hipEventRecord(ctx->ev_fork2, s));
     HIPTRY(hipStreamWaitEvent(ctx->side2, ctx->ev_fork2, 0));
-    // The record line's chain (main stream) is the critical one -- its token blocks share the GPU
-    // with the reference strip, ~0.1 ms on chr1 (gpurun_out/r05t/dprof) -- so it is issued first
-    // (the host issues launches one at a time); the run lines' parses follow on side2 and are
-    // joined before the N check.
+    // The host issues launches one at a time, so the chain issued first starts ~40 us earlier.
+    // Round 6: the run lines' chain (side2) is the critical one -- with the reference strip's
+    // write pass shortened, the record line's token blocks end ~70 us before the run lines'
+    // parse on chr1 (profiles/r06/dprof_timeline.txt) -- so it goes first (SCCG_DC_RUNS_FIRST=0:
+    // the record line's chain first, as in round 5, when the strip's grid delayed the token blocks).
+    // The two are joined before the N check.
+    static const bool runs_first = [] { const char* e = getenv("SCCG_DC_RUNS_FIRST"); return !e || atoi(e) > 0; }();
     DcRuns lr{}, nr{};
     lr.start = ls; lr.len = ll; lr.cum = lc;
     nr.start = ns; nr.len = nlr; nr.cum = nc;
+    if (runs_first) {
+        TRY(dc_parse_runs2(lower, nlower, &lr, sc + 14, nline, nnl, &nr, sc + 16, lp, flag, dlt, part, d_err, ctx->side2));
+        HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
+    }
     TRY(dc_decode_prepare(enc, nenc, lp2, contrib, dlt2, doff, dsum, sc + 9, ctx->ev_rstrip, part2, d_err, sc + 12,
                           s, fused ? &tk : nullptr));
-    TRY(dc_parse_runs2(lower, nlower, &lr, sc + 14, nline, nnl, &nr, sc + 16, lp, flag, dlt, part, d_err, ctx->side2));
-    HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
+    if (!runs_first) {
+        TRY(dc_parse_runs2(lower, nlower, &lr, sc + 14, nline, nnl, &nr, sc + 16, lp, flag, dlt, part, d_err, ctx->side2));
+        HIPTRY(hipEventRecord(ctx->ev_lines, ctx->side2));
+    }
     HIPTRY(hipStreamWaitEvent(s, ctx->ev_lines, 0));
     // The usual call queues the token fill right behind the N check, before the host knows the
     // decoded length D, into a buffer of the output's capacity (D <= nres < out_cap whenever the
