@@ -982,7 +982,8 @@ __global__ __launch_bounds__(256) void k_format_span(const uint8_t* __restrict__
 #endif
 constexpr int OPT = 16, OB = 256 * OPT, OFRUNS = SCCG_OFRUNS;   // (a block with more runs takes the global-runs path)
 constexpr int TW = 5;   // k_out_index entries per block boundary
-constexpr int FMT_U_DEFAULT = 4;   // (U = 1 / 2 / 4 on one box, chr1: 0.638-0.647 / 0.634-0.639 / 0.624-0.626 ms)
+constexpr int FMT_U_DEFAULT = 4;   // (U = 1 / 2 / 4 on one box, chr1: 0.638-0.647 / 0.634-0.639 / 0.624-0.626 ms;
+                                    //  round 6, U = 8: 42 KiB of LDS per block, 0.677-0.682 against 0.614-0.638)
 constexpr bool FMT_NT_DEFAULT = false;
 
 // Block boundaries: output offset o_b = o_first + b * OB clamped to [0, total]; its position
