@@ -7,6 +7,10 @@
   below the decoded length itself), a far larger one, and tokens beyond the reference (:223-229,
   SCCG_E_RANGE).  The knob is read once per process, so the
   checks run in a child process.
+* The same child with the round-5 orders and passes: SCCG_STRIP_KC=0 (the strips' write pass
+  classifies every tile again instead of taking plain tiles' masks from the summary) and
+  SCCG_DC_RUNS_FIRST=0 (the record line's parse chain issued before the run lines'); the record
+  streams are checked against the oracle there too.
 * sccg_profile with a family mask brackets only those families (bench.py's timed region).
 """
 import json
@@ -34,11 +38,12 @@ import json, sys
 sys.path.insert(0, HERE)
 import torch
 import synthlib
+import oraclelib
 from pkg import sccg
 dev = torch.device("cuda", 0)
 torch.zeros(1, device=dev)   # torch's HIP runtime before the library context
 ctx = sccg.Context(0)
-out = {"round_trips": [], "nomem": None, "range": []}
+out = {"round_trips": [], "nomem": None, "range": [], "oracle": []}
 
 def dev_bytes(b):
     return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
@@ -53,6 +58,7 @@ def run(rfa, rec, cap):
 for prof, rl, tl, seed in (("hg", 200_000, 201_000, 3), ("hg", 1_000_000, 1_003_000, 4), ("t2t", 300_000, 300_000, 5)):
     rfa, tfa = synthlib.synth_pair(prof, rl, tl, seed)
     rec = ctx.compress(rfa, tfa)
+    out["oracle"].append(rec == oraclelib.compress(rfa, tfa))
     need = ctx.reconstruct_device(dev_bytes(rfa).data_ptr(), len(rfa), dev_bytes(rec).data_ptr(), len(rec), 0, 0)
     got = run(rfa, rec, need + 64)
     out["round_trips"].append(got == tfa)
@@ -83,17 +89,19 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("spec", ["0", None], ids=["fill_after_readback", "speculative_fill"])
-def test_fill_round_trips_and_errors(spec):
+@pytest.mark.parametrize("knobs", [{"SCCG_DC_SPEC": "0"}, {}, {"SCCG_STRIP_KC": "0", "SCCG_DC_RUNS_FIRST": "0"}],
+                         ids=["fill_after_readback", "speculative_fill", "round5_strip_and_order"])
+def test_fill_round_trips_and_errors(knobs):
     env = dict(os.environ)
-    env.pop("SCCG_DC_SPEC", None)
-    if spec is not None:
-        env["SCCG_DC_SPEC"] = spec
+    for k in ("SCCG_DC_SPEC", "SCCG_STRIP_KC", "SCCG_DC_RUNS_FIRST"):
+        env.pop(k, None)
+    env.update(knobs)
     p = subprocess.run([sys.executable, "-c", f"HERE = {HERE!r}\n" + CHILD], env=env, capture_output=True, text=True,
                        timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads(p.stdout.strip().splitlines()[-1])
     assert d["round_trips"] == [True, True, True], d
+    assert d["oracle"] == [True, True, True], d
     assert d["nomem"] == sccg.ERR_CODES["SCCG_E_NOMEM"], d
     assert d["nomem_below_d"] == sccg.ERR_CODES["SCCG_E_NOMEM"], d
     assert d["big_cap"] is True, d
